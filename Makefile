@@ -1,0 +1,50 @@
+# Build for MI355X (gfx950). Outputs stay in-tree so they travel to the GPU box with gpurun.
+#   make            -> oceansimulation_amd/liboceanfft.so (C ABI), libwaves.so (C++ Waves API),
+#                      oracle/build/liboceanoracle.so (CPU checker), tests/cpp/test_waves
+HIPCC ?= /opt/rocm/bin/hipcc
+ARCH ?= gfx950
+JOBS ?= 8
+
+PKG := oceansimulation_amd
+CSRC := $(PKG)/csrc
+# -fno-slp-vectorize: the SLP vectoriser packs the complex butterflies into v_pk_* with op_sel
+# shuffles and pushes the column pass past 128 VGPRs (spills); scalar f32 code needs ~100.
+HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -fno-slp-vectorize -Wall -Iinclude -I$(CSRC)
+
+LIB := $(PKG)/liboceanfft.so
+WAVES := $(PKG)/libwaves.so
+ORACLE := oracle/build/liboceanoracle.so
+CPPTEST := tests/cpp/test_waves
+
+all: $(LIB) $(WAVES) $(ORACLE) $(CPPTEST)
+
+$(CSRC)/build/ocean_kernels.o: $(CSRC)/ocean_kernels.hip $(CSRC)/ocean_internal.h
+	@mkdir -p $(CSRC)/build
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+$(CSRC)/build/ocean_capi.o: $(CSRC)/ocean_capi.cpp $(CSRC)/ocean_internal.h include/oceanfft.h
+	@mkdir -p $(CSRC)/build
+	$(HIPCC) $(HIPFLAGS) -x hip -c $< -o $@
+
+$(LIB): $(CSRC)/build/ocean_kernels.o $(CSRC)/build/ocean_capi.o
+	$(HIPCC) --offload-arch=$(ARCH) -shared -o $@ $^ -Wl,-soname,liboceanfft.so
+
+# C++ drop-in layer (Waves::FFTCalculator / Waves::Generator / Vision::RenderDevice shim) over the C ABI.
+WAVES_SRC := $(CSRC)/waves/RenderDevice.cpp $(CSRC)/waves/FFTCalculator.cpp $(CSRC)/waves/Generator.cpp
+$(WAVES): $(WAVES_SRC) include/waves/Generator.h include/waves/FFTCalculator.h include/vision/RenderDevice.h $(LIB)
+	g++ -O2 -std=c++17 -fPIC -shared -Iinclude -I/opt/rocm/include -D__HIP_PLATFORM_AMD__ -o $@ $(WAVES_SRC) \
+	    -L$(PKG) -loceanfft -Wl,-rpath,'$$ORIGIN' -L/opt/rocm/lib -lamdhip64
+
+$(ORACLE): oracle/ocean_oracle.c oracle/ocean_oracle.h
+	$(MAKE) -s -C oracle
+
+$(CPPTEST): tests/cpp/test_waves.cpp $(WAVES) $(ORACLE)
+	g++ -O2 -std=c++17 -Iinclude -Ioracle -I/opt/rocm/include -D__HIP_PLATFORM_AMD__ -o $@ $< \
+	    -L$(PKG) -lwaves -loceanfft -Loracle/build -loceanoracle \
+	    -Wl,-rpath,'$$ORIGIN/../../$(PKG)' -Wl,-rpath,'$$ORIGIN/../../oracle/build' -L/opt/rocm/lib -lamdhip64
+
+clean:
+	rm -rf $(CSRC)/build $(LIB) $(WAVES) $(CPPTEST)
+	$(MAKE) -s -C oracle clean
+
+.PHONY: all clean

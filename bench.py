@@ -1,0 +1,221 @@
+#!/usr/bin/env python3
+"""bench.py — height-field points/s of the ocean hot path on MI355X (BASELINE.json metric).
+
+One step = one reference frame (Waves::Generator::CalculateOcean, src/Generator.cpp:45-83) for every
+cascade a rank owns: h(k,t) evolution + packing, two packed 2D inverse FFTs (4 complex fields) and the
+Jacobian, i.e. the full reference payload. h0 is seeded in warm-up and, as in the reference API
+(src/Generator.h:39-45), only regenerated on a settings change; its cost is reported separately.
+
+Workload (BASELINE.json configs[3], per GPU): 8 independent 4096^2 cascades, default settings, plane
+sizes 5/17/101/251/509/1021/2039/4093 m (extending src/Waves.cpp:27). Ranks own disjoint cascade
+sets (seed offset 4097*rank: non-overlapping noise tiles) — weak scaling, no data-path collective.
+
+Launch: python bench.py [--gpus N --steps K --warmup W]; N > 1 via torch.distributed.run, one rank
+per GPU (RCCL only for the barrier and the max-over-ranks timing reduction).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+PLANES = [5.0, 17.0, 101.0, 251.0, 509.0, 1021.0, 2039.0, 4093.0]
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md, chip-level parameters)
+# Algorithmic HBM bytes per height-field point:
+ROW_BYTES = 16 + 32          # read h0 texel, write heightMap + displacementMap texels
+COL_BYTES = 32 + 32 + 4      # read + write both maps (in place), write the Jacobian
+FRAME_BYTES = ROW_BYTES + COL_BYTES  # 116 B / point
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--n", type=int, default=4096, help="grid side N")
+    ap.add_argument("--cascades", type=int, default=8, help="cascades per GPU")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0, help="target CPU-baseline sample length")
+    ap.add_argument("--no-profile", action="store_true", help="skip per-kernel HIP event timing")
+    return ap.parse_args()
+
+
+def dist_setup():
+    import torch
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if torch.cuda.is_available():
+        torch.cuda.set_device(local)
+    if world > 1:
+        import torch.distributed as dist
+
+        backend = "nccl" if torch.cuda.is_available() else "gloo"
+        dist.init_process_group(backend=backend)
+    return rank, world, local
+
+
+def barrier(world):
+    if world > 1:
+        import torch.distributed as dist
+
+        dist.barrier()
+
+
+def max_over_ranks(x: float, world: int) -> float:
+    if world == 1:
+        return x
+    import torch
+    import torch.distributed as dist
+
+    dev = "cuda" if torch.cuda.is_available() and dist.get_backend() == "nccl" else "cpu"
+    t = torch.tensor([x], dtype=torch.float64, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def sync():
+    import torch
+
+    if torch.cuda.is_available():
+        torch.cuda.synchronize()
+
+
+def cascade_settings(rank: int, c: int) -> dict:
+    return dict(planeSize=PLANES[c % len(PLANES)], seed=(12342 + 4097 * rank, 8934 + 4097 * (c // len(PLANES))))
+
+
+def cpu_baseline(n: int, target_s: float):
+    """The oracle (CPU restatement of the reference FFTCalculator/Generator) on host cores."""
+    from oracle import oracle as O
+
+    O.build()
+    threads = min(16, os.cpu_count() or 1)
+    O.set_threads(threads)
+    g = O.OracleGenerator(n, O.default_settings(planeSize=PLANES[0]))
+    g.calculate_ocean(1.0 / 60.0)  # seeds h0 (excluded, like the GPU warm-up)
+    frames, t0 = 0, time.perf_counter()
+    while True:
+        g.calculate_ocean(1.0 / 60.0)
+        frames += 1
+        el = time.perf_counter() - t0
+        if el >= target_s or frames >= 50:
+            break
+    return {
+        "value": n * n * frames / el,
+        "unit": "height-field points/s",
+        "cores": O.get_threads(),
+        "kind": "port",
+        "sample": f"1 cascade {n}x{n}, {frames} frames of CalculateOcean (fp32 radix-2 restatement of "
+                  f"src/FFTCalculator.cpp + spectrum.compute, OpenMP {O.get_threads()} threads), {el:.1f} s",
+    }
+
+
+def main():
+    args = parse()
+    rank, world, local = dist_setup()
+    import oceansimulation_amd as ocean
+
+    n, C = args.n, args.cascades
+    fft = ocean.FFTCalculator(n)  # default (null) stream == torch's default stream
+    gen = ocean.Generator(fft, C)
+    for c in range(C):
+        ocean.apply_settings(gen.GetOceanSettings(c), **cascade_settings(rank, c))
+
+    dt = 1.0 / 60.0
+    # h0 seeding, timed separately (time-independent; the reference API regenerates only on change)
+    gen.set_profiling(True)
+    gen.GenerateSpectrum()
+    ms, cnt = gen.kernel_times()
+    h0_ms = ms[0]
+    for _ in range(args.warmup):
+        gen.CalculateOcean(dt)
+    gen.set_profiling(not args.no_profile)
+    gen.kernel_times()  # reset
+    sync()
+    barrier(world)
+    sync()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        gen.CalculateOcean(dt)
+    sync()
+    barrier(world)
+    sync()
+    el = time.perf_counter() - t0
+    el_max = max_over_ranks(el, world)
+    ms, cnt = gen.kernel_times()
+
+    points = float(n) * n * C * args.steps * world
+    value = points / el_max
+    out = {
+        "metric": "height-field points/sec (N² iFFT) at 1/2/4/8 MI355X; % HBM roofline",
+        "value": value,
+        "unit": "height-field points/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": 1000.0 * el_max / args.steps,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic (procedural JONSWAP h0 from the reference hash; default settings)",
+        "config": {
+            "workload": f"{C} independent {n}x{n} cascades per GPU, full payload (height+slopes, choppy Dx/Dz, "
+                        f"Jacobian); step = CalculateOcean for all (evolve + 2 packed 2D iFFTs + foam)",
+            "n": n,
+            "cascades_per_gpu": C,
+            "plane_sizes_m": [PLANES[c % len(PLANES)] for c in range(C)],
+            "parallelism": f"cascades sharded over {world} GPU(s), no collective",
+            "frame_hbm_bytes_per_point": FRAME_BYTES,
+        },
+    }
+    if not args.no_profile and cnt[1] > 0 and cnt[2] > 0:
+        row_ms, col_ms = ms[1] / cnt[1], ms[2] / cnt[2]
+        per_launch_pts = float(n) * n * C
+        kernels = {
+            "row_pass": {"avg_ms": row_ms, "bytes": ROW_BYTES * per_launch_pts},
+            "column_pass": {"avg_ms": col_ms, "bytes": COL_BYTES * per_launch_pts},
+        }
+        dom_name = max(kernels, key=lambda k: kernels[k]["avg_ms"])
+        dom = kernels[dom_name]
+        achieved = dom["bytes"] / (dom["avg_ms"] * 1e-3) / 1e9
+        out["roofline"] = {
+            "bound": "hbm",
+            "kernel": dom_name,
+            "achieved": achieved,
+            "peak": HBM_PEAK_GBS,
+            "unit": "GB/s",
+            "frac": achieved / HBM_PEAK_GBS,
+            "traffic": None,
+        }
+        frame_gbs = FRAME_BYTES * per_launch_pts / ((row_ms + col_ms) * 1e-3) / 1e9
+        out["kernels"] = {
+            k: {"avg_ms": v["avg_ms"], "GB_per_s": v["bytes"] / (v["avg_ms"] * 1e-3) / 1e9,
+                "frac_hbm_peak": v["bytes"] / (v["avg_ms"] * 1e-3) / 1e9 / HBM_PEAK_GBS}
+            for k, v in kernels.items()
+        }
+        out["kernels"]["frame_both_passes"] = {"avg_ms": row_ms + col_ms, "GB_per_s": frame_gbs,
+                                               "frac_hbm_peak": frame_gbs / HBM_PEAK_GBS}
+        out["kernels"]["h0_seed_ms"] = h0_ms
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(n, args.cpu_seconds)
+    gen.close()
+    fft.close()
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        import torch.distributed as dist
+
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,135 @@
+/*
+ * oceanfft.h — C ABI of the MI355X ocean height-field library (liboceanfft.so).
+ *
+ * Drop-in boundary for the hot path of James51332/OceanSimulation:
+ *   Waves::FFTCalculator  (src/FFTCalculator.h:11-59, src/FFTCalculator.cpp:10-114)
+ *   Waves::Generator      (src/Generator.h:33-93,     src/Generator.cpp:14-154)
+ *   Waves::GeneratorSettings (src/Generator.h:12-30)
+ * Every entry point below cites the reference member it replaces. The C++ classes with the
+ * reference's exact signatures (include/waves/Generator.h, FFTCalculator.h) are thin wrappers over this ABI; INTEGRATION.md
+ * shows the ctypes/C++ bindings.
+ *
+ * Conventions
+ *   - Plain C types only. Device buffers are `float*` into HBM: RGBA32F images are N*N float4,
+ *     row-major, x fastest (image x = column, resources/fft.compute:72-73); R32F maps are N*N float.
+ *   - Every function returns an int status (OCEAN_OK == 0) unless it is a getter; on failure
+ *     ocean_last_error() gives a thread-local message. (The reference has no error path at all —
+ *     its calls are void and misuse such as N != SIZE silently corrupts results; here misuse fails.)
+ *   - One context per HIP stream: all work of an ocean_fft and of the generators bound to it is
+ *     issued on the stream given at ocean_fft_create (nullptr = the default stream). Calls only
+ *     enqueue work (the reference's "encode into a command buffer"); ocean_fft_synchronize waits.
+ *   - Library-owned outputs are borrowed by the caller and valid until the owner is destroyed
+ *     (the reference's Vision::ID handles, src/Generator.h:48-50).
+ */
+#ifndef OCEANFFT_H
+#define OCEANFFT_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define OCEAN_OK 0
+#define OCEAN_ERR_INVALID 1   /* bad argument (size not a power of two in [16, 16384], null, range) */
+#define OCEAN_ERR_HIP 2       /* HIP runtime error (message in ocean_last_error) */
+#define OCEAN_ERR_NO_DEVICE 3 /* no GPU visible */
+#define OCEAN_ERR_OOM 4       /* device allocation failed */
+
+#define OCEAN_MAX_CASCADES 64
+
+/* Waves::GeneratorSettings (src/Generator.h:12-30); same 64-byte layout as the std140 UBO
+ * spectrumSettings (resources/spectrum.compute:10-27). */
+typedef struct ocean_settings
+{
+  int32_t seed[2];         /* seed for the hash noise */
+  float U_10;              /* wind speed */
+  float theta_0;           /* wind direction (the reference subtracts it from radians as-is) */
+  float F;                 /* fetch */
+  float g;                 /* gravity */
+  float swell;             /* swell factor */
+  float h;                 /* depth */
+  float displacement;      /* choppiness lambda used by the Jacobian */
+  float time;              /* seconds, accumulated in fp32 by calculate() */
+  float planeSize;         /* metres covered by the tile */
+  float scale;             /* global amplitude scale */
+  float spread;            /* directional spread blend */
+  int32_t boundWavelength; /* uploaded but unused by the reference (spectrum.compute:24) */
+  float wavelengthMin;     /* idem */
+  float wavelengthMax;     /* idem */
+} ocean_settings;
+
+typedef struct ocean_fft ocean_fft;             /* Waves::FFTCalculator */
+typedef struct ocean_generator ocean_generator; /* one or more Waves::Generator cascades */
+
+/* ---- library ---------------------------------------------------------------------------- */
+const char* ocean_last_error(void);
+const char* ocean_version(void);
+/* GeneratorSettings default member initialisers, src/Generator.h:14-29. */
+void ocean_default_settings(ocean_settings* s);
+/* Number of visible GPUs (0 when none); does not create a context. */
+int ocean_device_count(void);
+
+/* ---- FFTCalculator ------------------------------------------------------------------------ */
+/* FFTCalculator::FFTCalculator(RenderDevice*, size_t textureSize) — src/FFTCalculator.cpp:10-58.
+ * Builds the twiddle table on the device; texture_size must be a power of two in [16, 16384]. */
+int ocean_fft_create(ocean_fft** out, size_t texture_size, void* hip_stream);
+/* FFTCalculator::~FFTCalculator — src/FFTCalculator.cpp:61-71. */
+int ocean_fft_destroy(ocean_fft* fft);
+/* FFTCalculator::GetTextureResolution — src/FFTCalculator.h:24. */
+size_t ocean_fft_texture_resolution(const ocean_fft* fft);
+/* FFTCalculator::EncodeIFFT(Vision::ID image) — src/FFTCalculator.cpp:73-114. In place on a
+ * device RGBA32F N*N image: out = N^2 * ifft2(ifftshift(in)) on lanes xy and zw independently
+ * (no normalisation, like the reference). No work image is needed. */
+int ocean_fft_encode_ifft(ocean_fft* fft, float* image);
+/* Batched EncodeIFFT over n_images contiguous images (image i at image + i*N*N*4 floats). */
+int ocean_fft_encode_ifft_batch(ocean_fft* fft, float* images, int n_images);
+/* Wait for all work enqueued on the plan's stream (the reference's SubmitCommandBuffer + fence,
+ * src/Waves.cpp:106). */
+int ocean_fft_synchronize(ocean_fft* fft);
+/* Multiprocessor (CU) count of the plan's device. */
+int ocean_fft_device_cus(const ocean_fft* fft);
+
+/* ---- Generator ---------------------------------------------------------------------------- */
+/* Generator::Generator(RenderDevice*, FFTCalculator*) — src/Generator.cpp:14-27, batched over
+ * `cascades` independent cascades (1..OCEAN_MAX_CASCADES) that share the plan's size N. Allocates
+ * per cascade: initialSpectrum, heightMap, displacementMap (RGBA32F N*N) and jacobian (R32F N*N)
+ * (src/Generator.cpp:99-133). Settings start at the defaults; the first calculate() seeds h0. */
+int ocean_generator_create(ocean_generator** out, ocean_fft* fft, int cascades);
+/* Generator::~Generator — src/Generator.cpp:29-43 (also frees the jacobian the reference leaks). */
+int ocean_generator_destroy(ocean_generator* gen);
+int ocean_generator_cascades(const ocean_generator* gen);
+/* Generator::GetOceanSettings — src/Generator.h:41. Host-side, mutable; read at calculate(). */
+ocean_settings* ocean_generator_settings(ocean_generator* gen, int cascade);
+/* Generator::CalculateOcean(float timestep, bool updateOcean) — src/Generator.cpp:45-83, for all
+ * cascades: time += timestep (fp32); regenerate h0 when update_spectrum != 0 or on first use;
+ * evolve + pack + two EncodeIFFTs + foam. Two fused launches (row pass, column pass). */
+int ocean_generator_calculate(ocean_generator* gen, float timestep, int update_spectrum);
+/* Generator::GenerateSpectrum — src/Generator.cpp:148-154 (the generateSpectrum dispatch). */
+int ocean_generator_generate_spectrum(ocean_generator* gen);
+/* Getters — src/Generator.h:48-50. Device pointers; heightMap = (h, dh/dx, dh/dz, Dx),
+ * displacementMap = (Dz, dDx/dx, dDz/dz, dDx/dz) (src/Generator.h:76-80), jacobian = R32F. */
+float* ocean_generator_height_map(ocean_generator* gen, int cascade);
+float* ocean_generator_displacement_map(ocean_generator* gen, int cascade);
+float* ocean_generator_jacobian_map(ocean_generator* gen, int cascade);
+/* The initialSpectrum image (src/Generator.h:86): (h0(k), conj(h0(-k))) per texel. */
+float* ocean_generator_initial_spectrum(ocean_generator* gen, int cascade);
+
+/* ---- instrumentation (bench) ------------------------------------------------------------- */
+/* When enabled, each kernel launch of the generator is bracketed by HIP events on its stream. */
+int ocean_generator_set_profiling(ocean_generator* gen, int enable);
+/* Synchronises, then returns per-kernel totals since the last call and resets them.
+ * Index 0 = spectrum (h0), 1 = row pass (evolve + x iFFT), 2 = column pass (y iFFT + foam). */
+int ocean_generator_kernel_times(ocean_generator* gen, double ms_total[3], int64_t launches[3]);
+
+/* ---- debug -------------------------------------------------------------------------------- */
+/* Device Hash (resources/spectrum.compute:109-117) of count (x, y) pairs in device memory:
+ * raw[i] = uint32 n, uv[2i..2i+1] = the two uniforms. For bit-exact parity tests. */
+int ocean_debug_hash(const uint32_t* xy, int count, uint32_t* raw, float* uv, void* hip_stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* OCEANFFT_H */

@@ -1,0 +1,81 @@
+// waves/Generator.h — drop-in for Waves::Generator / Waves::GeneratorSettings
+// (reference src/Generator.h:12-93). Same members and semantics; the GLSL kernels are replaced by
+// the fused HIP row/column passes of liboceanfft.
+#pragma once
+
+#include <cstddef>
+#include <cstdint>
+
+#include "oceanfft.h"
+#include "vision/RenderDevice.h"
+#include "waves/FFTCalculator.h"
+
+namespace Waves
+{
+
+// glm::ivec2 stand-in with the same layout (the reference's only glm use in the settings).
+struct IVec2
+{
+  int32_t x, y;
+};
+
+// src/Generator.h:12-30 — identical defaults and 64-byte layout.
+struct GeneratorSettings
+{
+  IVec2 seed = {12342, 8934};  // The seed for random generation.
+
+  float U_10 = 40.0f;         // The speed of the wind.
+  float theta_0 = 25.0f;      // The CCW direction of the wind rel. to +x-axis.
+  float F = 800000.0f;        // The distance to a downwind shore (fetch).
+  float g = 9.8f;             // The acceleration due to gravity.
+  float swell = 0.5f;         // The factor of non-wind based waves.
+  float h = 100.0f;           // The depth of the ocean.
+  float displacement = 0.4f;  // The scalar used in displacing the vertices.
+  float time = 0.0f;          // The time in seconds since the program began.
+  float planeSize = 40.0f;    // The size of the plane in meters that this plane is simulating.
+  float scale = 1.0f;         // The global heightmap scalar.
+  float spread = 0.2f;        // The intensity of waves perp. to wind.
+  int boundWavelength = 0;    // Whether or not we bound the wavelength (1 = bound, 0 = unbound)
+  float wavelengthMin = 0.0f; // The minimum wavelength that is allowed
+  float wavelengthMax = 0.0f; // The maximum wavelength that is allowed
+};
+static_assert(sizeof(GeneratorSettings) == 64, "GeneratorSettings must stay 64 bytes (std140 UBO)");
+
+class Generator
+{
+public:
+  // src/Generator.h:36-37
+  Generator(Vision::RenderDevice* device, FFTCalculator* calc);
+  ~Generator();
+  Generator(const Generator&) = delete;
+  Generator& operator=(const Generator&) = delete;
+
+  // src/Generator.h:41. If the spectrum is modified, pass updateOcean = true to the next call.
+  GeneratorSettings& GetOceanSettings();
+
+  // src/Generator.h:45. time += timestep; (re)seed h0 if requested or first call; evolve, 2D iFFT
+  // of both packed maps, Jacobian. Enqueued on the device's stream (no host sync).
+  void CalculateOcean(float timestep, bool updateOcean = false);
+
+  // src/Generator.h:48-50. heightMap = (h, dh/dx, dh/dz, Dx), displacementMap =
+  // (Dz, dDx/dx, dDz/dz, dDx/dz), jacobian = R32F. IDs resolve through the RenderDevice.
+  Vision::ID GetHeightMap() const { return heightMap; }
+  Vision::ID GetDisplacementMap() const { return displacementMap; }
+  Vision::ID GetJacobianMap() const { return jacobian; }
+  Vision::ID GetInitialSpectrum() const { return initialSpectrum; }
+
+  // src/Generator.h:53. Kernels are compiled into liboceanfft for gfx950; nothing to reload.
+  void LoadShaders(bool reload = false);
+
+private:
+  Vision::RenderDevice* renderDevice = nullptr;
+  FFTCalculator* fftCalc = nullptr;
+  std::size_t textureSize = 0;
+  ocean_generator* gen = nullptr;
+  Vision::ID heightMap = 0;
+  Vision::ID displacementMap = 0;
+  Vision::ID initialSpectrum = 0;
+  Vision::ID jacobian = 0;
+};
+
+}  // namespace Waves

@@ -1,0 +1,455 @@
+// ocean_capi.cpp — implementation of the C ABI in include/oceanfft.h.
+//
+// Host-side orchestration of the reference's FFTCalculator / Generator (src/FFTCalculator.cpp,
+// src/Generator.cpp) over the HIP kernels in ocean_kernels.hip. No CPU fallback exists: without a
+// GPU every entry point fails with OCEAN_ERR_NO_DEVICE / OCEAN_ERR_HIP.
+#include "oceanfft.h"
+
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "ocean_internal.h"
+
+using namespace oceanfft;
+
+static_assert(sizeof(ocean_settings) == sizeof(OceanSettings), "settings layout");
+
+namespace
+{
+thread_local std::string g_err;
+
+int fail(int code, const std::string& msg)
+{
+  g_err = msg;
+  return code;
+}
+
+int hip_fail(hipError_t e, const char* what)
+{
+  return fail(OCEAN_ERR_HIP, std::string(what) + ": " + hipGetErrorString(e));
+}
+
+#define HIP_TRY(expr, what)                                                                        \
+  do                                                                                               \
+  {                                                                                                \
+    hipError_t e_ = (expr);                                                                        \
+    if (e_ != hipSuccess)                                                                          \
+      return hip_fail(e_, what);                                                                   \
+  } while (0)
+
+int log2_exact(size_t n)
+{
+  int l = 0;
+  while (((size_t)1 << l) < n)
+    l++;
+  return ((size_t)1 << l) == n ? l : -1;
+}
+
+struct EventPair
+{
+  int kind;
+  hipEvent_t a, b;
+};
+}  // namespace
+
+struct ocean_fft
+{
+  int n = 0;
+  int logn = 0;
+  int device = 0;
+  int cus = 0;
+  hipStream_t stream = nullptr;
+  float2* twiddles = nullptr;  // two-level table, see FftShape in ocean_kernels.hip
+};
+
+struct ocean_generator
+{
+  ocean_fft* fft = nullptr;
+  int cascades = 0;
+  std::vector<ocean_settings> settings;
+  bool update_spectrum = true;  // src/Generator.h:72
+  float4* h0 = nullptr;         // [cascade][N][N]
+  float4* maps = nullptr;       // [cascade][2][N][N]: heightMap, displacementMap
+  float* jac = nullptr;         // [cascade][N][N]
+  bool profiling = false;
+  std::vector<EventPair> pending;
+  std::vector<hipEvent_t> pool;
+  double ms[3] = {0, 0, 0};
+  int64_t launches[3] = {0, 0, 0};
+};
+
+extern "C" {
+
+const char* ocean_last_error(void) { return g_err.c_str(); }
+
+const char* ocean_version(void) { return "oceanfft 0.1 (gfx950)"; }
+
+void ocean_default_settings(ocean_settings* s)
+{
+  // src/Generator.h:14-29
+  std::memset(s, 0, sizeof(*s));
+  s->seed[0] = 12342;
+  s->seed[1] = 8934;
+  s->U_10 = 40.0f;
+  s->theta_0 = 25.0f;
+  s->F = 800000.0f;
+  s->g = 9.8f;
+  s->swell = 0.5f;
+  s->h = 100.0f;
+  s->displacement = 0.4f;
+  s->time = 0.0f;
+  s->planeSize = 40.0f;
+  s->scale = 1.0f;
+  s->spread = 0.2f;
+  s->boundWavelength = 0;
+  s->wavelengthMin = 0.0f;
+  s->wavelengthMax = 0.0f;
+}
+
+int ocean_device_count(void)
+{
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess)
+    return 0;
+  return n;
+}
+
+int ocean_fft_create(ocean_fft** out, size_t texture_size, void* hip_stream)
+{
+  if (!out)
+    return fail(OCEAN_ERR_INVALID, "ocean_fft_create: out is null");
+  *out = nullptr;
+  int logn = log2_exact(texture_size);
+  if (logn < 4 || logn > 14)
+    return fail(OCEAN_ERR_INVALID, "ocean_fft_create: texture_size must be a power of two in [16, 16384], got " +
+                                       std::to_string(texture_size));
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0)
+    return fail(OCEAN_ERR_NO_DEVICE, "ocean_fft_create: no HIP device visible");
+
+  auto* f = new ocean_fft();
+  f->n = (int)texture_size;
+  f->logn = logn;
+  f->stream = (hipStream_t)hip_stream;
+  hipError_t e = hipGetDevice(&f->device);
+  if (e == hipSuccess)
+    e = hipDeviceGetAttribute(&f->cus, hipDeviceAttributeMultiprocessorCount, f->device);
+  if (e != hipSuccess)
+  {
+    delete f;
+    return hip_fail(e, "ocean_fft_create: device query");
+  }
+
+  // Twiddle table exp(+2 pi i e / N), two levels (FFTCalculator's pass table analogue,
+  // src/FFTCalculator.cpp:14-32): [0, TB) = low part, [TB, TB+TA) = high part.
+  int lb = logn / 2;
+  int tb = 1 << lb, ta = 1 << (logn - lb);
+  std::vector<float2> tab(tb + ta);
+  const double two_pi = 6.283185307179586476925286766559;
+  for (int e2 = 0; e2 < tb; e2++)
+  {
+    double a = two_pi * e2 / (double)f->n;
+    tab[e2] = make_float2((float)std::cos(a), (float)std::sin(a));
+  }
+  for (int e2 = 0; e2 < ta; e2++)
+  {
+    double a = two_pi * ((double)e2 * tb) / (double)f->n;
+    tab[tb + e2] = make_float2((float)std::cos(a), (float)std::sin(a));
+  }
+  e = hipMalloc(&f->twiddles, tab.size() * sizeof(float2));
+  if (e == hipSuccess)
+    e = hipMemcpy(f->twiddles, tab.data(), tab.size() * sizeof(float2), hipMemcpyHostToDevice);
+  if (e != hipSuccess)
+  {
+    if (f->twiddles)
+      (void)hipFree(f->twiddles);
+    delete f;
+    return hip_fail(e, "ocean_fft_create: twiddle table");
+  }
+  *out = f;
+  return OCEAN_OK;
+}
+
+int ocean_fft_destroy(ocean_fft* fft)
+{
+  if (!fft)
+    return OCEAN_OK;
+  if (fft->twiddles)
+    (void)hipFree(fft->twiddles);
+  delete fft;
+  return OCEAN_OK;
+}
+
+size_t ocean_fft_texture_resolution(const ocean_fft* fft) { return fft ? (size_t)fft->n : 0; }
+
+int ocean_fft_device_cus(const ocean_fft* fft) { return fft ? fft->cus : 0; }
+
+int ocean_fft_encode_ifft_batch(ocean_fft* fft, float* images, int n_images)
+{
+  if (!fft || !images || n_images < 1)
+    return fail(OCEAN_ERR_INVALID, "ocean_fft_encode_ifft_batch: null plan/image or n_images < 1");
+  auto* img = reinterpret_cast<float4*>(images);
+  HIP_TRY(launch_rows_ifft(fft->logn, n_images, img, fft->twiddles, fft->stream, fft->cus), "row pass");
+  HIP_TRY(launch_cols(fft->logn, n_images, img, nullptr, nullptr, fft->twiddles, fft->stream, fft->cus),
+          "column pass");
+  return OCEAN_OK;
+}
+
+int ocean_fft_encode_ifft(ocean_fft* fft, float* image) { return ocean_fft_encode_ifft_batch(fft, image, 1); }
+
+int ocean_fft_synchronize(ocean_fft* fft)
+{
+  if (!fft)
+    return fail(OCEAN_ERR_INVALID, "ocean_fft_synchronize: null plan");
+  HIP_TRY(hipStreamSynchronize(fft->stream), "hipStreamSynchronize");
+  return OCEAN_OK;
+}
+
+}  // extern "C"
+
+namespace
+{
+hipEvent_t take_event(ocean_generator* g)
+{
+  if (!g->pool.empty())
+  {
+    hipEvent_t e = g->pool.back();
+    g->pool.pop_back();
+    return e;
+  }
+  hipEvent_t e = nullptr;
+  (void)hipEventCreate(&e);
+  return e;
+}
+
+// Runs `launch` bracketed by events when profiling is on.
+template <typename F>
+hipError_t timed(ocean_generator* g, int kind, F&& launch)
+{
+  if (!g->profiling)
+    return launch();
+  EventPair p{kind, take_event(g), take_event(g)};
+  hipError_t e = hipEventRecord(p.a, g->fft->stream);
+  if (e != hipSuccess)
+    return e;
+  e = launch();
+  if (e != hipSuccess)
+    return e;
+  e = hipEventRecord(p.b, g->fft->stream);
+  g->pending.push_back(p);
+  return e;
+}
+}  // namespace
+
+extern "C" {
+
+// ---------------------------------------------------------------------------------------------
+// Generator
+// ---------------------------------------------------------------------------------------------
+int ocean_generator_create(ocean_generator** out, ocean_fft* fft, int cascades)
+{
+  if (!out || !fft)
+    return fail(OCEAN_ERR_INVALID, "ocean_generator_create: null argument");
+  *out = nullptr;
+  if (cascades < 1 || cascades > OCEAN_MAX_CASCADES)
+    return fail(OCEAN_ERR_INVALID, "ocean_generator_create: cascades must be in [1, 64]");
+  auto* g = new ocean_generator();
+  g->fft = fft;
+  g->cascades = cascades;
+  g->settings.resize(cascades);
+  for (auto& s : g->settings)
+    ocean_default_settings(&s);
+  const size_t texels = (size_t)fft->n * fft->n;
+  hipError_t e = hipMalloc(&g->h0, texels * cascades * sizeof(float4));
+  if (e == hipSuccess)
+    e = hipMalloc(&g->maps, texels * cascades * 2 * sizeof(float4));
+  if (e == hipSuccess)
+    e = hipMalloc(&g->jac, texels * cascades * sizeof(float));
+  // Textures start zeroed like the reference's (Data = nullptr) images.
+  if (e == hipSuccess)
+    e = hipMemsetAsync(g->h0, 0, texels * cascades * sizeof(float4), fft->stream);
+  if (e == hipSuccess)
+    e = hipMemsetAsync(g->maps, 0, texels * cascades * 2 * sizeof(float4), fft->stream);
+  if (e == hipSuccess)
+    e = hipMemsetAsync(g->jac, 0, texels * cascades * sizeof(float), fft->stream);
+  if (e != hipSuccess)
+  {
+    int code = (e == hipErrorOutOfMemory) ? OCEAN_ERR_OOM : OCEAN_ERR_HIP;
+    ocean_generator_destroy(g);
+    return fail(code, std::string("ocean_generator_create: allocation: ") + hipGetErrorString(e));
+  }
+  *out = g;
+  return OCEAN_OK;
+}
+
+int ocean_generator_destroy(ocean_generator* g)
+{
+  if (!g)
+    return OCEAN_OK;
+  if (g->fft)
+    (void)hipStreamSynchronize(g->fft->stream);
+  for (auto& p : g->pending)
+  {
+    (void)hipEventDestroy(p.a);
+    (void)hipEventDestroy(p.b);
+  }
+  for (auto ev : g->pool)
+    (void)hipEventDestroy(ev);
+  if (g->h0)
+    (void)hipFree(g->h0);
+  if (g->maps)
+    (void)hipFree(g->maps);
+  if (g->jac)
+    (void)hipFree(g->jac);
+  delete g;
+  return OCEAN_OK;
+}
+
+int ocean_generator_cascades(const ocean_generator* g) { return g ? g->cascades : 0; }
+
+ocean_settings* ocean_generator_settings(ocean_generator* g, int c)
+{
+  if (!g || c < 0 || c >= g->cascades)
+  {
+    fail(OCEAN_ERR_INVALID, "ocean_generator_settings: cascade out of range");
+    return nullptr;
+  }
+  return &g->settings[c];
+}
+
+
+int ocean_generator_generate_spectrum(ocean_generator* g)
+{
+  if (!g)
+    return fail(OCEAN_ERR_INVALID, "ocean_generator_generate_spectrum: null generator");
+  ocean_fft* f = g->fft;
+  const size_t texels = (size_t)f->n * f->n;
+  for (int c = 0; c < g->cascades; c++)
+  {
+    OceanSettings s;
+    std::memcpy(&s, &g->settings[c], sizeof(s));
+    HIP_TRY(timed(g, 0, [&] { return launch_generate_spectrum(s, f->n, g->h0 + texels * c, f->stream, f->cus); }),
+            "generateSpectrum");
+  }
+  return OCEAN_OK;
+}
+
+int ocean_generator_calculate(ocean_generator* g, float timestep, int update_spectrum)
+{
+  if (!g)
+    return fail(OCEAN_ERR_INVALID, "ocean_generator_calculate: null generator");
+  ocean_fft* f = g->fft;
+  // src/Generator.cpp:50 — fp32 accumulation on the host, per cascade.
+  for (auto& s : g->settings)
+    s.time += timestep;
+  // src/Generator.cpp:55-59
+  if (g->update_spectrum || update_spectrum)
+  {
+    g->update_spectrum = false;
+    int rc = ocean_generator_generate_spectrum(g);
+    if (rc != OCEAN_OK)
+      return rc;
+  }
+  FrameParams fp{};
+  FoamParams foam{};
+  fp.cascades = g->cascades;
+  for (int c = 0; c < g->cascades; c++)
+  {
+    const ocean_settings& s = g->settings[c];
+    // spectrum.compute:189 — `2.0 * M_PI / planeSize` in fp32
+    fp.c[c].dk = 2.0f * 3.14159265358f / s.planeSize;
+    fp.c[c].time = s.time;
+    fp.c[c].g = s.g;
+    fp.c[c].h = s.h;
+    foam.displacement[c] = s.displacement;
+  }
+  // prepareFFT + the x passes of both EncodeIFFTs (src/Generator.cpp:63-72)
+  HIP_TRY(timed(g, 1, [&] { return launch_rows_evolve(f->logn, fp, g->h0, g->maps, f->twiddles, f->stream, f->cus); }),
+          "row pass");
+  // the y passes of both EncodeIFFTs + computeFoam (src/Generator.cpp:71-80)
+  HIP_TRY(timed(g, 2, [&] {
+            return launch_cols(f->logn, 2 * g->cascades, g->maps, g->jac, &foam, f->twiddles, f->stream, f->cus);
+          }),
+          "column pass");
+  return OCEAN_OK;
+}
+
+float* ocean_generator_height_map(ocean_generator* g, int c)
+{
+  if (!g || c < 0 || c >= g->cascades)
+    return nullptr;
+  return reinterpret_cast<float*>(g->maps + (size_t)g->fft->n * g->fft->n * (2 * c));
+}
+
+float* ocean_generator_displacement_map(ocean_generator* g, int c)
+{
+  if (!g || c < 0 || c >= g->cascades)
+    return nullptr;
+  return reinterpret_cast<float*>(g->maps + (size_t)g->fft->n * g->fft->n * (2 * c + 1));
+}
+
+float* ocean_generator_jacobian_map(ocean_generator* g, int c)
+{
+  if (!g || c < 0 || c >= g->cascades)
+    return nullptr;
+  return g->jac + (size_t)g->fft->n * g->fft->n * c;
+}
+
+float* ocean_generator_initial_spectrum(ocean_generator* g, int c)
+{
+  if (!g || c < 0 || c >= g->cascades)
+    return nullptr;
+  return reinterpret_cast<float*>(g->h0 + (size_t)g->fft->n * g->fft->n * c);
+}
+
+int ocean_generator_set_profiling(ocean_generator* g, int enable)
+{
+  if (!g)
+    return fail(OCEAN_ERR_INVALID, "ocean_generator_set_profiling: null generator");
+  g->profiling = enable != 0;
+  return OCEAN_OK;
+}
+
+int ocean_generator_kernel_times(ocean_generator* g, double ms_total[3], int64_t launches[3])
+{
+  if (!g)
+    return fail(OCEAN_ERR_INVALID, "ocean_generator_kernel_times: null generator");
+  HIP_TRY(hipStreamSynchronize(g->fft->stream), "hipStreamSynchronize");
+  for (auto& p : g->pending)
+  {
+    float ms = 0.0f;
+    HIP_TRY(hipEventElapsedTime(&ms, p.a, p.b), "hipEventElapsedTime");
+    g->ms[p.kind] += ms;
+    g->launches[p.kind] += 1;
+    g->pool.push_back(p.a);
+    g->pool.push_back(p.b);
+  }
+  g->pending.clear();
+  for (int k = 0; k < 3; k++)
+  {
+    if (ms_total)
+      ms_total[k] = g->ms[k];
+    if (launches)
+      launches[k] = g->launches[k];
+    g->ms[k] = 0;
+    g->launches[k] = 0;
+  }
+  return OCEAN_OK;
+}
+
+int ocean_debug_hash(const uint32_t* xy, int count, uint32_t* raw, float* uv, void* hip_stream)
+{
+  if (!xy || !raw || !uv || count < 0)
+    return fail(OCEAN_ERR_INVALID, "ocean_debug_hash: null argument");
+  if (count == 0)
+    return OCEAN_OK;
+  HIP_TRY(launch_hash(xy, count, raw, reinterpret_cast<float2*>(uv), (hipStream_t)hip_stream), "hash");
+  return OCEAN_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,65 @@
+// ocean_internal.h — types shared between the device code and the C-ABI implementation.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+namespace oceanfft
+{
+
+// Waves::GeneratorSettings (src/Generator.h:12-30) == spectrumSettings UBO (spectrum.compute:10-27).
+struct OceanSettings
+{
+  int32_t seed[2];
+  float U_10;
+  float theta_0;
+  float F;
+  float g;
+  float swell;
+  float h;
+  float displacement;
+  float time;
+  float planeSize;
+  float scale;
+  float spread;
+  int32_t boundWavelength;
+  float wavelengthMin;
+  float wavelengthMax;
+};
+static_assert(sizeof(OceanSettings) == 64, "GeneratorSettings is 64 bytes");
+
+constexpr int kMaxCascades = 64;  // cascades per launch (kernel-argument tables below)
+
+// Per-cascade values the evolve/row kernel needs (passed by value: no per-frame H2D copy).
+struct CascadeFrame
+{
+  float dk;    // 2*pi/planeSize, evaluated in fp32 exactly as spectrum.compute:189
+  float time;  // accumulated in fp32 like src/Generator.cpp:50
+  float g;
+  float h;
+};
+
+struct FrameParams
+{
+  int cascades;
+  int pad[3];
+  CascadeFrame c[kMaxCascades];
+};
+
+struct FoamParams
+{
+  float displacement[kMaxCascades];
+};
+
+hipError_t launch_generate_spectrum(const OceanSettings& s, int n, float4* h0, hipStream_t stream, int cus);
+hipError_t launch_hash(const uint32_t* xy, int count, uint32_t* raw, float2* uv, hipStream_t stream);
+hipError_t launch_rows_evolve(int logn, const FrameParams& fp, const float4* h0, float4* maps,
+                              const float2* tw, hipStream_t stream, int cus);
+hipError_t launch_rows_ifft(int logn, int n_images, float4* images, const float2* tw, hipStream_t stream,
+                            int cus);
+hipError_t launch_cols(int logn, int n_images, float4* images, float* jac, const FoamParams* foam,
+                       const float2* tw, hipStream_t stream, int cus);
+int twiddle_entries(int logn);
+
+}  // namespace oceanfft

@@ -1,0 +1,953 @@
+// ocean_kernels.hip — gfx950 device code for the ocean hot path:
+//   h0(k) JONSWAP seeding  ->  h(k,t) evolution fused into the row iFFT  ->  column iFFT + foam.
+//
+// Reference semantics (paths relative to the reference root):
+//   spectrum seeding      resources/spectrum.compute:38-172   (generateSpectrum)
+//   evolve + packing      resources/spectrum.compute:183-240  (prepareFFT)
+//   2D inverse FFT        resources/fft.compute:21-88 driven by src/FFTCalculator.cpp:73-114
+//                         == N^2 * ifft2(ifftshift(X)) per complex lane, no normalisation
+//   Jacobian / foam       resources/spectrum.compute:246-259
+//
+// MI355X design (DESIGN.md has the byte accounting):
+//   * 2 HBM passes per frame. Row pass: read h0 (16 B/texel), evolve in registers, 4 complex fields
+//     transformed along x, write heightMap + displacementMap rows (32 B). Column pass: read each
+//     image's column strips (16 B), transform along y, write back in place (16 B), and for the
+//     displacement image write the Jacobian (4 B). 116 B per height-field point.
+//   * Each 1D transform is a self-sorting Stockham FFT: one radix-16 butterfly per thread per
+//     stage held in VGPRs (16 points x 1-2 complex lanes), LDS only for the exchange between
+//     stages (N = 4096 = 16^3 -> 2 exchanges). fftShift is folded into the load index; no
+//     bit-reversal pass exists.
+//   * Twiddles: exact (host-double-rounded) two-level table in LDS, w = A[e>>LB] * B[e & mask].
+//   * Column pass: a strip of C texel columns per workgroup, 4 lanes per row segment (64 B at
+//     N = 4096); strips 2m and 2m+1 are given to blocks b and b+8 (same XCD under the observed
+//     round-robin placement) so both halves of each 128-B line are consumed from one L2.
+//   * Persistent grids sized from occupancy; every loop has a plain item-count exit.
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <cstdio>
+
+#include "ocean_internal.h"
+
+namespace oceanfft
+{
+
+// ------------------------------------------------------------------------------------------------
+// Constants (resources/spectrum.compute:4, :34-35; resources/fft.compute:14 rounds to the same float)
+// ------------------------------------------------------------------------------------------------
+#define OCEAN_PI 3.14159265358f
+static constexpr float kSigmaSurface = 0.072f;
+static constexpr float kRhoWater = 1000.0f;
+
+// ------------------------------------------------------------------------------------------------
+// Spectrum math — float32 restatement of resources/spectrum.compute, same operation order.
+// ------------------------------------------------------------------------------------------------
+__device__ __forceinline__ float dispersion(float k, float g, float h)
+{
+  // spectrum.compute:38-44
+  float kh = k * h;
+  float tanhKH = kh >= 2.0f * OCEAN_PI ? 1.0f : tanhf(kh);
+  float omegaSquared = (g * k + kSigmaSurface / kRhoWater * k * k * k) * tanhKH;
+  return sqrtf(omegaSquared);
+}
+
+__device__ __forceinline__ float dispersion_derivative(float k, float g, float h)
+{
+  // spectrum.compute:50-57
+  float phi = dispersion(k, g, h);
+  float sech = 1.0f / coshf(h * k);
+  float numerator = h * (kSigmaSurface / kRhoWater * k * k * k + g * k) * sech * sech + phi * phi;
+  return numerator / (2.0f * phi);
+}
+
+__device__ __forceinline__ float smoothstep_f(float e0, float e1, float x)
+{
+  float t = (x - e0) / (e1 - e0);
+  t = fminf(fmaxf(t, 0.0f), 1.0f);
+  return t * t * (3.0f - 2.0f * t);
+}
+
+__device__ __forceinline__ float jonswap(const OceanSettings& s, float omega, float omega_p)
+{
+  // spectrum.compute:60-78
+  float alpha = 0.076f * powf(s.U_10 * s.U_10 / (s.F * s.g), 0.22f);
+  float gamma = 3.3f;
+  float sigma = omega > omega_p ? 0.09f : 0.07f;
+  float omegaDiff = fabsf(omega - omega_p);
+  float omegaRatio = omega_p / omega;
+  float r = expf(-omegaDiff * omegaDiff / (2.0f * sigma * sigma * omega_p * omega_p));
+  float S = alpha * s.g * s.g / powf(omega, 5.0f) * expf(-1.25f * powf(omegaRatio, 4.0f)) *
+            powf(gamma, r);
+  float w_h = fminf(omega * sqrtf(s.h / s.g), 2.0f);
+  return S * smoothstep_f(0.0f, 2.2f, w_h);
+}
+
+__device__ __forceinline__ float lh_normalization(float s)
+{
+  // spectrum.compute:81-88
+  float a = sqrtf(s);
+  return (s < 0.4f) ? (0.5f / OCEAN_PI) + s * (0.220636f + s * (-0.109f + s * 0.090f))
+                    : (1.0f / sqrtf(OCEAN_PI)) * (a * 0.5f + (1.0f / a) * 0.0625f);
+}
+
+__device__ __forceinline__ float hasselmann(const OceanSettings& st, float w, float w_p, float theta)
+{
+  // spectrum.compute:91-106
+  float p = w / w_p;
+  float s = (w <= w_p) ? 6.97f * powf(fabsf(p), 4.06f)
+                       : 9.77f * powf(fabsf(p), -2.33f - 1.45f * (st.U_10 * w_p / st.g - 1.17f));
+  float s_xi = 16.0f * tanhf(w_p / w) * st.swell * st.swell;
+  float sh = s + s_xi;
+  return lh_normalization(sh) * powf(fabsf(cosf(theta * 0.5f)), 2.0f * sh);
+}
+
+__device__ __forceinline__ uint32_t hash_raw(uint32_t x, uint32_t y)
+{
+  // spectrum.compute:109-114
+  uint32_t h32 = y + 374761393u + x * 3266489917u;
+  h32 = 2246822519u * (h32 ^ (h32 >> 15));
+  h32 = 3266489917u * (h32 ^ (h32 >> 13));
+  return h32 ^ (h32 >> 16);
+}
+
+__device__ __forceinline__ float2 hash_uniform(uint32_t x, uint32_t y)
+{
+  // spectrum.compute:115-116
+  uint32_t n = hash_raw(x, y);
+  uint32_t rz1 = n * 48271u;
+  return make_float2((float)((n >> 1) & 0x7FFFFFFFu) / (float)0x7FFFFFFF,
+                     (float)((rz1 >> 1) & 0x7FFFFFFFu) / (float)0x7FFFFFFF);
+}
+
+__device__ __forceinline__ float2 spectrum_amplitude(const OceanSettings& s, float tx, float ty,
+                                                     float dim)
+{
+  // spectrum.compute:129-155
+  float dk = 2.0f * OCEAN_PI / s.planeSize;
+  float kx = (tx - dim / 2.0f) * dk;
+  float ky = (ty - dim / 2.0f) * dk;
+  float k = sqrtf(kx * kx + ky * ky);
+  float theta = atan2f(ky, kx) - s.theta_0;
+  if (k == 0.0f)
+    return make_float2(0.0f, 0.0f);
+
+  float omega = dispersion(k, s.g, s.h);
+  float omega_p = 22.0f * powf(s.g * s.g / (s.U_10 * s.F), 0.333f);
+  float Sj = jonswap(s, omega, omega_p);
+  float d = ((1.0f - s.spread) * hasselmann(s, omega, omega_p, theta) +
+             (s.spread) / (2.0f * OCEAN_PI));
+  float chain = dispersion_derivative(k, s.g, s.h) / k * dk * dk;
+
+  // uvec2(thread + seed): float add, then conversion (seeds and indices are non-negative).
+  uint32_t hx = (uint32_t)(int64_t)(tx + (float)s.seed[0]);
+  uint32_t hy = (uint32_t)(int64_t)(ty + (float)s.seed[1]);
+  float2 u = hash_uniform(hx, hy);
+  // Gaussian, spectrum.compute:121-127
+  float r = sqrtf(-2.0f * logf(u.x));
+  float th = 2.0f * OCEAN_PI * u.y;
+  float sn, cs;
+  sincosf(th, &sn, &cs);
+  float amp = sqrtf(2.0f * Sj * d * chain);
+  float c = 0.1f * s.scale;
+  return make_float2(c * (r * cs) * amp, c * (r * sn) * amp);
+}
+
+// generateSpectrum (spectrum.compute:157-172): texel = (h0(k), conj(h0(-k))), -k taken as N - i.
+__global__ __launch_bounds__(256) void k_generate_spectrum(OceanSettings s, int n, float4* __restrict__ h0)
+{
+  const int64_t total = (int64_t)n * n;
+  const float dim = (float)n;
+  for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < total;
+       idx += (int64_t)gridDim.x * blockDim.x)
+  {
+    int y = (int)(idx / n), x = (int)(idx - (int64_t)y * n);
+    float2 a = spectrum_amplitude(s, (float)x, (float)y, dim);
+    float2 b = spectrum_amplitude(s, dim - (float)x, dim - (float)y, dim);
+    h0[idx] = make_float4(a.x, a.y, b.x, -b.y);
+  }
+}
+
+// Debug entry for bit-exact Hash parity (spectrum.compute:109-117).
+__global__ void k_hash(const uint32_t* __restrict__ xy, int count, uint32_t* __restrict__ raw,
+                       float2* __restrict__ uv)
+{
+  int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < count)
+  {
+    raw[i] = hash_raw(xy[2 * i], xy[2 * i + 1]);
+    uv[i] = hash_uniform(xy[2 * i], xy[2 * i + 1]);
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// Buffer (SRD) global access: wave-uniform base in SGPRs + one 32-bit lane offset (T8 in the CDNA
+// guide). Keeps the 16 per-thread element addresses out of VGPRs. Offsets stay < 2^31 bytes.
+// ------------------------------------------------------------------------------------------------
+typedef float f4v __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t srd(const void* base, int num_bytes)
+{
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, num_bytes, 0x00020000);
+}
+
+// Raw-buffer range checking: a load at or past num_bytes returns 0 and a store there is dropped,
+// which handles ragged row blocks without branches.
+constexpr int kAllBytes = 0x7FFFFFFF;
+
+__device__ __forceinline__ float4 ld4(const void* base, int voff_bytes, int num_bytes = kAllBytes)
+{
+  f4v r = __builtin_amdgcn_raw_buffer_load_b128(srd(base, num_bytes), voff_bytes, 0, 0);
+  return make_float4(r.x, r.y, r.z, r.w);
+}
+
+__device__ __forceinline__ void st4(void* base, int voff_bytes, float4 v, int num_bytes = kAllBytes)
+{
+  f4v r = {v.x, v.y, v.z, v.w};
+  __builtin_amdgcn_raw_buffer_store_b128(r, srd(base, num_bytes), voff_bytes, 0, 0);
+}
+
+__device__ __forceinline__ void st1(void* base, int voff_bytes, float v)
+{
+  __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), srd(base, kAllBytes), voff_bytes, 0, 0);
+}
+
+__device__ __forceinline__ int clamp_bytes(int64_t b)
+{
+  return b > kAllBytes ? kAllBytes : (b < 0 ? 0 : (int)b);
+}
+
+// ------------------------------------------------------------------------------------------------
+// Complex helpers. V is float2 (one complex lane) or float4 (two lanes: xy, zw), as in the
+// reference's packed RGBA32F images (fft.compute:83-84 transforms xy and zw independently).
+// ------------------------------------------------------------------------------------------------
+__device__ __forceinline__ float2 operator+(float2 a, float2 b) { return make_float2(a.x + b.x, a.y + b.y); }
+__device__ __forceinline__ float2 operator-(float2 a, float2 b) { return make_float2(a.x - b.x, a.y - b.y); }
+__device__ __forceinline__ float4 operator+(float4 a, float4 b)
+{
+  return make_float4(a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w);
+}
+__device__ __forceinline__ float4 operator-(float4 a, float4 b)
+{
+  return make_float4(a.x - b.x, a.y - b.y, a.z - b.z, a.w - b.w);
+}
+// multiply by +i (inverse-transform sign)
+__device__ __forceinline__ float2 mul_i(float2 a) { return make_float2(-a.y, a.x); }
+__device__ __forceinline__ float4 mul_i(float4 a) { return make_float4(-a.y, a.x, -a.w, a.z); }
+// multiply by -i
+__device__ __forceinline__ float2 mul_mi(float2 a) { return make_float2(a.y, -a.x); }
+__device__ __forceinline__ float4 mul_mi(float4 a) { return make_float4(a.y, -a.x, a.w, -a.z); }
+__device__ __forceinline__ float2 cmul(float2 a, float2 w)
+{
+  return make_float2(a.x * w.x - a.y * w.y, a.x * w.y + a.y * w.x);
+}
+__device__ __forceinline__ float4 cmul(float4 a, float2 w)
+{
+  return make_float4(a.x * w.x - a.y * w.y, a.x * w.y + a.y * w.x, a.z * w.x - a.w * w.y,
+                     a.z * w.y + a.w * w.x);
+}
+
+// ------------------------------------------------------------------------------------------------
+// Small inverse DFTs (sign +): X[k] = sum_n x[n] exp(+2 pi i n k / r)
+// ------------------------------------------------------------------------------------------------
+template <typename V>
+__device__ __forceinline__ void idft2(V& a0, V& a1)
+{
+  V t = a0 - a1;
+  a0 = a0 + a1;
+  a1 = t;
+}
+
+template <typename V>
+__device__ __forceinline__ void idft4(V& a0, V& a1, V& a2, V& a3)
+{
+  V s0 = a0 + a2, d0 = a0 - a2, s1 = a1 + a3, d1 = a1 - a3;
+  a0 = s0 + s1;
+  a2 = s0 - s1;
+  a1 = d0 + mul_i(d1);
+  a3 = d0 - mul_i(d1);
+}
+
+// In: v[n], n = 0..7. Out: v[k] = X[k] (natural order).
+template <typename V>
+__device__ __forceinline__ void idft8(V* v)
+{
+  const float R2 = 0.70710678118654752f;
+  // n = 2*n1 + n2: DFT4 over n1 for n2 = 0, 1
+  idft4(v[0], v[2], v[4], v[6]);
+  idft4(v[1], v[3], v[5], v[7]);
+  // Y[n2=1][k1] *= W8^k1 (inverse)
+  v[3] = cmul(v[3], make_float2(R2, R2));
+  v[5] = mul_i(v[5]);
+  v[7] = cmul(v[7], make_float2(-R2, R2));
+  // DFT2 over n2: X[k1] = Y0[k1] + Y1[k1], X[k1 + 4] = Y0[k1] - Y1[k1]
+  V y00 = v[0], y01 = v[2], y02 = v[4], y03 = v[6];
+  V y10 = v[1], y11 = v[3], y12 = v[5], y13 = v[7];
+  v[0] = y00 + y10;
+  v[4] = y00 - y10;
+  v[1] = y01 + y11;
+  v[5] = y01 - y11;
+  v[2] = y02 + y12;
+  v[6] = y02 - y12;
+  v[3] = y03 + y13;
+  v[7] = y03 - y13;
+}
+
+// In: v[n], n = 0..15. Out: v[k] = X[k] (natural order). 4 x 4 decomposition.
+template <typename V>
+__device__ __forceinline__ void idft16(V* v)
+{
+  const float C1 = 0.92387953251128674f;  // cos(pi/8)
+  const float S1 = 0.38268343236508977f;  // sin(pi/8)
+  const float R2 = 0.70710678118654752f;
+  // n = 4*n1 + n2: DFT4 over n1 for each n2 -> Y[n2][k1] at v[4*k1 + n2]
+  idft4(v[0], v[4], v[8], v[12]);
+  idft4(v[1], v[5], v[9], v[13]);
+  idft4(v[2], v[6], v[10], v[14]);
+  idft4(v[3], v[7], v[11], v[15]);
+  // twiddle Y[n2][k1] *= W16^(n2*k1), inverse sign
+  v[5] = cmul(v[5], make_float2(C1, S1));     // n2=1,k1=1: W^1
+  v[9] = cmul(v[9], make_float2(R2, R2));     // n2=1,k1=2: W^2
+  v[13] = cmul(v[13], make_float2(S1, C1));   // n2=1,k1=3: W^3
+  v[6] = cmul(v[6], make_float2(R2, R2));     // n2=2,k1=1: W^2
+  v[10] = mul_i(v[10]);                       // n2=2,k1=2: W^4
+  v[14] = cmul(v[14], make_float2(-R2, R2));  // n2=2,k1=3: W^6
+  v[7] = cmul(v[7], make_float2(S1, C1));     // n2=3,k1=1: W^3
+  v[11] = cmul(v[11], make_float2(-R2, R2));  // n2=3,k1=2: W^6
+  v[15] = cmul(v[15], make_float2(-C1, -S1)); // n2=3,k1=3: W^9
+  // DFT4 over n2 for each k1: X[k1 + 4*k2]
+  idft4(v[0], v[1], v[2], v[3]);
+  idft4(v[4], v[5], v[6], v[7]);
+  idft4(v[8], v[9], v[10], v[11]);
+  idft4(v[12], v[13], v[14], v[15]);
+  // now v[4*k1 + k2] = X[k1 + 4*k2]; transpose the 4x4 index to natural order
+  V t;
+  t = v[1], v[1] = v[4], v[4] = t;
+  t = v[2], v[2] = v[8], v[8] = t;
+  t = v[3], v[3] = v[12], v[12] = t;
+  t = v[6], v[6] = v[9], v[9] = t;
+  t = v[7], v[7] = v[13], v[13] = t;
+  t = v[11], v[11] = v[14], v[14] = t;
+}
+
+// ------------------------------------------------------------------------------------------------
+// Stockham radix-16 FFT of length N = 2^LOGN held by T = N/16 cooperating threads.
+// Thread i owns v[m] = x[i + m*T]. Stage with radix r and span p (Bainville's formulation):
+//   butterfly b, k = b mod p: inputs x[b + t*N/r], twiddle exp(+2 pi i t k / (r p)),
+//   outputs y[(b/p)*r*p + k + t*p].
+// The first stage uses radix R0 = 2^(LOGN mod 4) (or 16) with p = 1; the rest are radix 16.
+// After the last stage (p = T) thread i holds X[i + m*T] directly — no final exchange.
+// ------------------------------------------------------------------------------------------------
+template <int LOGN>
+struct FftShape
+{
+  static constexpr int N = 1 << LOGN;
+  static constexpr int T = N >> 4;
+  static constexpr int LOG_R0 = (LOGN & 3) ? (LOGN & 3) : 4;
+  static constexpr int R0 = 1 << LOG_R0;
+  static constexpr int NSTAGE = 1 + (LOGN - LOG_R0) / 4;
+  static constexpr int PADDED = N + N / 16;  // one pad slot per 16: conflict-free Stockham writes
+  static constexpr int LB = LOGN / 2;        // two-level twiddle table split
+  static constexpr int TB = 1 << LB;
+  static constexpr int TA = N >> LB;
+  static constexpr int TW_ENTRIES = TA + TB;
+};
+
+__device__ __forceinline__ int pad16(int a) { return a + (a >> 4); }
+
+// Hide a loop-invariant value from LICM: without this, hipcc hoists ~100 per-thread LDS/global
+// address computations out of the persistent loops and spills them to scratch.
+__device__ __forceinline__ int opaque(int v)
+{
+  asm volatile("" : "+v"(v));
+  return v;
+}
+
+// w = exp(+2 pi i e / N) from the two-level table (exact host-rounded entries, one cmul).
+template <int LOGN>
+__device__ __forceinline__ float2 twiddle(int e, const float2* __restrict__ tw)
+{
+  using S = FftShape<LOGN>;
+  float2 lo = tw[e & (S::TB - 1)];
+  float2 hi = tw[S::TB + (e >> S::LB)];
+  return cmul(lo, hi);
+}
+
+// v[t] *= w^t for t = 1..15, w = exp(+2 pi i e1 / N). w and w^4 come from the exact table; the
+// other powers are products of at most three table values (error <= ~3 ulp), which keeps only a
+// handful of twiddles live instead of 30 hoisted LDS reads.
+template <int LOGN, typename V>
+__device__ __forceinline__ void apply_stage_twiddles(V* v, int e1, const float2* __restrict__ tw)
+{
+  constexpr int N = 1 << LOGN;
+  const float2 w1 = twiddle<LOGN>(e1, tw);
+  const float2 w4 = twiddle<LOGN>((4 * e1) & (N - 1), tw);
+  const float2 w2 = cmul(w1, w1);
+  const float2 w3 = cmul(w2, w1);
+  v[1] = cmul(v[1], w1);
+  v[2] = cmul(v[2], w2);
+  v[3] = cmul(v[3], w3);
+  v[4] = cmul(v[4], w4);
+  v[5] = cmul(v[5], cmul(w4, w1));
+  v[6] = cmul(v[6], cmul(w4, w2));
+  v[7] = cmul(v[7], cmul(w4, w3));
+  const float2 w8 = cmul(w4, w4);
+  v[8] = cmul(v[8], w8);
+  v[9] = cmul(v[9], cmul(w8, w1));
+  v[10] = cmul(v[10], cmul(w8, w2));
+  v[11] = cmul(v[11], cmul(w8, w3));
+  const float2 w12 = cmul(w8, w4);
+  v[12] = cmul(v[12], w12);
+  v[13] = cmul(v[13], cmul(w12, w1));
+  v[14] = cmul(v[14], cmul(w12, w2));
+  v[15] = cmul(v[15], cmul(w12, w3));
+}
+
+// LDS exchange layout. Element a of the transform lives at padded index pa = a + (a >> 4) (one pad
+// slot per 16 elements: conflict-free Stockham writes). Region `reg`:
+//   row kernels:    slot = reg * PADDED + pa                 (float4 or float2 slots)
+//   column kernels: slot = pa * CI + reg  (CI columns interleaved: conflict-free for 4/8/16 lanes)
+// Write/read indices are passed as PADDED indices in closed form (base + t*stride where the
+// stride is a multiple of 16 elements), so the per-t offsets fold into ds_* immediates instead
+// of occupying 16 address VGPRs.
+template <int CI, int PADDED>
+__device__ __forceinline__ int lds_slot(int reg, int pa)
+{
+  if constexpr (CI > 0)
+    return pa * CI + reg;
+  else
+    return reg * PADDED + pa;
+}
+
+// Padded index of x[i + m*T] (the next stage's inputs).
+template <int LOGN>
+__device__ __forceinline__ int read_pidx(int i, int m)
+{
+  constexpr int T = FftShape<LOGN>::T;
+  if constexpr ((T & 15) == 0)
+    return pad16(i) + m * (T + T / 16);
+  else
+    return pad16(i + m * T);
+}
+
+// Write the 16 stage outputs (padded indices wp(t)), barrier, read back the next stage's inputs,
+// barrier. SPLIT: float4 data exchanged as two float2 lanes through a float2 buffer (half the LDS).
+template <int LOGN, int CI, bool SPLIT, typename V, typename WP>
+__device__ __forceinline__ void exchange(V* v, int i, int reg, void* lds_raw, WP wp)
+{
+  using S = FftShape<LOGN>;
+  if constexpr (!SPLIT)
+  {
+    V* lds = reinterpret_cast<V*>(lds_raw);
+#pragma unroll
+    for (int t = 0; t < 16; t++)
+      lds[lds_slot<CI, S::PADDED>(reg, wp(t))] = v[t];
+    __syncthreads();
+#pragma unroll
+    for (int m = 0; m < 16; m++)
+      v[m] = lds[lds_slot<CI, S::PADDED>(reg, read_pidx<LOGN>(i, m))];
+    __syncthreads();
+  }
+  else
+  {
+    static_assert(sizeof(V) == 16, "SPLIT exchange is for float4 data");
+    float2* lds = reinterpret_cast<float2*>(lds_raw);
+#pragma unroll
+    for (int half = 0; half < 2; half++)
+    {
+#pragma unroll
+      for (int t = 0; t < 16; t++)
+        lds[lds_slot<CI, S::PADDED>(reg, wp(t))] =
+            half ? make_float2(v[t].z, v[t].w) : make_float2(v[t].x, v[t].y);
+      __syncthreads();
+#pragma unroll
+      for (int m = 0; m < 16; m++)
+      {
+        float2 r = lds[lds_slot<CI, S::PADDED>(reg, read_pidx<LOGN>(i, m))];
+        if (half)
+          v[m].z = r.x, v[m].w = r.y;
+        else
+          v[m].x = r.x, v[m].y = r.y;
+      }
+      __syncthreads();
+    }
+  }
+}
+
+// Full 1D inverse FFT (unnormalised) on the data held by this thread group.
+template <int LOGN, int CI, bool SPLIT, typename V>
+__device__ __forceinline__ void fft_run(V* v, int i, int reg, void* lds, const float2* __restrict__ tw)
+{
+  using S = FftShape<LOGN>;
+  constexpr int N = S::N, T = S::T, R0 = S::R0;
+
+  // ---- stage 0: radix R0, p = 1 (no twiddles) ----
+  if constexpr (R0 == 16)
+  {
+    idft16(v);
+    if constexpr (S::NSTAGE > 1)
+    {
+      const int base = 17 * i;  // pad16(16 i + t) = 17 i + t
+      exchange<LOGN, CI, SPLIT>(v, i, reg, lds, [&](int t) { return base + t; });
+    }
+  }
+  else
+  {
+    constexpr int U = 16 / R0;  // butterflies per thread; butterfly u uses v[u + t*U]
+#pragma unroll
+    for (int u = 0; u < U; u++)
+    {
+      V w[R0];
+#pragma unroll
+      for (int t = 0; t < R0; t++)
+        w[t] = v[u + t * U];
+      if constexpr (R0 == 2)
+        idft2(w[0], w[1]);
+      else if constexpr (R0 == 4)
+        idft4(w[0], w[1], w[2], w[3]);
+      else
+        idft8(w);
+#pragma unroll
+      for (int t = 0; t < R0; t++)
+        v[u + t * U] = w[t];
+    }
+    // output of butterfly b = i + u*T, element t -> y[b*R0 + t]; v index q = u + t*U
+    exchange<LOGN, CI, SPLIT>(v, i, reg, lds, [&](int q) {
+      int u = q % U, t = q / U;
+      return pad16((i + u * T) * R0 + t);
+    });
+  }
+
+  // ---- radix-16 stages ----
+  int p = R0;
+#pragma unroll
+  for (int s = 1; s < S::NSTAGE; s++)
+  {
+    const int k = i & (p - 1);
+    const int stride = N / (16 * p);  // twiddle exponent unit for this stage, in 2 pi / N
+    apply_stage_twiddles<LOGN>(v, k * stride, tw);
+    idft16(v);
+    if (s + 1 < S::NSTAGE)
+    {
+      const int j = (i / p) * 16 * p + k;
+      const int pp = p;
+      if (pp >= 16)
+      {
+        const int base = pad16(j), st = pp + pp / 16;
+        exchange<LOGN, CI, SPLIT>(v, i, reg, lds, [&](int t) { return base + t * st; });
+      }
+      else
+        exchange<LOGN, CI, SPLIT>(v, i, reg, lds, [&](int t) { return pad16(j + t * pp); });
+    }
+    p *= 16;
+  }
+}
+
+template <int LOGN>
+__device__ __forceinline__ void load_twiddles(float2* tw_lds, const float2* __restrict__ tw_glob)
+{
+  using S = FftShape<LOGN>;
+  for (int e = threadIdx.x; e < S::TW_ENTRIES; e += blockDim.x)
+    tw_lds[e] = tw_glob[e];
+  __syncthreads();
+}
+
+// ------------------------------------------------------------------------------------------------
+// Evolution + packing, resources/spectrum.compute:183-240.
+// ------------------------------------------------------------------------------------------------
+struct KVec
+{
+  float kx, kz, dirx, dirz, k;
+};
+
+__device__ __forceinline__ KVec make_kvec(int x, int y, float dim, float dk)
+{
+  KVec r;
+  r.kx = ((float)x - dim / 2.0f) * dk;
+  r.kz = ((float)y - dim / 2.0f) * dk;
+  float len = sqrtf(r.kx * r.kx + r.kz * r.kz);
+  bool zero = (r.kx == 0.0f && r.kz == 0.0f);
+  r.dirx = zero ? 0.0f : r.kx / len;
+  r.dirz = zero ? 0.0f : r.kz / len;
+  r.k = len + 1e-6f;
+  return r;
+}
+
+// heightAmp = h0 * e^{i w t} + conj-partner * e^{-i w t}
+__device__ __forceinline__ float2 evolve(float4 a, float k, const CascadeFrame& f)
+{
+  float phase = dispersion(k, f.g, f.h) * f.time;
+  float ws, wc;
+  sincosf(phase, &ws, &wc);
+  float ampx = a.x * wc - a.y * ws;
+  float ampy = a.x * ws + a.y * wc;
+  float ws2 = -ws;
+  float oppx = a.z * wc - a.w * ws2;
+  float oppy = a.z * ws2 + a.w * wc;
+  return make_float2(ampx + oppx, ampy + oppy);
+}
+
+// heightMap texel = (H + i*dH/dx, dH/dz + i*Dx)   (spectrum.compute:236)
+__device__ __forceinline__ float4 pack_height(float2 H, const KVec& q)
+{
+  float hx = H.x, hy = H.y;
+  float dhdx_x = q.kx * (-hy), dhdx_y = q.kx * hx;
+  float dhdz_x = q.kz * (-hy), dhdz_y = q.kz * hx;
+  float disX_x = q.dirx * (-hy), disX_y = q.dirx * hx;
+  return make_float4(hx - dhdx_y, hy + dhdx_x, dhdz_x - disX_y, dhdz_y + disX_x);
+}
+
+// displacementMap texel = (Dz + i*dDx/dx, dDz/dz + i*dDx/dz)   (spectrum.compute:237)
+__device__ __forceinline__ float4 pack_displacement(float2 H, const KVec& q)
+{
+  float hx = H.x, hy = H.y;
+  float disZ_x = q.dirz * (-hy), disZ_y = q.dirz * hx;
+  float a = -q.kx * q.dirx, b = -q.kz * q.dirz, c = -q.kz * q.dirx;
+  float dDXdx_x = a * hx, dDXdx_y = a * hy;
+  float dDZdz_x = b * hx, dDZdz_y = b * hy;
+  float dDXdz_x = c * hx, dDXdz_y = c * hy;
+  return make_float4(disZ_x - dDXdx_y, disZ_y + dDXdx_x, dDZdz_x - dDXdz_y, dDZdz_y + dDXdz_x);
+}
+
+// ------------------------------------------------------------------------------------------------
+// Row pass, fused with evolution: one x-direction transform per (cascade, row) for all 4 fields.
+// maps layout: [cascade][2][N][N] float4 (image 0 = heightMap, 1 = displacementMap).
+// ------------------------------------------------------------------------------------------------
+template <int LOGN>
+struct RowCfg
+{
+  using S = FftShape<LOGN>;
+  static constexpr int RPW = S::T >= 256 ? 1 : 256 / S::T;  // rows per workgroup iteration
+  static constexpr int WG = S::T * RPW;
+  static constexpr bool SPLIT = (S::N * 16 > 96 * 1024);   // float4 exchange would not fit
+  static constexpr int LDS_BYTES = RPW * S::PADDED * (SPLIT ? 8 : 16);
+  // waves per SIMD the LDS budget admits (>= 1): caps VGPRs so registers never limit residency
+  static constexpr int WGS_PER_CU = (150 * 1024) / (LDS_BYTES + 2048) < 1 ? 1 : (150 * 1024) / (LDS_BYTES + 2048);
+  static constexpr int MIN_WAVES_RAW = WGS_PER_CU * (WG / 64) / 4;
+  static constexpr int MIN_WAVES = MIN_WAVES_RAW < 1 ? 1 : (MIN_WAVES_RAW > 8 ? 8 : MIN_WAVES_RAW);
+};
+
+template <int LOGN>
+__global__ __launch_bounds__(RowCfg<LOGN>::WG, RowCfg<LOGN>::MIN_WAVES) void k_rows_evolve(
+    FrameParams fp, const float4* __restrict__ h0, float4* __restrict__ maps, const float2* __restrict__ tw_glob)
+{
+  using S = FftShape<LOGN>;
+  using R = RowCfg<LOGN>;
+  constexpr int N = S::N, T = S::T;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  float2* tw = reinterpret_cast<float2*>(smem);
+  void* xch = smem + ((S::TW_ENTRIES * 8 + 15) / 16) * 16;
+  load_twiddles<LOGN>(tw, tw_glob);
+
+  const int rho = threadIdx.x / T, i0 = threadIdx.x % T;
+  const int total = fp.cascades * N;
+  const float dim = (float)N;
+  for (int row0 = blockIdx.x * R::RPW; row0 < total; row0 += gridDim.x * R::RPW)
+  {
+    const int i = opaque(i0), rho_ = R::RPW == 1 ? 0 : opaque(rho);
+    // Rows of h0 ([cascade][N][N]) are contiguous: uniform base + lane offset; rows past the last
+    // one (ragged tail, N < 64 only) read 0 through the range limit.
+    const float4* src = h0 + ((size_t)row0 << LOGN);
+    const int lim = clamp_bytes((int64_t)(total - row0) * N * 16);
+    const int voff = ((rho_ << LOGN) + i) * 16;
+    const int row = row0 + rho_;
+    const int c = min(row >> LOGN, fp.cascades - 1), y = row & (N - 1);
+    const CascadeFrame f = fp.c[c];
+
+    float4 raw[16];
+#pragma unroll
+    for (int m = 0; m < 16; m++)
+      raw[m] = ld4(src + ((m + 8) & 15) * T, voff, lim);  // fftShift on x folded into the load
+    float2 H[16];
+#pragma unroll
+    for (int m = 0; m < 16; m++)
+    {
+      const int x = i + ((m + 8) & 15) * T;
+      KVec q = make_kvec(x, y, dim, f.dk);
+      H[m] = evolve(raw[m], q.k, f);
+    }
+
+    float4 v[16];
+#pragma unroll
+    for (int img = 0; img < 2; img++)
+    {
+#pragma unroll
+      for (int m = 0; m < 16; m++)
+      {
+        const int x = i + ((m + 8) & 15) * T;
+        KVec q = make_kvec(x, y, dim, f.dk);
+        v[m] = img == 0 ? pack_height(H[m], q) : pack_displacement(H[m], q);
+      }
+      fft_run<LOGN, 0, R::SPLIT>(v, i, rho_, xch, tw);
+      if constexpr (N >= R::RPW)
+      {
+        // the block's rows share one cascade: maps[c][img][y0 + rho] from a uniform base
+        const int c0 = row0 >> LOGN, y0 = row0 & (N - 1);
+        float4* dst = maps + ((size_t)(2 * c0 + img) << (2 * LOGN)) + ((size_t)y0 << LOGN);
+#pragma unroll
+        for (int m = 0; m < 16; m++)
+          st4(dst + m * T, voff, v[m]);
+      }
+      else
+      {
+        // N < 64: rows of one block straddle cascades; per-lane destination, tail rows skipped
+        if (row < total)
+        {
+          float4* dst = maps + ((size_t)(2 * c + img) << (2 * LOGN)) + ((size_t)y << LOGN);
+#pragma unroll
+          for (int m = 0; m < 16; m++)
+            dst[i + m * T] = v[m];
+        }
+      }
+    }
+  }
+}
+
+// Row pass of a plain EncodeIFFT on packed images [n_images][N][N] float4, in place.
+template <int LOGN>
+__global__ __launch_bounds__(RowCfg<LOGN>::WG, RowCfg<LOGN>::MIN_WAVES) void k_rows_ifft(
+    int n_images, float4* __restrict__ images, const float2* __restrict__ tw_glob)
+{
+  using S = FftShape<LOGN>;
+  using R = RowCfg<LOGN>;
+  constexpr int N = S::N, T = S::T;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  float2* tw = reinterpret_cast<float2*>(smem);
+  void* xch = smem + ((S::TW_ENTRIES * 8 + 15) / 16) * 16;
+  load_twiddles<LOGN>(tw, tw_glob);
+
+  const int rho0 = threadIdx.x / T, i0 = threadIdx.x % T;
+  const int total = n_images * N;
+  for (int row0 = blockIdx.x * R::RPW; row0 < total; row0 += gridDim.x * R::RPW)
+  {
+    const int i = opaque(i0), rho = R::RPW == 1 ? 0 : opaque(rho0);
+    // rows row0 .. row0+RPW-1 are contiguous: uniform base, lane offset (rho*N + i)*16; the
+    // range limit zeroes/drops rows past the last image (ragged tail for small N)
+    float4* lines = images + ((size_t)row0 << LOGN);
+    const int lim = clamp_bytes((int64_t)(total - row0) * N * 16);
+    const int voff = ((rho << LOGN) + i) * 16;
+    float4 v[16];
+#pragma unroll
+    for (int m = 0; m < 16; m++)
+      v[m] = ld4(lines + ((m + 8) & 15) * T, voff, lim);  // fftShift on x folded into the load
+    fft_run<LOGN, 0, R::SPLIT>(v, i, rho, xch, tw);
+#pragma unroll
+    for (int m = 0; m < 16; m++)
+      st4(lines + m * T, voff, v[m], lim);
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// Column pass: strips of C texel columns, transformed along y in place. FOAM: images with odd
+// index are displacement maps of cascade img/2 and also produce the Jacobian
+// (spectrum.compute:246-259) into jac[img/2].
+// ------------------------------------------------------------------------------------------------
+template <int LOGN>
+struct ColCfg
+{
+  using S = FftShape<LOGN>;
+  static constexpr int C = S::T >= 1024 ? 1 : (1024 / S::T > 16 ? 16 : 1024 / S::T);
+  static constexpr int WG = S::T * C;
+  static constexpr int LDS_BYTES = C * S::PADDED * 8;  // float2 (SPLIT) exchange
+  static constexpr int STRIPS = S::N / C;
+};
+
+// Block -> work-slot map that gives blocks b and b+8 (same XCD under round-robin placement)
+// adjacent strips, so both 64-B halves of a 128-B line meet in one L2. Speed only; any placement
+// is correct.
+__device__ __forceinline__ int xcd_pair_slot(int b, int G)
+{
+  if ((G & 15) != 0)
+    return b;
+  int xcd = b & 7, j = b >> 3;
+  int pair = xcd * (G >> 4) + (j >> 1);
+  return 2 * pair + (j & 1);
+}
+
+template <int LOGN, bool FOAM>
+__global__ __launch_bounds__(ColCfg<LOGN>::WG) void k_cols(
+    int n_images, float4* __restrict__ images, float* __restrict__ jac, FoamParams foam,
+    const float2* __restrict__ tw_glob)
+{
+  using S = FftShape<LOGN>;
+  using K = ColCfg<LOGN>;
+  constexpr int T = S::T, C = K::C;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  float2* tw = reinterpret_cast<float2*>(smem);
+  void* xch = smem + ((S::TW_ENTRIES * 8 + 15) / 16) * 16;
+  load_twiddles<LOGN>(tw, tw_glob);
+
+  const int c0 = threadIdx.x % C, i0 = threadIdx.x / C;
+  const int total = n_images * K::STRIPS;
+  for (int item = xcd_pair_slot(blockIdx.x, gridDim.x); item < total; item += gridDim.x)
+  {
+    const int c = opaque(c0), i = opaque(i0);
+    const int img = item / K::STRIPS, strip = item - img * K::STRIPS;
+    const int x = strip * C + c;
+    // image rows i + mm*T: uniform base per mm (SGPR), lane offset (i*N + x)*16 shared by all mm
+    const float4* ibase = images + ((size_t)img << (2 * LOGN));
+    const int voff = ((i << LOGN) + x) * 16;
+    float4 v[16];
+#pragma unroll
+    for (int m = 0; m < 16; m++)
+    {
+      // input q = i + m*T sits in row (q + N/2) mod N = i + ((m + 8) mod 16)*T: fftShift on y
+      const int mm = (m + 8) & 15;
+      v[m] = ld4(ibase + ((size_t)(mm * T) << LOGN), voff);
+    }
+    fft_run<LOGN, C, true>(v, i, c, xch, tw);
+    float4* obase = images + ((size_t)img << (2 * LOGN));
+#pragma unroll
+    for (int m = 0; m < 16; m++)
+      st4(obase + ((size_t)(m * T) << LOGN), voff, v[m]);
+    if constexpr (FOAM)
+    {
+      if (img & 1)
+      {
+        const float lam = foam.displacement[img >> 1];
+        float* jb = jac + ((size_t)(img >> 1) << (2 * LOGN));
+        const int joff = ((i << LOGN) + x) * 4;
+#pragma unroll
+        for (int m = 0; m < 16; m++)
+        {
+          float4 d = v[m];
+          st1(jb + ((size_t)(m * T) << LOGN), joff,
+              (1.0f + lam * d.y) * (1.0f + lam * d.z) - lam * lam * d.w * d.w);
+        }
+      }
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// Host-side launchers (dispatch on log2 N).
+// ------------------------------------------------------------------------------------------------
+template <int LOGN>
+static int lds_bytes_rows()
+{
+  using S = FftShape<LOGN>;
+  return ((S::TW_ENTRIES * 8 + 15) / 16) * 16 + RowCfg<LOGN>::LDS_BYTES;
+}
+template <int LOGN>
+static int lds_bytes_cols()
+{
+  using S = FftShape<LOGN>;
+  return ((S::TW_ENTRIES * 8 + 15) / 16) * 16 + ColCfg<LOGN>::LDS_BYTES;
+}
+
+template <typename F>
+static hipError_t with_logn(int logn, F&& f)
+{
+  switch (logn)
+  {
+  case 4: return f(std::integral_constant<int, 4>{});
+  case 5: return f(std::integral_constant<int, 5>{});
+  case 6: return f(std::integral_constant<int, 6>{});
+  case 7: return f(std::integral_constant<int, 7>{});
+  case 8: return f(std::integral_constant<int, 8>{});
+  case 9: return f(std::integral_constant<int, 9>{});
+  case 10: return f(std::integral_constant<int, 10>{});
+  case 11: return f(std::integral_constant<int, 11>{});
+  case 12: return f(std::integral_constant<int, 12>{});
+  case 13: return f(std::integral_constant<int, 13>{});
+  case 14: return f(std::integral_constant<int, 14>{});
+  default: return hipErrorInvalidValue;
+  }
+}
+
+// Persistent grid: resident blocks per CU x CUs, capped by the work item count.
+template <typename K>
+static int persistent_grid(K kernel, int wg, int lds, int items, int cus)
+{
+  int per_cu = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, wg, lds) != hipSuccess || per_cu < 1)
+    per_cu = 1;
+  long g = (long)per_cu * cus;
+  if (g > items)
+    g = items;
+  return g < 1 ? 1 : (int)g;
+}
+
+hipError_t launch_generate_spectrum(const OceanSettings& s, int n, float4* h0, hipStream_t stream, int cus)
+{
+  long total = (long)n * n;
+  long blocks = (total + 255) / 256;
+  long cap = (long)cus * 16;
+  if (blocks > cap)
+    blocks = cap;
+  hipLaunchKernelGGL(k_generate_spectrum, dim3((unsigned)blocks), dim3(256), 0, stream, s, n, h0);
+  return hipGetLastError();
+}
+
+hipError_t launch_hash(const uint32_t* xy, int count, uint32_t* raw, float2* uv, hipStream_t stream)
+{
+  hipLaunchKernelGGL(k_hash, dim3((count + 255) / 256), dim3(256), 0, stream, xy, count, raw, uv);
+  return hipGetLastError();
+}
+
+hipError_t launch_rows_evolve(int logn, const FrameParams& fp, const float4* h0, float4* maps,
+                              const float2* tw, hipStream_t stream, int cus)
+{
+  return with_logn(logn, [&](auto L) -> hipError_t {
+    constexpr int LOGN = decltype(L)::value;
+    using R = RowCfg<LOGN>;
+    auto kern = k_rows_evolve<LOGN>;
+    int lds = lds_bytes_rows<LOGN>();
+    (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+    int items = ((fp.cascades << LOGN) + R::RPW - 1) / R::RPW;
+    int grid = persistent_grid(kern, R::WG, lds, items, cus);
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(R::WG), lds, stream, fp, h0, maps, tw);
+    return hipGetLastError();
+  });
+}
+
+hipError_t launch_rows_ifft(int logn, int n_images, float4* images, const float2* tw, hipStream_t stream, int cus)
+{
+  return with_logn(logn, [&](auto L) -> hipError_t {
+    constexpr int LOGN = decltype(L)::value;
+    using R = RowCfg<LOGN>;
+    auto kern = k_rows_ifft<LOGN>;
+    int lds = lds_bytes_rows<LOGN>();
+    (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+    int items = ((n_images << LOGN) + R::RPW - 1) / R::RPW;
+    int grid = persistent_grid(kern, R::WG, lds, items, cus);
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(R::WG), lds, stream, n_images, images, tw);
+    return hipGetLastError();
+  });
+}
+
+hipError_t launch_cols(int logn, int n_images, float4* images, float* jac, const FoamParams* foam,
+                       const float2* tw, hipStream_t stream, int cus)
+{
+  return with_logn(logn, [&](auto L) -> hipError_t {
+    constexpr int LOGN = decltype(L)::value;
+    using K = ColCfg<LOGN>;
+    int lds = lds_bytes_cols<LOGN>();
+    int items = n_images * K::STRIPS;
+    FoamParams fpar{};
+    if (foam)
+      fpar = *foam;
+    if (foam && jac)
+    {
+      auto kern = k_cols<LOGN, true>;
+      (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+      int grid = persistent_grid(kern, K::WG, lds, items, cus);
+      hipLaunchKernelGGL(kern, dim3(grid), dim3(K::WG), lds, stream, n_images, images, jac, fpar, tw);
+    }
+    else
+    {
+      auto kern = k_cols<LOGN, false>;
+      (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+      int grid = persistent_grid(kern, K::WG, lds, items, cus);
+      hipLaunchKernelGGL(kern, dim3(grid), dim3(K::WG), lds, stream, n_images, images, jac, fpar, tw);
+    }
+    return hipGetLastError();
+  });
+}
+
+int twiddle_entries(int logn)
+{
+  int lb = logn / 2;
+  return (1 << lb) + (1 << (logn - lb));
+}
+
+}  // namespace oceanfft

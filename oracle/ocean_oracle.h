@@ -1,0 +1,81 @@
+/*
+ * ocean_oracle.h — CPU restatement of the reference ocean hot path (TEST INFRASTRUCTURE ONLY).
+ *
+ * This is the parity checker and the CPU baseline for oceansimulation_amd. It is NOT part of the
+ * product: only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may load it.
+ *
+ * Parity status: UNPINNED by reference outputs. The reference (James51332/OceanSimulation) has no
+ * tests, fixtures or golden vectors, and its path is GLSL executed through the absent Vision engine,
+ * so it cannot run in this container. The restatement is cross-checked instead against an
+ * independently written numpy formulation (tests/golden/make_golden.py) and analytic FFT
+ * known-answer tests (tests/test_oracle.py). See DESIGN.md §Oracle.
+ *
+ * Every function cites the reference file:line it restates (paths relative to the reference root).
+ */
+#ifndef OCEAN_ORACLE_H
+#define OCEAN_ORACLE_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Same 64-byte layout as Waves::GeneratorSettings (src/Generator.h:12-30) and the std140
+ * spectrumSettings UBO (resources/spectrum.compute:10-27). */
+typedef struct oracle_settings
+{
+  int32_t seed[2];
+  float U_10;
+  float theta_0;
+  float F;
+  float g;
+  float swell;
+  float h;
+  float displacement;
+  float time;
+  float planeSize;
+  float scale;
+  float spread;
+  int32_t boundWavelength;
+  float wavelengthMin;
+  float wavelengthMax;
+} oracle_settings;
+
+/* Defaults of src/Generator.h:14-29. */
+void oracle_default_settings(oracle_settings* s);
+
+/* resources/spectrum.compute:109-117 — returns the two uniforms; raw gets the uint32 n (may be 0). */
+void oracle_hash(uint32_t x, uint32_t y, float out[2], uint32_t* raw);
+
+/* resources/spectrum.compute:129-155 for one (thread, dimensions) pair. */
+void oracle_spectrum_amplitude(const oracle_settings* s, float tx, float ty, float dimx, float dimy,
+                               float out[2]);
+
+/* resources/spectrum.compute:157-172 over the whole N x N image. h0: N*N float4 (row-major, x fastest). */
+void oracle_generate_spectrum(const oracle_settings* s, int n, float* h0);
+
+/* resources/spectrum.compute:183-240. height, disp: N*N float4 each. */
+void oracle_prepare_fft(const oracle_settings* s, int n, const float* h0, float* height, float* disp);
+
+/* src/FFTCalculator.cpp:73-114 with resources/fft.compute:21-88 (SIZE generalised to n).
+ * In-place on image (N*N float4); work: scratch N*N float4 (the reference's workImage). */
+void oracle_encode_ifft(int n, float* image, float* work);
+
+/* resources/spectrum.compute:246-259. jac: N*N float. */
+void oracle_compute_foam(const oracle_settings* s, int n, const float* disp, float* jac);
+
+/* src/Generator.cpp:45-83 — one CalculateOcean: time += timestep (fp32), optional spectrum
+ * regeneration, evolve+pack, two EncodeIFFTs, foam. work: N*N float4 scratch. */
+void oracle_calculate_ocean(oracle_settings* s, int n, float timestep, int update_spectrum,
+                            float* h0, float* height, float* disp, float* jac, float* work);
+
+/* Threads used by the OpenMP loops (1 when built without OpenMP). */
+void oracle_set_threads(int threads);
+int oracle_get_threads(void);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif

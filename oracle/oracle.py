@@ -1,0 +1,149 @@
+"""ctypes wrapper of the CPU oracle (TEST INFRASTRUCTURE ONLY).
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg import this module, and only
+as the checker / the timed CPU baseline — never as the product path. Parity status: UNPINNED by
+reference outputs (see ocean_oracle.h and DESIGN.md §Oracle).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB_PATH = os.path.join(_HERE, "build", "liboceanoracle.so")
+
+
+class OracleSettings(ctypes.Structure):
+    """Waves::GeneratorSettings (src/Generator.h:12-30), 64 bytes."""
+
+    _fields_ = [
+        ("seed", ctypes.c_int32 * 2),
+        ("U_10", ctypes.c_float),
+        ("theta_0", ctypes.c_float),
+        ("F", ctypes.c_float),
+        ("g", ctypes.c_float),
+        ("swell", ctypes.c_float),
+        ("h", ctypes.c_float),
+        ("displacement", ctypes.c_float),
+        ("time", ctypes.c_float),
+        ("planeSize", ctypes.c_float),
+        ("scale", ctypes.c_float),
+        ("spread", ctypes.c_float),
+        ("boundWavelength", ctypes.c_int32),
+        ("wavelengthMin", ctypes.c_float),
+        ("wavelengthMax", ctypes.c_float),
+    ]
+
+
+_lib = None
+
+
+def build() -> str:
+    """Compile the oracle with its own Makefile (gcc)."""
+    subprocess.run(["make", "-s", "-C", _HERE], check=True)
+    return _LIB_PATH
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(_LIB_PATH):
+            build()
+        L = ctypes.CDLL(_LIB_PATH)
+        fp = ctypes.POINTER(ctypes.c_float)
+        sp = ctypes.POINTER(OracleSettings)
+        L.oracle_default_settings.argtypes = [sp]
+        L.oracle_hash.argtypes = [ctypes.c_uint32, ctypes.c_uint32, fp, ctypes.POINTER(ctypes.c_uint32)]
+        L.oracle_generate_spectrum.argtypes = [sp, ctypes.c_int, fp]
+        L.oracle_prepare_fft.argtypes = [sp, ctypes.c_int, fp, fp, fp]
+        L.oracle_encode_ifft.argtypes = [ctypes.c_int, fp, fp]
+        L.oracle_compute_foam.argtypes = [sp, ctypes.c_int, fp, fp]
+        L.oracle_calculate_ocean.argtypes = [sp, ctypes.c_int, ctypes.c_float, ctypes.c_int, fp, fp, fp, fp, fp]
+        L.oracle_set_threads.argtypes = [ctypes.c_int]
+        L.oracle_get_threads.restype = ctypes.c_int
+        _lib = L
+    return _lib
+
+
+def _fp(a: np.ndarray):
+    assert a.dtype == np.float32 and a.flags.c_contiguous
+    return a.ctypes.data_as(ctypes.POINTER(ctypes.c_float))
+
+
+def default_settings(**overrides) -> OracleSettings:
+    s = OracleSettings()
+    lib().oracle_default_settings(ctypes.byref(s))
+    for k, v in overrides.items():
+        if k == "seed":
+            s.seed[0], s.seed[1] = int(v[0]), int(v[1])
+        else:
+            setattr(s, k, v)
+    return s
+
+
+def set_threads(n: int) -> None:
+    lib().oracle_set_threads(int(n))
+
+
+def get_threads() -> int:
+    return int(lib().oracle_get_threads())
+
+
+def hash_uv(x: int, y: int):
+    out = (ctypes.c_float * 2)()
+    raw = ctypes.c_uint32()
+    lib().oracle_hash(x, y, out, ctypes.byref(raw))
+    return float(out[0]), float(out[1]), int(raw.value)
+
+
+def generate_spectrum(s: OracleSettings, n: int) -> np.ndarray:
+    h0 = np.zeros((n, n, 4), np.float32)
+    lib().oracle_generate_spectrum(ctypes.byref(s), n, _fp(h0))
+    return h0
+
+
+def prepare_fft(s: OracleSettings, n: int, h0: np.ndarray):
+    height = np.zeros((n, n, 4), np.float32)
+    disp = np.zeros((n, n, 4), np.float32)
+    lib().oracle_prepare_fft(ctypes.byref(s), n, _fp(np.ascontiguousarray(h0, np.float32)), _fp(height), _fp(disp))
+    return height, disp
+
+
+def encode_ifft(img: np.ndarray) -> np.ndarray:
+    """FFTCalculator::EncodeIFFT on a copy of img (N x N x 4 float32)."""
+    n = img.shape[0]
+    out = np.array(img, dtype=np.float32, order="C", copy=True)
+    work = np.zeros_like(out)
+    lib().oracle_encode_ifft(n, _fp(out), _fp(work))
+    return out
+
+
+def compute_foam(s: OracleSettings, disp: np.ndarray) -> np.ndarray:
+    n = disp.shape[0]
+    jac = np.zeros((n, n), np.float32)
+    lib().oracle_compute_foam(ctypes.byref(s), n, _fp(np.ascontiguousarray(disp, np.float32)), _fp(jac))
+    return jac
+
+
+class OracleGenerator:
+    """Generator::CalculateOcean state machine (src/Generator.cpp:45-83) on the CPU."""
+
+    def __init__(self, n: int, settings: OracleSettings | None = None):
+        self.n = n
+        self.settings = settings if settings is not None else default_settings()
+        self.h0 = np.zeros((n, n, 4), np.float32)
+        self.height = np.zeros((n, n, 4), np.float32)
+        self.disp = np.zeros((n, n, 4), np.float32)
+        self.jac = np.zeros((n, n), np.float32)
+        self.work = np.zeros((n, n, 4), np.float32)
+        self._update = True  # Generator.h:72 updateSpectrum = true
+
+    def calculate_ocean(self, timestep: float, update_ocean: bool = False) -> None:
+        upd = 1 if (self._update or update_ocean) else 0
+        self._update = False
+        lib().oracle_calculate_ocean(
+            ctypes.byref(self.settings), self.n, ctypes.c_float(timestep), upd,
+            _fp(self.h0), _fp(self.height), _fp(self.disp), _fp(self.jac), _fp(self.work))

@@ -1,0 +1,128 @@
+// test_waves.cpp — drives the C++ drop-in API the way the reference app does and checks it
+// against the CPU oracle (test infrastructure: links oracle/build/liboceanoracle.so as checker).
+//
+// Scene = WaveApp's (src/Waves.cpp:14-39): one FFTCalculator shared by 3 Generators, plane sizes
+// 5/17/101 m, boundWavelength = 1, wavelength bounds; per frame CalculateOcean(dt, true) for
+// every generator (src/Waves.cpp:90-91: updateSpectrum is never cleared). Also checks
+// FFTCalculator::EncodeIFFT on a random image. Exit code 0 = all within tolerance.
+#include <hip/hip_runtime_api.h>
+
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <random>
+#include <vector>
+
+#include "ocean_oracle.h"
+#include "waves/FFTCalculator.h"
+#include "waves/Generator.h"
+
+static double rel_err(const std::vector<float>& got, const std::vector<float>& ref, int stride, int ch)
+{
+  double maxref = 0, maxerr = 0;
+  for (size_t i = ch; i < ref.size(); i += stride)
+  {
+    maxref = std::fmax(maxref, std::fabs((double)ref[i]));
+    maxerr = std::fmax(maxerr, std::fabs((double)got[i] - (double)ref[i]));
+  }
+  return maxref > 0 ? maxerr / maxref : maxerr;
+}
+
+int main(int argc, char** argv)
+{
+  const int n = argc > 1 ? std::atoi(argv[1]) : 256;
+  const int frames = argc > 2 ? std::atoi(argv[2]) : 3;
+  int failures = 0;
+
+  Vision::RenderDevice device;  // default stream
+  Waves::FFTCalculator fft(&device, n);
+
+  // ---- EncodeIFFT on a random image (tolerance 1e-5 of max|ref| per channel) ----
+  {
+    Vision::Texture2DDesc desc;
+    desc.Width = n;
+    desc.Height = n;
+    std::vector<float> img((size_t)n * n * 4), work(img.size()), out(img.size());
+    std::mt19937 rng(1234);
+    std::normal_distribution<float> nd(0.0f, 1.0f);
+    for (auto& v : img)
+      v = nd(rng);
+    desc.Data = img.data();
+    Vision::ID id = device.CreateTexture2D(desc);
+    device.BeginCommandBuffer();
+    fft.EncodeIFFT(id);
+    device.SubmitCommandBuffer();
+    device.GetTexture2DDataRaw(id, out.data());
+    oracle_encode_ifft(n, img.data(), work.data());
+    for (int ch = 0; ch < 4; ch++)
+    {
+      double e = rel_err(out, img, 4, ch);
+      std::printf("encode_ifft n=%d ch=%d rel_err=%.3e\n", n, ch, e);
+      if (!(e <= 1e-5))
+        failures++;
+    }
+    device.DestroyTexture2D(id);
+  }
+
+  // ---- 3-cascade scene (src/Waves.cpp:20-39) ----
+  std::vector<Waves::Generator*> generators;
+  std::vector<oracle_settings> osettings(3);
+  static const float primeFactors[] = {5.0f, 17.0f, 101.0f};
+  for (int i = 0; i < 3; i++)
+  {
+    auto* g = new Waves::Generator(&device, &fft);
+    Waves::GeneratorSettings& s = g->GetOceanSettings();
+    s.planeSize = primeFactors[i];
+    s.boundWavelength = 1;
+    s.wavelengthMax = s.planeSize / 2.0;
+    s.wavelengthMin = (i == 0) ? 0.0 : primeFactors[i - 1] / 2.0;
+    static_assert(sizeof(oracle_settings) == sizeof(Waves::GeneratorSettings), "layout");
+    std::memcpy(&osettings[i], &s, sizeof(s));
+    generators.push_back(g);
+  }
+
+  const size_t texels = (size_t)n * n;
+  std::vector<float> h0(texels * 4), height(texels * 4), disp(texels * 4), jac(texels), work(texels * 4);
+  std::vector<std::vector<float>> ref_h(3), ref_d(3), ref_j(3);
+  const float dt = 1.0f / 60.0f;
+  for (int f = 0; f < frames; f++)
+  {
+    device.BeginCommandBuffer();
+    for (auto* g : generators)
+      g->CalculateOcean(dt, true);
+    device.SubmitCommandBuffer();
+  }
+  for (int i = 0; i < 3; i++)
+  {
+    for (int f = 0; f < frames; f++)
+      oracle_calculate_ocean(&osettings[i], n, dt, 1, h0.data(), height.data(), disp.data(), jac.data(),
+                             work.data());
+    std::vector<float> gh(texels * 4), gd(texels * 4), gj(texels);
+    device.GetTexture2DDataRaw(generators[i]->GetHeightMap(), gh.data());
+    device.GetTexture2DDataRaw(generators[i]->GetDisplacementMap(), gd.data());
+    device.GetTexture2DDataRaw(generators[i]->GetJacobianMap(), gj.data());
+    const float t_gpu = generators[i]->GetOceanSettings().time;
+    if (t_gpu != osettings[i].time)
+    {
+      std::printf("cascade %d: time mismatch %.9g vs %.9g\n", i, t_gpu, osettings[i].time);
+      failures++;
+    }
+    for (int ch = 0; ch < 4; ch++)
+    {
+      double eh = rel_err(gh, height, 4, ch), ed = rel_err(gd, disp, 4, ch);
+      std::printf("cascade %d L=%g heightMap ch%d rel_err=%.3e  displacementMap ch%d rel_err=%.3e\n", i,
+                  primeFactors[i], ch, eh, ch, ed);
+      if (!(eh <= 1e-4) || !(ed <= 1e-4))
+        failures++;
+    }
+    double ej = rel_err(gj, jac, 1, 0);
+    std::printf("cascade %d jacobian rel_err=%.3e\n", i, ej);
+    if (!(ej <= 1e-4))
+      failures++;
+  }
+  for (auto* g : generators)
+    delete g;
+  std::printf("%s (%d failures)\n", failures ? "FAIL" : "PASS", failures);
+  return failures ? 1 : 0;
+}

@@ -1,0 +1,35 @@
+"""Parity metrics and tolerances used by the tests (stated once, here).
+
+lane_err: for a packed RGBA32F image, the two complex lanes (xy, zw) are compared separately:
+          max |got - ref| over the lane / max |ref| over the lane (complex modulus).
+Tolerances (float32 path):
+  FFT_TOL   = 2e-5  — EncodeIFFT alone. The reference's own fp32 radix-2 structure is 0.2-5e-6 from
+                      float64 at N <= 1024 (oracle vs numpy, tests/test_oracle.py); the HIP Stockham
+                      radix-16 path must land within this of the oracle.
+  FRAME_TOL = 1e-4  — full CalculateOcean from h0 (transcendental ulp differences libm vs ocml).
+  H0_TOL    = 1e-5  — generateSpectrum (relative to max |h0| per lane).
+  Hash: bit-exact.
+"""
+import numpy as np
+
+FFT_TOL = 2e-5
+FRAME_TOL = 1e-4
+H0_TOL = 1e-5
+
+
+def lane_err(got: np.ndarray, ref: np.ndarray):
+    out = []
+    for lane in range(2):
+        g = got[..., 2 * lane].astype(np.float64) + 1j * got[..., 2 * lane + 1].astype(np.float64)
+        r = ref[..., 2 * lane].astype(np.float64) + 1j * ref[..., 2 * lane + 1].astype(np.float64)
+        scale = np.max(np.abs(r))
+        err = np.max(np.abs(g - r))
+        out.append(float(err / scale) if scale > 0 else float(err))
+    return out
+
+
+def scalar_err(got: np.ndarray, ref: np.ndarray) -> float:
+    ref = np.asarray(ref, np.float64)
+    scale = np.max(np.abs(ref))
+    err = np.max(np.abs(np.asarray(got, np.float64) - ref))
+    return float(err / scale) if scale > 0 else float(err)

@@ -1,0 +1,258 @@
+"""GPU parity: liboceanfft.so (HIP, gfx950) against the CPU oracle on the same seeded inputs.
+
+Every call goes through the C ABI (include/oceanfft.h) via oceansimulation_amd.capi; the oracle is
+only the checker. Tolerances and metrics: tests/parity.py.
+"""
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+import numpy_ref as R
+from parity import FFT_TOL, FRAME_TOL, H0_TOL, lane_err, scalar_err
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.fixture(scope="module")
+def ocean():
+    import oceansimulation_amd as o
+    from oceansimulation_amd import capi
+
+    assert capi.lib().ocean_device_count() > 0, "no GPU visible to liboceanfft.so"
+    return o
+
+
+def _rand_image(n, seed):
+    rng = np.random.default_rng(seed)
+    return rng.standard_normal((n, n, 4)).astype(np.float32)
+
+
+def _gpu_ifft(ocean, img):
+    from oceansimulation_amd.hip import DeviceBuffer
+
+    n = img.shape[0]
+    fft = ocean.FFTCalculator(n)
+    buf = DeviceBuffer.from_array(img)
+    fft.EncodeIFFT(buf.ptr)
+    fft.synchronize()
+    out = buf.to_host(img.shape)
+    buf.free()
+    fft.close()
+    return out
+
+
+# ---- Hash: bit exact (spectrum.compute:109-117) --------------------------------------------
+def test_hash_bit_exact(ocean, oracle):
+    from oceansimulation_amd.hip import DeviceBuffer
+
+    rng = np.random.default_rng(7)
+    xy = rng.integers(0, 2**32, size=(4096, 2), dtype=np.uint64).astype(np.uint32)
+    xy[:8] = [[0, 0], [1, 0], [0, 1], [12342, 8934], [12342 + 16384, 8934 + 16384],
+              [2**32 - 1, 2**32 - 1], [2**31, 7], [5, 2**31]]
+    dxy = DeviceBuffer.from_array(xy)
+    raw = DeviceBuffer(4 * len(xy))
+    uv = DeviceBuffer(8 * len(xy))
+    ocean.waves.debug_hash(dxy.ptr, len(xy), raw.ptr, uv.ptr)
+    from oceansimulation_amd import hip
+    hip.synchronize()
+    g_raw = raw.to_host((len(xy),), np.uint32)
+    g_uv = uv.to_host((len(xy), 2), np.float32)
+    u0, u1, n = R.hash2(xy[:, 0], xy[:, 1])
+    assert np.array_equal(g_raw, n)
+    assert np.array_equal(g_uv[:, 0].view(np.uint32), u0.view(np.uint32))
+    assert np.array_equal(g_uv[:, 1].view(np.uint32), u1.view(np.uint32))
+    for i in range(16):
+        a, b, r = oracle.hash_uv(int(xy[i, 0]), int(xy[i, 1]))
+        assert r == int(g_raw[i]) and np.float32(a) == g_uv[i, 0] and np.float32(b) == g_uv[i, 1]
+
+
+# ---- generateSpectrum (spectrum.compute:157-172) ---------------------------------------------
+@pytest.mark.parametrize("n", [16, 64, 256, 1024])
+@pytest.mark.parametrize("plane", [5.0, 17.0, 40.0, 101.0])
+def test_generate_spectrum(ocean, oracle, n, plane):
+    fft = ocean.FFTCalculator(n)
+    gen = ocean.Generator(fft, 1)
+    ocean.apply_settings(gen.GetOceanSettings(0), planeSize=plane)
+    gen.GenerateSpectrum()
+    got = gen.initial_spectrum_host(0)
+    ref = oracle.generate_spectrum(oracle.default_settings(planeSize=plane), n)
+    assert np.isfinite(got).all()
+    errs = lane_err(got, ref)
+    assert max(errs) <= H0_TOL, errs
+
+
+# ---- EncodeIFFT (src/FFTCalculator.cpp:73-114) ----------------------------------------------
+@pytest.mark.parametrize("n", [16, 32, 64, 128, 256, 512, 1024, 2048])
+def test_encode_ifft_vs_oracle(ocean, oracle, n):
+    img = _rand_image(n, n)
+    got = _gpu_ifft(ocean, img)
+    ref = oracle.encode_ifft(img)
+    errs = lane_err(got, ref)
+    assert max(errs) <= FFT_TOL, errs
+
+
+@pytest.mark.parametrize("n", [4096, 8192])
+def test_encode_ifft_large_vs_float64(ocean, n):
+    """Full-size transform against numpy float64 (the oracle's radix-2 is too slow here)."""
+    img = _rand_image(n, 99)
+    got = _gpu_ifft(ocean, img)
+    ref = R.encode_ifft(img)
+    errs = lane_err(got, ref)
+    assert max(errs) <= FFT_TOL, errs
+
+
+def test_encode_ifft_batch_matches_single(ocean):
+    from oceansimulation_amd.hip import DeviceBuffer
+
+    n, b = 512, 5
+    imgs = np.stack([_rand_image(n, 100 + i) for i in range(b)])
+    fft = ocean.FFTCalculator(n)
+    buf = DeviceBuffer.from_array(imgs)
+    fft.encode_ifft_batch(buf.ptr, b)
+    fft.synchronize()
+    got = buf.to_host(imgs.shape)
+    for i in range(b):
+        single = _gpu_ifft(ocean, imgs[i])
+        assert np.array_equal(got[i], single)
+
+
+# ---- FFT known-answer tests (size-independent properties) --------------------------------
+@pytest.mark.parametrize("n", [256, 4096])
+def test_kat_delta_and_plane_wave(ocean, n):
+    img = np.zeros((n, n, 4), np.float32)
+    # delta at the centred DC (index N/2, N/2 after the reference's fftShift convention) -> constant
+    img[n // 2, n // 2, 0] = 1.0
+    # a single bin on lane 2 -> plane wave exp(+2 pi i (kx x + ky y)/N)
+    kx, ky = 3, n // 2 - 5
+    img[n // 2 + ky, n // 2 + kx, 2] = 1.0
+    got = _gpu_ifft(ocean, img)
+    assert np.allclose(got[..., 0], 1.0, atol=1e-6) and np.allclose(got[..., 1], 0.0, atol=1e-6)
+    y, x = np.meshgrid(np.arange(n), np.arange(n), indexing="ij")
+    ph = 2 * np.pi * ((kx * x + ky * y) % n) / n
+    assert np.max(np.abs(got[..., 2] - np.cos(ph))) < 2e-5
+    assert np.max(np.abs(got[..., 3] - np.sin(ph))) < 2e-5
+
+
+@pytest.mark.parametrize("n", [1024, 4096])
+def test_property_parseval_linearity_hermitian(ocean, n):
+    rng = np.random.default_rng(5)
+    a = rng.standard_normal((n, n, 4)).astype(np.float32)
+    b = rng.standard_normal((n, n, 4)).astype(np.float32)
+    fa, fb = _gpu_ifft(ocean, a), _gpu_ifft(ocean, b)
+    fab = _gpu_ifft(ocean, (2.0 * a - 0.5 * b).astype(np.float32))
+    # linearity
+    assert max(lane_err(fab, 2.0 * fa.astype(np.float64) - 0.5 * fb.astype(np.float64))) < FFT_TOL
+    # Parseval with the unnormalised N^2 factor: sum |y|^2 = N^2 sum |x|^2 per lane
+    for lane in range(2):
+        ex = np.sum(a[..., 2 * lane:2 * lane + 2].astype(np.float64) ** 2)
+        ey = np.sum(fa[..., 2 * lane:2 * lane + 2].astype(np.float64) ** 2)
+        assert abs(ey / (n * n * ex) - 1.0) < 1e-5
+    # Hermitian input (in the shifted index convention) -> real output
+    z = a[..., 0] + 1j * a[..., 1]
+    zs = np.fft.ifftshift(z)
+    herm = 0.5 * (zs + np.conj(np.roll(np.flip(zs, (0, 1)), 1, (0, 1))))
+    hz = np.fft.fftshift(herm)
+    h = np.zeros_like(a)
+    h[..., 0], h[..., 1] = hz.real, hz.imag
+    fh = _gpu_ifft(ocean, h)
+    assert np.max(np.abs(fh[..., 1])) < 2e-5 * np.max(np.abs(fh[..., 0]))
+
+
+# ---- Full CalculateOcean frames (src/Generator.cpp:45-83) -----------------------------------
+def _frame_check(got_h, got_d, got_j, o):
+    eh, ed = lane_err(got_h, o.height), lane_err(got_d, o.disp)
+    ej = scalar_err(got_j - 1.0, o.jac - 1.0)
+    assert max(eh + ed) <= FRAME_TOL and ej <= FRAME_TOL, (eh, ed, ej)
+
+
+@pytest.mark.parametrize("n", [64, 256, 1024])
+def test_calculate_ocean_three_cascades(ocean, oracle, n):
+    """WaveApp's scene (src/Waves.cpp:20-39) as one batched generator, 4 frames at dt = 1/60."""
+    planes = [5.0, 17.0, 101.0]
+    fft = ocean.FFTCalculator(n)
+    gen = ocean.Generator(fft, 3)
+    refs = []
+    for c, L in enumerate(planes):
+        kw = dict(planeSize=L, boundWavelength=1, wavelengthMax=L / 2.0,
+                  wavelengthMin=0.0 if c == 0 else planes[c - 1] / 2.0)
+        ocean.apply_settings(gen.GetOceanSettings(c), **kw)
+        refs.append(oracle.OracleGenerator(n, oracle.default_settings(**kw)))
+    for f in range(4):
+        gen.CalculateOcean(1.0 / 60.0, update_ocean=(f == 0))
+        for r in refs:
+            r.calculate_ocean(1.0 / 60.0, update_ocean=(f == 0))
+    for c in range(3):
+        assert gen.GetOceanSettings(c).time == refs[c].settings.time
+        _frame_check(gen.height_map_host(c), gen.displacement_map_host(c), gen.jacobian_map_host(c), refs[c])
+
+
+@pytest.mark.parametrize("n", [256, 2048])
+def test_calculate_ocean_default_t1(ocean, oracle, n):
+    """Default settings (L = 40 m) at t = 1.0 s: the configuration the golden fixtures pin."""
+    fft = ocean.FFTCalculator(n)
+    gen = ocean.Generator(fft, 1)
+    gen.CalculateOcean(1.0)
+    ref = oracle.OracleGenerator(n)
+    ref.calculate_ocean(1.0)
+    _frame_check(gen.height_map_host(0), gen.displacement_map_host(0), gen.jacobian_map_host(0), ref)
+
+
+def test_batched_cascades_equal_individual(ocean):
+    """A cascade's maps do not depend on which batch it runs in (bit-exact)."""
+    n = 512
+    planes = [5.0, 17.0, 101.0, 251.0]
+    fft = ocean.FFTCalculator(n)
+    batch = ocean.Generator(fft, len(planes))
+    for c, L in enumerate(planes):
+        ocean.apply_settings(batch.GetOceanSettings(c), planeSize=L, seed=(12342 + 4097 * c, 8934))
+    batch.CalculateOcean(0.75)
+    for c, L in enumerate(planes):
+        one = ocean.Generator(fft, 1)
+        ocean.apply_settings(one.GetOceanSettings(0), planeSize=L, seed=(12342 + 4097 * c, 8934))
+        one.CalculateOcean(0.75)
+        assert np.array_equal(one.height_map_host(0), batch.height_map_host(c))
+        assert np.array_equal(one.displacement_map_host(0), batch.displacement_map_host(c))
+        assert np.array_equal(one.jacobian_map_host(0), batch.jacobian_map_host(c))
+
+
+def test_update_spectrum_semantics(ocean, oracle):
+    """h0 is regenerated on the first call and when update_ocean is set (src/Generator.cpp:55-59)."""
+    n = 128
+    fft = ocean.FFTCalculator(n)
+    gen = ocean.Generator(fft, 1)
+    gen.CalculateOcean(0.5)
+    h0_a = gen.initial_spectrum_host(0)
+    ocean.apply_settings(gen.GetOceanSettings(0), U_10=20.0)
+    gen.CalculateOcean(0.5)  # settings changed but no update flag: h0 unchanged
+    assert np.array_equal(gen.initial_spectrum_host(0), h0_a)
+    gen.CalculateOcean(0.5, update_ocean=True)
+    ref = oracle.generate_spectrum(oracle.default_settings(U_10=20.0), n)
+    assert max(lane_err(gen.initial_spectrum_host(0), ref)) <= H0_TOL
+    assert gen.GetOceanSettings(0).time == np.float32(1.5)
+
+
+def test_errors_fail_loudly(ocean):
+    from oceansimulation_amd.capi import OceanError
+
+    with pytest.raises(OceanError):
+        ocean.FFTCalculator(300)
+    with pytest.raises(OceanError):
+        ocean.FFTCalculator(32768)
+    fft = ocean.FFTCalculator(64)
+    with pytest.raises(OceanError):
+        ocean.Generator(fft, 0)
+    with pytest.raises(OceanError):
+        ocean.Generator(fft, 65)
+
+
+def test_cpp_dropin_binary():
+    """The C++ Waves:: drop-in (reference signatures) driven like WaveApp, checked vs the oracle."""
+    exe = os.path.join(ROOT, "tests", "cpp", "test_waves")
+    assert os.path.exists(exe), "build with `make` first"
+    r = subprocess.run([exe, "256", "3"], capture_output=True, text=True, timeout=300)
+    print(r.stdout)
+    assert r.returncode == 0, r.stdout + r.stderr

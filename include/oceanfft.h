@@ -104,7 +104,8 @@ int ocean_generator_cascades(const ocean_generator* gen);
 ocean_settings* ocean_generator_settings(ocean_generator* gen, int cascade);
 /* Generator::CalculateOcean(float timestep, bool updateOcean) — src/Generator.cpp:45-83, for all
  * cascades: time += timestep (fp32); regenerate h0 when update_spectrum != 0 or on first use;
- * evolve + pack + two EncodeIFFTs + foam. Two fused launches (row pass, column pass). */
+ * evolve + pack + two EncodeIFFTs + foam. Two fused launches: column pass (evolve + y iFFT of
+ * both packed maps) and row pass (x iFFT + row-major maps + Jacobian). */
 int ocean_generator_calculate(ocean_generator* gen, float timestep, int update_spectrum);
 /* Generator::GenerateSpectrum — src/Generator.cpp:148-154 (the generateSpectrum dispatch). */
 int ocean_generator_generate_spectrum(ocean_generator* gen);
@@ -113,14 +114,17 @@ int ocean_generator_generate_spectrum(ocean_generator* gen);
 float* ocean_generator_height_map(ocean_generator* gen, int cascade);
 float* ocean_generator_displacement_map(ocean_generator* gen, int cascade);
 float* ocean_generator_jacobian_map(ocean_generator* gen, int cascade);
-/* The initialSpectrum image (src/Generator.h:86): (h0(k), conj(h0(-k))) per texel. */
+/* The initialSpectrum image (private in the reference, src/Generator.h:86): (h0(k), conj(h0(-k)))
+ * per texel, stored strip-blocked: texel (x, y) at index ((x / B) * N + y) * B + (x % B) with
+ * B = ocean_generator_spectrum_block(gen), so the column pass streams it contiguously. */
 float* ocean_generator_initial_spectrum(ocean_generator* gen, int cascade);
+int ocean_generator_spectrum_block(const ocean_generator* gen);
 
 /* ---- instrumentation (bench) ------------------------------------------------------------- */
 /* When enabled, each kernel launch of the generator is bracketed by HIP events on its stream. */
 int ocean_generator_set_profiling(ocean_generator* gen, int enable);
 /* Synchronises, then returns per-kernel totals since the last call and resets them.
- * Index 0 = spectrum (h0), 1 = row pass (evolve + x iFFT), 2 = column pass (y iFFT + foam). */
+ * Index 0 = spectrum (h0), 1 = column pass (evolve + y iFFT), 2 = row pass (x iFFT + foam). */
 int ocean_generator_kernel_times(ocean_generator* gen, double ms_total[3], int64_t launches[3]);
 
 /* ---- debug -------------------------------------------------------------------------------- */

@@ -62,7 +62,6 @@ public:
   Vision::ID GetHeightMap() const { return heightMap; }
   Vision::ID GetDisplacementMap() const { return displacementMap; }
   Vision::ID GetJacobianMap() const { return jacobian; }
-  Vision::ID GetInitialSpectrum() const { return initialSpectrum; }
 
   // src/Generator.h:53. Kernels are compiled into liboceanfft for gfx950; nothing to reload.
   void LoadShaders(bool reload = false);
@@ -74,7 +73,6 @@ private:
   ocean_generator* gen = nullptr;
   Vision::ID heightMap = 0;
   Vision::ID displacementMap = 0;
-  Vision::ID initialSpectrum = 0;
   Vision::ID jacobian = 0;
 };
 

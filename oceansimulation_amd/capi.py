@@ -73,6 +73,7 @@ SIGNATURES = {
     "ocean_generator_displacement_map": (_vp, [_vp, _i]),
     "ocean_generator_jacobian_map": (_vp, [_vp, _i]),
     "ocean_generator_initial_spectrum": (_vp, [_vp, _i]),
+    "ocean_generator_spectrum_block": (_i, [_vp]),
     "ocean_generator_set_profiling": (_i, [_vp, _i]),
     "ocean_generator_kernel_times": (_i, [_vp, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int64)]),
     "ocean_debug_hash": (_i, [_vp, _i, _vp, _vp, _vp]),

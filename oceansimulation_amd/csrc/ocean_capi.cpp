@@ -73,8 +73,9 @@ struct ocean_generator
   int cascades = 0;
   std::vector<ocean_settings> settings;
   bool update_spectrum = true;  // src/Generator.h:72
-  float4* h0 = nullptr;         // [cascade][N][N]
-  float4* maps = nullptr;       // [cascade][2][N][N]: heightMap, displacementMap
+  float4* h0 = nullptr;         // [cascade][N/B][N][B] strip-blocked (B = spectrum_block)
+  float4* inter = nullptr;      // [cascade][2][N/B][N][B] after the y pass (strip-blocked)
+  float4* maps = nullptr;       // [cascade][2][N][N]: heightMap, displacementMap (row-major)
   float* jac = nullptr;         // [cascade][N][N]
   bool profiling = false;
   std::vector<EventPair> pending;
@@ -195,8 +196,7 @@ int ocean_fft_encode_ifft_batch(ocean_fft* fft, float* images, int n_images)
     return fail(OCEAN_ERR_INVALID, "ocean_fft_encode_ifft_batch: null plan/image or n_images < 1");
   auto* img = reinterpret_cast<float4*>(images);
   HIP_TRY(launch_rows_ifft(fft->logn, n_images, img, fft->twiddles, fft->stream, fft->cus), "row pass");
-  HIP_TRY(launch_cols(fft->logn, n_images, img, nullptr, nullptr, fft->twiddles, fft->stream, fft->cus),
-          "column pass");
+  HIP_TRY(launch_cols(fft->logn, n_images, img, fft->twiddles, fft->stream, fft->cus), "column pass");
   return OCEAN_OK;
 }
 
@@ -267,6 +267,8 @@ int ocean_generator_create(ocean_generator** out, ocean_fft* fft, int cascades)
   const size_t texels = (size_t)fft->n * fft->n;
   hipError_t e = hipMalloc(&g->h0, texels * cascades * sizeof(float4));
   if (e == hipSuccess)
+    e = hipMalloc(&g->inter, texels * cascades * 2 * sizeof(float4));
+  if (e == hipSuccess)
     e = hipMalloc(&g->maps, texels * cascades * 2 * sizeof(float4));
   if (e == hipSuccess)
     e = hipMalloc(&g->jac, texels * cascades * sizeof(float));
@@ -302,6 +304,8 @@ int ocean_generator_destroy(ocean_generator* g)
     (void)hipEventDestroy(ev);
   if (g->h0)
     (void)hipFree(g->h0);
+  if (g->inter)
+    (void)hipFree(g->inter);
   if (g->maps)
     (void)hipFree(g->maps);
   if (g->jac)
@@ -368,14 +372,15 @@ int ocean_generator_calculate(ocean_generator* g, float timestep, int update_spe
     fp.c[c].h = s.h;
     foam.displacement[c] = s.displacement;
   }
-  // prepareFFT + the x passes of both EncodeIFFTs (src/Generator.cpp:63-72)
-  HIP_TRY(timed(g, 1, [&] { return launch_rows_evolve(f->logn, fp, g->h0, g->maps, f->twiddles, f->stream, f->cus); }),
-          "row pass");
-  // the y passes of both EncodeIFFTs + computeFoam (src/Generator.cpp:71-80)
-  HIP_TRY(timed(g, 2, [&] {
-            return launch_cols(f->logn, 2 * g->cascades, g->maps, g->jac, &foam, f->twiddles, f->stream, f->cus);
-          }),
+  // pass 1: prepareFFT fused with the y direction of both EncodeIFFTs (src/Generator.cpp:63-72)
+  HIP_TRY(timed(g, 1, [&] { return launch_cols_evolve(f->logn, fp, g->h0, g->inter, f->twiddles, f->stream, f->cus, true); }),
           "column pass");
+  // pass 2: the x direction of both EncodeIFFTs + computeFoam (src/Generator.cpp:71-80)
+  HIP_TRY(timed(g, 2, [&] {
+            return launch_rows_final(f->logn, g->cascades, g->inter, g->maps, g->jac, foam, f->twiddles, f->stream,
+                                     f->cus);
+          }),
+          "row pass");
   return OCEAN_OK;
 }
 
@@ -405,6 +410,11 @@ float* ocean_generator_initial_spectrum(ocean_generator* g, int c)
   if (!g || c < 0 || c >= g->cascades)
     return nullptr;
   return reinterpret_cast<float*>(g->h0 + (size_t)g->fft->n * g->fft->n * c);
+}
+
+int ocean_generator_spectrum_block(const ocean_generator* g)
+{
+  return g ? spectrum_block(g->fft->logn) : 0;
 }
 
 int ocean_generator_set_profiling(ocean_generator* g, int enable)

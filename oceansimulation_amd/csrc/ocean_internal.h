@@ -52,14 +52,19 @@ struct FoamParams
   float displacement[kMaxCascades];
 };
 
+// h0 is stored strip-blocked [xb][y][blk]; blk = spectrum_block(log2 N).
+int spectrum_block(int logn);
 hipError_t launch_generate_spectrum(const OceanSettings& s, int n, float4* h0, hipStream_t stream, int cus);
 hipError_t launch_hash(const uint32_t* xy, int count, uint32_t* raw, float2* uv, hipStream_t stream);
-hipError_t launch_rows_evolve(int logn, const FrameParams& fp, const float4* h0, float4* maps,
-                              const float2* tw, hipStream_t stream, int cus);
+// Generator frame: pass 1 (evolve + y iFFT, blocked intermediate), pass 2 (x iFFT + maps + Jacobian).
+hipError_t launch_cols_evolve(int logn, const FrameParams& fp, const float4* h0, float4* inter, const float2* tw,
+                              hipStream_t stream, int cus, bool keep_h = false);
+hipError_t launch_rows_final(int logn, int cascades, const float4* inter, float4* maps, float* jac,
+                             const FoamParams& foam, const float2* tw, hipStream_t stream, int cus);
+// EncodeIFFT on row-major images, in place: row pass then column pass.
 hipError_t launch_rows_ifft(int logn, int n_images, float4* images, const float2* tw, hipStream_t stream,
                             int cus);
-hipError_t launch_cols(int logn, int n_images, float4* images, float* jac, const FoamParams* foam,
-                       const float2* tw, hipStream_t stream, int cus);
+hipError_t launch_cols(int logn, int n_images, float4* images, const float2* tw, hipStream_t stream, int cus);
 int twiddle_entries(int logn);
 
 }  // namespace oceanfft

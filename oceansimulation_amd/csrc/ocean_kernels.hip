@@ -26,6 +26,8 @@
 
 #include <cstdint>
 #include <cstdio>
+#include <mutex>
+#include <vector>
 
 #include "ocean_internal.h"
 
@@ -153,17 +155,24 @@ __device__ __forceinline__ float2 spectrum_amplitude(const OceanSettings& s, flo
 }
 
 // generateSpectrum (spectrum.compute:157-172): texel = (h0(k), conj(h0(-k))), -k taken as N - i.
-__global__ __launch_bounds__(256) void k_generate_spectrum(OceanSettings s, int n, float4* __restrict__ h0)
+// Stored strip-blocked, h0[xb][y][blk] (blk texel columns per strip, see ColFirstCfg), so the
+// column pass reads each strip as one contiguous run. The reference keeps this image private
+// (src/Generator.h:86), so its layout is internal.
+__global__ __launch_bounds__(256) void k_generate_spectrum(OceanSettings s, int n, int blk, float4* __restrict__ h0)
 {
   const int64_t total = (int64_t)n * n;
   const float dim = (float)n;
   for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < total;
        idx += (int64_t)gridDim.x * blockDim.x)
   {
-    int y = (int)(idx / n), x = (int)(idx - (int64_t)y * n);
+    // idx enumerates the blocked layout: b fastest, then y, then xb
+    const int b = (int)(idx % blk);
+    const int64_t rest = idx / blk;
+    const int y = (int)(rest % n), xb = (int)(rest / n);
+    const int x = xb * blk + b;
     float2 a = spectrum_amplitude(s, (float)x, (float)y, dim);
-    float2 b = spectrum_amplitude(s, dim - (float)x, dim - (float)y, dim);
-    h0[idx] = make_float4(a.x, a.y, b.x, -b.y);
+    float2 c = spectrum_amplitude(s, dim - (float)x, dim - (float)y, dim);
+    h0[idx] = make_float4(a.x, a.y, c.x, -c.y);
   }
 }
 
@@ -404,8 +413,9 @@ __device__ __forceinline__ void apply_stage_twiddles(V* v, int e1, const float2*
 
 // LDS exchange layout. Element a of the transform lives at padded index pa = a + (a >> 4) (one pad
 // slot per 16 elements: conflict-free Stockham writes). Region `reg`:
-//   row kernels:    slot = reg * PADDED + pa                 (float4 or float2 slots)
-//   column kernels: slot = pa * CI + reg  (CI columns interleaved: conflict-free for 4/8/16 lanes)
+//   row layout (CI == 0):  slot = reg * RSTRIDE + pa, RSTRIDE = PADDED + 4 (the +4 staggers regions
+//                          by 8 banks, so lanes that differ only in reg do not collide)
+//   column layout (CI > 0): slot = pa * CI + reg (CI columns interleaved)
 // Write/read indices are passed as PADDED indices in closed form (base + t*stride where the
 // stride is a multiple of 16 elements), so the per-t offsets fold into ds_* immediates instead
 // of occupying 16 address VGPRs.
@@ -415,7 +425,13 @@ __device__ __forceinline__ int lds_slot(int reg, int pa)
   if constexpr (CI > 0)
     return pa * CI + reg;
   else
-    return reg * PADDED + pa;
+    return reg * (PADDED + 4) + pa;
+}
+
+template <int LOGN>
+__host__ __device__ constexpr int lds_row_slots(int regions)
+{
+  return regions * (FftShape<LOGN>::PADDED + 4);
 }
 
 // Padded index of x[i + m*T] (the next stage's inputs).
@@ -429,10 +445,11 @@ __device__ __forceinline__ int read_pidx(int i, int m)
     return pad16(i + m * T);
 }
 
-// Write the 16 stage outputs (padded indices wp(t)), barrier, read back the next stage's inputs,
-// barrier. SPLIT: float4 data exchanged as two float2 lanes through a float2 buffer (half the LDS).
+// Write the 16 stage outputs (padded indices wp(t), region reg_w), barrier, read back the next
+// stage's inputs for the thread's (possibly different) position i_r in region reg_r, barrier.
+// SPLIT: float4 data exchanged as two float2 lanes through a float2 buffer (half the LDS).
 template <int LOGN, int CI, bool SPLIT, typename V, typename WP>
-__device__ __forceinline__ void exchange(V* v, int i, int reg, void* lds_raw, WP wp)
+__device__ __forceinline__ void exchange(V* v, int reg_w, int i_r, int reg_r, void* lds_raw, WP wp)
 {
   using S = FftShape<LOGN>;
   if constexpr (!SPLIT)
@@ -440,11 +457,11 @@ __device__ __forceinline__ void exchange(V* v, int i, int reg, void* lds_raw, WP
     V* lds = reinterpret_cast<V*>(lds_raw);
 #pragma unroll
     for (int t = 0; t < 16; t++)
-      lds[lds_slot<CI, S::PADDED>(reg, wp(t))] = v[t];
+      lds[lds_slot<CI, S::PADDED>(reg_w, wp(t))] = v[t];
     __syncthreads();
 #pragma unroll
     for (int m = 0; m < 16; m++)
-      v[m] = lds[lds_slot<CI, S::PADDED>(reg, read_pidx<LOGN>(i, m))];
+      v[m] = lds[lds_slot<CI, S::PADDED>(reg_r, read_pidx<LOGN>(i_r, m))];
     __syncthreads();
   }
   else
@@ -456,13 +473,13 @@ __device__ __forceinline__ void exchange(V* v, int i, int reg, void* lds_raw, WP
     {
 #pragma unroll
       for (int t = 0; t < 16; t++)
-        lds[lds_slot<CI, S::PADDED>(reg, wp(t))] =
+        lds[lds_slot<CI, S::PADDED>(reg_w, wp(t))] =
             half ? make_float2(v[t].z, v[t].w) : make_float2(v[t].x, v[t].y);
       __syncthreads();
 #pragma unroll
       for (int m = 0; m < 16; m++)
       {
-        float2 r = lds[lds_slot<CI, S::PADDED>(reg, read_pidx<LOGN>(i, m))];
+        float2 r = lds[lds_slot<CI, S::PADDED>(reg_r, read_pidx<LOGN>(i_r, m))];
         if (half)
           v[m].z = r.x, v[m].w = r.y;
         else
@@ -473,9 +490,15 @@ __device__ __forceinline__ void exchange(V* v, int i, int reg, void* lds_raw, WP
   }
 }
 
-// Full 1D inverse FFT (unnormalised) on the data held by this thread group.
+// Full 1D inverse FFT (unnormalised) of the transforms held by the workgroup.
+// On entry thread holds v[m] = x[i + m*T] of transform `reg`; the first exchange re-deals the data
+// so that from then on (and on exit, v[m] = X[i2 + m*T]) the thread is position i2 of transform
+// reg2. Any bijection (i, reg) -> (i2, reg2) over the workgroup is valid: it lets the global loads
+// and the global stores use different lane mappings for free. Transforms with a single stage
+// (N = 16) have no exchange and require i2 == i, reg2 == reg.
 template <int LOGN, int CI, bool SPLIT, typename V>
-__device__ __forceinline__ void fft_run(V* v, int i, int reg, void* lds, const float2* __restrict__ tw)
+__device__ __forceinline__ void fft_run(V* v, int i, int reg, int i2, int reg2, void* lds,
+                                        const float2* __restrict__ tw)
 {
   using S = FftShape<LOGN>;
   constexpr int N = S::N, T = S::T, R0 = S::R0;
@@ -487,7 +510,7 @@ __device__ __forceinline__ void fft_run(V* v, int i, int reg, void* lds, const f
     if constexpr (S::NSTAGE > 1)
     {
       const int base = 17 * i;  // pad16(16 i + t) = 17 i + t
-      exchange<LOGN, CI, SPLIT>(v, i, reg, lds, [&](int t) { return base + t; });
+      exchange<LOGN, CI, SPLIT>(v, reg, i2, reg2, lds, [&](int t) { return base + t; });
     }
   }
   else
@@ -511,35 +534,41 @@ __device__ __forceinline__ void fft_run(V* v, int i, int reg, void* lds, const f
         v[u + t * U] = w[t];
     }
     // output of butterfly b = i + u*T, element t -> y[b*R0 + t]; v index q = u + t*U
-    exchange<LOGN, CI, SPLIT>(v, i, reg, lds, [&](int q) {
+    exchange<LOGN, CI, SPLIT>(v, reg, i2, reg2, lds, [&](int q) {
       int u = q % U, t = q / U;
       return pad16((i + u * T) * R0 + t);
     });
   }
 
-  // ---- radix-16 stages ----
+  // ---- radix-16 stages (position i2 of transform reg2) ----
   int p = R0;
 #pragma unroll
   for (int s = 1; s < S::NSTAGE; s++)
   {
-    const int k = i & (p - 1);
+    const int k = i2 & (p - 1);
     const int stride = N / (16 * p);  // twiddle exponent unit for this stage, in 2 pi / N
     apply_stage_twiddles<LOGN>(v, k * stride, tw);
     idft16(v);
     if (s + 1 < S::NSTAGE)
     {
-      const int j = (i / p) * 16 * p + k;
+      const int j = (i2 / p) * 16 * p + k;
       const int pp = p;
       if (pp >= 16)
       {
         const int base = pad16(j), st = pp + pp / 16;
-        exchange<LOGN, CI, SPLIT>(v, i, reg, lds, [&](int t) { return base + t * st; });
+        exchange<LOGN, CI, SPLIT>(v, reg2, i2, reg2, lds, [&](int t) { return base + t * st; });
       }
       else
-        exchange<LOGN, CI, SPLIT>(v, i, reg, lds, [&](int t) { return pad16(j + t * pp); });
+        exchange<LOGN, CI, SPLIT>(v, reg2, i2, reg2, lds, [&](int t) { return pad16(j + t * pp); });
     }
     p *= 16;
   }
+}
+
+template <int LOGN, int CI, bool SPLIT, typename V>
+__device__ __forceinline__ void fft_run(V* v, int i, int reg, void* lds, const float2* __restrict__ tw)
+{
+  fft_run<LOGN, CI, SPLIT>(v, i, reg, i, reg, lds, tw);
 }
 
 template <int LOGN>
@@ -566,18 +595,58 @@ __device__ __forceinline__ KVec make_kvec(int x, int y, float dim, float dk)
   r.kz = ((float)y - dim / 2.0f) * dk;
   float len = sqrtf(r.kx * r.kx + r.kz * r.kz);
   bool zero = (r.kx == 0.0f && r.kz == 0.0f);
-  r.dirx = zero ? 0.0f : r.kx / len;
-  r.dirz = zero ? 0.0f : r.kz / len;
+  // normalize(kVec) (spectrum.compute:191) as kVec * (1/|k|): one division instead of two
+  const float inv = zero ? 0.0f : 1.0f / len;
+  r.dirx = r.kx * inv;
+  r.dirz = r.kz * inv;
   r.k = len + 1e-6f;
   return r;
+}
+
+// Dispersion (spectrum.compute:38-44) for the per-frame evolution. Same formula; tanh(kh), needed
+// only when kh < 2*pi (very long waves), is evaluated as an odd series for kh < 1/8 (|err| < 1e-10)
+// and as 1 - 2/(1 + e^{2kh}) above — a few VGPRs instead of ocml tanhf's.
+__device__ __forceinline__ float dispersion_evolve(float k, float g, float h)
+{
+  const float kh = k * h;
+  float t = 1.0f;
+  if (kh < 2.0f * OCEAN_PI)
+  {
+    const float x2 = kh * kh;
+    t = kh < 0.125f ? kh * fmaf(fmaf(fmaf(-17.0f / 315.0f, x2, 2.0f / 15.0f), x2, -1.0f / 3.0f), x2, 1.0f)
+                    : 1.0f - 2.0f / (1.0f + expf(2.0f * kh));
+  }
+  const float omegaSquared = (g * k + kSigmaSurface / kRhoWater * k * k * k) * t;
+  return sqrtf(omegaSquared);
+}
+
+// sin/cos of a large fp32 phase (w*t reaches 1e3-1e7 rad). Reduction by pi/2 in double (exact to
+// ~1e-9 rad for |x| < 1e7, far below the fp32 ulp of the result), then float minimax polynomials on
+// [-pi/4, pi/4] (Cephes sinf/cosf kernels, <= ~1 ulp). Replaces ocml's sincosf, whose Payne-Hanek
+// slow path costs ~60 VGPRs that a 1024-thread workgroup does not have.
+__device__ __forceinline__ void sincos_phase(float x, float* s, float* c)
+{
+  const double xd = (double)x;
+  const double kq = rint(xd * 0.63661977236758134308);  // 2/pi
+  const float r = (float)fma(-kq, 1.57079632679489661923, xd);
+  const int q = (int)(int64_t)kq;
+  const float z = r * r;
+  const float sp = r + r * z * fmaf(fmaf(-1.9515295891e-4f, z, 8.3321608736e-3f), z, -1.6666654611e-1f);
+  const float cp = 1.0f - 0.5f * z +
+                   z * z * fmaf(fmaf(2.443315711809948e-5f, z, -1.388731625493765e-3f), z, 4.166664568298827e-2f);
+  // quadrant q mod 4: (sin, cos) = (sp, cp), (cp, -sp), (-sp, -cp), (-cp, sp)
+  const bool swap = q & 1;
+  const float sv = swap ? cp : sp, cv = swap ? sp : cp;
+  *s = (q & 2) ? -sv : sv;
+  *c = ((q + 1) & 2) ? -cv : cv;
 }
 
 // heightAmp = h0 * e^{i w t} + conj-partner * e^{-i w t}
 __device__ __forceinline__ float2 evolve(float4 a, float k, const CascadeFrame& f)
 {
-  float phase = dispersion(k, f.g, f.h) * f.time;
+  float phase = dispersion_evolve(k, f.g, f.h) * f.time;
   float ws, wc;
-  sincosf(phase, &ws, &wc);
+  sincos_phase(phase, &ws, &wc);
   float ampx = a.x * wc - a.y * ws;
   float ampy = a.x * ws + a.y * wc;
   float ws2 = -ws;
@@ -609,8 +678,8 @@ __device__ __forceinline__ float4 pack_displacement(float2 H, const KVec& q)
 }
 
 // ------------------------------------------------------------------------------------------------
-// Row pass, fused with evolution: one x-direction transform per (cascade, row) for all 4 fields.
-// maps layout: [cascade][2][N][N] float4 (image 0 = heightMap, 1 = displacementMap).
+// FFTCalculator::EncodeIFFT path on caller-owned row-major images: row pass then column pass,
+// both in place (no work image).
 // ------------------------------------------------------------------------------------------------
 template <int LOGN>
 struct RowCfg
@@ -619,88 +688,12 @@ struct RowCfg
   static constexpr int RPW = S::T >= 256 ? 1 : 256 / S::T;  // rows per workgroup iteration
   static constexpr int WG = S::T * RPW;
   static constexpr bool SPLIT = (S::N * 16 > 96 * 1024);   // float4 exchange would not fit
-  static constexpr int LDS_BYTES = RPW * S::PADDED * (SPLIT ? 8 : 16);
+  static constexpr int LDS_BYTES = lds_row_slots<LOGN>(RPW) * (SPLIT ? 8 : 16);
   // waves per SIMD the LDS budget admits (>= 1): caps VGPRs so registers never limit residency
   static constexpr int WGS_PER_CU = (150 * 1024) / (LDS_BYTES + 2048) < 1 ? 1 : (150 * 1024) / (LDS_BYTES + 2048);
   static constexpr int MIN_WAVES_RAW = WGS_PER_CU * (WG / 64) / 4;
   static constexpr int MIN_WAVES = MIN_WAVES_RAW < 1 ? 1 : (MIN_WAVES_RAW > 8 ? 8 : MIN_WAVES_RAW);
 };
-
-template <int LOGN>
-__global__ __launch_bounds__(RowCfg<LOGN>::WG, RowCfg<LOGN>::MIN_WAVES) void k_rows_evolve(
-    FrameParams fp, const float4* __restrict__ h0, float4* __restrict__ maps, const float2* __restrict__ tw_glob)
-{
-  using S = FftShape<LOGN>;
-  using R = RowCfg<LOGN>;
-  constexpr int N = S::N, T = S::T;
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  float2* tw = reinterpret_cast<float2*>(smem);
-  void* xch = smem + ((S::TW_ENTRIES * 8 + 15) / 16) * 16;
-  load_twiddles<LOGN>(tw, tw_glob);
-
-  const int rho = threadIdx.x / T, i0 = threadIdx.x % T;
-  const int total = fp.cascades * N;
-  const float dim = (float)N;
-  for (int row0 = blockIdx.x * R::RPW; row0 < total; row0 += gridDim.x * R::RPW)
-  {
-    const int i = opaque(i0), rho_ = R::RPW == 1 ? 0 : opaque(rho);
-    // Rows of h0 ([cascade][N][N]) are contiguous: uniform base + lane offset; rows past the last
-    // one (ragged tail, N < 64 only) read 0 through the range limit.
-    const float4* src = h0 + ((size_t)row0 << LOGN);
-    const int lim = clamp_bytes((int64_t)(total - row0) * N * 16);
-    const int voff = ((rho_ << LOGN) + i) * 16;
-    const int row = row0 + rho_;
-    const int c = min(row >> LOGN, fp.cascades - 1), y = row & (N - 1);
-    const CascadeFrame f = fp.c[c];
-
-    float4 raw[16];
-#pragma unroll
-    for (int m = 0; m < 16; m++)
-      raw[m] = ld4(src + ((m + 8) & 15) * T, voff, lim);  // fftShift on x folded into the load
-    float2 H[16];
-#pragma unroll
-    for (int m = 0; m < 16; m++)
-    {
-      const int x = i + ((m + 8) & 15) * T;
-      KVec q = make_kvec(x, y, dim, f.dk);
-      H[m] = evolve(raw[m], q.k, f);
-    }
-
-    float4 v[16];
-#pragma unroll
-    for (int img = 0; img < 2; img++)
-    {
-#pragma unroll
-      for (int m = 0; m < 16; m++)
-      {
-        const int x = i + ((m + 8) & 15) * T;
-        KVec q = make_kvec(x, y, dim, f.dk);
-        v[m] = img == 0 ? pack_height(H[m], q) : pack_displacement(H[m], q);
-      }
-      fft_run<LOGN, 0, R::SPLIT>(v, i, rho_, xch, tw);
-      if constexpr (N >= R::RPW)
-      {
-        // the block's rows share one cascade: maps[c][img][y0 + rho] from a uniform base
-        const int c0 = row0 >> LOGN, y0 = row0 & (N - 1);
-        float4* dst = maps + ((size_t)(2 * c0 + img) << (2 * LOGN)) + ((size_t)y0 << LOGN);
-#pragma unroll
-        for (int m = 0; m < 16; m++)
-          st4(dst + m * T, voff, v[m]);
-      }
-      else
-      {
-        // N < 64: rows of one block straddle cascades; per-lane destination, tail rows skipped
-        if (row < total)
-        {
-          float4* dst = maps + ((size_t)(2 * c + img) << (2 * LOGN)) + ((size_t)y << LOGN);
-#pragma unroll
-          for (int m = 0; m < 16; m++)
-            dst[i + m * T] = v[m];
-        }
-      }
-    }
-  }
-}
 
 // Row pass of a plain EncodeIFFT on packed images [n_images][N][N] float4, in place.
 template <int LOGN>
@@ -763,10 +756,9 @@ __device__ __forceinline__ int xcd_pair_slot(int b, int G)
   return 2 * pair + (j & 1);
 }
 
-template <int LOGN, bool FOAM>
-__global__ __launch_bounds__(ColCfg<LOGN>::WG) void k_cols(
-    int n_images, float4* __restrict__ images, float* __restrict__ jac, FoamParams foam,
-    const float2* __restrict__ tw_glob)
+template <int LOGN>
+__global__ __launch_bounds__(ColCfg<LOGN>::WG) void k_cols(int n_images, float4* __restrict__ images,
+                                                           const float2* __restrict__ tw_glob)
 {
   using S = FftShape<LOGN>;
   using K = ColCfg<LOGN>;
@@ -784,7 +776,7 @@ __global__ __launch_bounds__(ColCfg<LOGN>::WG) void k_cols(
     const int img = item / K::STRIPS, strip = item - img * K::STRIPS;
     const int x = strip * C + c;
     // image rows i + mm*T: uniform base per mm (SGPR), lane offset (i*N + x)*16 shared by all mm
-    const float4* ibase = images + ((size_t)img << (2 * LOGN));
+    float4* ibase = images + ((size_t)img << (2 * LOGN));
     const int voff = ((i << LOGN) + x) * 16;
     float4 v[16];
 #pragma unroll
@@ -795,25 +787,164 @@ __global__ __launch_bounds__(ColCfg<LOGN>::WG) void k_cols(
       v[m] = ld4(ibase + ((size_t)(mm * T) << LOGN), voff);
     }
     fft_run<LOGN, C, true>(v, i, c, xch, tw);
-    float4* obase = images + ((size_t)img << (2 * LOGN));
 #pragma unroll
     for (int m = 0; m < 16; m++)
-      st4(obase + ((size_t)(m * T) << LOGN), voff, v[m]);
-    if constexpr (FOAM)
+      st4(ibase + ((size_t)(m * T) << LOGN), voff, v[m]);
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// Generator path, column-first (2 HBM passes, every global access a >= 256-byte run per wave):
+//   h0      [cascade][xb][y][B]                 strip-blocked (written by k_generate_spectrum)
+//   pass 1  k_cols_evolve: per strip of B columns: evolve (spectrum.compute:183-240), iFFT along y
+//           of both packed images, write inter[cascade][img][xb][y][B] (contiguous runs)
+//   pass 2  k_rows_final: per RPW2 rows of one image: read the blocked intermediate (lanes
+//           interleaved so 8 lanes cover one 256-byte run of B texels x RPW2 rows), iFFT along x,
+//           write the row-major map (the reference's RGBA32F image) and, for displacement maps,
+//           the Jacobian (spectrum.compute:246-259).
+// The reference transforms rows first (src/FFTCalculator.cpp:19-20); the 2D iFFT is separable, so
+// the order changes only rounding (covered by the parity tolerance).
+// ------------------------------------------------------------------------------------------------
+template <int LOGN>
+struct ColFirstCfg
+{
+  using S = FftShape<LOGN>;
+  static constexpr int N = S::N, T = S::T;
+  static constexpr int B = T >= 1024 ? 1 : (T >= 512 ? 2 : (T < 4 ? T : 4));  // texels per block row
+  static constexpr int SPW_RAW = 256 / (T * B) < 1 ? 1 : 256 / (T * B);
+  static constexpr int SPW = SPW_RAW > N / B ? N / B : SPW_RAW;  // strips per pass-1 item
+  static constexpr int C1 = B * SPW;                              // columns per pass-1 item
+  static constexpr int WG1 = T * C1;
+  static constexpr int LDS1 = C1 * S::PADDED * 8;  // float2 (split-lane) exchange
+  static constexpr int RPW2_RAW = 256 / T >= 4 ? 256 / T : (1024 / T < 4 ? 1024 / T : 4);
+  static constexpr int RPW2 = RPW2_RAW > N ? N : RPW2_RAW;  // rows per pass-2 item
+  static constexpr int WG2 = T * RPW2;
+  static constexpr int LDS2 = lds_row_slots<LOGN>(RPW2) * 8;
+};
+
+// KEEP_H: evolve once and keep H (32 VGPRs) live across both transforms; otherwise re-read the
+// strip's h0 for the second image (a re-read of bytes streamed microseconds earlier) and evolve
+// again, which keeps the 1024-thread workgroup within 128 VGPRs without spills.
+template <int LOGN, bool KEEP_H>
+__global__ __launch_bounds__(ColFirstCfg<LOGN>::WG1) void k_cols_evolve(
+    FrameParams fp, const float4* __restrict__ h0, float4* __restrict__ inter, const float2* __restrict__ tw_glob)
+{
+  using S = FftShape<LOGN>;
+  using K = ColFirstCfg<LOGN>;
+  constexpr int N = S::N, T = S::T, B = K::B, SPW = K::SPW;
+  constexpr int GROUPS = (N / B) / SPW;  // pass-1 items per cascade
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  float2* tw = reinterpret_cast<float2*>(smem);
+  void* xch = smem + ((S::TW_ENTRIES * 8 + 15) / 16) * 16;
+  load_twiddles<LOGN>(tw, tw_glob);
+
+  const int b0 = threadIdx.x % B, i0 = (threadIdx.x / B) % T, sl0 = threadIdx.x / (B * T);
+  const int total = fp.cascades * GROUPS;
+  const float dim = (float)N;
+  for (int item = blockIdx.x; item < total; item += gridDim.x)
+  {
+    const int b = opaque(b0), sl = SPW == 1 ? 0 : opaque(sl0);
+    const int c = item / GROUPS, xb0 = (item - c * GROUPS) * SPW;
+    const CascadeFrame f = fp.c[c];
+    // this item's SPW strips are one contiguous run of SPW*N*B texels
+    const size_t run = ((size_t)c * (N / B) + xb0) * N * B;
+    const float4* src = h0 + run;
+    const int x = (xb0 + sl) * B + b;
+
+    float2 H[KEEP_H ? 16 : 1];
+    if constexpr (KEEP_H)
     {
-      if (img & 1)
+      const int i = opaque(i0);
+      const int voff = ((sl * N + i) * B + b) * 16;
+      float4 raw[16];
+#pragma unroll
+      for (int m = 0; m < 16; m++)
+        raw[m] = ld4(src + ((m + 8) & 15) * T * B, voff);  // fftShift on y folded into the load
+#pragma unroll
+      for (int m = 0; m < 16; m++)
       {
-        const float lam = foam.displacement[img >> 1];
-        float* jb = jac + ((size_t)(img >> 1) << (2 * LOGN));
-        const int joff = ((i << LOGN) + x) * 4;
+        const int y = i + ((m + 8) & 15) * T;
+        KVec q = make_kvec(x, y, dim, f.dk);
+        H[m] = evolve(raw[m], q.k, f);
+      }
+    }
+#pragma unroll 1
+    for (int img = 0; img < 2; img++)
+    {
+      const int i = opaque(i0);  // keep the k-vector math inside this loop (see opaque())
+      const int voff = ((sl * N + i) * B + b) * 16;
+      float4 v[16];
+      if constexpr (!KEEP_H)
+      {
 #pragma unroll
         for (int m = 0; m < 16; m++)
-        {
-          float4 d = v[m];
-          st1(jb + ((size_t)(m * T) << LOGN), joff,
-              (1.0f + lam * d.y) * (1.0f + lam * d.z) - lam * lam * d.w * d.w);
-        }
+          v[m] = ld4(src + ((m + 8) & 15) * T * B, voff);  // fftShift on y folded into the load
       }
+#pragma unroll
+      for (int m = 0; m < 16; m++)
+      {
+        const int y = i + ((m + 8) & 15) * T;
+        KVec q = make_kvec(x, y, dim, f.dk);
+        const float2 Hm = KEEP_H ? H[m] : evolve(v[m], q.k, f);
+        v[m] = img == 0 ? pack_height(Hm, q) : pack_displacement(Hm, q);
+      }
+      fft_run<LOGN, K::C1, true>(v, i, sl * B + b, xch, tw);
+      float4* dst = inter + ((size_t)(2 * c + img) * (N / B) + xb0) * N * B;
+#pragma unroll
+      for (int m = 0; m < 16; m++)
+        st4(dst + m * T * B, voff, v[m]);
+    }
+  }
+}
+
+template <int LOGN>
+__global__ __launch_bounds__(ColFirstCfg<LOGN>::WG2) void k_rows_final(
+    int cascades, const float4* __restrict__ inter, float4* __restrict__ maps, float* __restrict__ jac,
+    FoamParams foam, const float2* __restrict__ tw_glob)
+{
+  using S = FftShape<LOGN>;
+  using K = ColFirstCfg<LOGN>;
+  constexpr int N = S::N, T = S::T, B = K::B, RPW = K::RPW2;
+  constexpr int BLOCKS = N / RPW;  // pass-2 items per image
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  float2* tw = reinterpret_cast<float2*>(smem);
+  void* xch = smem + ((S::TW_ENTRIES * 8 + 15) / 16) * 16;
+  load_twiddles<LOGN>(tw, tw_glob);
+
+  // Loads: lanes b fastest, then row r, then ihi, so 16 consecutive lanes read one B*RPW*16-byte
+  // run [xb][y0..y0+RPW-1][0..B-1]. After the first exchange the thread becomes position i2 of
+  // row r2 with i2 fastest, so each wave stores 64 consecutive texels (1 KiB) of one row.
+  const int b0 = threadIdx.x % B, r0 = (threadIdx.x / B) % RPW, ihi0 = threadIdx.x / (B * RPW);
+  const int i20 = threadIdx.x % T, r20 = threadIdx.x / T;
+  constexpr bool REMAP = S::NSTAGE > 1;
+  const int total = cascades * 2 * BLOCKS;
+  for (int item = blockIdx.x; item < total; item += gridDim.x)
+  {
+    const int b = opaque(b0), r = RPW == 1 ? 0 : opaque(r0), ihi = opaque(ihi0);
+    const int i = ihi * B + b;
+    const int i2 = REMAP ? opaque(i20) : i, r2 = REMAP ? (RPW == 1 ? 0 : opaque(r20)) : r;
+    const int img = item / BLOCKS, y0 = (item - img * BLOCKS) * RPW;
+    const float4* src = inter + ((size_t)img << (2 * LOGN)) + (size_t)y0 * B;
+    const int voff = ((ihi * N + r) * B + b) * 16;
+    float4 v[16];
+#pragma unroll
+    for (int m = 0; m < 16; m++)
+      v[m] = ld4(src + (size_t)(((m + 8) & 15) * (T / B)) * N * B, voff);  // fftShift on x
+    fft_run<LOGN, 0, true>(v, i, r, i2, r2, xch, tw);
+    float4* dst = maps + ((size_t)img << (2 * LOGN)) + ((size_t)y0 << LOGN);
+    const int woff = ((r2 << LOGN) + i2) * 16;
+#pragma unroll
+    for (int m = 0; m < 16; m++)
+      st4(dst + m * T, woff, v[m]);
+    if (img & 1)
+    {
+      // displacementMap (Dz, dDx/dx, dDz/dz, dDx/dz): Jacobian, spectrum.compute:246-259
+      const float lam = foam.displacement[img >> 1];
+      float* jb = jac + ((size_t)(img >> 1) << (2 * LOGN)) + ((size_t)y0 << LOGN);
+      const int joff = ((r2 << LOGN) + i2) * 4;
+#pragma unroll
+      for (int m = 0; m < 16; m++)
+        st1(jb + m * T, joff, (1.0f + lam * v[m].y) * (1.0f + lam * v[m].z) - lam * lam * v[m].w * v[m].w);
     }
   }
 }
@@ -854,27 +985,59 @@ static hipError_t with_logn(int logn, F&& f)
   }
 }
 
-// Persistent grid: resident blocks per CU x CUs, capped by the work item count.
+// Persistent grid: resident blocks per CU x CUs, capped by the work item count. The occupancy
+// query and the dynamic-LDS attribute are set once per kernel instantiation (host API calls cost
+// microseconds; a frame is two launches).
+struct LaunchCacheEntry
+{
+  const void* kernel;
+  int lds;
+  int per_cu;
+};
+
 template <typename K>
 static int persistent_grid(K kernel, int wg, int lds, int items, int cus)
 {
-  int per_cu = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, wg, lds) != hipSuccess || per_cu < 1)
-    per_cu = 1;
+  static std::mutex mu;
+  static std::vector<LaunchCacheEntry> cache;
+  int per_cu = -1;
+  {
+    std::lock_guard<std::mutex> lock(mu);
+    for (const auto& e : cache)
+      if (e.kernel == (const void*)kernel && e.lds == lds)
+        per_cu = e.per_cu;
+    if (per_cu < 0)
+    {
+      per_cu = 0;
+      (void)hipFuncSetAttribute((const void*)kernel, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+      if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, wg, lds) != hipSuccess || per_cu < 1)
+        per_cu = 1;
+      cache.push_back({(const void*)kernel, lds, per_cu});
+    }
+  }
   long g = (long)per_cu * cus;
   if (g > items)
     g = items;
   return g < 1 ? 1 : (int)g;
 }
 
+int spectrum_block(int logn)
+{
+  int t = 1 << (logn - 4);
+  return t >= 1024 ? 1 : (t >= 512 ? 2 : (t < 4 ? t : 4));
+}
+
 hipError_t launch_generate_spectrum(const OceanSettings& s, int n, float4* h0, hipStream_t stream, int cus)
 {
+  int logn = 0;
+  while ((1 << logn) < n)
+    logn++;
   long total = (long)n * n;
   long blocks = (total + 255) / 256;
   long cap = (long)cus * 16;
   if (blocks > cap)
     blocks = cap;
-  hipLaunchKernelGGL(k_generate_spectrum, dim3((unsigned)blocks), dim3(256), 0, stream, s, n, h0);
+  hipLaunchKernelGGL(k_generate_spectrum, dim3((unsigned)blocks), dim3(256), 0, stream, s, n, spectrum_block(logn), h0);
   return hipGetLastError();
 }
 
@@ -884,18 +1047,34 @@ hipError_t launch_hash(const uint32_t* xy, int count, uint32_t* raw, float2* uv,
   return hipGetLastError();
 }
 
-hipError_t launch_rows_evolve(int logn, const FrameParams& fp, const float4* h0, float4* maps,
-                              const float2* tw, hipStream_t stream, int cus)
+hipError_t launch_cols_evolve(int logn, const FrameParams& fp, const float4* h0, float4* inter, const float2* tw,
+                              hipStream_t stream, int cus, bool keep_h)
 {
   return with_logn(logn, [&](auto L) -> hipError_t {
     constexpr int LOGN = decltype(L)::value;
-    using R = RowCfg<LOGN>;
-    auto kern = k_rows_evolve<LOGN>;
-    int lds = lds_bytes_rows<LOGN>();
-    (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
-    int items = ((fp.cascades << LOGN) + R::RPW - 1) / R::RPW;
-    int grid = persistent_grid(kern, R::WG, lds, items, cus);
-    hipLaunchKernelGGL(kern, dim3(grid), dim3(R::WG), lds, stream, fp, h0, maps, tw);
+    using K = ColFirstCfg<LOGN>;
+    using S = FftShape<LOGN>;
+    auto kern = keep_h ? k_cols_evolve<LOGN, true> : k_cols_evolve<LOGN, false>;
+    const int lds = ((S::TW_ENTRIES * 8 + 15) / 16) * 16 + K::LDS1;
+    const int items = fp.cascades * ((S::N / K::B) / K::SPW);
+    const int grid = persistent_grid(kern, K::WG1, lds, items, cus);
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(K::WG1), lds, stream, fp, h0, inter, tw);
+    return hipGetLastError();
+  });
+}
+
+hipError_t launch_rows_final(int logn, int cascades, const float4* inter, float4* maps, float* jac,
+                             const FoamParams& foam, const float2* tw, hipStream_t stream, int cus)
+{
+  return with_logn(logn, [&](auto L) -> hipError_t {
+    constexpr int LOGN = decltype(L)::value;
+    using K = ColFirstCfg<LOGN>;
+    using S = FftShape<LOGN>;
+    auto kern = k_rows_final<LOGN>;
+    const int lds = ((S::TW_ENTRIES * 8 + 15) / 16) * 16 + K::LDS2;
+    const int items = cascades * 2 * (S::N / K::RPW2);
+    const int grid = persistent_grid(kern, K::WG2, lds, items, cus);
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(K::WG2), lds, stream, cascades, inter, maps, jac, foam, tw);
     return hipGetLastError();
   });
 }
@@ -907,7 +1086,6 @@ hipError_t launch_rows_ifft(int logn, int n_images, float4* images, const float2
     using R = RowCfg<LOGN>;
     auto kern = k_rows_ifft<LOGN>;
     int lds = lds_bytes_rows<LOGN>();
-    (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
     int items = ((n_images << LOGN) + R::RPW - 1) / R::RPW;
     int grid = persistent_grid(kern, R::WG, lds, items, cus);
     hipLaunchKernelGGL(kern, dim3(grid), dim3(R::WG), lds, stream, n_images, images, tw);
@@ -915,31 +1093,16 @@ hipError_t launch_rows_ifft(int logn, int n_images, float4* images, const float2
   });
 }
 
-hipError_t launch_cols(int logn, int n_images, float4* images, float* jac, const FoamParams* foam,
-                       const float2* tw, hipStream_t stream, int cus)
+hipError_t launch_cols(int logn, int n_images, float4* images, const float2* tw, hipStream_t stream, int cus)
 {
   return with_logn(logn, [&](auto L) -> hipError_t {
     constexpr int LOGN = decltype(L)::value;
     using K = ColCfg<LOGN>;
     int lds = lds_bytes_cols<LOGN>();
     int items = n_images * K::STRIPS;
-    FoamParams fpar{};
-    if (foam)
-      fpar = *foam;
-    if (foam && jac)
-    {
-      auto kern = k_cols<LOGN, true>;
-      (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
-      int grid = persistent_grid(kern, K::WG, lds, items, cus);
-      hipLaunchKernelGGL(kern, dim3(grid), dim3(K::WG), lds, stream, n_images, images, jac, fpar, tw);
-    }
-    else
-    {
-      auto kern = k_cols<LOGN, false>;
-      (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
-      int grid = persistent_grid(kern, K::WG, lds, items, cus);
-      hipLaunchKernelGGL(kern, dim3(grid), dim3(K::WG), lds, stream, n_images, images, jac, fpar, tw);
-    }
+    auto kern = k_cols<LOGN>;
+    int grid = persistent_grid(kern, K::WG, lds, items, cus);
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(K::WG), lds, stream, n_images, images, tw);
     return hipGetLastError();
   });
 }

@@ -22,8 +22,6 @@ Generator::Generator(Vision::RenderDevice* device, FFTCalculator* calc)
                                               Vision::PixelType::RGBA32Float);
   displacementMap = renderDevice->RegisterTexture2D(ocean_generator_displacement_map(gen, 0), n, n,
                                                     Vision::PixelType::RGBA32Float);
-  initialSpectrum = renderDevice->RegisterTexture2D(ocean_generator_initial_spectrum(gen, 0), n, n,
-                                                    Vision::PixelType::RGBA32Float);
   jacobian = renderDevice->RegisterTexture2D(ocean_generator_jacobian_map(gen, 0), n, n,
                                              Vision::PixelType::R32Float);
 }
@@ -32,7 +30,6 @@ Generator::~Generator()
 {
   renderDevice->DestroyTexture2D(heightMap);
   renderDevice->DestroyTexture2D(displacementMap);
-  renderDevice->DestroyTexture2D(initialSpectrum);
   renderDevice->DestroyTexture2D(jacobian);
   ocean_generator_destroy(gen);
 }

@@ -133,15 +133,18 @@ class Generator:
         return hip.to_host(self.GetJacobianMap(cascade), (self.n, self.n))
 
     def initial_spectrum_host(self, cascade: int = 0) -> np.ndarray:
+        """h0 as an N x N x 4 row-major image (de-blocked from the device's strip-blocked layout)."""
         self.fft.synchronize()
-        return hip.to_host(self.GetInitialSpectrum(cascade), (self.n, self.n, 4))
+        b = int(lib().ocean_generator_spectrum_block(self._h))
+        blocked = hip.to_host(self.GetInitialSpectrum(cascade), (self.n // b, self.n, b, 4))
+        return np.ascontiguousarray(blocked.transpose(1, 0, 2, 3).reshape(self.n, self.n, 4))
 
     # ---- instrumentation ----
     def set_profiling(self, enable: bool) -> None:
         check(lib().ocean_generator_set_profiling(self._h, 1 if enable else 0), "ocean_generator_set_profiling")
 
     def kernel_times(self):
-        """(ms totals, launch counts) for [spectrum, row pass, column pass] since the last call."""
+        """(ms totals, launch counts) for [spectrum, column pass, row pass] since the last call."""
         ms = (ctypes.c_double * 3)()
         cnt = (ctypes.c_int64 * 3)()
         check(lib().ocean_generator_kernel_times(self._h, ms, cnt), "ocean_generator_kernel_times")

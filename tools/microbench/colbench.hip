@@ -1,0 +1,393 @@
+// colbench.hip — microbenchmarks separating the column pass's memory pattern from its compute.
+// Build: hipcc --offload-arch=gfx950 -O3 -fno-slp-vectorize -std=c++17 -I include -I oceansimulation_amd/csrc \
+//        tools/microbench/colbench.hip -o tools/microbench/colbench
+// Runs on 8 images of 4096^2 float4 (2 GiB), in place, and prints GB/s for each variant.
+#include "../../oceansimulation_amd/csrc/ocean_kernels.hip"
+
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+
+using namespace oceanfft;
+
+#define CHECK(x)                                                                                   \
+  do                                                                                               \
+  {                                                                                                \
+    hipError_t e = (x);                                                                            \
+    if (e != hipSuccess)                                                                           \
+    {                                                                                              \
+      std::printf("HIP error %s at %s:%d\n", hipGetErrorString(e), __FILE__, __LINE__);            \
+      std::exit(1);                                                                                \
+    }                                                                                              \
+  } while (0)
+
+constexpr int LOGN = 12, N = 1 << LOGN;
+
+// Contiguous in-place float4 read+write (reference for achievable streaming bandwidth).
+__global__ __launch_bounds__(256) void k_rowcopy(float4* p, long n4)
+{
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n4; i += (long)gridDim.x * 256)
+  {
+    float4 v = p[i];
+    v.x += 1.0f;
+    p[i] = v;
+  }
+}
+
+// Column-strip pattern: C texels wide (C*16 B segments), ROWS_PER_M rows per m step, 16 m steps.
+// All 16 loads in flight, then 16 stores. PAIR: XCD pair mapping of adjacent strips.
+template <int C, int THREADS, bool PAIR>
+__global__ __launch_bounds__(THREADS) void k_colpat(float4* images, int n_images)
+{
+  constexpr int RPM = THREADS / C;       // rows covered by one m step
+  constexpr int ROWS = RPM * 16;         // rows per item
+  constexpr int ITEMS_PER_STRIP = N / ROWS;
+  constexpr int STRIPS = N / C;
+  const int c = threadIdx.x % C, i = threadIdx.x / C;
+  const int total = n_images * STRIPS * ITEMS_PER_STRIP;
+  for (int item = PAIR ? xcd_pair_slot(blockIdx.x, gridDim.x) : blockIdx.x; item < total; item += gridDim.x)
+  {
+    // adjacent items = adjacent strips (so pairs share 128-B lines)
+    const int strip = item % STRIPS;
+    const int rest = item / STRIPS;
+    const int part = rest % ITEMS_PER_STRIP, img = rest / ITEMS_PER_STRIP;
+    const int x = strip * C + opaque(c);
+    const int r0 = part * ROWS + opaque(i);
+    float4* base = images + ((size_t)img << (2 * LOGN));
+    const int voff = ((r0 << LOGN) + x) * 16;
+    float4 v[16];
+#pragma unroll
+    for (int m = 0; m < 16; m++)
+      v[m] = ld4(base + ((size_t)(m * RPM) << LOGN), voff);
+#pragma unroll
+    for (int m = 0; m < 16; m++)
+    {
+      v[m].x += 1.0f;
+      st4(base + ((size_t)(m * RPM) << LOGN), voff, v[m]);
+    }
+  }
+}
+
+// Separate read/write patterns between a row-major buffer A and a strip-blocked buffer B
+// (B[img][strip][y][C]: a C-column strip is one contiguous N*C*16-byte run).
+// RS: read A strided (C*16 B per row), else read B contiguous. WS: write A strided, else write B.
+template <int C, int THREADS, bool RS, bool WS>
+__global__ __launch_bounds__(THREADS) void k_rw(const float4* A, float4* Bout, const float4* Bin, float4* Aout, int n_images)
+{
+  constexpr int RPM = THREADS / C;
+  constexpr int ROWS = RPM * 16;
+  constexpr int ITEMS_PER_STRIP = N / ROWS;
+  constexpr int STRIPS = N / C;
+  const int c = threadIdx.x % C, i = threadIdx.x / C;
+  const int total = n_images * STRIPS * ITEMS_PER_STRIP;
+  for (int item = blockIdx.x; item < total; item += gridDim.x)
+  {
+    const int strip = item % STRIPS;
+    const int rest = item / STRIPS;
+    const int part = rest % ITEMS_PER_STRIP, img = rest / ITEMS_PER_STRIP;
+    const int x = strip * C + opaque(c);
+    const int r0 = part * ROWS + opaque(i);
+    const size_t ib = (size_t)img << (2 * LOGN);
+    const float4* ra = A + ib;
+    const float4* rb = Bin + ib + (size_t)strip * N * C;
+    float4 v[16];
+#pragma unroll
+    for (int m = 0; m < 16; m++)
+    {
+      if (RS)
+        v[m] = ld4(ra + ((size_t)(m * RPM) << LOGN), ((r0 << LOGN) + x) * 16);
+      else
+        v[m] = ld4(rb + (size_t)(m * RPM) * C, (r0 * C + c) * 16);
+    }
+    float4* wa = Aout + ib;
+    float4* wb = Bout + ib + (size_t)strip * N * C;
+#pragma unroll
+    for (int m = 0; m < 16; m++)
+    {
+      v[m].x += 1.0f;
+      if (WS)
+        st4(wa + ((size_t)(m * RPM) << LOGN), ((r0 << LOGN) + x) * 16, v[m]);
+      else
+        st4(wb + (size_t)(m * RPM) * C, (r0 * C + c) * 16, v[m]);
+    }
+  }
+}
+
+template <int C, int THREADS, bool RS, bool WS>
+static void run_rw(float4* a, float4* b, int n_images, int cus, double bytes)
+{
+  auto k = k_rw<C, THREADS, RS, WS>;
+  int per_cu = 0;
+  CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k, THREADS, 0));
+  int grid = per_cu * cus;
+  // read from one buffer, write to the other (out of place)
+  float ms = time_ms([&] { hipLaunchKernelGGL(k, dim3(grid), dim3(THREADS), 0, 0, a, b, b, a, n_images); }, 10);
+  std::printf("rw C=%2d thr=%4d read=%s write=%s : %7.3f ms  %7.1f GB/s\n", C, THREADS,
+              RS ? "strided " : "contig  ", WS ? "strided " : "contig  ", ms, bytes / ms / 1e6);
+}
+
+// Pass-2 pattern of the column-first design: intermediate blocked [img][xb][y][B] (B texels wide),
+// a workgroup handles RPW consecutive rows of one image (T=N/16 threads per row, 16 texels per
+// thread at x = i + m*T); reads from the blocked layout, writes the row-major image contiguous.
+template <int B, int RPW>
+__global__ __launch_bounds__(256 * RPW) void k_pass2pat(const float4* inter, float4* out, int n_images)
+{
+  constexpr int T = N / 16;
+  const int r = threadIdx.x / T, i = threadIdx.x % T;
+  const int total = n_images * (N / RPW);
+  for (int item = blockIdx.x; item < total; item += gridDim.x)
+  {
+    const int img = item / (N / RPW), y = (item % (N / RPW)) * RPW + opaque(r);
+    const int ii = opaque(i);
+    const float4* src = inter + ((size_t)img << (2 * LOGN));
+    float4 v[16];
+#pragma unroll
+    for (int m = 0; m < 16; m++)
+    {
+      const int x = ii + m * T;  // m*T multiple of B
+      v[m] = ld4(src + (size_t)(m * T / B) * N * B, (((ii / B) * N + y) * B + (ii % B)) * 16);
+    }
+    float4* dst = out + ((size_t)img << (2 * LOGN)) + ((size_t)y << LOGN);
+#pragma unroll
+    for (int m = 0; m < 16; m++)
+    {
+      v[m].x += 1.0f;
+      st4(dst + m * T, ii * 16, v[m]);
+    }
+  }
+}
+
+// Same, lanes mapped (b, r) fastest: 8 lanes read one B*RPW*16-byte chunk [xb][y..y+RPW-1][0..B-1].
+template <int B, int RPW>
+__global__ __launch_bounds__(256 * RPW) void k_pass2il(const float4* inter, float4* out, int n_images)
+{
+  constexpr int T = N / 16;
+  const int t = threadIdx.x;
+  const int b = t % B, r = (t / B) % RPW, ihi = t / (B * RPW);
+  const int i = ihi * B + b;
+  const int total = n_images * (N / RPW);
+  for (int item = blockIdx.x; item < total; item += gridDim.x)
+  {
+    const int img = item / (N / RPW), y0 = (item % (N / RPW)) * RPW;
+    const int ii = opaque(i), rr = opaque(r);
+    const float4* src = inter + ((size_t)img << (2 * LOGN));
+    float4 v[16];
+#pragma unroll
+    for (int m = 0; m < 16; m++)
+      v[m] = ld4(src + (size_t)(m * T / B) * N * B, (((ii / B) * N + y0 + rr) * B + (ii % B)) * 16);
+    float4* dst = out + ((size_t)img << (2 * LOGN)) + ((size_t)y0 << LOGN);
+#pragma unroll
+    for (int m = 0; m < 16; m++)
+    {
+      v[m].x += 1.0f;
+      st4(dst + m * T, ((rr << LOGN) + ii) * 16, v[m]);
+    }
+  }
+}
+
+// Interleaved (b, r, ihi) reads as above, but stores remapped so each wave writes 64 consecutive
+// texels of one row (what a final LDS re-distribution would give).
+template <int B, int RPW>
+__global__ __launch_bounds__(256 * RPW) void k_pass2il_cw(const float4* inter, float4* out, int n_images)
+{
+  constexpr int T = N / 16;
+  const int t = threadIdx.x;
+  const int b = t % B, r = (t / B) % RPW, ihi = t / (B * RPW);
+  const int i = ihi * B + b;
+  const int wr = t / T, wi = t % T;  // store mapping: row wr, position wi (i-fastest)
+  const int total = n_images * (N / RPW);
+  for (int item = blockIdx.x; item < total; item += gridDim.x)
+  {
+    const int img = item / (N / RPW), y0 = (item % (N / RPW)) * RPW;
+    const int ii = opaque(i), rr = opaque(r);
+    const float4* src = inter + ((size_t)img << (2 * LOGN));
+    float4 v[16];
+#pragma unroll
+    for (int m = 0; m < 16; m++)
+      v[m] = ld4(src + (size_t)(m * T / B) * N * B, (((ii / B) * N + y0 + rr) * B + (ii % B)) * 16);
+    float4* dst = out + ((size_t)img << (2 * LOGN)) + ((size_t)y0 << LOGN);
+    const int woff = ((opaque(wr) << LOGN) + opaque(wi)) * 16;
+#pragma unroll
+    for (int m = 0; m < 16; m++)
+    {
+      v[m].x += 1.0f;
+      st4(dst + m * T, woff, v[m]);
+    }
+  }
+}
+
+template <int B, int RPW>
+static void run_pass2il_cw(float4* a, float4* b, int n_images, int cus, double bytes)
+{
+  auto k = k_pass2il_cw<B, RPW>;
+  int per_cu = 0;
+  CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k, 256 * RPW, 0));
+  int grid = per_cu * cus;
+  float ms = time_ms([&] { hipLaunchKernelGGL(k, dim3(grid), dim3(256 * RPW), 0, 0, a, b, n_images); }, 10);
+  std::printf("pass2 interleaved-read contig-write B=%d rows/wg=%d blocks/CU=%d: %7.3f ms  %7.1f GB/s\n", B, RPW,
+              per_cu, ms, bytes / ms / 1e6);
+}
+
+template <int B, int RPW>
+static void run_pass2il(float4* a, float4* b, int n_images, int cus, double bytes)
+{
+  auto k = k_pass2il<B, RPW>;
+  int per_cu = 0;
+  CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k, 256 * RPW, 0));
+  int grid = per_cu * cus;
+  float ms = time_ms([&] { hipLaunchKernelGGL(k, dim3(grid), dim3(256 * RPW), 0, 0, a, b, n_images); }, 10);
+  std::printf("pass2 interleaved B=%d rows/wg=%d (chunk %3d B) blocks/CU=%d: %7.3f ms  %7.1f GB/s\n", B, RPW,
+              B * RPW * 16, per_cu, ms, bytes / ms / 1e6);
+}
+
+template <int B, int RPW>
+static void run_pass2(float4* a, float4* b, int n_images, int cus, double bytes)
+{
+  auto k = k_pass2pat<B, RPW>;
+  int per_cu = 0;
+  CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k, 256 * RPW, 0));
+  int grid = per_cu * cus;
+  float ms = time_ms([&] { hipLaunchKernelGGL(k, dim3(grid), dim3(256 * RPW), 0, 0, a, b, n_images); }, 10);
+  std::printf("pass2 pattern B=%d rows/wg=%d (read %3d B chunks) blocks/CU=%d: %7.3f ms  %7.1f GB/s\n", B, RPW,
+              B * RPW * 16, per_cu, ms, bytes / ms / 1e6);
+}
+
+// The production column kernel body with global traffic removed (compute + LDS only).
+template <bool FOAM>
+__global__ __launch_bounds__(1024) void k_cols_compute_only(int n_images, float4* images, const float2* tw_glob)
+{
+  using S = FftShape<LOGN>;
+  using K = ColCfg<LOGN>;
+  constexpr int T = S::T, C = K::C;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  float2* tw = reinterpret_cast<float2*>(smem);
+  void* xch = smem + ((S::TW_ENTRIES * 8 + 15) / 16) * 16;
+  load_twiddles<LOGN>(tw, tw_glob);
+  const int c0 = threadIdx.x % C, i0 = threadIdx.x / C;
+  const int total = n_images * K::STRIPS;
+  for (int item = blockIdx.x; item < total; item += gridDim.x)
+  {
+    const int c = opaque(c0), i = opaque(i0);
+    float4 v[16];
+#pragma unroll
+    for (int m = 0; m < 16; m++)
+      v[m] = make_float4((float)(m + item), (float)i, (float)c, 1.0f);
+    fft_run<LOGN, C, true>(v, i, c, xch, tw);
+#pragma unroll
+    for (int m = 0; m < 16; m++)
+      asm volatile("" ::"v"(v[m].x), "v"(v[m].y), "v"(v[m].z), "v"(v[m].w));
+  }
+}
+
+template <typename F>
+static float time_ms(F&& launch, int reps)
+{
+  hipEvent_t a, b;
+  CHECK(hipEventCreate(&a));
+  CHECK(hipEventCreate(&b));
+  launch();
+  CHECK(hipDeviceSynchronize());
+  CHECK(hipEventRecord(a));
+  for (int r = 0; r < reps; r++)
+    launch();
+  CHECK(hipEventRecord(b));
+  CHECK(hipEventSynchronize(b));
+  float ms;
+  CHECK(hipEventElapsedTime(&ms, a, b));
+  return ms / reps;
+}
+
+template <int C, int THREADS, bool PAIR>
+static void run_colpat(float4* d, int n_images, int cus, double bytes)
+{
+  auto k = k_colpat<C, THREADS, PAIR>;
+  int per_cu = 0;
+  CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k, THREADS, 0));
+  int grid = per_cu * cus;
+  float ms = time_ms([&] { hipLaunchKernelGGL(k, dim3(grid), dim3(THREADS), 0, 0, d, n_images); }, 10);
+  std::printf("colpat C=%2d (%3d B seg) threads=%4d pair=%d blocks/CU=%d : %7.3f ms  %7.1f GB/s\n", C, C * 16,
+              THREADS, (int)PAIR, per_cu, ms, bytes / ms / 1e6);
+}
+
+int main()
+{
+  int cus = 0;
+  CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0));
+  const int n_images = 8;
+  const size_t texels = (size_t)N * N * n_images;
+  float4* d;
+  CHECK(hipMalloc(&d, texels * sizeof(float4)));
+  CHECK(hipMemset(d, 0, texels * sizeof(float4)));
+  const double bytes = 2.0 * texels * sizeof(float4);  // read + write
+
+  {
+    int grid = cus * 8;
+    float ms = time_ms([&] { hipLaunchKernelGGL(k_rowcopy, dim3(grid), dim3(256), 0, 0, d, (long)texels); }, 10);
+    std::printf("rowcopy (contiguous)                              : %7.3f ms  %7.1f GB/s\n", ms, bytes / ms / 1e6);
+  }
+  {
+    float4* d2;
+    CHECK(hipMalloc(&d2, texels * sizeof(float4)));
+    CHECK(hipMemset(d2, 0, texels * sizeof(float4)));
+    // RS/WS combos; note k_rw(a, b, b, a): RS reads a, !RS reads b; WS writes a, !WS writes b
+    run_rw<4, 1024, true, false>(d, d2, n_images, cus, bytes);
+    run_rw<4, 1024, false, true>(d2, d, n_images, cus, bytes);
+    run_rw<4, 1024, false, false>(d, d2, n_images, cus, bytes);
+    run_rw<4, 256, true, false>(d, d2, n_images, cus, bytes);
+    run_rw<4, 256, false, true>(d2, d, n_images, cus, bytes);
+    run_rw<4, 256, false, false>(d, d2, n_images, cus, bytes);
+    run_rw<8, 256, true, false>(d, d2, n_images, cus, bytes);
+    run_rw<8, 256, false, true>(d2, d, n_images, cus, bytes);
+    run_rw<2, 256, true, false>(d, d2, n_images, cus, bytes);
+    run_rw<2, 256, false, true>(d2, d, n_images, cus, bytes);
+    run_rw<16, 256, false, false>(d, d2, n_images, cus, bytes);
+    run_rw<2, 512, false, false>(d, d2, n_images, cus, bytes);
+    run_pass2il<4, 4>(d, d2, n_images, cus, bytes);
+    run_pass2il_cw<4, 4>(d, d2, n_images, cus, bytes);
+    run_pass2il_cw<4, 2>(d, d2, n_images, cus, bytes);
+    run_pass2il_cw<2, 4>(d, d2, n_images, cus, bytes);
+    run_pass2il<2, 4>(d, d2, n_images, cus, bytes);
+    run_pass2il<2, 2>(d, d2, n_images, cus, bytes);
+    run_pass2il<4, 2>(d, d2, n_images, cus, bytes);
+    run_pass2il<2, 1>(d, d2, n_images, cus, bytes);
+    run_pass2<2, 4>(d, d2, n_images, cus, bytes);
+    run_pass2<2, 2>(d, d2, n_images, cus, bytes);
+    run_pass2<2, 1>(d, d2, n_images, cus, bytes);
+    run_pass2<4, 2>(d, d2, n_images, cus, bytes);
+    run_pass2<4, 4>(d, d2, n_images, cus, bytes);
+    run_pass2<8, 1>(d, d2, n_images, cus, bytes);
+    run_pass2<8, 2>(d, d2, n_images, cus, bytes);
+    CHECK(hipFree(d2));
+  }
+  run_colpat<4, 1024, true>(d, n_images, cus, bytes);
+  run_colpat<4, 1024, false>(d, n_images, cus, bytes);
+  run_colpat<4, 256, true>(d, n_images, cus, bytes);
+  run_colpat<4, 256, false>(d, n_images, cus, bytes);
+  run_colpat<8, 1024, true>(d, n_images, cus, bytes);
+  run_colpat<8, 1024, false>(d, n_images, cus, bytes);
+  run_colpat<8, 256, false>(d, n_images, cus, bytes);
+  run_colpat<16, 1024, false>(d, n_images, cus, bytes);
+  run_colpat<16, 256, false>(d, n_images, cus, bytes);
+  run_colpat<32, 1024, false>(d, n_images, cus, bytes);
+
+  // compute-only column kernel
+  {
+    std::vector<float2> tab(FftShape<LOGN>::TW_ENTRIES, make_float2(1.0f, 0.0f));
+    float2* tw;
+    CHECK(hipMalloc(&tw, tab.size() * sizeof(float2)));
+    CHECK(hipMemcpy(tw, tab.data(), tab.size() * sizeof(float2), hipMemcpyHostToDevice));
+    int lds = ((FftShape<LOGN>::TW_ENTRIES * 8 + 15) / 16) * 16 + ColCfg<LOGN>::LDS_BYTES;
+    auto k = k_cols_compute_only<false>;
+    CHECK(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, lds));
+    float ms = time_ms([&] { hipLaunchKernelGGL(k, dim3(cus), dim3(1024), lds, 0, n_images, d, tw); }, 10);
+    std::printf("column kernel compute+LDS only (no HBM)           : %7.3f ms\n", ms);
+    // production column kernel for comparison
+    FoamParams fp{};
+    ms = time_ms([&] { (void)launch_cols(LOGN, n_images, d, tw, 0, cus); }, 10);
+    std::printf("column kernel (production, no foam)               : %7.3f ms  %7.1f GB/s\n", ms, bytes / ms / 1e6);
+    ms = time_ms([&] { (void)launch_rows_ifft(LOGN, n_images, d, tw, 0, cus); }, 10);
+    std::printf("row ifft kernel (production)                      : %7.3f ms  %7.1f GB/s\n", ms, bytes / ms / 1e6);
+  }
+  CHECK(hipFree(d));
+  return 0;
+}

@@ -1,0 +1,120 @@
+// genbench.hip — interleaved A/B timing of the generator frame passes (8 cascades x 4096^2).
+// Build: see Makefile target `microbench`.
+#include "../../oceansimulation_amd/csrc/ocean_kernels.hip"
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+
+using namespace oceanfft;
+
+#define CHECK(x)                                                                                   \
+  do                                                                                               \
+  {                                                                                                \
+    hipError_t e = (x);                                                                            \
+    if (e != hipSuccess)                                                                           \
+    {                                                                                              \
+      std::printf("HIP error %s at %s:%d\n", hipGetErrorString(e), __FILE__, __LINE__);            \
+      std::exit(1);                                                                                \
+    }                                                                                              \
+  } while (0)
+
+template <typename F>
+static float time_ms(F&& launch, int reps)
+{
+  hipEvent_t a, b;
+  CHECK(hipEventCreate(&a));
+  CHECK(hipEventCreate(&b));
+  CHECK(hipEventRecord(a));
+  for (int r = 0; r < reps; r++)
+    CHECK(launch());
+  CHECK(hipEventRecord(b));
+  CHECK(hipEventSynchronize(b));
+  float ms;
+  CHECK(hipEventElapsedTime(&ms, a, b));
+  CHECK(hipEventDestroy(a));
+  CHECK(hipEventDestroy(b));
+  return ms / reps;
+}
+
+int main(int argc, char** argv)
+{
+  const int logn = argc > 1 ? std::atoi(argv[1]) : 12;
+  const int C = argc > 2 ? std::atoi(argv[2]) : 8;
+  const int n = 1 << logn;
+  int cus = 0;
+  CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0));
+  const size_t tex = (size_t)n * n;
+  float4 *h0, *inter, *maps;
+  float* jac;
+  float2* tw;
+  CHECK(hipMalloc(&h0, tex * C * sizeof(float4)));
+  CHECK(hipMalloc(&inter, tex * C * 2 * sizeof(float4)));
+  CHECK(hipMalloc(&maps, tex * C * 2 * sizeof(float4)));
+  CHECK(hipMalloc(&jac, tex * C * sizeof(float)));
+  int lb = logn / 2, tb = 1 << lb, ta = 1 << (logn - lb);
+  std::vector<float2> tab(tb + ta);
+  for (int e = 0; e < tb; e++)
+    tab[e] = make_float2((float)std::cos(2 * M_PI * e / n), (float)std::sin(2 * M_PI * e / n));
+  for (int e = 0; e < ta; e++)
+    tab[tb + e] = make_float2((float)std::cos(2 * M_PI * e * tb / n), (float)std::sin(2 * M_PI * e * tb / n));
+  CHECK(hipMalloc(&tw, tab.size() * sizeof(float2)));
+  CHECK(hipMemcpy(tw, tab.data(), tab.size() * sizeof(float2), hipMemcpyHostToDevice));
+
+  static const float planes[] = {5, 17, 101, 251, 509, 1021, 2039, 4093};
+  FrameParams fp{};
+  FoamParams foam{};
+  fp.cascades = C;
+  for (int c = 0; c < C; c++)
+  {
+    OceanSettings s{};
+    s.seed[0] = 12342;
+    s.seed[1] = 8934;
+    s.U_10 = 40;
+    s.theta_0 = 25;
+    s.F = 800000;
+    s.g = 9.8f;
+    s.swell = 0.5f;
+    s.h = 100;
+    s.displacement = 0.4f;
+    s.planeSize = planes[c % 8];
+    s.scale = 1;
+    s.spread = 0.2f;
+    CHECK(launch_generate_spectrum(s, n, h0 + tex * c, 0, cus));
+    fp.c[c] = {2.0f * 3.14159265358f / s.planeSize, 1.0f, s.g, s.h};
+    foam.displacement[c] = s.displacement;
+  }
+  CHECK(hipDeviceSynchronize());
+  const double pts = (double)tex * C;
+  auto p1r = [&] { return launch_cols_evolve(logn, fp, h0, inter, tw, 0, cus, false); };
+  auto p1k = [&] { return launch_cols_evolve(logn, fp, h0, inter, tw, 0, cus, true); };
+  auto p2 = [&] { return launch_rows_final(logn, C, inter, maps, jac, foam, tw, 0, cus); };
+  auto frame = [&] {
+    hipError_t e = p1r();
+    return e == hipSuccess ? p2() : e;
+  };
+  p1r(); p1k(); p2();
+  CHECK(hipDeviceSynchronize());
+  const int rounds = 7, reps = 10;
+  std::vector<float> t1r, t1k, t2, tf;
+  for (int r = 0; r < rounds; r++)
+  {
+    t1r.push_back(time_ms(p1r, reps));
+    t1k.push_back(time_ms(p1k, reps));
+    t2.push_back(time_ms(p2, reps));
+    tf.push_back(time_ms(frame, reps));
+  }
+  auto report = [&](const char* name, std::vector<float>& v, double bytes_per_pt) {
+    std::sort(v.begin(), v.end());
+    std::printf("%-34s median %7.3f ms  min %7.3f ms  %7.1f GB/s (algorithmic %.0f B/pt)\n", name, v[v.size() / 2],
+                v[0], bytes_per_pt * pts / v[v.size() / 2] / 1e6, bytes_per_pt);
+  };
+  std::printf("N=%d cascades=%d CUs=%d\n", n, C, cus);
+  report("pass1 cols_evolve (re-read h0)", t1r, 48);
+  report("pass1 cols_evolve (keep H)", t1k, 48);
+  report("pass2 rows_final", t2, 68);
+  report("frame (pass1 re-read + pass2)", tf, 116);
+  return 0;
+}

@@ -373,7 +373,7 @@ int ocean_generator_calculate(ocean_generator* g, float timestep, int update_spe
     foam.displacement[c] = s.displacement;
   }
   // pass 1: prepareFFT fused with the y direction of both EncodeIFFTs (src/Generator.cpp:63-72)
-  HIP_TRY(timed(g, 1, [&] { return launch_cols_evolve(f->logn, fp, g->h0, g->inter, f->twiddles, f->stream, f->cus, true); }),
+  HIP_TRY(timed(g, 1, [&] { return launch_cols_evolve(f->logn, fp, g->h0, g->inter, f->twiddles, f->stream, f->cus, default_keep(f->logn)); }),
           "column pass");
   // pass 2: the x direction of both EncodeIFFTs + computeFoam (src/Generator.cpp:71-80)
   HIP_TRY(timed(g, 2, [&] {

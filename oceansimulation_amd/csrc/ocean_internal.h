@@ -57,8 +57,10 @@ int spectrum_block(int logn);
 hipError_t launch_generate_spectrum(const OceanSettings& s, int n, float4* h0, hipStream_t stream, int cus);
 hipError_t launch_hash(const uint32_t* xy, int count, uint32_t* raw, float2* uv, hipStream_t stream);
 // Generator frame: pass 1 (evolve + y iFFT, blocked intermediate), pass 2 (x iFFT + maps + Jacobian).
+// keep: evolved amplitudes kept live between the two packed images (0, 8 or 16; see the kernel).
 hipError_t launch_cols_evolve(int logn, const FrameParams& fp, const float4* h0, float4* inter, const float2* tw,
-                              hipStream_t stream, int cus, bool keep_h = false);
+                              hipStream_t stream, int cus, int keep);
+int default_keep(int logn);
 hipError_t launch_rows_final(int logn, int cascades, const float4* inter, float4* maps, float* jac,
                              const FoamParams& foam, const float2* tw, hipStream_t stream, int cus);
 // EncodeIFFT on row-major images, in place: row pass then column pass.

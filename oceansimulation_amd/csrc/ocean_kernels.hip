@@ -822,10 +822,11 @@ struct ColFirstCfg
   static constexpr int LDS2 = lds_row_slots<LOGN>(RPW2) * 8;
 };
 
-// KEEP_H: evolve once and keep H (32 VGPRs) live across both transforms; otherwise re-read the
-// strip's h0 for the second image (a re-read of bytes streamed microseconds earlier) and evolve
-// again, which keeps the 1024-thread workgroup within 128 VGPRs without spills.
-template <int LOGN, bool KEEP_H>
+// KEEP: how many of the thread's 16 evolved amplitudes H (2 VGPRs each) stay live from the first
+// packed image to the second; the rest are re-read from h0 (bytes this workgroup streamed a few
+// microseconds earlier) and evolved again. KEEP = 16 does not fit the 128 VGPRs of a 1024-thread
+// workgroup at N = 4096 (spills, which cost HBM traffic); KEEP = 8 does.
+template <int LOGN, int KEEP>
 __global__ __launch_bounds__(ColFirstCfg<LOGN>::WG1) void k_cols_evolve(
     FrameParams fp, const float4* __restrict__ h0, float4* __restrict__ inter, const float2* __restrict__ tw_glob)
 {
@@ -838,54 +839,42 @@ __global__ __launch_bounds__(ColFirstCfg<LOGN>::WG1) void k_cols_evolve(
   void* xch = smem + ((S::TW_ENTRIES * 8 + 15) / 16) * 16;
   load_twiddles<LOGN>(tw, tw_glob);
 
-  const int b0 = threadIdx.x % B, i0 = (threadIdx.x / B) % T, sl0 = threadIdx.x / (B * T);
   const int total = fp.cascades * GROUPS;
   const float dim = (float)N;
   for (int item = blockIdx.x; item < total; item += gridDim.x)
   {
-    const int b = opaque(b0), sl = SPW == 1 ? 0 : opaque(sl0);
+    // thread coordinates re-derived from one opaque copy of threadIdx.x (fewer live VGPRs)
+    const int tid = opaque((int)threadIdx.x);
+    const int b = tid % B, sl = SPW == 1 ? 0 : tid / (B * T);
     const int c = item / GROUPS, xb0 = (item - c * GROUPS) * SPW;
     const CascadeFrame f = fp.c[c];
     // this item's SPW strips are one contiguous run of SPW*N*B texels
-    const size_t run = ((size_t)c * (N / B) + xb0) * N * B;
-    const float4* src = h0 + run;
+    const float4* src = h0 + ((size_t)c * (N / B) + xb0) * N * B;
     const int x = (xb0 + sl) * B + b;
-
-    float2 H[KEEP_H ? 16 : 1];
-    if constexpr (KEEP_H)
-    {
-      const int i = opaque(i0);
-      const int voff = ((sl * N + i) * B + b) * 16;
-      float4 raw[16];
-#pragma unroll
-      for (int m = 0; m < 16; m++)
-        raw[m] = ld4(src + ((m + 8) & 15) * T * B, voff);  // fftShift on y folded into the load
-#pragma unroll
-      for (int m = 0; m < 16; m++)
-      {
-        const int y = i + ((m + 8) & 15) * T;
-        KVec q = make_kvec(x, y, dim, f.dk);
-        H[m] = evolve(raw[m], q.k, f);
-      }
-    }
+    float2 H[KEEP > 0 ? KEEP : 1];
 #pragma unroll 1
     for (int img = 0; img < 2; img++)
     {
-      const int i = opaque(i0);  // keep the k-vector math inside this loop (see opaque())
+      // keep the k-vector math inside this iteration (see opaque())
+      const int i = (opaque((int)threadIdx.x) / B) % T;
       const int voff = ((sl * N + i) * B + b) * 16;
       float4 v[16];
-      if constexpr (!KEEP_H)
-      {
 #pragma unroll
-        for (int m = 0; m < 16; m++)
+      for (int m = 0; m < 16; m++)
+        if (img == 0 || m >= KEEP)
           v[m] = ld4(src + ((m + 8) & 15) * T * B, voff);  // fftShift on y folded into the load
-      }
 #pragma unroll
       for (int m = 0; m < 16; m++)
       {
         const int y = i + ((m + 8) & 15) * T;
         KVec q = make_kvec(x, y, dim, f.dk);
-        const float2 Hm = KEEP_H ? H[m] : evolve(v[m], q.k, f);
+        float2 Hm;
+        if (img == 1 && m < KEEP)
+          Hm = H[m];
+        else
+          Hm = evolve(v[m], q.k, f);
+        if (img == 0 && m < KEEP)
+          H[m] = Hm;
         v[m] = img == 0 ? pack_height(Hm, q) : pack_displacement(Hm, q);
       }
       fft_run<LOGN, K::C1, true>(v, i, sl * B + b, xch, tw);
@@ -1048,13 +1037,13 @@ hipError_t launch_hash(const uint32_t* xy, int count, uint32_t* raw, float2* uv,
 }
 
 hipError_t launch_cols_evolve(int logn, const FrameParams& fp, const float4* h0, float4* inter, const float2* tw,
-                              hipStream_t stream, int cus, bool keep_h)
+                              hipStream_t stream, int cus, int keep)
 {
   return with_logn(logn, [&](auto L) -> hipError_t {
     constexpr int LOGN = decltype(L)::value;
     using K = ColFirstCfg<LOGN>;
     using S = FftShape<LOGN>;
-    auto kern = keep_h ? k_cols_evolve<LOGN, true> : k_cols_evolve<LOGN, false>;
+    auto kern = keep >= 16 ? k_cols_evolve<LOGN, 16> : (keep >= 8 ? k_cols_evolve<LOGN, 8> : k_cols_evolve<LOGN, 0>);
     const int lds = ((S::TW_ENTRIES * 8 + 15) / 16) * 16 + K::LDS1;
     const int items = fp.cascades * ((S::N / K::B) / K::SPW);
     const int grid = persistent_grid(kern, K::WG1, lds, items, cus);
@@ -1062,6 +1051,9 @@ hipError_t launch_cols_evolve(int logn, const FrameParams& fp, const float4* h0,
     return hipGetLastError();
   });
 }
+
+// The largest H-retention that compiles without spills for this size (see k_cols_evolve).
+int default_keep(int logn) { return logn >= 12 ? 8 : 16; }
 
 hipError_t launch_rows_final(int logn, int cascades, const float4* inter, float4* maps, float* jac,
                              const FoamParams& foam, const float2* tw, hipStream_t stream, int cus)

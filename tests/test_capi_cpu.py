@@ -1,0 +1,113 @@
+"""The C ABI library without a GPU: it loads, exports exactly what include/oceanfft.h declares,
+the settings layout matches, and every compute entry point fails loudly (no CPU fallback)."""
+import ctypes
+import os
+import re
+import subprocess
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "oceanfft.h")
+
+
+def _declared_functions():
+    text = open(HEADER).read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return sorted(set(re.findall(r"\b(ocean_[a-z0-9_]+)\s*\(", text)))
+
+
+@pytest.fixture(scope="module")
+def capi():
+    from oceansimulation_amd import capi
+
+    capi.lib()
+    return capi
+
+
+def test_every_declared_symbol_is_exported_and_bound(capi):
+    names = _declared_functions()
+    assert len(names) >= 20
+    for name in names:
+        assert hasattr(capi.lib(), name), f"{name} declared in oceanfft.h but not exported"
+        assert name in capi.SIGNATURES, f"{name} not bound in oceansimulation_amd/capi.py"
+    assert set(capi.SIGNATURES) == set(names)
+
+
+def test_settings_layout_matches_header(capi):
+    text = open(HEADER).read()
+    body = text[text.index("typedef struct ocean_settings"):text.index("} ocean_settings;")]
+    fields = re.findall(r"^\s*(?:int32_t|float)\s+(\w+)(?:\[2\])?;", body, flags=re.M)
+    assert fields == [f[0] for f in capi.OceanSettings._fields_]
+    assert ctypes.sizeof(capi.OceanSettings) == 64
+    offs = {f[0]: getattr(capi.OceanSettings, f[0]).offset for f in capi.OceanSettings._fields_}
+    assert offs["U_10"] == 8 and offs["time"] == 36 and offs["wavelengthMax"] == 60
+
+
+def test_default_settings_are_the_reference_defaults(capi):
+    s = capi.OceanSettings()
+    capi.lib().ocean_default_settings(ctypes.byref(s))
+    # src/Generator.h:14-29
+    assert (s.seed[0], s.seed[1]) == (12342, 8934)
+    exp = dict(U_10=40.0, theta_0=25.0, F=800000.0, g=9.8, swell=0.5, h=100.0, displacement=0.4, time=0.0,
+               planeSize=40.0, scale=1.0, spread=0.2, boundWavelength=0, wavelengthMin=0.0, wavelengthMax=0.0)
+    for k, v in exp.items():
+        assert getattr(s, k) == pytest.approx(v, rel=0, abs=1e-6), k
+
+
+def test_invalid_arguments_fail_without_touching_a_device(capi):
+    L = capi.lib()
+    h = ctypes.c_void_p()
+    for bad in (0, 8, 300, 1000, 32768, 1 << 20):
+        assert L.ocean_fft_create(ctypes.byref(h), bad, None) == capi.OCEAN_ERR_INVALID
+        assert b"power of two" in L.ocean_last_error()
+    assert L.ocean_fft_create(None, 256, None) == capi.OCEAN_ERR_INVALID
+    assert L.ocean_fft_encode_ifft(None, None) == capi.OCEAN_ERR_INVALID
+    assert L.ocean_generator_calculate(None, ctypes.c_float(0.1), 0) == capi.OCEAN_ERR_INVALID
+    assert L.ocean_generator_create(ctypes.byref(h), None, 1) == capi.OCEAN_ERR_INVALID
+    assert L.ocean_generator_height_map(None, 0) is None
+    assert L.ocean_fft_texture_resolution(None) == 0
+    assert L.ocean_debug_hash(None, 4, None, None, None) == capi.OCEAN_ERR_INVALID
+
+
+def test_no_cpu_fallback_without_gpu(capi):
+    L = capi.lib()
+    if L.ocean_device_count() > 0:
+        pytest.skip("a GPU is visible; covered by the gpu tests")
+    h = ctypes.c_void_p()
+    assert L.ocean_fft_create(ctypes.byref(h), 256, None) == capi.OCEAN_ERR_NO_DEVICE
+    import oceansimulation_amd as ocean
+
+    with pytest.raises(ocean.OceanError):
+        ocean.FFTCalculator(256)
+
+
+def test_cpp_dropin_library_exports_reference_signatures():
+    so = os.path.join(ROOT, "oceansimulation_amd", "libwaves.so")
+    assert os.path.exists(so), "run make"
+    syms = subprocess.run(["nm", "-DC", "--defined-only", so], capture_output=True, text=True).stdout
+    for sig in ["Waves::FFTCalculator::FFTCalculator(Vision::RenderDevice*, unsigned long)",
+                "Waves::FFTCalculator::EncodeIFFT(unsigned int)",
+                "Waves::Generator::Generator(Vision::RenderDevice*, Waves::FFTCalculator*)",
+                "Waves::Generator::CalculateOcean(float, bool)",
+                "Waves::Generator::GetOceanSettings()",
+                "Waves::Generator::LoadShaders(bool)"]:
+        assert sig in syms, sig
+
+
+def test_cpp_headers_compile_standalone(tmp_path):
+    """A Renderer-style consumer compiles against the drop-in headers unchanged."""
+    src = tmp_path / "consumer.cpp"
+    src.write_text(
+        '#include "waves/Generator.h"\n'
+        "#include <vector>\n"
+        "void render(Vision::RenderDevice* d, std::vector<Waves::Generator*>& gens) {\n"
+        "  for (size_t i = 0; i < gens.size(); i++) {\n"
+        "    Vision::ID h = gens[i]->GetHeightMap(), dm = gens[i]->GetDisplacementMap(), j = gens[i]->GetJacobianMap();\n"
+        "    float plane = gens[i]->GetOceanSettings().planeSize, disp = gens[i]->GetOceanSettings().displacement;\n"
+        "    (void)d->GetTexturePointer(h); (void)dm; (void)j; (void)plane; (void)disp;\n"
+        "  }\n"
+        "}\n")
+    r = subprocess.run(["g++", "-std=c++17", "-fsyntax-only", f"-I{ROOT}/include", "-I/opt/rocm/include",
+                        "-D__HIP_PLATFORM_AMD__", str(src)], capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr

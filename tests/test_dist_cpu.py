@@ -1,0 +1,58 @@
+"""bench.py's multi-rank plumbing on CPU: world_size 2 over gloo (127.0.0.1). Each rank runs the same
+barrier + max-over-ranks protocol the GPU bench uses; the aggregate must be whole-job throughput."""
+import importlib.util
+import os
+import socket
+
+import pytest
+import torch.multiprocessing as mp
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    spec = importlib.util.spec_from_file_location("bench", os.path.join(ROOT, "bench.py"))
+    b = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(b)
+    r, w, _ = b.dist_setup()
+    assert (r, w) == (rank, world)
+    b.barrier(w)
+    local_elapsed = 1.0 + rank  # rank 1 is the slow one
+    el_max = b.max_over_ranks(local_elapsed, w)
+    # per-rank disjoint work: cascades owned by this rank
+    owned = [(b.cascade_settings(r, c)["planeSize"],) + tuple(b.cascade_settings(r, c)["seed"]) for c in range(8)]
+    import torch.distributed as dist
+
+    gathered = [None] * w
+    dist.all_gather_object(gathered, owned)
+    b.barrier(w)
+    dist.destroy_process_group()
+    q.put((rank, el_max, gathered))
+
+
+@pytest.mark.timeout(120)
+def test_world2_max_over_ranks_and_disjoint_cascades():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=100) for _ in procs]
+    for p in procs:
+        p.join(timeout=30)
+        assert p.exitcode == 0
+    for rank, el_max, gathered in res:
+        assert el_max == 2.0  # max over ranks, not rank-local time
+        flat = [tuple(k) for ranks in gathered for k in ranks]
+        assert len(set(flat)) == len(flat)  # no cascade computed twice across ranks

@@ -256,3 +256,23 @@ def test_cpp_dropin_binary():
     r = subprocess.run([exe, "256", "3"], capture_output=True, text=True, timeout=300)
     print(r.stdout)
     assert r.returncode == 0, r.stdout + r.stderr
+
+
+# ---- committed golden vectors (tests/golden/make_golden.py) ---------------------------------
+def test_golden_fixtures_gpu(ocean):
+    import json
+
+    gdir = os.path.join(ROOT, "tests", "golden")
+    z = np.load(os.path.join(gdir, "ocean_golden.npz"))
+    manifest = json.load(open(os.path.join(gdir, "manifest.json")))
+    for name, case in manifest["cases"].items():
+        fft = ocean.FFTCalculator(case["n"])
+        gen = ocean.Generator(fft, 1)
+        ocean.apply_settings(gen.GetOceanSettings(0), **case["settings"])
+        for dt in case["timesteps"]:
+            gen.CalculateOcean(dt)
+        assert gen.GetOceanSettings(0).time == np.float32(case["final_time"])
+        assert max(lane_err(gen.initial_spectrum_host(0), z[f"{name}/h0"])) <= H0_TOL, name
+        assert max(lane_err(gen.height_map_host(0), z[f"{name}/height"])) <= FRAME_TOL, name
+        assert max(lane_err(gen.displacement_map_host(0), z[f"{name}/disp"])) <= FRAME_TOL, name
+        assert scalar_err(gen.jacobian_map_host(0) - 1.0, z[f"{name}/jac"] - 1.0) <= FRAME_TOL, name

@@ -1,0 +1,56 @@
+"""Host-side logic that needs no GPU: bench workload definition, parity metrics, Python mirror."""
+import importlib.util
+import os
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _bench():
+    spec = importlib.util.spec_from_file_location("bench", os.path.join(ROOT, "bench.py"))
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    return mod
+
+
+def test_bench_byte_accounting():
+    b = _bench()
+    assert b.PASS1_BYTES == 48 and b.PASS2_BYTES == 68 and b.FRAME_BYTES == 116
+
+
+def test_bench_cascade_sharding_is_disjoint():
+    """Every (rank, cascade) gets a distinct noise tile: seeds differ by >= 4097 > N = 4096, so
+    Hash(thread + seed) windows (spectrum.compute:153) never overlap except at the +N edge index."""
+    b = _bench()
+    seen = set()
+    for rank in range(8):
+        for c in range(16):
+            s = b.cascade_settings(rank, c)
+            key = (s["planeSize"], s["seed"])
+            assert key not in seen
+            seen.add(key)
+            assert s["seed"][0] >= 12342 and s["seed"][1] >= 8934
+    assert b.cascade_settings(0, 0)["planeSize"] == 5.0
+    assert [b.cascade_settings(0, c)["planeSize"] for c in range(3)] == [5.0, 17.0, 101.0]  # Waves.cpp:27
+
+
+def test_lane_err_metric():
+    from parity import lane_err, scalar_err
+
+    a = np.zeros((4, 4, 4), np.float32)
+    a[..., 0] = 2.0
+    b = a.copy()
+    b[0, 0, 0] += 0.002
+    e = lane_err(b, a)
+    assert abs(e[0] - 1e-3) < 1e-7 and e[1] == 0.0
+    assert abs(scalar_err(b[..., 0], a[..., 0]) - 1e-3) < 1e-7
+
+
+def test_python_mirror_settings_helpers():
+    import oceansimulation_amd as ocean
+
+    s = ocean.default_settings(planeSize=17.0, seed=(1, 2))
+    assert s.planeSize == 17.0 and (s.seed[0], s.seed[1]) == (1, 2) and s.U_10 == 40.0
+    ocean.apply_settings(s, time=2.5)
+    assert s.time == 2.5

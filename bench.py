@@ -42,6 +42,9 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="target CPU-baseline sample length")
     ap.add_argument("--no-profile", action="store_true", help="skip per-kernel HIP event timing")
+    ap.add_argument("--no-slab", action="store_true", help="skip the config-5 slab-decomposed grid")
+    ap.add_argument("--slab-n", type=int, default=16384, help="side of the single slab-decomposed grid")
+    ap.add_argument("--slab-steps", type=int, default=10)
     return ap.parse_args()
 
 
@@ -56,8 +59,11 @@ def dist_setup():
     if world > 1:
         import torch.distributed as dist
 
+        from datetime import timedelta
+
         backend = "nccl" if torch.cuda.is_available() else "gloo"
-        dist.init_process_group(backend=backend)
+        # bounded collectives: a failing optional leg must not hang the job
+        dist.init_process_group(backend=backend, timeout=timedelta(seconds=300))
     return rank, world, local
 
 
@@ -115,6 +121,63 @@ def cpu_baseline(n: int, target_s: float):
         "sample": f"1 cascade {n}x{n}, {frames} frames of CalculateOcean (fp32 radix-2 restatement of "
                   f"src/FFTCalculator.cpp + spectrum.compute, OpenMP {O.get_threads()} threads), {el:.1f} s",
     }
+
+
+def slab_grid(args, rank: int, world: int, local: int) -> dict:
+    """BASELINE configs[4]: one N x N grid (default 16384^2, full payload) split over the ranks.
+    Column pass on a column slab, one equal-split RCCL all-to-all (torch all_to_all_single on the
+    "nccl" backend), row pass on a row slab. At world == 1 the whole grid runs on one GPU with no
+    exchange — the scaling denominator."""
+    import torch
+
+    import oceansimulation_amd as ocean
+    from oceansimulation_amd.slab import SlabGenerator, TorchExchange
+
+    n = args.slab_n
+    fft = ocean.FFTCalculator(n)
+    g = SlabGenerator(fft, rank, world)
+    ex = TorchExchange(g.exchange_bytes, torch.device("cuda", local)) if world > 1 else None
+
+    def frame(dt, update=False):
+        if ex is None:
+            g.columns(dt, update)
+            g.rows_pass()
+        else:
+            g.columns(dt, update, ex.send.data_ptr())
+            ex()
+            g.rows_pass(ex.recv.data_ptr())
+
+    frame(1.0 / 60.0, update=True)  # seeds this rank's h0 column slab
+    frame(1.0 / 60.0)
+    g.set_profiling(True)
+    g.kernel_times()
+    sync()
+    barrier(world)
+    sync()
+    t0 = time.perf_counter()
+    for _ in range(args.slab_steps):
+        frame(1.0 / 60.0)
+    sync()
+    barrier(world)
+    sync()
+    el = max_over_ranks(time.perf_counter() - t0, world)
+    ms, cnt = g.kernel_times()
+    per = args.slab_steps
+    out = {
+        "config": f"single {n}x{n} grid, full payload, slab-decomposed over {world} GPU(s)",
+        "ranks": world,
+        "ms_per_frame": 1000.0 * el / per,
+        "points_per_s": float(n) * n * per / el,
+        "column_pass_ms": ms[1] / max(cnt[1], 1),
+        "row_pass_ms": ms[2] / max(cnt[2], 1),
+        "exchange_bytes_per_rank": g.exchange_bytes * (world - 1) // world if world > 1 else 0,
+    }
+    out["exchange_and_gaps_ms"] = out["ms_per_frame"] - out["column_pass_ms"] - out["row_pass_ms"]
+    g.close()
+    fft.close()
+    del ex
+    torch.cuda.empty_cache()
+    return out
 
 
 def main():
@@ -204,10 +267,15 @@ def main():
         out["kernels"]["frame_both_passes"] = {"avg_ms": p1_ms + p2_ms, "GB_per_s": frame_gbs,
                                                "frac_hbm_peak": frame_gbs / HBM_PEAK_GBS}
         out["kernels"]["h0_seed_ms"] = h0_ms
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        out["cpu_baseline"] = cpu_baseline(n, args.cpu_seconds)
     gen.close()
     fft.close()
+    if not args.no_slab:
+        try:
+            out["slab"] = slab_grid(args, rank, world, local)
+        except Exception as e:  # reported, never fatal to the headline measurement
+            out["slab"] = {"error": f"{type(e).__name__}: {e}"}
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(n, args.cpu_seconds)
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:

@@ -120,6 +120,22 @@ float* ocean_generator_jacobian_map(ocean_generator* gen, int cascade);
 float* ocean_generator_initial_spectrum(ocean_generator* gen, int cascade);
 int ocean_generator_spectrum_block(const ocean_generator* gen);
 
+/* ---- slab decomposition of one grid over several GPUs ------------------------------------- */
+/* One N x N cascade split over `ranks` GPUs (power of two <= 16), this process being `rank`: the
+ * column pass works on columns [rank*w, rank*w + w), the row pass on rows [rank*w, rank*w + w),
+ * w = N / ranks (the reference runs everything on one device). A frame is:
+ *   ocean_generator_slab_columns(gen, dt, update, send)  time += dt, h0 if needed, evolve + y iFFT
+ *   all-to-all with equal splits of ocean_generator_exchange_bytes(gen) / ranks bytes: the block at
+ *     send + q * bytes/ranks goes to rank q and arrives at recv + rank_src * bytes/ranks (RCCL)
+ *   ocean_generator_slab_rows(gen, recv)                 x iFFT + maps + Jacobian of the row slab
+ * send/recv are caller-owned device buffers (null = the generator's internal buffer, which is what
+ * ranks == 1 uses). The map getters then address the row slab: w rows x N texels, row-major. */
+int ocean_generator_create_slab(ocean_generator** out, ocean_fft* fft, int rank, int ranks);
+size_t ocean_generator_exchange_bytes(const ocean_generator* gen);
+int ocean_generator_slab_columns(ocean_generator* gen, float timestep, int update_spectrum, float* send);
+int ocean_generator_slab_rows(ocean_generator* gen, const float* recv);
+int ocean_generator_slab_info(const ocean_generator* gen, int* rank, int* ranks, int* row0, int* rows);
+
 /* ---- instrumentation (bench) ------------------------------------------------------------- */
 /* When enabled, each kernel launch of the generator is bracketed by HIP events on its stream. */
 int ocean_generator_set_profiling(ocean_generator* gen, int enable);

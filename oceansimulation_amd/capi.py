@@ -74,6 +74,11 @@ SIGNATURES = {
     "ocean_generator_jacobian_map": (_vp, [_vp, _i]),
     "ocean_generator_initial_spectrum": (_vp, [_vp, _i]),
     "ocean_generator_spectrum_block": (_i, [_vp]),
+    "ocean_generator_create_slab": (_i, [ctypes.POINTER(_vp), _vp, _i, _i]),
+    "ocean_generator_exchange_bytes": (_sz, [_vp]),
+    "ocean_generator_slab_columns": (_i, [_vp, _f, _i, _vp]),
+    "ocean_generator_slab_rows": (_i, [_vp, _vp]),
+    "ocean_generator_slab_info": (_i, [_vp, ctypes.POINTER(_i), ctypes.POINTER(_i), ctypes.POINTER(_i), ctypes.POINTER(_i)]),
     "ocean_generator_set_profiling": (_i, [_vp, _i]),
     "ocean_generator_kernel_times": (_i, [_vp, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int64)]),
     "ocean_debug_hash": (_i, [_vp, _i, _vp, _vp, _vp]),

@@ -71,12 +71,15 @@ struct ocean_generator
 {
   ocean_fft* fft = nullptr;
   int cascades = 0;
+  int rank = 0, ranks = 1;  // slab decomposition of one grid (ranks == 1: whole grids, batched)
+  SlabGeom geom{};          // this rank's column slab [x0, x0 + w) and row slab width w
   std::vector<ocean_settings> settings;
   bool update_spectrum = true;  // src/Generator.h:72
-  float4* h0 = nullptr;         // [cascade][N/B][N][B] strip-blocked (B = spectrum_block)
-  float4* inter = nullptr;      // [cascade][2][N/B][N][B] after the y pass (strip-blocked)
-  float4* maps = nullptr;       // [cascade][2][N][N]: heightMap, displacementMap (row-major)
-  float* jac = nullptr;         // [cascade][N][N]
+  float4* h0 = nullptr;         // [cascade][w/B][N][B] strip-blocked column slab (B = spectrum_block)
+  float4* inter = nullptr;      // [cascade][ranks][2][w/B][w][B] after the y pass (destination-block order)
+  float4* scratch = nullptr;    // [cascade][2][w][N] row-major, only when B == 1 (N = 16384)
+  float4* maps = nullptr;       // [cascade][2][w][N]: heightMap, displacementMap rows (row-major)
+  float* jac = nullptr;         // [cascade][w][N]
   bool profiling = false;
   std::vector<EventPair> pending;
   std::vector<hipEvent_t> pool;
@@ -251,6 +254,45 @@ extern "C" {
 // ---------------------------------------------------------------------------------------------
 // Generator
 // ---------------------------------------------------------------------------------------------
+static int generator_alloc(ocean_generator** out, ocean_fft* fft, int cascades, int rank, int ranks)
+{
+  auto* g = new ocean_generator();
+  g->fft = fft;
+  g->cascades = cascades;
+  g->rank = rank;
+  g->ranks = ranks;
+  g->geom.w = fft->n / ranks;
+  g->geom.x0 = rank * g->geom.w;
+  g->settings.resize(cascades);
+  for (auto& s : g->settings)
+    ocean_default_settings(&s);
+  const size_t slab = (size_t)fft->n * g->geom.w;  // texels per cascade image slab
+  hipError_t e = hipMalloc(&g->h0, slab * cascades * sizeof(float4));
+  if (e == hipSuccess)
+    e = hipMalloc(&g->inter, slab * cascades * 2 * sizeof(float4));
+  if (e == hipSuccess && rows_need_transpose(fft->logn))
+    e = hipMalloc(&g->scratch, slab * cascades * 2 * sizeof(float4));
+  if (e == hipSuccess)
+    e = hipMalloc(&g->maps, slab * cascades * 2 * sizeof(float4));
+  if (e == hipSuccess)
+    e = hipMalloc(&g->jac, slab * cascades * sizeof(float));
+  // Textures start zeroed like the reference's (Data = nullptr) images.
+  if (e == hipSuccess)
+    e = hipMemsetAsync(g->h0, 0, slab * cascades * sizeof(float4), fft->stream);
+  if (e == hipSuccess)
+    e = hipMemsetAsync(g->maps, 0, slab * cascades * 2 * sizeof(float4), fft->stream);
+  if (e == hipSuccess)
+    e = hipMemsetAsync(g->jac, 0, slab * cascades * sizeof(float), fft->stream);
+  if (e != hipSuccess)
+  {
+    int code = (e == hipErrorOutOfMemory) ? OCEAN_ERR_OOM : OCEAN_ERR_HIP;
+    ocean_generator_destroy(g);
+    return fail(code, std::string("generator allocation: ") + hipGetErrorString(e));
+  }
+  *out = g;
+  return OCEAN_OK;
+}
+
 int ocean_generator_create(ocean_generator** out, ocean_fft* fft, int cascades)
 {
   if (!out || !fft)
@@ -258,35 +300,23 @@ int ocean_generator_create(ocean_generator** out, ocean_fft* fft, int cascades)
   *out = nullptr;
   if (cascades < 1 || cascades > OCEAN_MAX_CASCADES)
     return fail(OCEAN_ERR_INVALID, "ocean_generator_create: cascades must be in [1, 64]");
-  auto* g = new ocean_generator();
-  g->fft = fft;
-  g->cascades = cascades;
-  g->settings.resize(cascades);
-  for (auto& s : g->settings)
-    ocean_default_settings(&s);
-  const size_t texels = (size_t)fft->n * fft->n;
-  hipError_t e = hipMalloc(&g->h0, texels * cascades * sizeof(float4));
-  if (e == hipSuccess)
-    e = hipMalloc(&g->inter, texels * cascades * 2 * sizeof(float4));
-  if (e == hipSuccess)
-    e = hipMalloc(&g->maps, texels * cascades * 2 * sizeof(float4));
-  if (e == hipSuccess)
-    e = hipMalloc(&g->jac, texels * cascades * sizeof(float));
-  // Textures start zeroed like the reference's (Data = nullptr) images.
-  if (e == hipSuccess)
-    e = hipMemsetAsync(g->h0, 0, texels * cascades * sizeof(float4), fft->stream);
-  if (e == hipSuccess)
-    e = hipMemsetAsync(g->maps, 0, texels * cascades * 2 * sizeof(float4), fft->stream);
-  if (e == hipSuccess)
-    e = hipMemsetAsync(g->jac, 0, texels * cascades * sizeof(float), fft->stream);
-  if (e != hipSuccess)
-  {
-    int code = (e == hipErrorOutOfMemory) ? OCEAN_ERR_OOM : OCEAN_ERR_HIP;
-    ocean_generator_destroy(g);
-    return fail(code, std::string("ocean_generator_create: allocation: ") + hipGetErrorString(e));
-  }
-  *out = g;
-  return OCEAN_OK;
+  return generator_alloc(out, fft, cascades, 0, 1);
+}
+
+int ocean_generator_create_slab(ocean_generator** out, ocean_fft* fft, int rank, int ranks)
+{
+  if (!out || !fft)
+    return fail(OCEAN_ERR_INVALID, "ocean_generator_create_slab: null argument");
+  *out = nullptr;
+  const int blk = spectrum_block(fft->logn);
+  if (ranks < 1 || ranks > 16 || (ranks & (ranks - 1)) != 0 || rank < 0 || rank >= ranks)
+    return fail(OCEAN_ERR_INVALID, "ocean_generator_create_slab: ranks must be a power of two in [1, 16], 0 <= rank < ranks");
+  const int w = fft->n / ranks;
+  if (w % blk != 0 || w < fft->n / 16 || w < slab_min_width(fft->logn))
+    return fail(OCEAN_ERR_INVALID, "ocean_generator_create_slab: N / ranks = " + std::to_string(w) +
+                                       " is below this size's minimum slab width " +
+                                       std::to_string(slab_min_width(fft->logn)));
+  return generator_alloc(out, fft, 1, rank, ranks);
 }
 
 int ocean_generator_destroy(ocean_generator* g)
@@ -306,6 +336,8 @@ int ocean_generator_destroy(ocean_generator* g)
     (void)hipFree(g->h0);
   if (g->inter)
     (void)hipFree(g->inter);
+  if (g->scratch)
+    (void)hipFree(g->scratch);
   if (g->maps)
     (void)hipFree(g->maps);
   if (g->jac)
@@ -332,26 +364,27 @@ int ocean_generator_generate_spectrum(ocean_generator* g)
   if (!g)
     return fail(OCEAN_ERR_INVALID, "ocean_generator_generate_spectrum: null generator");
   ocean_fft* f = g->fft;
-  const size_t texels = (size_t)f->n * f->n;
+  const size_t slab = (size_t)f->n * g->geom.w;
   for (int c = 0; c < g->cascades; c++)
   {
     OceanSettings s;
     std::memcpy(&s, &g->settings[c], sizeof(s));
-    HIP_TRY(timed(g, 0, [&] { return launch_generate_spectrum(s, f->n, g->h0 + texels * c, f->stream, f->cus); }),
+    HIP_TRY(timed(g, 0, [&] {
+              return launch_generate_spectrum(s, f->n, g->h0 + slab * c, f->stream, f->cus, g->geom.x0, g->geom.w);
+            }),
             "generateSpectrum");
   }
   return OCEAN_OK;
 }
 
-int ocean_generator_calculate(ocean_generator* g, float timestep, int update_spectrum)
+// First half of CalculateOcean: time += dt (src/Generator.cpp:50), h0 if requested (:55-59),
+// prepareFFT fused with the y direction of both EncodeIFFTs (:63-72). Output in destination-block
+// order into `out` (the internal buffer when null).
+static int generator_columns(ocean_generator* g, float timestep, int update_spectrum, float4* out)
 {
-  if (!g)
-    return fail(OCEAN_ERR_INVALID, "ocean_generator_calculate: null generator");
   ocean_fft* f = g->fft;
-  // src/Generator.cpp:50 — fp32 accumulation on the host, per cascade.
   for (auto& s : g->settings)
     s.time += timestep;
-  // src/Generator.cpp:55-59
   if (g->update_spectrum || update_spectrum)
   {
     g->update_spectrum = false;
@@ -360,7 +393,6 @@ int ocean_generator_calculate(ocean_generator* g, float timestep, int update_spe
       return rc;
   }
   FrameParams fp{};
-  FoamParams foam{};
   fp.cascades = g->cascades;
   for (int c = 0; c < g->cascades; c++)
   {
@@ -370,17 +402,72 @@ int ocean_generator_calculate(ocean_generator* g, float timestep, int update_spe
     fp.c[c].time = s.time;
     fp.c[c].g = s.g;
     fp.c[c].h = s.h;
-    foam.displacement[c] = s.displacement;
   }
-  // pass 1: prepareFFT fused with the y direction of both EncodeIFFTs (src/Generator.cpp:63-72)
-  HIP_TRY(timed(g, 1, [&] { return launch_cols_evolve(f->logn, fp, g->h0, g->inter, f->twiddles, f->stream, f->cus, default_keep(f->logn)); }),
+  HIP_TRY(timed(g, 1, [&] {
+            return launch_cols_evolve(f->logn, fp, g->geom, g->h0, out, f->twiddles, f->stream, f->cus,
+                                      default_keep(f->logn));
+          }),
           "column pass");
-  // pass 2: the x direction of both EncodeIFFTs + computeFoam (src/Generator.cpp:71-80)
+  return OCEAN_OK;
+}
+
+// Second half: the x direction of both EncodeIFFTs + computeFoam (src/Generator.cpp:71-80).
+static int generator_rows(ocean_generator* g, const float4* in)
+{
+  ocean_fft* f = g->fft;
+  FoamParams foam{};
+  for (int c = 0; c < g->cascades; c++)
+    foam.displacement[c] = g->settings[c].displacement;
   HIP_TRY(timed(g, 2, [&] {
-            return launch_rows_final(f->logn, g->cascades, g->inter, g->maps, g->jac, foam, f->twiddles, f->stream,
-                                     f->cus);
+            return launch_rows_final(f->logn, g->cascades, g->geom, in, g->scratch, g->maps, g->jac, foam, f->twiddles,
+                                     f->stream, f->cus);
           }),
           "row pass");
+  return OCEAN_OK;
+}
+
+int ocean_generator_calculate(ocean_generator* g, float timestep, int update_spectrum)
+{
+  if (!g)
+    return fail(OCEAN_ERR_INVALID, "ocean_generator_calculate: null generator");
+  if (g->ranks != 1)
+    return fail(OCEAN_ERR_INVALID, "ocean_generator_calculate: slab generators step with "
+                                   "ocean_generator_slab_columns / exchange / ocean_generator_slab_rows");
+  int rc = generator_columns(g, timestep, update_spectrum, g->inter);
+  return rc != OCEAN_OK ? rc : generator_rows(g, g->inter);
+}
+
+size_t ocean_generator_exchange_bytes(const ocean_generator* g)
+{
+  return g ? (size_t)g->cascades * 2 * g->fft->n * g->geom.w * sizeof(float4) : 0;
+}
+
+int ocean_generator_slab_columns(ocean_generator* g, float timestep, int update_spectrum, float* send)
+{
+  if (!g)
+    return fail(OCEAN_ERR_INVALID, "ocean_generator_slab_columns: null generator");
+  return generator_columns(g, timestep, update_spectrum, send ? reinterpret_cast<float4*>(send) : g->inter);
+}
+
+int ocean_generator_slab_rows(ocean_generator* g, const float* recv)
+{
+  if (!g)
+    return fail(OCEAN_ERR_INVALID, "ocean_generator_slab_rows: null generator");
+  return generator_rows(g, recv ? reinterpret_cast<const float4*>(recv) : g->inter);
+}
+
+int ocean_generator_slab_info(const ocean_generator* g, int* rank, int* ranks, int* row0, int* rows)
+{
+  if (!g)
+    return fail(OCEAN_ERR_INVALID, "ocean_generator_slab_info: null generator");
+  if (rank)
+    *rank = g->rank;
+  if (ranks)
+    *ranks = g->ranks;
+  if (row0)
+    *row0 = g->rank * g->geom.w;
+  if (rows)
+    *rows = g->geom.w;
   return OCEAN_OK;
 }
 
@@ -388,28 +475,28 @@ float* ocean_generator_height_map(ocean_generator* g, int c)
 {
   if (!g || c < 0 || c >= g->cascades)
     return nullptr;
-  return reinterpret_cast<float*>(g->maps + (size_t)g->fft->n * g->fft->n * (2 * c));
+  return reinterpret_cast<float*>(g->maps + (size_t)g->fft->n * g->geom.w * (2 * c));
 }
 
 float* ocean_generator_displacement_map(ocean_generator* g, int c)
 {
   if (!g || c < 0 || c >= g->cascades)
     return nullptr;
-  return reinterpret_cast<float*>(g->maps + (size_t)g->fft->n * g->fft->n * (2 * c + 1));
+  return reinterpret_cast<float*>(g->maps + (size_t)g->fft->n * g->geom.w * (2 * c + 1));
 }
 
 float* ocean_generator_jacobian_map(ocean_generator* g, int c)
 {
   if (!g || c < 0 || c >= g->cascades)
     return nullptr;
-  return g->jac + (size_t)g->fft->n * g->fft->n * c;
+  return g->jac + (size_t)g->fft->n * g->geom.w * c;
 }
 
 float* ocean_generator_initial_spectrum(ocean_generator* g, int c)
 {
   if (!g || c < 0 || c >= g->cascades)
     return nullptr;
-  return reinterpret_cast<float*>(g->h0 + (size_t)g->fft->n * g->fft->n * c);
+  return reinterpret_cast<float*>(g->h0 + (size_t)g->fft->n * g->geom.w * c);
 }
 
 int ocean_generator_spectrum_block(const ocean_generator* g)

@@ -52,17 +52,34 @@ struct FoamParams
   float displacement[kMaxCascades];
 };
 
-// h0 is stored strip-blocked [xb][y][blk]; blk = spectrum_block(log2 N).
+// Slab decomposition of one N x N grid over `ranks` GPUs (ranks == 1: the whole grid). This rank
+// owns columns [x0, x0 + w) in the column pass and rows [rank*w, rank*w + w) in the row pass,
+// w = N / ranks. Pass 1 writes its output in destination-block order (block q = rows q*w..q*w+w-1),
+// so one equal-split all-to-all turns it into the row pass's input.
+struct SlabGeom
+{
+  int x0;
+  int w;
+};
+
+// h0 is stored strip-blocked [xb][y][blk]; blk = spectrum_block(log2 N). x0/width select a column
+// slab (width <= 0: the whole grid).
 int spectrum_block(int logn);
-hipError_t launch_generate_spectrum(const OceanSettings& s, int n, float4* h0, hipStream_t stream, int cus);
+hipError_t launch_generate_spectrum(const OceanSettings& s, int n, float4* h0, hipStream_t stream, int cus, int x0 = 0,
+                                    int width = 0);
 hipError_t launch_hash(const uint32_t* xy, int count, uint32_t* raw, float2* uv, hipStream_t stream);
-// Generator frame: pass 1 (evolve + y iFFT, blocked intermediate), pass 2 (x iFFT + maps + Jacobian).
-// keep: evolved amplitudes kept live between the two packed images (0, 8 or 16; see the kernel).
-hipError_t launch_cols_evolve(int logn, const FrameParams& fp, const float4* h0, float4* inter, const float2* tw,
-                              hipStream_t stream, int cus, int keep);
+// Generator frame: pass 1 (evolve + y iFFT, destination-block-ordered output), pass 2 (x iFFT +
+// maps + Jacobian). keep: evolved amplitudes kept live between the two packed images (0, 8, 16).
+hipError_t launch_cols_evolve(int logn, const FrameParams& fp, const SlabGeom& g, const float4* h0, float4* inter,
+                              const float2* tw, hipStream_t stream, int cus, int keep);
 int default_keep(int logn);
-hipError_t launch_rows_final(int logn, int cascades, const float4* inter, float4* maps, float* jac,
-                             const FoamParams& foam, const float2* tw, hipStream_t stream, int cus);
+// Smallest slab width (N / ranks) the column/row pass work items fit in.
+int slab_min_width(int logn);
+// True when pass 2 needs the B == 1 transpose into a row-major scratch buffer (N = 16384).
+bool rows_need_transpose(int logn);
+hipError_t launch_rows_final(int logn, int cascades, const SlabGeom& g, const float4* inter, float4* scratch,
+                             float4* maps, float* jac, const FoamParams& foam, const float2* tw, hipStream_t stream,
+                             int cus);
 // EncodeIFFT on row-major images, in place: row pass then column pass.
 hipError_t launch_rows_ifft(int logn, int n_images, float4* images, const float2* tw, hipStream_t stream,
                             int cus);

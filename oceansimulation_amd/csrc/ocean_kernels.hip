@@ -158,9 +158,11 @@ __device__ __forceinline__ float2 spectrum_amplitude(const OceanSettings& s, flo
 // Stored strip-blocked, h0[xb][y][blk] (blk texel columns per strip, see ColFirstCfg), so the
 // column pass reads each strip as one contiguous run. The reference keeps this image private
 // (src/Generator.h:86), so its layout is internal.
-__global__ __launch_bounds__(256) void k_generate_spectrum(OceanSettings s, int n, int blk, float4* __restrict__ h0)
+__global__ __launch_bounds__(256) void k_generate_spectrum(OceanSettings s, int n, int blk, int x0, int width,
+                                                          float4* __restrict__ h0)
 {
-  const int64_t total = (int64_t)n * n;
+  // columns [x0, x0 + width) of the N x N spectrum (a rank's column slab; width = n for a whole grid)
+  const int64_t total = (int64_t)width * n;
   const float dim = (float)n;
   for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < total;
        idx += (int64_t)gridDim.x * blockDim.x)
@@ -169,7 +171,7 @@ __global__ __launch_bounds__(256) void k_generate_spectrum(OceanSettings s, int 
     const int b = (int)(idx % blk);
     const int64_t rest = idx / blk;
     const int y = (int)(rest % n), xb = (int)(rest / n);
-    const int x = xb * blk + b;
+    const int x = x0 + xb * blk + b;
     float2 a = spectrum_amplitude(s, (float)x, (float)y, dim);
     float2 c = spectrum_amplitude(s, dim - (float)x, dim - (float)y, dim);
     h0[idx] = make_float4(a.x, a.y, c.x, -c.y);
@@ -828,29 +830,31 @@ struct ColFirstCfg
 // workgroup at N = 4096 (spills, which cost HBM traffic); KEEP = 8 does.
 template <int LOGN, int KEEP>
 __global__ __launch_bounds__(ColFirstCfg<LOGN>::WG1) void k_cols_evolve(
-    FrameParams fp, const float4* __restrict__ h0, float4* __restrict__ inter, const float2* __restrict__ tw_glob)
+    FrameParams fp, SlabGeom g, const float4* __restrict__ h0, float4* __restrict__ inter,
+    const float2* __restrict__ tw_glob)
 {
   using S = FftShape<LOGN>;
   using K = ColFirstCfg<LOGN>;
   constexpr int N = S::N, T = S::T, B = K::B, SPW = K::SPW;
-  constexpr int GROUPS = (N / B) / SPW;  // pass-1 items per cascade
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   float2* tw = reinterpret_cast<float2*>(smem);
   void* xch = smem + ((S::TW_ENTRIES * 8 + 15) / 16) * 16;
   load_twiddles<LOGN>(tw, tw_glob);
 
-  const int total = fp.cascades * GROUPS;
+  const int w = g.w, wb = g.w / B;  // slab columns (= rows per destination block), strips in slab
+  const int groups = wb / SPW;      // pass-1 items per cascade
+  const int total = fp.cascades * groups;
   const float dim = (float)N;
   for (int item = blockIdx.x; item < total; item += gridDim.x)
   {
     // thread coordinates re-derived from one opaque copy of threadIdx.x (fewer live VGPRs)
     const int tid = opaque((int)threadIdx.x);
     const int b = tid % B, sl = SPW == 1 ? 0 : tid / (B * T);
-    const int c = item / GROUPS, xb0 = (item - c * GROUPS) * SPW;
+    const int c = item / groups, xb0 = (item - c * groups) * SPW;
     const CascadeFrame f = fp.c[c];
-    // this item's SPW strips are one contiguous run of SPW*N*B texels
-    const float4* src = h0 + ((size_t)c * (N / B) + xb0) * N * B;
-    const int x = (xb0 + sl) * B + b;
+    // this item's SPW strips of the slab's h0 are one contiguous run of SPW*N*B texels
+    const float4* src = h0 + ((size_t)c * wb + xb0) * N * B;
+    const int x = g.x0 + (xb0 + sl) * B + b;  // global column (k index)
     float2 H[KEEP > 0 ? KEEP : 1];
 #pragma unroll 1
     for (int img = 0; img < 2; img++)
@@ -878,49 +882,89 @@ __global__ __launch_bounds__(ColFirstCfg<LOGN>::WG1) void k_cols_evolve(
         v[m] = img == 0 ? pack_height(Hm, q) : pack_displacement(Hm, q);
       }
       fft_run<LOGN, K::C1, true>(v, i, sl * B + b, xch, tw);
-      float4* dst = inter + ((size_t)(2 * c + img) * (N / B) + xb0) * N * B;
+      // Output rows y = i + m*T go to destination block q = y / w (uniform per m since T | w),
+      // laid out inter[c][q][img][xb_local][y - q*w][B]: each destination's block is one
+      // contiguous range (what the all-to-all sends; for ranks == 1 it is [c][img][xb][y][B]).
+      float4* dst = inter + (size_t)c * 2 * N * w;
+      const int soff = ((sl * w + i) * B + b) * 16;
 #pragma unroll
       for (int m = 0; m < 16; m++)
-        st4(dst + m * T * B, voff, v[m]);
+      {
+        const int q = (m * T) / w, yl = (m * T) % w;
+        st4(dst + (((size_t)(q * 2 + img) * wb + xb0) * w + yl) * B, soff, v[m]);
+      }
     }
   }
 }
 
-template <int LOGN>
+// BLOCKED: input is pass 1's output after the exchange, inter[c][src][img][xb_local][y][B] for this
+// rank's w rows (xb = src * (w/B) + xb_local); otherwise row-major [c][img][y][x] (after
+// k_blocks_to_rows, used when B == 1).
+template <int LOGN, bool BLOCKED>
 __global__ __launch_bounds__(ColFirstCfg<LOGN>::WG2) void k_rows_final(
-    int cascades, const float4* __restrict__ inter, float4* __restrict__ maps, float* __restrict__ jac,
+    int cascades, SlabGeom g, const float4* __restrict__ inter, float4* __restrict__ maps, float* __restrict__ jac,
     FoamParams foam, const float2* __restrict__ tw_glob)
 {
   using S = FftShape<LOGN>;
   using K = ColFirstCfg<LOGN>;
-  constexpr int N = S::N, T = S::T, B = K::B, RPW = K::RPW2;
-  constexpr int BLOCKS = N / RPW;  // pass-2 items per image
+  constexpr int N = S::N, T = S::T, B = BLOCKED ? K::B : 1, RPW = K::RPW2;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   float2* tw = reinterpret_cast<float2*>(smem);
   void* xch = smem + ((S::TW_ENTRIES * 8 + 15) / 16) * 16;
   load_twiddles<LOGN>(tw, tw_glob);
 
-  // Loads: lanes b fastest, then row r, then ihi, so 16 consecutive lanes read one B*RPW*16-byte
-  // run [xb][y0..y0+RPW-1][0..B-1]. After the first exchange the thread becomes position i2 of
-  // row r2 with i2 fastest, so each wave stores 64 consecutive texels (1 KiB) of one row.
+  const int w = g.w, wb = g.w / B;
+  const int blocks = w / RPW;  // pass-2 items per image
+  // Loads (blocked input): lanes b fastest, then row r, then ihi, so 16 consecutive lanes read one
+  // B*RPW*16-byte run [xb][y0..y0+RPW-1][0..B-1]. After the first exchange the thread becomes
+  // position i2 of row r2 with i2 fastest, so each wave stores 64 consecutive texels of one row.
+  // Row-major input: i fastest for both.
   const int b0 = threadIdx.x % B, r0 = (threadIdx.x / B) % RPW, ihi0 = threadIdx.x / (B * RPW);
   const int i20 = threadIdx.x % T, r20 = threadIdx.x / T;
-  constexpr bool REMAP = S::NSTAGE > 1;
-  const int total = cascades * 2 * BLOCKS;
+  constexpr bool REMAP = BLOCKED && S::NSTAGE > 1;
+  const int total = cascades * 2 * blocks;
   for (int item = blockIdx.x; item < total; item += gridDim.x)
   {
-    const int b = opaque(b0), r = RPW == 1 ? 0 : opaque(r0), ihi = opaque(ihi0);
-    const int i = ihi * B + b;
+    int i, r;
+    if constexpr (BLOCKED)
+    {
+      const int b = opaque(b0), ihi = opaque(ihi0);
+      r = RPW == 1 ? 0 : opaque(r0);
+      i = ihi * B + b;
+    }
+    else
+    {
+      i = opaque(i20);
+      r = RPW == 1 ? 0 : opaque(r20);
+    }
     const int i2 = REMAP ? opaque(i20) : i, r2 = REMAP ? (RPW == 1 ? 0 : opaque(r20)) : r;
-    const int img = item / BLOCKS, y0 = (item - img * BLOCKS) * RPW;
-    const float4* src = inter + ((size_t)img << (2 * LOGN)) + (size_t)y0 * B;
-    const int voff = ((ihi * N + r) * B + b) * 16;
+    const int cimg = item / blocks, y0 = (item - cimg * blocks) * RPW;
+    const int c = cimg >> 1, img = cimg & 1;
     float4 v[16];
+    if constexpr (BLOCKED)
+    {
+      const float4* src = inter + (size_t)c * 2 * N * w + (size_t)y0 * B;
+      const int ihi = i / B, b = i % B;
+      const int voff = ((ihi * w + r) * B + b) * 16;
 #pragma unroll
-    for (int m = 0; m < 16; m++)
-      v[m] = ld4(src + (size_t)(((m + 8) & 15) * (T / B)) * N * B, voff);  // fftShift on x
+      for (int m = 0; m < 16; m++)
+      {
+        // column block xb = ihi + mm*T/B: source rank and local block are uniform per m
+        const int xbm = ((m + 8) & 15) * (T / B);  // fftShift on x
+        const int srcr = xbm / wb, xbl = xbm % wb;
+        v[m] = ld4(src + ((size_t)(srcr * 2 + img) * wb + xbl) * w * B, voff);
+      }
+    }
+    else
+    {
+      const float4* src = inter + ((size_t)cimg * w + y0) * N;
+      const int voff = ((r << LOGN) + i) * 16;
+#pragma unroll
+      for (int m = 0; m < 16; m++)
+        v[m] = ld4(src + ((m + 8) & 15) * T, voff);  // fftShift on x
+    }
     fft_run<LOGN, 0, true>(v, i, r, i2, r2, xch, tw);
-    float4* dst = maps + ((size_t)img << (2 * LOGN)) + ((size_t)y0 << LOGN);
+    float4* dst = maps + ((size_t)cimg * w + y0) * N;
     const int woff = ((r2 << LOGN) + i2) * 16;
 #pragma unroll
     for (int m = 0; m < 16; m++)
@@ -928,13 +972,45 @@ __global__ __launch_bounds__(ColFirstCfg<LOGN>::WG2) void k_rows_final(
     if (img & 1)
     {
       // displacementMap (Dz, dDx/dx, dDz/dz, dDx/dz): Jacobian, spectrum.compute:246-259
-      const float lam = foam.displacement[img >> 1];
-      float* jb = jac + ((size_t)(img >> 1) << (2 * LOGN)) + ((size_t)y0 << LOGN);
+      const float lam = foam.displacement[c];
+      float* jb = jac + ((size_t)c * w + y0) * N;
       const int joff = ((r2 << LOGN) + i2) * 4;
 #pragma unroll
       for (int m = 0; m < 16; m++)
         st1(jb + m * T, joff, (1.0f + lam * v[m].y) * (1.0f + lam * v[m].z) - lam * lam * v[m].w * v[m].w);
     }
+  }
+}
+
+// B == 1 (N = 16384: one 256-KiB column per CU) makes the blocked layout column-major, whose rows
+// the row pass could only read 16 bytes at a time. This tiled transpose (64 x 64 texels through
+// LDS, 1-KiB runs on both sides) turns inter[c][src][img][x_local][y] into row-major
+// out[c][img][y][x] for the rank's w rows.
+__global__ __launch_bounds__(256) void k_blocks_to_rows(int cascades, int n, int w, const float4* __restrict__ in,
+                                                        float4* __restrict__ out)
+{
+  __shared__ float4 tile[64][65];
+  const int tiles_x = n / 64, tiles_y = w / 64;
+  const int total = cascades * 2 * tiles_x * tiles_y;
+  for (int item = blockIdx.x; item < total; item += gridDim.x)
+  {
+    const int cimg = item / (tiles_x * tiles_y), t = item % (tiles_x * tiles_y);
+    const int c = cimg >> 1, img = cimg & 1;
+    const int tx = t % tiles_x, ty = t / tiles_x;
+    // read: 64 columns x 64 rows; column x is contiguous in y
+    for (int k = 0; k < 16; k++)
+    {
+      const int L = k * 256 + threadIdx.x, col = L >> 6, row = L & 63;
+      const int x = tx * 64 + col, srcr = x / w, xl = x % w;
+      tile[col][row] = in[(size_t)c * 2 * n * w + ((size_t)(srcr * 2 + img) * w + xl) * w + ty * 64 + row];
+    }
+    __syncthreads();
+    for (int k = 0; k < 16; k++)
+    {
+      const int L = k * 256 + threadIdx.x, row = L >> 6, col = L & 63;
+      out[((size_t)cimg * w + ty * 64 + row) * n + tx * 64 + col] = tile[col][row];
+    }
+    __syncthreads();
   }
 }
 
@@ -1016,17 +1092,21 @@ int spectrum_block(int logn)
   return t >= 1024 ? 1 : (t >= 512 ? 2 : (t < 4 ? t : 4));
 }
 
-hipError_t launch_generate_spectrum(const OceanSettings& s, int n, float4* h0, hipStream_t stream, int cus)
+hipError_t launch_generate_spectrum(const OceanSettings& s, int n, float4* h0, hipStream_t stream, int cus, int x0,
+                                    int width)
 {
   int logn = 0;
   while ((1 << logn) < n)
     logn++;
-  long total = (long)n * n;
+  if (width <= 0)
+    width = n;
+  long total = (long)n * width;
   long blocks = (total + 255) / 256;
   long cap = (long)cus * 16;
   if (blocks > cap)
     blocks = cap;
-  hipLaunchKernelGGL(k_generate_spectrum, dim3((unsigned)blocks), dim3(256), 0, stream, s, n, spectrum_block(logn), h0);
+  hipLaunchKernelGGL(k_generate_spectrum, dim3((unsigned)blocks), dim3(256), 0, stream, s, n, spectrum_block(logn), x0,
+                     width, h0);
   return hipGetLastError();
 }
 
@@ -1036,8 +1116,8 @@ hipError_t launch_hash(const uint32_t* xy, int count, uint32_t* raw, float2* uv,
   return hipGetLastError();
 }
 
-hipError_t launch_cols_evolve(int logn, const FrameParams& fp, const float4* h0, float4* inter, const float2* tw,
-                              hipStream_t stream, int cus, int keep)
+hipError_t launch_cols_evolve(int logn, const FrameParams& fp, const SlabGeom& g, const float4* h0, float4* inter,
+                              const float2* tw, hipStream_t stream, int cus, int keep)
 {
   return with_logn(logn, [&](auto L) -> hipError_t {
     constexpr int LOGN = decltype(L)::value;
@@ -1045,9 +1125,9 @@ hipError_t launch_cols_evolve(int logn, const FrameParams& fp, const float4* h0,
     using S = FftShape<LOGN>;
     auto kern = keep >= 16 ? k_cols_evolve<LOGN, 16> : (keep >= 8 ? k_cols_evolve<LOGN, 8> : k_cols_evolve<LOGN, 0>);
     const int lds = ((S::TW_ENTRIES * 8 + 15) / 16) * 16 + K::LDS1;
-    const int items = fp.cascades * ((S::N / K::B) / K::SPW);
+    const int items = fp.cascades * ((g.w / K::B) / K::SPW);
     const int grid = persistent_grid(kern, K::WG1, lds, items, cus);
-    hipLaunchKernelGGL(kern, dim3(grid), dim3(K::WG1), lds, stream, fp, h0, inter, tw);
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(K::WG1), lds, stream, fp, g, h0, inter, tw);
     return hipGetLastError();
   });
 }
@@ -1055,18 +1135,70 @@ hipError_t launch_cols_evolve(int logn, const FrameParams& fp, const float4* h0,
 // The largest H-retention that compiles without spills for this size (see k_cols_evolve).
 int default_keep(int logn) { return logn >= 12 ? 8 : 16; }
 
-hipError_t launch_rows_final(int logn, int cascades, const float4* inter, float4* maps, float* jac,
-                             const FoamParams& foam, const float2* tw, hipStream_t stream, int cus)
+bool rows_need_transpose(int logn) { return spectrum_block(logn) == 1 && (1 << logn) >= 64; }
+
+template <int LOGN>
+static int slab_min_width_impl()
 {
+  using K = ColFirstCfg<LOGN>;
+  int m = K::C1 > K::RPW2 ? K::C1 : K::RPW2;
+  if (rows_need_transpose(LOGN))
+    m = m > 64 ? m : 64;
+  return m;
+}
+
+int slab_min_width(int logn)
+{
+  switch (logn)
+  {
+  case 4: return slab_min_width_impl<4>();
+  case 5: return slab_min_width_impl<5>();
+  case 6: return slab_min_width_impl<6>();
+  case 7: return slab_min_width_impl<7>();
+  case 8: return slab_min_width_impl<8>();
+  case 9: return slab_min_width_impl<9>();
+  case 10: return slab_min_width_impl<10>();
+  case 11: return slab_min_width_impl<11>();
+  case 12: return slab_min_width_impl<12>();
+  case 13: return slab_min_width_impl<13>();
+  case 14: return slab_min_width_impl<14>();
+  default: return 1 << 30;
+  }
+}
+
+hipError_t launch_rows_final(int logn, int cascades, const SlabGeom& g, const float4* inter, float4* scratch,
+                             float4* maps, float* jac, const FoamParams& foam, const float2* tw, hipStream_t stream,
+                             int cus)
+{
+  const bool transpose = rows_need_transpose(logn) && scratch != nullptr;
+  if (transpose)
+  {
+    const int n = 1 << logn;
+    const int items = cascades * 2 * (n / 64) * (g.w / 64);
+    const int grid = persistent_grid(k_blocks_to_rows, 256, 0, items, cus);
+    hipLaunchKernelGGL(k_blocks_to_rows, dim3(grid), dim3(256), 0, stream, cascades, n, g.w, inter, scratch);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess)
+      return e;
+  }
   return with_logn(logn, [&](auto L) -> hipError_t {
     constexpr int LOGN = decltype(L)::value;
     using K = ColFirstCfg<LOGN>;
     using S = FftShape<LOGN>;
-    auto kern = k_rows_final<LOGN>;
     const int lds = ((S::TW_ENTRIES * 8 + 15) / 16) * 16 + K::LDS2;
-    const int items = cascades * 2 * (S::N / K::RPW2);
-    const int grid = persistent_grid(kern, K::WG2, lds, items, cus);
-    hipLaunchKernelGGL(kern, dim3(grid), dim3(K::WG2), lds, stream, cascades, inter, maps, jac, foam, tw);
+    const int items = cascades * 2 * (g.w / K::RPW2);
+    if (transpose)
+    {
+      auto kern = k_rows_final<LOGN, false>;
+      const int grid = persistent_grid(kern, K::WG2, lds, items, cus);
+      hipLaunchKernelGGL(kern, dim3(grid), dim3(K::WG2), lds, stream, cascades, g, scratch, maps, jac, foam, tw);
+    }
+    else
+    {
+      auto kern = k_rows_final<LOGN, true>;
+      const int grid = persistent_grid(kern, K::WG2, lds, items, cus);
+      hipLaunchKernelGGL(kern, dim3(grid), dim3(K::WG2), lds, stream, cascades, g, inter, maps, jac, foam, tw);
+    }
     return hipGetLastError();
   });
 }

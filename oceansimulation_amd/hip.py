@@ -83,3 +83,7 @@ class DeviceBuffer:
             self.free()
         except Exception:
             pass
+
+
+def copy_d2d(dst_ptr: int, src_ptr: int, nbytes: int) -> None:
+    _check(hip().hipMemcpy(ctypes.c_void_p(dst_ptr), ctypes.c_void_p(src_ptr), nbytes, D2D), "hipMemcpy D2D")

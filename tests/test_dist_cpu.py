@@ -56,3 +56,44 @@ def test_world2_max_over_ranks_and_disjoint_cascades():
         assert el_max == 2.0  # max over ranks, not rank-local time
         flat = [tuple(k) for ranks in gathered for k in ranks]
         assert len(set(flat)) == len(flat)  # no cascade computed twice across ranks
+
+
+def _a2a_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    import torch
+    import torch.distributed as dist
+
+    dist.init_process_group("gloo")
+    import sys
+
+    sys.path.insert(0, ROOT)
+    from oceansimulation_amd.slab import TorchExchange, block_moves
+
+    nbytes = 16 * world
+    ex = TorchExchange(nbytes, torch.device("cpu"))
+    ex.send.copy_(torch.tensor([rank * 16 + qq for qq in range(world) for _ in range(16)], dtype=torch.uint8))
+    ex()
+    got = ex.recv.tolist()
+    # the emulated exchange's block map must describe exactly what the collective did
+    expect = [0] * nbytes
+    for s, so, dst, do, size in block_moves(world, nbytes):
+        if dst == rank:
+            expect[do:do + size] = [s * 16 + (so // 16)] * size
+    dist.destroy_process_group()
+    q.put((rank, got == expect))
+
+
+@pytest.mark.timeout(120)
+def test_world2_alltoall_matches_emulated_block_moves():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_a2a_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=100) for _ in procs]
+    for p in procs:
+        p.join(timeout=30)
+        assert p.exitcode == 0
+    assert all(ok for _, ok in res)

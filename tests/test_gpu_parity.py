@@ -276,3 +276,93 @@ def test_golden_fixtures_gpu(ocean):
         assert max(lane_err(gen.height_map_host(0), z[f"{name}/height"])) <= FRAME_TOL, name
         assert max(lane_err(gen.displacement_map_host(0), z[f"{name}/disp"])) <= FRAME_TOL, name
         assert scalar_err(gen.jacobian_map_host(0) - 1.0, z[f"{name}/jac"] - 1.0) <= FRAME_TOL, name
+
+
+# ---- slab decomposition (one grid over P ranks, emulated in one process) --------------------
+def _slab_run(ocean, n, ranks, steps, settings):
+    from oceansimulation_amd.hip import DeviceBuffer
+    from oceansimulation_amd.slab import SlabGenerator, emulate_frame
+
+    fft = ocean.FFTCalculator(n)
+    slabs = [SlabGenerator(fft, r, ranks) for r in range(ranks)]
+    for g in slabs:
+        ocean.apply_settings(g.GetOceanSettings(), **settings)
+    sends = [DeviceBuffer(g.exchange_bytes) for g in slabs]
+    recvs = [DeviceBuffer(g.exchange_bytes) for g in slabs]
+    for k, dt in enumerate(steps):
+        emulate_frame(slabs, sends, recvs, dt, update_ocean=(k == 0))
+    h = np.concatenate([g.height_map_host() for g in slabs])
+    d = np.concatenate([g.displacement_map_host() for g in slabs])
+    j = np.concatenate([g.jacobian_map_host() for g in slabs])
+    return h, d, j
+
+
+@pytest.mark.parametrize("n,ranks", [(512, 2), (256, 2), (256, 4), (1024, 8), (4096, 4), (2048, 16)])
+def test_slab_decomposition_matches_whole_grid(ocean, n, ranks):
+    """Rank-split column pass + all-to-all + rank-split row pass == the single-GPU generator,
+    bit for bit (the same kernels compute every column and every row)."""
+    settings = dict(planeSize=17.0)
+    steps = [0.25, 1.0 / 60.0]
+    h, d, j = _slab_run(ocean, n, ranks, steps, settings)
+    fft = ocean.FFTCalculator(n)
+    gen = ocean.Generator(fft, 1)
+    ocean.apply_settings(gen.GetOceanSettings(0), **settings)
+    for dt in steps:
+        gen.CalculateOcean(dt)
+    assert np.array_equal(h, gen.height_map_host(0))
+    assert np.array_equal(d, gen.displacement_map_host(0))
+    assert np.array_equal(j, gen.jacobian_map_host(0))
+
+
+def test_slab_rejects_too_narrow_slabs(ocean):
+    from oceansimulation_amd.capi import OceanError
+    from oceansimulation_amd.slab import SlabGenerator
+
+    fft = ocean.FFTCalculator(64)
+    with pytest.raises(OceanError):
+        SlabGenerator(fft, 0, 2)  # 32-wide slabs < the 64-column work item at N = 64
+    with pytest.raises(OceanError):
+        SlabGenerator(ocean.FFTCalculator(256), 0, 3)  # not a power of two
+
+
+def test_slab_small_grid_vs_oracle(ocean, oracle):
+    n, ranks = 256, 4
+    h, d, j = _slab_run(ocean, n, ranks, [1.0], dict(planeSize=5.0))
+    ref = oracle.OracleGenerator(n, oracle.default_settings(planeSize=5.0))
+    ref.calculate_ocean(1.0)
+    _frame_check(h, d, j, ref)
+
+
+def _sampled_idft(field, pts):
+    """Direct float64 evaluation of N^2 * ifft2(ifftshift(field)) at a few output points."""
+    n = field.shape[0]
+    k = (np.arange(n) - n // 2).astype(np.float64)
+    out = []
+    for (y, x) in pts:
+        ex = np.exp(2j * np.pi * k * x / n)
+        ey = np.exp(2j * np.pi * k * y / n)
+        out.append(ey @ field @ ex)
+    return np.array(out)
+
+
+@pytest.mark.slow
+def test_generator_16384_transpose_path_sampled(ocean):
+    """N = 16384 (B = 1: column pass + tiled transpose + row pass): sampled outputs against a
+    float64 direct 2D iDFT of the GPU's own h0, evolved in float64."""
+    n = 16384
+    fft = ocean.FFTCalculator(n)
+    gen = ocean.Generator(fft, 1)
+    gen.CalculateOcean(0.5)
+    h0 = gen.initial_spectrum_host(0).astype(np.float64)
+    s = R.settings_dict(gen.GetOceanSettings(0))
+    hm, dm = R.prepare_fft(s, n, h0.astype(np.float32))  # float32 evolve like the reference
+    pts = [(0, 0), (123, 4567), (8191, 16383), (16000, 77)]
+    got_h = gen.height_map_host(0)
+    got_d = gen.displacement_map_host(0)
+    for img, (field, got) in enumerate(((hm, got_h), (dm, got_d))):
+        for lane in range(2):
+            z = field[..., 2 * lane].astype(np.float64) + 1j * field[..., 2 * lane + 1].astype(np.float64)
+            ref = _sampled_idft(z, pts)
+            g = np.array([got[y, x, 2 * lane] + 1j * got[y, x, 2 * lane + 1] for (y, x) in pts])
+            scale = np.sqrt(np.sum(np.abs(z) ** 2))  # rms of the output field (Parseval)
+            assert np.max(np.abs(g - ref)) <= FRAME_TOL * scale * 4, (img, lane)

@@ -88,10 +88,14 @@ int main(int argc, char** argv)
   }
   CHECK(hipDeviceSynchronize());
   const double pts = (double)tex * C;
-  auto p1r = [&] { return launch_cols_evolve(logn, fp, h0, inter, tw, 0, cus, 0); };
-  auto p1k = [&] { return launch_cols_evolve(logn, fp, h0, inter, tw, 0, cus, 16); };
-  auto p1h = [&] { return launch_cols_evolve(logn, fp, h0, inter, tw, 0, cus, 8); };
-  auto p2 = [&] { return launch_rows_final(logn, C, inter, maps, jac, foam, tw, 0, cus); };
+  SlabGeom geom{0, n};
+  float4* scratch = nullptr;
+  if (rows_need_transpose(logn))
+    CHECK(hipMalloc(&scratch, tex * C * 2 * sizeof(float4)));
+  auto p1r = [&] { return launch_cols_evolve(logn, fp, geom, h0, inter, tw, 0, cus, 0); };
+  auto p1k = [&] { return launch_cols_evolve(logn, fp, geom, h0, inter, tw, 0, cus, 16); };
+  auto p1h = [&] { return launch_cols_evolve(logn, fp, geom, h0, inter, tw, 0, cus, 8); };
+  auto p2 = [&] { return launch_rows_final(logn, C, geom, inter, scratch, maps, jac, foam, tw, 0, cus); };
   auto frame = [&] {
     hipError_t e = p1h();
     return e == hipSuccess ? p2() : e;

@@ -44,12 +44,12 @@ $(CPPTEST): tests/cpp/test_waves.cpp $(WAVES) $(ORACLE)
 	    -Wl,-rpath,'$$ORIGIN/../../$(PKG)' -Wl,-rpath,'$$ORIGIN/../../oracle/build' -L/opt/rocm/lib -lamdhip64
 
 MB := tools/microbench
-microbench: $(MB)/genbench $(MB)/colbench
+microbench: $(MB)/genbench $(MB)/colbench $(MB)/copybench
 $(MB)/%: $(MB)/%.hip $(CSRC)/ocean_kernels.hip $(CSRC)/ocean_internal.h
 	$(HIPCC) $(HIPFLAGS) $< -o $@
 
 clean:
-	rm -rf $(MB)/genbench $(MB)/colbench $(CSRC)/build $(LIB) $(WAVES) $(CPPTEST)
+	rm -rf $(MB)/genbench $(MB)/colbench $(MB)/copybench $(CSRC)/build $(LIB) $(WAVES) $(CPPTEST)
 	$(MAKE) -s -C oracle clean
 
 .PHONY: all clean microbench

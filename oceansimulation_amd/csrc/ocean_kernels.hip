@@ -205,21 +205,25 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t srd(const void* base, int num_
 // which handles ragged row blocks without branches.
 constexpr int kAllBytes = 0x7FFFFFFF;
 
+// AUX: cache-policy bits of the buffer instruction (0 = default; 2 = nt, streaming / non-temporal).
+template <int AUX = 0>
 __device__ __forceinline__ float4 ld4(const void* base, int voff_bytes, int num_bytes = kAllBytes)
 {
-  f4v r = __builtin_amdgcn_raw_buffer_load_b128(srd(base, num_bytes), voff_bytes, 0, 0);
+  f4v r = __builtin_amdgcn_raw_buffer_load_b128(srd(base, num_bytes), voff_bytes, 0, AUX);
   return make_float4(r.x, r.y, r.z, r.w);
 }
 
+template <int AUX = 0>
 __device__ __forceinline__ void st4(void* base, int voff_bytes, float4 v, int num_bytes = kAllBytes)
 {
   f4v r = {v.x, v.y, v.z, v.w};
-  __builtin_amdgcn_raw_buffer_store_b128(r, srd(base, num_bytes), voff_bytes, 0, 0);
+  __builtin_amdgcn_raw_buffer_store_b128(r, srd(base, num_bytes), voff_bytes, 0, AUX);
 }
 
+template <int AUX = 0>
 __device__ __forceinline__ void st1(void* base, int voff_bytes, float v)
 {
-  __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), srd(base, kAllBytes), voff_bytes, 0, 0);
+  __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), srd(base, kAllBytes), voff_bytes, 0, AUX);
 }
 
 __device__ __forceinline__ int clamp_bytes(int64_t b)
@@ -828,7 +832,12 @@ struct ColFirstCfg
 // packed image to the second; the rest are re-read from h0 (bytes this workgroup streamed a few
 // microseconds earlier) and evolved again. KEEP = 16 does not fit the 128 VGPRs of a 1024-thread
 // workgroup at N = 4096 (spills, which cost HBM traffic); KEEP = 8 does.
-template <int LOGN, int KEEP>
+// Streaming (non-temporal) policy for the frame passes' HBM traffic: every byte is touched once
+// per frame and the working set is far beyond L2 and the 256 MiB Infinity Cache; measured 3-5 %
+// faster per pass than the default policy (tools/microbench/genbench, launch_policy_variant).
+constexpr int kStream = 2;
+
+template <int LOGN, int KEEP, int LA = kStream, int SA = kStream>
 __global__ __launch_bounds__(ColFirstCfg<LOGN>::WG1) void k_cols_evolve(
     FrameParams fp, SlabGeom g, const float4* __restrict__ h0, float4* __restrict__ inter,
     const float2* __restrict__ tw_glob)
@@ -866,7 +875,7 @@ __global__ __launch_bounds__(ColFirstCfg<LOGN>::WG1) void k_cols_evolve(
 #pragma unroll
       for (int m = 0; m < 16; m++)
         if (img == 0 || m >= KEEP)
-          v[m] = ld4(src + ((m + 8) & 15) * T * B, voff);  // fftShift on y folded into the load
+          v[m] = ld4<LA>(src + ((m + 8) & 15) * T * B, voff);  // fftShift on y folded into the load
 #pragma unroll
       for (int m = 0; m < 16; m++)
       {
@@ -891,7 +900,7 @@ __global__ __launch_bounds__(ColFirstCfg<LOGN>::WG1) void k_cols_evolve(
       for (int m = 0; m < 16; m++)
       {
         const int q = (m * T) / w, yl = (m * T) % w;
-        st4(dst + (((size_t)(q * 2 + img) * wb + xb0) * w + yl) * B, soff, v[m]);
+        st4<SA>(dst + (((size_t)(q * 2 + img) * wb + xb0) * w + yl) * B, soff, v[m]);
       }
     }
   }
@@ -900,7 +909,7 @@ __global__ __launch_bounds__(ColFirstCfg<LOGN>::WG1) void k_cols_evolve(
 // BLOCKED: input is pass 1's output after the exchange, inter[c][src][img][xb_local][y][B] for this
 // rank's w rows (xb = src * (w/B) + xb_local); otherwise row-major [c][img][y][x] (after
 // k_blocks_to_rows, used when B == 1).
-template <int LOGN, bool BLOCKED>
+template <int LOGN, bool BLOCKED, int LA = kStream, int SA = kStream>
 __global__ __launch_bounds__(ColFirstCfg<LOGN>::WG2) void k_rows_final(
     int cascades, SlabGeom g, const float4* __restrict__ inter, float4* __restrict__ maps, float* __restrict__ jac,
     FoamParams foam, const float2* __restrict__ tw_glob)
@@ -952,7 +961,7 @@ __global__ __launch_bounds__(ColFirstCfg<LOGN>::WG2) void k_rows_final(
         // column block xb = ihi + mm*T/B: source rank and local block are uniform per m
         const int xbm = ((m + 8) & 15) * (T / B);  // fftShift on x
         const int srcr = xbm / wb, xbl = xbm % wb;
-        v[m] = ld4(src + ((size_t)(srcr * 2 + img) * wb + xbl) * w * B, voff);
+        v[m] = ld4<LA>(src + ((size_t)(srcr * 2 + img) * wb + xbl) * w * B, voff);
       }
     }
     else
@@ -961,14 +970,14 @@ __global__ __launch_bounds__(ColFirstCfg<LOGN>::WG2) void k_rows_final(
       const int voff = ((r << LOGN) + i) * 16;
 #pragma unroll
       for (int m = 0; m < 16; m++)
-        v[m] = ld4(src + ((m + 8) & 15) * T, voff);  // fftShift on x
+        v[m] = ld4<LA>(src + ((m + 8) & 15) * T, voff);  // fftShift on x
     }
     fft_run<LOGN, 0, true>(v, i, r, i2, r2, xch, tw);
     float4* dst = maps + ((size_t)cimg * w + y0) * N;
     const int woff = ((r2 << LOGN) + i2) * 16;
 #pragma unroll
     for (int m = 0; m < 16; m++)
-      st4(dst + m * T, woff, v[m]);
+      st4<SA>(dst + m * T, woff, v[m]);
     if (img & 1)
     {
       // displacementMap (Dz, dDx/dx, dDz/dz, dDx/dz): Jacobian, spectrum.compute:246-259
@@ -977,7 +986,7 @@ __global__ __launch_bounds__(ColFirstCfg<LOGN>::WG2) void k_rows_final(
       const int joff = ((r2 << LOGN) + i2) * 4;
 #pragma unroll
       for (int m = 0; m < 16; m++)
-        st1(jb + m * T, joff, (1.0f + lam * v[m].y) * (1.0f + lam * v[m].z) - lam * lam * v[m].w * v[m].w);
+        st1<SA>(jb + m * T, joff, (1.0f + lam * v[m].y) * (1.0f + lam * v[m].z) - lam * lam * v[m].w * v[m].w);
     }
   }
 }
@@ -1229,6 +1238,36 @@ hipError_t launch_cols(int logn, int n_images, float4* images, const float2* tw,
     hipLaunchKernelGGL(kern, dim3(grid), dim3(K::WG), lds, stream, n_images, images, tw);
     return hipGetLastError();
   });
+}
+
+// A/B hook for tools/microbench/genbench: pass 1 / pass 2 at N = 4096 with cache-policy variant
+// `policy` (0 default, 1 nt stores, 2 nt loads + stores).
+hipError_t launch_policy_variant(int pass, int policy, const FrameParams& fp, const SlabGeom& g, const float4* in,
+                                 float4* out, float* jac, const FoamParams& foam, const float2* tw, hipStream_t stream,
+                                 int cus)
+{
+  constexpr int LOGN = 12;
+  using K = ColFirstCfg<LOGN>;
+  using S = FftShape<LOGN>;
+  if (pass == 1)
+  {
+    auto kern = policy == 0 ? k_cols_evolve<LOGN, 8, 0, 0>
+                            : (policy == 1 ? k_cols_evolve<LOGN, 8, 0, 2> : k_cols_evolve<LOGN, 8, 2, 2>);
+    const int lds = ((S::TW_ENTRIES * 8 + 15) / 16) * 16 + K::LDS1;
+    const int items = fp.cascades * ((g.w / K::B) / K::SPW);
+    const int grid = persistent_grid(kern, K::WG1, lds, items, cus);
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(K::WG1), lds, stream, fp, g, in, out, tw);
+  }
+  else
+  {
+    auto kern = policy == 0 ? k_rows_final<LOGN, true, 0, 0>
+                            : (policy == 1 ? k_rows_final<LOGN, true, 0, 2> : k_rows_final<LOGN, true, 2, 2>);
+    const int lds = ((S::TW_ENTRIES * 8 + 15) / 16) * 16 + K::LDS2;
+    const int items = fp.cascades * 2 * (g.w / K::RPW2);
+    const int grid = persistent_grid(kern, K::WG2, lds, items, cus);
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(K::WG2), lds, stream, fp.cascades, g, in, out, jac, foam, tw);
+  }
+  return hipGetLastError();
 }
 
 int twiddle_entries(int logn)

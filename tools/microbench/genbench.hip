@@ -96,6 +96,12 @@ int main(int argc, char** argv)
   auto p1k = [&] { return launch_cols_evolve(logn, fp, geom, h0, inter, tw, 0, cus, 16); };
   auto p1h = [&] { return launch_cols_evolve(logn, fp, geom, h0, inter, tw, 0, cus, 8); };
   auto p2 = [&] { return launch_rows_final(logn, C, geom, inter, scratch, maps, jac, foam, tw, 0, cus); };
+  auto pv = [&](int pass, int pol) {
+    return [&, pass, pol] {
+      return pass == 1 ? launch_policy_variant(1, pol, fp, geom, h0, inter, nullptr, foam, tw, 0, cus)
+                       : launch_policy_variant(2, pol, fp, geom, inter, maps, jac, foam, tw, 0, cus);
+    };
+  };
   auto frame = [&] {
     hipError_t e = p1h();
     return e == hipSuccess ? p2() : e;
@@ -104,6 +110,7 @@ int main(int argc, char** argv)
   CHECK(hipDeviceSynchronize());
   const int rounds = 7, reps = 10;
   std::vector<float> t1r, t1k, t1h, t2, tf;
+  std::vector<std::vector<float>> tp(6);
   for (int r = 0; r < rounds; r++)
   {
     t1r.push_back(time_ms(p1r, reps));
@@ -111,6 +118,10 @@ int main(int argc, char** argv)
     t1h.push_back(time_ms(p1h, reps));
     t2.push_back(time_ms(p2, reps));
     tf.push_back(time_ms(frame, reps));
+    if (logn == 12)
+      for (int pass = 1; pass <= 2; pass++)
+        for (int pol = 0; pol < 3; pol++)
+          tp[(pass - 1) * 3 + pol].push_back(time_ms(pv(pass, pol), reps));
   }
   auto report = [&](const char* name, std::vector<float>& v, double bytes_per_pt) {
     std::sort(v.begin(), v.end());
@@ -123,5 +134,16 @@ int main(int argc, char** argv)
   report("pass1 cols_evolve (keep 8 H)", t1h, 48);
   report("pass2 rows_final", t2, 68);
   report("frame (pass1 keep 8 + pass2)", tf, 116);
+  if (logn == 12)
+  {
+    const char* pn[] = {"default", "nt stores", "nt loads+stores"};
+    for (int pass = 1; pass <= 2; pass++)
+      for (int pol = 0; pol < 3; pol++)
+      {
+        char name[80];
+        std::snprintf(name, sizeof name, "pass%d policy %s", pass, pn[pol]);
+        report(name, tp[(pass - 1) * 3 + pol], pass == 1 ? 48 : 68);
+      }
+  }
   return 0;
 }

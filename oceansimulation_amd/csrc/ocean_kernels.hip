@@ -261,6 +261,49 @@ __device__ __forceinline__ float4 cmul(float4 a, float2 w)
                      a.z * w.y + a.w * w.x);
 }
 
+// Two complex lanes in split planes: re = (re0, re1), im = (im0, im1). Every FFT add/sub and
+// twiddle multiply is then one v_pk_{add,mul,fma}_f32 over both lanes (the twiddle's parts are
+// op_sel splats; multiplying by +-i is operand renaming plus a neg modifier), half the VALU issue
+// of the interleaved float4 form. The reference layout (re0, im0, re1, im1) is converted only at
+// global loads/stores of caller-visible images; the generator's intermediate stays split.
+typedef float f2v __attribute__((ext_vector_type(2)));
+struct __attribute__((aligned(16))) CPair
+{
+  f2v re, im;
+};
+__device__ __forceinline__ CPair operator+(CPair a, CPair b) { return {a.re + b.re, a.im + b.im}; }
+__device__ __forceinline__ CPair operator-(CPair a, CPair b) { return {a.re - b.re, a.im - b.im}; }
+__device__ __forceinline__ CPair mul_i(CPair a) { return {-a.im, a.re}; }
+__device__ __forceinline__ CPair mul_mi(CPair a) { return {a.im, -a.re}; }
+__device__ __forceinline__ CPair cmul(CPair a, float2 w)
+{
+  const f2v wx = {w.x, w.x}, wy = {w.y, w.y};
+  return {a.re * wx - a.im * wy, a.re * wy + a.im * wx};
+}
+// reference texel (re0, im0, re1, im1) <-> split planes
+__device__ __forceinline__ CPair to_pair(float4 t) { return {f2v{t.x, t.z}, f2v{t.y, t.w}}; }
+__device__ __forceinline__ float4 from_pair(CPair c) { return make_float4(c.re.x, c.im.x, c.re.y, c.im.y); }
+// the split texel as raw 16 bytes (re0, re1, im0, im1), for the generator's intermediate
+__device__ __forceinline__ CPair raw_pair(float4 t) { return {f2v{t.x, t.y}, f2v{t.z, t.w}}; }
+__device__ __forceinline__ float4 pair_raw(CPair c) { return make_float4(c.re.x, c.re.y, c.im.x, c.im.y); }
+// the two float2 halves a SPLIT LDS exchange moves one at a time
+__device__ __forceinline__ float2 half_of(float4 v, int h) { return h ? make_float2(v.z, v.w) : make_float2(v.x, v.y); }
+__device__ __forceinline__ float2 half_of(CPair v, int h) { return h ? make_float2(v.im.x, v.im.y) : make_float2(v.re.x, v.re.y); }
+__device__ __forceinline__ void set_half(float4& v, int h, float2 r)
+{
+  if (h)
+    v.z = r.x, v.w = r.y;
+  else
+    v.x = r.x, v.y = r.y;
+}
+__device__ __forceinline__ void set_half(CPair& v, int h, float2 r)
+{
+  if (h)
+    v.im = f2v{r.x, r.y};
+  else
+    v.re = f2v{r.x, r.y};
+}
+
 // ------------------------------------------------------------------------------------------------
 // Small inverse DFTs (sign +): X[k] = sum_n x[n] exp(+2 pi i n k / r)
 // ------------------------------------------------------------------------------------------------
@@ -451,6 +494,16 @@ __device__ __forceinline__ int read_pidx(int i, int m)
     return pad16(i + m * T);
 }
 
+#if defined(OCEAN_ABLATE_EXCHANGE) || defined(OCEAN_ABLATE_BARRIER)
+__device__ __forceinline__ void touch(float4& v) { asm volatile("" : "+v"(v.x), "+v"(v.y), "+v"(v.z), "+v"(v.w)); }
+__device__ __forceinline__ void touch(CPair& v) { asm volatile("" : "+v"(v.re), "+v"(v.im)); }
+#endif
+#if defined(OCEAN_ABLATE_BARRIER)  // microbench-only timing ablation (results are wrong)
+#define XSYNC() asm volatile("" ::: "memory")
+#else
+#define XSYNC() __syncthreads()
+#endif
+
 // Write the 16 stage outputs (padded indices wp(t), region reg_w), barrier, read back the next
 // stage's inputs for the thread's (possibly different) position i_r in region reg_r, barrier.
 // SPLIT: float4 data exchanged as two float2 lanes through a float2 buffer (half the LDS).
@@ -458,40 +511,38 @@ template <int LOGN, int CI, bool SPLIT, typename V, typename WP>
 __device__ __forceinline__ void exchange(V* v, int reg_w, int i_r, int reg_r, void* lds_raw, WP wp)
 {
   using S = FftShape<LOGN>;
+#if defined(OCEAN_ABLATE_EXCHANGE)  // microbench-only timing ablation (results are wrong)
+  for (int t = 0; t < 16; t++)
+    touch(v[t]);
+  return;
+#endif
   if constexpr (!SPLIT)
   {
     V* lds = reinterpret_cast<V*>(lds_raw);
 #pragma unroll
     for (int t = 0; t < 16; t++)
       lds[lds_slot<CI, S::PADDED>(reg_w, wp(t))] = v[t];
-    __syncthreads();
+    XSYNC();
 #pragma unroll
     for (int m = 0; m < 16; m++)
       v[m] = lds[lds_slot<CI, S::PADDED>(reg_r, read_pidx<LOGN>(i_r, m))];
-    __syncthreads();
+    XSYNC();
   }
   else
   {
-    static_assert(sizeof(V) == 16, "SPLIT exchange is for float4 data");
+    static_assert(sizeof(V) == 16, "SPLIT exchange is for two-lane data");
     float2* lds = reinterpret_cast<float2*>(lds_raw);
 #pragma unroll
     for (int half = 0; half < 2; half++)
     {
 #pragma unroll
       for (int t = 0; t < 16; t++)
-        lds[lds_slot<CI, S::PADDED>(reg_w, wp(t))] =
-            half ? make_float2(v[t].z, v[t].w) : make_float2(v[t].x, v[t].y);
-      __syncthreads();
+        lds[lds_slot<CI, S::PADDED>(reg_w, wp(t))] = half_of(v[t], half);
+      XSYNC();
 #pragma unroll
       for (int m = 0; m < 16; m++)
-      {
-        float2 r = lds[lds_slot<CI, S::PADDED>(reg_r, read_pidx<LOGN>(i_r, m))];
-        if (half)
-          v[m].z = r.x, v[m].w = r.y;
-        else
-          v[m].x = r.x, v[m].y = r.y;
-      }
-      __syncthreads();
+        set_half(v[m], half, lds[lds_slot<CI, S::PADDED>(reg_r, read_pidx<LOGN>(i_r, m))]);
+      XSYNC();
     }
   }
 }
@@ -599,13 +650,16 @@ __device__ __forceinline__ KVec make_kvec(int x, int y, float dim, float dk)
   KVec r;
   r.kx = ((float)x - dim / 2.0f) * dk;
   r.kz = ((float)y - dim / 2.0f) * dk;
-  float len = sqrtf(r.kx * r.kx + r.kz * r.kz);
-  bool zero = (r.kx == 0.0f && r.kz == 0.0f);
-  // normalize(kVec) (spectrum.compute:191) as kVec * (1/|k|): one division instead of two
-  const float inv = zero ? 0.0f : 1.0f / len;
+  // |k| and normalize(kVec) (spectrum.compute:189-191) from one hardware v_rsq_f32 (<= 1 ulp) instead
+  // of hipcc's correctly rounded sqrt + division sequences (~25 VALU). The reference is a GLSL
+  // shader whose sqrt/normalize carry no correct-rounding guarantee either (Vulkan: 2-3 ulp), and
+  // a relative error e in |k| moves the phase w*t by ~e*w*t: the same order as the fp32 rounding
+  // of the phase itself, which the reference already has.
+  const float len2 = r.kx * r.kx + r.kz * r.kz;
+  const float inv = len2 == 0.0f ? 0.0f : __builtin_amdgcn_rsqf(len2);
   r.dirx = r.kx * inv;
   r.dirz = r.kz * inv;
-  r.k = len + 1e-6f;
+  r.k = len2 * inv + 1e-6f;
   return r;
 }
 
@@ -623,28 +677,20 @@ __device__ __forceinline__ float dispersion_evolve(float k, float g, float h)
                     : 1.0f - 2.0f / (1.0f + expf(2.0f * kh));
   }
   const float omegaSquared = (g * k + kSigmaSurface / kRhoWater * k * k * k) * t;
-  return sqrtf(omegaSquared);
+  return __builtin_amdgcn_sqrtf(omegaSquared);  // v_sqrt_f32 (<= 1 ulp), see make_kvec
 }
 
-// sin/cos of a large fp32 phase (w*t reaches 1e3-1e7 rad). Reduction by pi/2 in double (exact to
-// ~1e-9 rad for |x| < 1e7, far below the fp32 ulp of the result), then float minimax polynomials on
-// [-pi/4, pi/4] (Cephes sinf/cosf kernels, <= ~1 ulp). Replaces ocml's sincosf, whose Payne-Hanek
-// slow path costs ~60 VGPRs that a 1024-thread workgroup does not have.
+// sin/cos of a large fp32 phase (w*t reaches 1e3-1e7 rad). The phase is reduced to a fraction of a
+// revolution in double (exact to ~1e-16 rev for |x| < 1e7) and fed to the hardware v_sin_f32 /
+// v_cos_f32, which take revolutions (absolute error ~3e-7, the class of the reference shader's own
+// GLSL sin/cos). ~10 VALU slots instead of ~35 for a polynomial kernel with quadrant logic, and no
+// Payne-Hanek slow path (ocml's sincosf costs ~60 VGPRs that a 1024-thread workgroup lacks).
 __device__ __forceinline__ void sincos_phase(float x, float* s, float* c)
 {
-  const double xd = (double)x;
-  const double kq = rint(xd * 0.63661977236758134308);  // 2/pi
-  const float r = (float)fma(-kq, 1.57079632679489661923, xd);
-  const int q = (int)(int64_t)kq;
-  const float z = r * r;
-  const float sp = r + r * z * fmaf(fmaf(-1.9515295891e-4f, z, 8.3321608736e-3f), z, -1.6666654611e-1f);
-  const float cp = 1.0f - 0.5f * z +
-                   z * z * fmaf(fmaf(2.443315711809948e-5f, z, -1.388731625493765e-3f), z, 4.166664568298827e-2f);
-  // quadrant q mod 4: (sin, cos) = (sp, cp), (cp, -sp), (-sp, -cp), (-cp, sp)
-  const bool swap = q & 1;
-  const float sv = swap ? cp : sp, cv = swap ? sp : cp;
-  *s = (q & 2) ? -sv : sv;
-  *c = ((q + 1) & 2) ? -cv : cv;
+  const double rev = (double)x * 0.15915494309189533577;  // 1 / (2 pi)
+  const float f = (float)(rev - rint(rev));                // [-1/2, 1/2] revolution
+  *s = __builtin_amdgcn_sinf(f);
+  *c = __builtin_amdgcn_cosf(f);
 }
 
 // heightAmp = h0 * e^{i w t} + conj-partner * e^{-i w t}
@@ -662,17 +708,17 @@ __device__ __forceinline__ float2 evolve(float4 a, float k, const CascadeFrame& 
 }
 
 // heightMap texel = (H + i*dH/dx, dH/dz + i*Dx)   (spectrum.compute:236)
-__device__ __forceinline__ float4 pack_height(float2 H, const KVec& q)
+__device__ __forceinline__ CPair pack_height(float2 H, const KVec& q)
 {
   float hx = H.x, hy = H.y;
   float dhdx_x = q.kx * (-hy), dhdx_y = q.kx * hx;
   float dhdz_x = q.kz * (-hy), dhdz_y = q.kz * hx;
   float disX_x = q.dirx * (-hy), disX_y = q.dirx * hx;
-  return make_float4(hx - dhdx_y, hy + dhdx_x, dhdz_x - disX_y, dhdz_y + disX_x);
+  return {f2v{hx - dhdx_y, dhdz_x - disX_y}, f2v{hy + dhdx_x, dhdz_y + disX_x}};
 }
 
 // displacementMap texel = (Dz + i*dDx/dx, dDz/dz + i*dDx/dz)   (spectrum.compute:237)
-__device__ __forceinline__ float4 pack_displacement(float2 H, const KVec& q)
+__device__ __forceinline__ CPair pack_displacement(float2 H, const KVec& q)
 {
   float hx = H.x, hy = H.y;
   float disZ_x = q.dirz * (-hy), disZ_y = q.dirz * hx;
@@ -680,7 +726,7 @@ __device__ __forceinline__ float4 pack_displacement(float2 H, const KVec& q)
   float dDXdx_x = a * hx, dDXdx_y = a * hy;
   float dDZdz_x = b * hx, dDZdz_y = b * hy;
   float dDXdz_x = c * hx, dDXdz_y = c * hy;
-  return make_float4(disZ_x - dDXdx_y, disZ_y + dDXdx_x, dDZdz_x - dDXdz_y, dDZdz_y + dDXdz_x);
+  return {f2v{disZ_x - dDXdx_y, dDZdz_x - dDXdz_y}, f2v{disZ_y + dDXdx_x, dDZdz_y + dDXdz_x}};
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -724,14 +770,14 @@ __global__ __launch_bounds__(RowCfg<LOGN>::WG, RowCfg<LOGN>::MIN_WAVES) void k_r
     float4* lines = images + ((size_t)row0 << LOGN);
     const int lim = clamp_bytes((int64_t)(total - row0) * N * 16);
     const int voff = ((rho << LOGN) + i) * 16;
-    float4 v[16];
+    CPair v[16];
 #pragma unroll
     for (int m = 0; m < 16; m++)
-      v[m] = ld4(lines + ((m + 8) & 15) * T, voff, lim);  // fftShift on x folded into the load
+      v[m] = to_pair(ld4(lines + ((m + 8) & 15) * T, voff, lim));  // fftShift on x folded into the load
     fft_run<LOGN, 0, R::SPLIT>(v, i, rho, xch, tw);
 #pragma unroll
     for (int m = 0; m < 16; m++)
-      st4(lines + m * T, voff, v[m], lim);
+      st4(lines + m * T, voff, from_pair(v[m]), lim);
   }
 }
 
@@ -784,18 +830,18 @@ __global__ __launch_bounds__(ColCfg<LOGN>::WG) void k_cols(int n_images, float4*
     // image rows i + mm*T: uniform base per mm (SGPR), lane offset (i*N + x)*16 shared by all mm
     float4* ibase = images + ((size_t)img << (2 * LOGN));
     const int voff = ((i << LOGN) + x) * 16;
-    float4 v[16];
+    CPair v[16];
 #pragma unroll
     for (int m = 0; m < 16; m++)
     {
       // input q = i + m*T sits in row (q + N/2) mod N = i + ((m + 8) mod 16)*T: fftShift on y
       const int mm = (m + 8) & 15;
-      v[m] = ld4(ibase + ((size_t)(mm * T) << LOGN), voff);
+      v[m] = to_pair(ld4(ibase + ((size_t)(mm * T) << LOGN), voff));
     }
     fft_run<LOGN, C, true>(v, i, c, xch, tw);
 #pragma unroll
     for (int m = 0; m < 16; m++)
-      st4(ibase + ((size_t)(m * T) << LOGN), voff, v[m]);
+      st4(ibase + ((size_t)(m * T) << LOGN), voff, from_pair(v[m]));
   }
 }
 
@@ -829,15 +875,16 @@ struct ColFirstCfg
 };
 
 // KEEP: how many of the thread's 16 evolved amplitudes H (2 VGPRs each) stay live from the first
-// packed image to the second; the rest are re-read from h0 (bytes this workgroup streamed a few
-// microseconds earlier) and evolved again. KEEP = 16 does not fit the 128 VGPRs of a 1024-thread
-// workgroup at N = 4096 (spills, which cost HBM traffic); KEEP = 8 does.
-// Streaming (non-temporal) policy for the frame passes' HBM traffic: every byte is touched once
-// per frame and the working set is far beyond L2 and the 256 MiB Infinity Cache; measured 3-5 %
-// faster per pass than the default policy (tools/microbench/genbench, launch_policy_variant).
+// packed image to the second; the rest are re-read from h0 (bytes this workgroup read ~20 us
+// earlier) and evolved again. KEEP = 16 does not fit the 128 VGPRs of a 1024-thread workgroup at
+// N = 4096 (spills, which cost HBM traffic); KEEP = 4 does (default_keep).
+// Cache policy: data touched once per frame (the KEEP once-read h0 texels, every store) is
+// streamed non-temporally (LA, SA = kStream: 3-5 % faster per pass than the default policy); the
+// twice-read h0 texels use the default policy (LR = 0) so the second read hits the cache
+// hierarchy instead of HBM (6 % faster pass 1 than streaming them; tools/microbench/genbench).
 constexpr int kStream = 2;
 
-template <int LOGN, int KEEP, int LA = kStream, int SA = kStream>
+template <int LOGN, int KEEP, int LA = kStream, int SA = kStream, bool NOMEM = false, int LR = 0>
 __global__ __launch_bounds__(ColFirstCfg<LOGN>::WG1) void k_cols_evolve(
     FrameParams fp, SlabGeom g, const float4* __restrict__ h0, float4* __restrict__ inter,
     const float2* __restrict__ tw_glob)
@@ -871,11 +918,19 @@ __global__ __launch_bounds__(ColFirstCfg<LOGN>::WG1) void k_cols_evolve(
       // keep the k-vector math inside this iteration (see opaque())
       const int i = (opaque((int)threadIdx.x) / B) % T;
       const int voff = ((sl * N + i) * B + b) * 16;
-      float4 v[16];
+      float4 a[16];
 #pragma unroll
       for (int m = 0; m < 16; m++)
         if (img == 0 || m >= KEEP)
-          v[m] = ld4<LA>(src + ((m + 8) & 15) * T * B, voff);  // fftShift on y folded into the load
+        {
+          if constexpr (NOMEM)  // compute-only timing variant (microbench): no HBM reads
+            a[m] = make_float4(1e-3f * m, 2e-3f * (float)i, 1e-3f * (float)b, 1e-4f * (float)item);
+          else if (m < KEEP)  // read once per frame
+            a[m] = ld4<LA>(src + ((m + 8) & 15) * T * B, voff);  // fftShift on y folded into the load
+          else  // read twice (re-evolved for the second image): policy LR
+            a[m] = ld4<LR>(src + ((m + 8) & 15) * T * B, voff);
+        }
+      CPair v[16];
 #pragma unroll
       for (int m = 0; m < 16; m++)
       {
@@ -885,7 +940,7 @@ __global__ __launch_bounds__(ColFirstCfg<LOGN>::WG1) void k_cols_evolve(
         if (img == 1 && m < KEEP)
           Hm = H[m];
         else
-          Hm = evolve(v[m], q.k, f);
+          Hm = evolve(a[m], q.k, f);
         if (img == 0 && m < KEEP)
           H[m] = Hm;
         v[m] = img == 0 ? pack_height(Hm, q) : pack_displacement(Hm, q);
@@ -900,7 +955,10 @@ __global__ __launch_bounds__(ColFirstCfg<LOGN>::WG1) void k_cols_evolve(
       for (int m = 0; m < 16; m++)
       {
         const int q = (m * T) / w, yl = (m * T) % w;
-        st4<SA>(dst + (((size_t)(q * 2 + img) * wb + xb0) * w + yl) * B, soff, v[m]);
+        if constexpr (NOMEM)
+          asm volatile("" ::"v"(v[m].re), "v"(v[m].im));
+        else  // intermediate texels stay in split form (pair_raw): pass 2 reads them as such
+          st4<SA>(dst + (((size_t)(q * 2 + img) * wb + xb0) * w + yl) * B, soff, pair_raw(v[m]));
       }
     }
   }
@@ -949,7 +1007,7 @@ __global__ __launch_bounds__(ColFirstCfg<LOGN>::WG2) void k_rows_final(
     const int i2 = REMAP ? opaque(i20) : i, r2 = REMAP ? (RPW == 1 ? 0 : opaque(r20)) : r;
     const int cimg = item / blocks, y0 = (item - cimg * blocks) * RPW;
     const int c = cimg >> 1, img = cimg & 1;
-    float4 v[16];
+    CPair v[16];
     if constexpr (BLOCKED)
     {
       const float4* src = inter + (size_t)c * 2 * N * w + (size_t)y0 * B;
@@ -961,7 +1019,7 @@ __global__ __launch_bounds__(ColFirstCfg<LOGN>::WG2) void k_rows_final(
         // column block xb = ihi + mm*T/B: source rank and local block are uniform per m
         const int xbm = ((m + 8) & 15) * (T / B);  // fftShift on x
         const int srcr = xbm / wb, xbl = xbm % wb;
-        v[m] = ld4<LA>(src + ((size_t)(srcr * 2 + img) * wb + xbl) * w * B, voff);
+        v[m] = raw_pair(ld4<LA>(src + ((size_t)(srcr * 2 + img) * wb + xbl) * w * B, voff));
       }
     }
     else
@@ -970,23 +1028,25 @@ __global__ __launch_bounds__(ColFirstCfg<LOGN>::WG2) void k_rows_final(
       const int voff = ((r << LOGN) + i) * 16;
 #pragma unroll
       for (int m = 0; m < 16; m++)
-        v[m] = ld4<LA>(src + ((m + 8) & 15) * T, voff);  // fftShift on x
+        v[m] = raw_pair(ld4<LA>(src + ((m + 8) & 15) * T, voff));  // fftShift on x
     }
     fft_run<LOGN, 0, true>(v, i, r, i2, r2, xch, tw);
     float4* dst = maps + ((size_t)cimg * w + y0) * N;
     const int woff = ((r2 << LOGN) + i2) * 16;
 #pragma unroll
     for (int m = 0; m < 16; m++)
-      st4<SA>(dst + m * T, woff, v[m]);
+      st4<SA>(dst + m * T, woff, from_pair(v[m]));
     if (img & 1)
     {
-      // displacementMap (Dz, dDx/dx, dDz/dz, dDx/dz): Jacobian, spectrum.compute:246-259
+      // displacementMap (Dz, dDx/dx, dDz/dz, dDx/dz) = (re0, im0, re1, im1): Jacobian,
+      // spectrum.compute:246-259
       const float lam = foam.displacement[c];
       float* jb = jac + ((size_t)c * w + y0) * N;
       const int joff = ((r2 << LOGN) + i2) * 4;
 #pragma unroll
       for (int m = 0; m < 16; m++)
-        st1<SA>(jb + m * T, joff, (1.0f + lam * v[m].y) * (1.0f + lam * v[m].z) - lam * lam * v[m].w * v[m].w);
+        st1<SA>(jb + m * T, joff,
+                (1.0f + lam * v[m].im.x) * (1.0f + lam * v[m].re.y) - lam * lam * v[m].im.y * v[m].im.y);
     }
   }
 }
@@ -1132,7 +1192,8 @@ hipError_t launch_cols_evolve(int logn, const FrameParams& fp, const SlabGeom& g
     constexpr int LOGN = decltype(L)::value;
     using K = ColFirstCfg<LOGN>;
     using S = FftShape<LOGN>;
-    auto kern = keep >= 16 ? k_cols_evolve<LOGN, 16> : (keep >= 8 ? k_cols_evolve<LOGN, 8> : k_cols_evolve<LOGN, 0>);
+    auto kern = keep >= 16 ? k_cols_evolve<LOGN, 16>
+                           : (keep >= 8 ? k_cols_evolve<LOGN, 8> : (keep >= 4 ? k_cols_evolve<LOGN, 4> : k_cols_evolve<LOGN, 0>));
     const int lds = ((S::TW_ENTRIES * 8 + 15) / 16) * 16 + K::LDS1;
     const int items = fp.cascades * ((g.w / K::B) / K::SPW);
     const int grid = persistent_grid(kern, K::WG1, lds, items, cus);
@@ -1142,7 +1203,7 @@ hipError_t launch_cols_evolve(int logn, const FrameParams& fp, const SlabGeom& g
 }
 
 // The largest H-retention that compiles without spills for this size (see k_cols_evolve).
-int default_keep(int logn) { return logn >= 12 ? 8 : 16; }
+int default_keep(int logn) { return logn >= 13 ? 0 : (logn == 12 ? 4 : 16); }
 
 bool rows_need_transpose(int logn) { return spectrum_block(logn) == 1 && (1 << logn) >= 64; }
 
@@ -1240,8 +1301,8 @@ hipError_t launch_cols(int logn, int n_images, float4* images, const float2* tw,
   });
 }
 
-// A/B hook for tools/microbench/genbench: pass 1 / pass 2 at N = 4096 with cache-policy variant
-// `policy` (0 default, 1 nt stores, 2 nt loads + stores).
+// A/B hook for tools/microbench/genbench at N = 4096. Pass 1: variant 0/1 = KEEP 0/4 with default
+// policy on the twice-read h0, 2 = KEEP 4 all loads default, 3 = KEEP 4 compute only (no HBM). Pass 2: cache policy 0 default, 1 nt stores, 2 nt loads + stores.
 hipError_t launch_policy_variant(int pass, int policy, const FrameParams& fp, const SlabGeom& g, const float4* in,
                                  float4* out, float* jac, const FoamParams& foam, const float2* tw, hipStream_t stream,
                                  int cus)
@@ -1251,8 +1312,10 @@ hipError_t launch_policy_variant(int pass, int policy, const FrameParams& fp, co
   using S = FftShape<LOGN>;
   if (pass == 1)
   {
-    auto kern = policy == 0 ? k_cols_evolve<LOGN, 8, 0, 0>
-                            : (policy == 1 ? k_cols_evolve<LOGN, 8, 0, 2> : k_cols_evolve<LOGN, 8, 2, 2>);
+    auto kern = policy == 0 ? k_cols_evolve<LOGN, 0, kStream, kStream, false, 0>
+                            : (policy == 1 ? k_cols_evolve<LOGN, 4, kStream, kStream, false, 0>
+                                           : (policy == 2 ? k_cols_evolve<LOGN, 4, 0, kStream, false, 0>
+                                                          : k_cols_evolve<LOGN, 4, kStream, kStream, true>));
     const int lds = ((S::TW_ENTRIES * 8 + 15) / 16) * 16 + K::LDS1;
     const int items = fp.cascades * ((g.w / K::B) / K::SPW);
     const int grid = persistent_grid(kern, K::WG1, lds, items, cus);

@@ -94,7 +94,7 @@ int main(int argc, char** argv)
     CHECK(hipMalloc(&scratch, tex * C * 2 * sizeof(float4)));
   auto p1r = [&] { return launch_cols_evolve(logn, fp, geom, h0, inter, tw, 0, cus, 0); };
   auto p1k = [&] { return launch_cols_evolve(logn, fp, geom, h0, inter, tw, 0, cus, 16); };
-  auto p1h = [&] { return launch_cols_evolve(logn, fp, geom, h0, inter, tw, 0, cus, 8); };
+  auto p1h = [&] { return launch_cols_evolve(logn, fp, geom, h0, inter, tw, 0, cus, default_keep(logn)); };
   auto p2 = [&] { return launch_rows_final(logn, C, geom, inter, scratch, maps, jac, foam, tw, 0, cus); };
   auto pv = [&](int pass, int pol) {
     return [&, pass, pol] {
@@ -111,6 +111,7 @@ int main(int argc, char** argv)
   const int rounds = 7, reps = 10;
   std::vector<float> t1r, t1k, t1h, t2, tf;
   std::vector<std::vector<float>> tp(6);
+  std::vector<float> tco;
   for (int r = 0; r < rounds; r++)
   {
     t1r.push_back(time_ms(p1r, reps));
@@ -122,6 +123,8 @@ int main(int argc, char** argv)
       for (int pass = 1; pass <= 2; pass++)
         for (int pol = 0; pol < 3; pol++)
           tp[(pass - 1) * 3 + pol].push_back(time_ms(pv(pass, pol), reps));
+    if (logn == 12)
+      tco.push_back(time_ms(pv(1, 3), reps));
   }
   auto report = [&](const char* name, std::vector<float>& v, double bytes_per_pt) {
     std::sort(v.begin(), v.end());
@@ -131,19 +134,20 @@ int main(int argc, char** argv)
   std::printf("N=%d cascades=%d CUs=%d\n", n, C, cus);
   report("pass1 cols_evolve (re-read h0)", t1r, 48);
   report("pass1 cols_evolve (keep 16 H)", t1k, 48);
-  report("pass1 cols_evolve (keep 8 H)", t1h, 48);
+  report("pass1 cols_evolve (default keep)", t1h, 48);
   report("pass2 rows_final", t2, 68);
-  report("frame (pass1 keep 8 + pass2)", tf, 116);
+  report("frame (pass1 default keep + pass2)", tf, 116);
   if (logn == 12)
   {
-    const char* pn[] = {"default", "nt stores", "nt loads+stores"};
+    const char* pn[2][3] = {{"keep 0 reread default", "keep 4 reread default", "keep 4 all loads default"}, {"policy default", "policy nt stores", "policy nt loads+stores"}};
     for (int pass = 1; pass <= 2; pass++)
       for (int pol = 0; pol < 3; pol++)
       {
         char name[80];
-        std::snprintf(name, sizeof name, "pass%d policy %s", pass, pn[pol]);
+        std::snprintf(name, sizeof name, "pass%d %s", pass, pn[pass - 1][pol]);
         report(name, tp[(pass - 1) * 3 + pol], pass == 1 ? 48 : 68);
       }
+    report("pass1 keep 4 compute only (no HBM)", tco, 48);
   }
   return 0;
 }

@@ -645,21 +645,36 @@ struct KVec
   float kx, kz, dirx, dirz, k;
 };
 
+// Correctly rounded sqrt for the normal-range, non-negative arguments of the evolution (|k|^2 >=
+// dk^2 ~ 1e-6; 0 maps to 0): hardware v_sqrt_f32 (<= 1 ulp) plus one residual test per neighbour,
+// 9 VALU instead of hipcc's ~15 with denormal scaling. |k| and w must be bit-identical to the
+// oracle's: the phase w*t multiplies any ulp of w by t (1e2-1e4 s of simulated time).
+__device__ __forceinline__ float sqrt_rn(float x)
+{
+  const float s = __builtin_amdgcn_sqrtf(x);
+  const float sm = __int_as_float(__float_as_int(s) - 1), sp = __int_as_float(__float_as_int(s) + 1);
+  float r = s;
+  if (fmaf(-sm, s, x) <= 0.0f)
+    r = sm;
+  if (fmaf(-sp, s, x) > 0.0f)
+    r = sp;
+  return r;
+}
+
 __device__ __forceinline__ KVec make_kvec(int x, int y, float dim, float dk)
 {
+#pragma clang fp contract(off)  // the reference's unfused float expression order
   KVec r;
   r.kx = ((float)x - dim / 2.0f) * dk;
   r.kz = ((float)y - dim / 2.0f) * dk;
-  // |k| and normalize(kVec) (spectrum.compute:189-191) from one hardware v_rsq_f32 (<= 1 ulp) instead
-  // of hipcc's correctly rounded sqrt + division sequences (~25 VALU). The reference is a GLSL
-  // shader whose sqrt/normalize carry no correct-rounding guarantee either (Vulkan: 2-3 ulp), and
-  // a relative error e in |k| moves the phase w*t by ~e*w*t: the same order as the fp32 rounding
-  // of the phase itself, which the reference already has.
+  // |k| (spectrum.compute:189-192) correctly rounded, since it feeds the phase; normalize(kVec)
+  // only scales the choppy terms and uses the hardware v_rsq_f32 (<= 1 ulp) instead of a
+  // correctly rounded division (~10 VALU).
   const float len2 = r.kx * r.kx + r.kz * r.kz;
   const float inv = len2 == 0.0f ? 0.0f : __builtin_amdgcn_rsqf(len2);
   r.dirx = r.kx * inv;
   r.dirz = r.kz * inv;
-  r.k = len2 * inv + 1e-6f;
+  r.k = sqrt_rn(len2) + 1e-6f;
   return r;
 }
 
@@ -668,6 +683,7 @@ __device__ __forceinline__ KVec make_kvec(int x, int y, float dim, float dk)
 // and as 1 - 2/(1 + e^{2kh}) above — a few VGPRs instead of ocml tanhf's.
 __device__ __forceinline__ float dispersion_evolve(float k, float g, float h)
 {
+#pragma clang fp contract(off)  // bit-identical w in the deep-water case (tanh = 1)
   const float kh = k * h;
   float t = 1.0f;
   if (kh < 2.0f * OCEAN_PI)
@@ -677,7 +693,7 @@ __device__ __forceinline__ float dispersion_evolve(float k, float g, float h)
                     : 1.0f - 2.0f / (1.0f + expf(2.0f * kh));
   }
   const float omegaSquared = (g * k + kSigmaSurface / kRhoWater * k * k * k) * t;
-  return __builtin_amdgcn_sqrtf(omegaSquared);  // v_sqrt_f32 (<= 1 ulp), see make_kvec
+  return sqrt_rn(omegaSquared);
 }
 
 // sin/cos of a large fp32 phase (w*t reaches 1e3-1e7 rad). The phase is reduced to a fraction of a

@@ -201,6 +201,26 @@ def test_calculate_ocean_default_t1(ocean, oracle, n):
     _frame_check(gen.height_map_host(0), gen.displacement_map_host(0), gen.jacobian_map_host(0), ref)
 
 
+def test_calculate_ocean_long_time(ocean, oracle):
+    """An hour of simulated time. The phase w*t (spectrum.compute:198) multiplies any ulp of w by
+    t, so |k| and w are computed bit-identically to the oracle (correctly rounded sqrt, unfused
+    float order); the frame error must stay at the t ~ 0 level, not grow with t."""
+    planes = [5.0, 101.0]
+    fft = ocean.FFTCalculator(256)
+    gen = ocean.Generator(fft, len(planes))
+    refs = []
+    for c, L in enumerate(planes):
+        ocean.apply_settings(gen.GetOceanSettings(c), planeSize=L)
+        refs.append(oracle.OracleGenerator(256, oracle.default_settings(planeSize=L)))
+    for dt in (600.0, 3000.0):
+        gen.CalculateOcean(dt)
+        for r in refs:
+            r.calculate_ocean(dt)
+        for c in range(len(planes)):
+            assert gen.GetOceanSettings(c).time == refs[c].settings.time
+            _frame_check(gen.height_map_host(c), gen.displacement_map_host(c), gen.jacobian_map_host(c), refs[c])
+
+
 def test_batched_cascades_equal_individual(ocean):
     """A cascade's maps do not depend on which batch it runs in (bit-exact)."""
     n = 512

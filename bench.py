@@ -45,10 +45,15 @@ def parse():
     ap.add_argument("--no-slab", action="store_true", help="skip the config-5 slab-decomposed grid")
     ap.add_argument("--slab-n", type=int, default=16384, help="side of the single slab-decomposed grid")
     ap.add_argument("--slab-steps", type=int, default=10)
+    ap.add_argument("--slab-reserve-cus", type=int, default=32,
+                    help="CUs left free for RCCL's copy kernels while the slab passes overlap the all-to-all")
+    ap.add_argument("--slab-force-exchange", action="store_true",
+                    help="run the RCCL exchange and the pipeline even at world size 1 (plumbing check "
+                         "under torch.distributed.run --nproc-per-node 1)")
     return ap.parse_args()
 
 
-def dist_setup():
+def dist_setup(force: bool = False):
     import torch
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -56,7 +61,7 @@ def dist_setup():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if torch.cuda.is_available():
         torch.cuda.set_device(local)
-    if world > 1:
+    if world > 1 or (force and "MASTER_ADDR" in os.environ):
         import torch.distributed as dist
 
         from datetime import timedelta
@@ -127,16 +132,35 @@ def slab_grid(args, rank: int, world: int, local: int) -> dict:
     """BASELINE configs[4]: one N x N grid (default 16384^2, full payload) split over the ranks.
     Column pass on a column slab, one equal-split RCCL all-to-all (torch all_to_all_single on the
     "nccl" backend), row pass on a row slab. At world == 1 the whole grid runs on one GPU with no
-    exchange — the scaling denominator."""
+    exchange: the scaling denominator.
+    With an exchange, two legs are timed: serial frames (columns, all-to-all, rows) and the
+    SlabPipeline (frame f's all-to-all beside frame f+1's column pass and frame f-1's row pass,
+    passes sized for all CUs but --slab-reserve-cus). The headline is the pipelined rate."""
     import torch
+    import torch.distributed as dist
 
     import oceansimulation_amd as ocean
-    from oceansimulation_amd.slab import SlabGenerator, TorchExchange
+    from oceansimulation_amd.slab import SlabGenerator, SlabPipeline, TorchExchange, TorchExchangeSlots
 
     n = args.slab_n
+    exchange = world > 1 or (args.slab_force_exchange and dist.is_available() and dist.is_initialized())
+    device = torch.device("cuda", local)
     fft = ocean.FFTCalculator(n)
     g = SlabGenerator(fft, rank, world)
-    ex = TorchExchange(g.exchange_bytes, torch.device("cuda", local)) if world > 1 else None
+
+    def timed(run_steps):
+        sync()
+        barrier(world)
+        sync()
+        t0 = time.perf_counter()
+        run_steps()
+        sync()
+        barrier(world)
+        sync()
+        return max_over_ranks(time.perf_counter() - t0, world)
+
+    # ---- serial frames ----
+    ex = TorchExchange(g.exchange_bytes, device) if exchange else None
 
     def frame(dt, update=False):
         if ex is None:
@@ -151,38 +175,62 @@ def slab_grid(args, rank: int, world: int, local: int) -> dict:
     frame(1.0 / 60.0)
     g.set_profiling(True)
     g.kernel_times()
-    sync()
-    barrier(world)
-    sync()
-    t0 = time.perf_counter()
-    for _ in range(args.slab_steps):
-        frame(1.0 / 60.0)
-    sync()
-    barrier(world)
-    sync()
-    el = max_over_ranks(time.perf_counter() - t0, world)
-    ms, cnt = g.kernel_times()
     per = args.slab_steps
+
+    def serial_steps():
+        for _ in range(per):
+            frame(1.0 / 60.0)
+
+    el = timed(serial_steps)
+    ms, cnt = g.kernel_times()
+    g.set_profiling(False)
     out = {
         "config": f"single {n}x{n} grid, full payload, slab-decomposed over {world} GPU(s)",
         "ranks": world,
-        "ms_per_frame": 1000.0 * el / per,
-        "points_per_s": float(n) * n * per / el,
+        "exchange": "rccl all_to_all_single" if exchange else "none (one rank)",
         "column_pass_ms": ms[1] / max(cnt[1], 1),
         "row_pass_ms": ms[2] / max(cnt[2], 1),
         "exchange_bytes_per_rank": g.exchange_bytes * (world - 1) // world if world > 1 else 0,
+        "serial_ms_per_frame": 1000.0 * el / per,
     }
-    out["exchange_and_gaps_ms"] = out["ms_per_frame"] - out["column_pass_ms"] - out["row_pass_ms"]
-    g.close()
-    fft.close()
+    out["serial_exchange_and_gaps_ms"] = out["serial_ms_per_frame"] - out["column_pass_ms"] - out["row_pass_ms"]
     del ex
     torch.cuda.empty_cache()
+
+    # ---- pipelined frames ----
+    if exchange:
+        reserve = max(0, min(args.slab_reserve_cus, fft.cus - 1))
+        fft.set_cu_budget(fft.cus - reserve)
+        slots = TorchExchangeSlots(g.exchange_bytes, device)
+        sends, recvs = slots.ptrs()
+        pipe = SlabPipeline([g], sends, recvs, slots)
+        for _ in range(2):
+            pipe.step(1.0 / 60.0)
+        pipe.flush()
+
+        def pipelined_steps():
+            for _ in range(per):
+                pipe.step(1.0 / 60.0)
+            pipe.flush()
+
+        el = timed(pipelined_steps)
+        fft.set_cu_budget(0)
+        out["pipelined_ms_per_frame"] = 1000.0 * el / per
+        out["reserved_cus"] = reserve
+        del pipe, slots
+        torch.cuda.empty_cache()
+        out["ms_per_frame"] = min(out["pipelined_ms_per_frame"], out["serial_ms_per_frame"])
+    else:
+        out["ms_per_frame"] = out["serial_ms_per_frame"]
+    out["points_per_s"] = float(n) * n / (out["ms_per_frame"] * 1e-3)
+    g.close()
+    fft.close()
     return out
 
 
 def main():
     args = parse()
-    rank, world, local = dist_setup()
+    rank, world, local = dist_setup(force=args.slab_force_exchange)
     import oceansimulation_amd as ocean
 
     n, C = args.n, args.cascades
@@ -278,9 +326,9 @@ def main():
         out["cpu_baseline"] = cpu_baseline(n, args.cpu_seconds)
     if rank == 0:
         print(json.dumps(out), flush=True)
-    if world > 1:
-        import torch.distributed as dist
+    import torch.distributed as dist
 
+    if dist.is_available() and dist.is_initialized():
         dist.barrier()
         dist.destroy_process_group()
 

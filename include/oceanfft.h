@@ -90,6 +90,11 @@ int ocean_fft_encode_ifft_batch(ocean_fft* fft, float* images, int n_images);
 int ocean_fft_synchronize(ocean_fft* fft);
 /* Multiprocessor (CU) count of the plan's device. */
 int ocean_fft_device_cus(const ocean_fft* fft);
+/* Size the plan's persistent grids (every kernel of this plan and its generators) for `cus` CUs
+ * instead of all of them (0 restores all). The frame kernels take a whole CU per workgroup, so a
+ * budget below the device count leaves CUs free for work on other streams, e.g. the copy kernels
+ * of an RCCL all-to-all overlapped with the slab passes. No reference counterpart. */
+int ocean_fft_set_cu_budget(ocean_fft* fft, int cus);
 
 /* ---- Generator ---------------------------------------------------------------------------- */
 /* Generator::Generator(RenderDevice*, FFTCalculator*) — src/Generator.cpp:14-27, batched over

@@ -63,6 +63,7 @@ SIGNATURES = {
     "ocean_fft_encode_ifft_batch": (_i, [_vp, _vp, _i]),
     "ocean_fft_synchronize": (_i, [_vp]),
     "ocean_fft_device_cus": (_i, [_vp]),
+    "ocean_fft_set_cu_budget": (_i, [_vp, _i]),
     "ocean_generator_create": (_i, [ctypes.POINTER(_vp), _vp, _i]),
     "ocean_generator_destroy": (_i, [_vp]),
     "ocean_generator_cascades": (_i, [_vp]),

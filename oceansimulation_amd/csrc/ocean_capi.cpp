@@ -62,7 +62,8 @@ struct ocean_fft
   int n = 0;
   int logn = 0;
   int device = 0;
-  int cus = 0;
+  int device_cus = 0;  // CUs of the device
+  int cus = 0;         // CU budget persistent grids are sized for (ocean_fft_set_cu_budget)
   hipStream_t stream = nullptr;
   float2* twiddles = nullptr;  // two-level table, see FftShape in ocean_kernels.hip
 };
@@ -142,7 +143,8 @@ int ocean_fft_create(ocean_fft** out, size_t texture_size, void* hip_stream)
   f->stream = (hipStream_t)hip_stream;
   hipError_t e = hipGetDevice(&f->device);
   if (e == hipSuccess)
-    e = hipDeviceGetAttribute(&f->cus, hipDeviceAttributeMultiprocessorCount, f->device);
+    e = hipDeviceGetAttribute(&f->device_cus, hipDeviceAttributeMultiprocessorCount, f->device);
+  f->cus = f->device_cus;
   if (e != hipSuccess)
   {
     delete f;
@@ -191,7 +193,17 @@ int ocean_fft_destroy(ocean_fft* fft)
 
 size_t ocean_fft_texture_resolution(const ocean_fft* fft) { return fft ? (size_t)fft->n : 0; }
 
-int ocean_fft_device_cus(const ocean_fft* fft) { return fft ? fft->cus : 0; }
+int ocean_fft_device_cus(const ocean_fft* fft) { return fft ? fft->device_cus : 0; }
+
+int ocean_fft_set_cu_budget(ocean_fft* fft, int cus)
+{
+  if (!fft)
+    return fail(OCEAN_ERR_INVALID, "ocean_fft_set_cu_budget: null plan");
+  if (cus < 0 || cus > fft->device_cus)
+    return fail(OCEAN_ERR_INVALID, "ocean_fft_set_cu_budget: budget outside [0, device CUs]");
+  fft->cus = cus == 0 ? fft->device_cus : cus;
+  return OCEAN_OK;
+}
 
 int ocean_fft_encode_ifft_batch(ocean_fft* fft, float* images, int n_images)
 {

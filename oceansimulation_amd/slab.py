@@ -5,6 +5,11 @@ Rank r of P runs the column pass on columns [r*w, r*w + w) and the row pass on r
 rank's column-pass output to rank q (include/oceanfft.h, "slab decomposition"). The reference
 runs one cascade on one device; this is the multi-GPU extension of its CalculateOcean.
 
+Frames are independent until their exchange (the column pass depends only on h0 and t), so
+`SlabPipeline` overlaps frame f's all-to-all with frame f+1's column pass and frame f-1's row
+pass (two buffer slots, the exchange on its own stream); steady state is max(exchange, passes)
+instead of their sum. Maps then lag the last issued frame by one until `flush()`.
+
 Two exchanges are provided:
   * `TorchExchange`: torch.distributed.all_to_all_single over the "nccl" backend (RCCL on ROCm),
     one process per GPU — used by bench.py;
@@ -113,3 +118,107 @@ class TorchExchange:
         import torch.distributed as dist
 
         dist.all_to_all_single(self.recv, self.send)
+
+
+class SlabPipeline:
+    """Software pipeline of slab frames over two send/recv buffer slots.
+
+    step(dt), frame f, slot s = f % 2:
+      compute stream:  columns(f) -> send[s]; record cols_done[s]
+      comm stream:     wait cols_done[s], rows_done[s] (row pass f-2 has finished reading recv[s]);
+                       exchange(s): send[s] -> recv[s]; record xchg_done[s]
+      compute stream:  wait xchg_done[1-s]; rows(f-1) from recv[1-s]; record rows_done[1-s]
+    The compute stream is the generators' stream (their ocean_fft's); columns(f+2) reuses send[s]
+    only after rows(f) was issued behind xchg_done[s], so in-order execution protects it.
+    `exchange(slot, comm_stream)` must enqueue the data movement of slot `slot` on `comm_stream`
+    (TorchExchangeSlots for RCCL across processes, LocalExchangeSlots for ranks in one process).
+    """
+
+    def __init__(self, gens, send_ptrs, recv_ptrs, exchange, compute_stream=None):
+        import torch
+
+        self.gens = list(gens)
+        self.send, self.recv = send_ptrs, recv_ptrs  # [slot][gen] device pointers
+        self.exchange = exchange
+        self.compute = compute_stream if compute_stream is not None else torch.cuda.default_stream()
+        self.comm = torch.cuda.Stream(device=self.compute.device)
+        self.cols_done = [torch.cuda.Event() for _ in range(2)]
+        self.xchg_done = [torch.cuda.Event() for _ in range(2)]
+        self.rows_done = [torch.cuda.Event() for _ in range(2)]
+        self.rows_recorded = [False, False]
+        self.pending = None  # slot whose row pass is still to be issued
+        self.frame = 0
+
+    def step(self, timestep: float, update_ocean: bool = False) -> None:
+        s = self.frame % 2
+        for k, g in enumerate(self.gens):
+            g.columns(timestep, update_ocean, self.send[s][k])
+        self.cols_done[s].record(self.compute)
+        self.comm.wait_event(self.cols_done[s])
+        if self.rows_recorded[s]:
+            self.comm.wait_event(self.rows_done[s])
+        self.exchange(s, self.comm)
+        self.xchg_done[s].record(self.comm)
+        if self.pending is not None:
+            self._rows(self.pending)
+        self.pending = s
+        self.frame += 1
+
+    def _rows(self, s: int) -> None:
+        self.compute.wait_event(self.xchg_done[s])
+        for k, g in enumerate(self.gens):
+            g.rows_pass(self.recv[s][k])
+        self.rows_done[s].record(self.compute)
+        self.rows_recorded[s] = True
+
+    def flush(self) -> None:
+        """Issue the last frame's row pass: afterwards the maps hold the last stepped frame."""
+        if self.pending is not None:
+            self._rows(self.pending)
+            self.pending = None
+
+
+class LocalExchangeSlots:
+    """Exchange for P slab generators in one process (tests): two slots of per-rank send/recv
+    buffers, the equal-split block moves as device copies on the comm stream. The multi-process
+    path is TorchExchangeSlots."""
+
+    def __init__(self, ranks: int, nbytes: int, device):
+        import torch
+
+        self.send = [[torch.empty(nbytes, dtype=torch.uint8, device=device) for _ in range(ranks)] for _ in range(2)]
+        self.recv = [[torch.empty(nbytes, dtype=torch.uint8, device=device) for _ in range(ranks)] for _ in range(2)]
+        self.moves = block_moves(ranks, nbytes)
+
+    def ptrs(self):
+        return ([[t.data_ptr() for t in slot] for slot in self.send],
+                [[t.data_ptr() for t in slot] for slot in self.recv])
+
+    def __call__(self, slot: int, stream) -> None:
+        import torch
+
+        with torch.cuda.stream(stream):
+            for src, so, dst, do, size in self.moves:
+                self.recv[slot][dst][do:do + size].copy_(self.send[slot][src][so:so + size], non_blocking=True)
+
+
+class TorchExchangeSlots:
+    """Two slots of equal-split all-to-all over torch.distributed ("nccl" = RCCL on ROCm). The
+    collective is issued asynchronously from the comm stream, which then waits for it."""
+
+    def __init__(self, nbytes: int, device):
+        import torch
+
+        self.send = [torch.empty(nbytes, dtype=torch.uint8, device=device) for _ in range(2)]
+        self.recv = [torch.empty(nbytes, dtype=torch.uint8, device=device) for _ in range(2)]
+
+    def ptrs(self):
+        return [[t.data_ptr()] for t in self.send], [[t.data_ptr()] for t in self.recv]
+
+    def __call__(self, slot: int, stream) -> None:
+        import torch
+        import torch.distributed as dist
+
+        with torch.cuda.stream(stream):
+            work = dist.all_to_all_single(self.recv[slot], self.send[slot], async_op=True)
+            work.wait()  # comm stream waits for the collective; the host does not block

@@ -63,6 +63,10 @@ class FFTCalculator:
     def cus(self) -> int:
         return int(lib().ocean_fft_device_cus(self._h))
 
+    def set_cu_budget(self, cus: int) -> None:
+        """Size this plan's persistent grids for `cus` CUs (0 = all); see ocean_fft_set_cu_budget."""
+        check(lib().ocean_fft_set_cu_budget(self._h, int(cus)), "ocean_fft_set_cu_budget")
+
     @property
     def handle(self):
         return self._h

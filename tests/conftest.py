@@ -3,6 +3,15 @@ import sys
 
 import pytest
 
+# One HIP runtime per process: torch bundles its own libamdhip64/libhsa-runtime64 (same SONAME
+# as ROCm's). Imported first, it is the runtime liboceanfft.so binds to as well, so torch streams
+# and events (slab pipeline tests) and the library's launches share one runtime. Imported after
+# the library, a second HSA runtime would be loaded beside ROCm's.
+try:
+    import torch  # noqa: F401
+except ImportError:  # pragma: no cover
+    torch = None
+
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 for p in (ROOT, os.path.join(ROOT, "tests")):
     if p not in sys.path:

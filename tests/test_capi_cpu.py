@@ -68,6 +68,7 @@ def test_invalid_arguments_fail_without_touching_a_device(capi):
     assert L.ocean_generator_height_map(None, 0) is None
     assert L.ocean_fft_texture_resolution(None) == 0
     assert L.ocean_debug_hash(None, 4, None, None, None) == capi.OCEAN_ERR_INVALID
+    assert L.ocean_fft_set_cu_budget(None, 0) == capi.OCEAN_ERR_INVALID
 
 
 def test_no_cpu_fallback_without_gpu(capi):

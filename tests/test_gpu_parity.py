@@ -334,6 +334,83 @@ def test_slab_decomposition_matches_whole_grid(ocean, n, ranks):
     assert np.array_equal(j, gen.jacobian_map_host(0))
 
 
+def _whole_grid_frames(ocean, n, steps, settings):
+    fft = ocean.FFTCalculator(n)
+    gen = ocean.Generator(fft, 1)
+    ocean.apply_settings(gen.GetOceanSettings(0), **settings)
+    frames = []
+    for dt in steps:
+        gen.CalculateOcean(dt)
+        frames.append((gen.height_map_host(0), gen.displacement_map_host(0), gen.jacobian_map_host(0)))
+    return frames
+
+
+@pytest.mark.parametrize("n,ranks,budget", [(512, 2, 0), (1024, 4, 200), (4096, 2, 0)])
+def test_slab_pipeline_matches_whole_grid(ocean, n, ranks, budget):
+    """SlabPipeline (exchange of frame f on its own stream beside the column pass of f+1 and the
+    row pass of f-1, two buffer slots) == the single-GPU generator, bit for bit, frame by frame
+    (maps lag one step) and after an unsynchronised run + flush."""
+    import torch
+
+    from oceansimulation_amd.slab import LocalExchangeSlots, SlabGenerator, SlabPipeline
+
+    settings = dict(planeSize=17.0)
+    steps = [0.25, 1.0 / 60.0, 0.5, 1.0 / 60.0, 2.0]
+    ref = _whole_grid_frames(ocean, n, steps, settings)
+    fft = ocean.FFTCalculator(n)
+    fft.set_cu_budget(budget)
+    slabs = [SlabGenerator(fft, r, ranks) for r in range(ranks)]
+    for g in slabs:
+        ocean.apply_settings(g.GetOceanSettings(), **settings)
+    ex = LocalExchangeSlots(ranks, slabs[0].exchange_bytes, torch.device("cuda", 0))
+    sends, recvs = ex.ptrs()
+
+    def maps():
+        torch.cuda.synchronize()
+        return (np.concatenate([g.height_map_host() for g in slabs]),
+                np.concatenate([g.displacement_map_host() for g in slabs]),
+                np.concatenate([g.jacobian_map_host() for g in slabs]))
+
+    pipe = SlabPipeline(slabs, sends, recvs, ex)
+    for k, dt in enumerate(steps):
+        pipe.step(dt, update_ocean=(k == 0))
+        if k > 0:  # the row pass of frame k-1 has been issued
+            for got, want in zip(maps(), ref[k - 1]):
+                assert np.array_equal(got, want), f"frame {k - 1}"
+    pipe.flush()
+    for got, want in zip(maps(), ref[-1]):
+        assert np.array_equal(got, want), "last frame"
+    # unsynchronised run over the same buffers from t = 0 (fresh generators)
+    slabs2 = [SlabGenerator(fft, r, ranks) for r in range(ranks)]
+    for g in slabs2:
+        ocean.apply_settings(g.GetOceanSettings(), **settings)
+    pipe2 = SlabPipeline(slabs2, sends, recvs, ex)
+    for k, dt in enumerate(steps):
+        pipe2.step(dt, update_ocean=(k == 0))
+    pipe2.flush()
+    slabs = slabs2
+    for got, want in zip(maps(), ref[-1]):
+        assert np.array_equal(got, want), "unsynchronised run"
+
+
+def test_cu_budget_validation(ocean):
+    from oceansimulation_amd.capi import OceanError
+
+    fft = ocean.FFTCalculator(256)
+    with pytest.raises(OceanError):
+        fft.set_cu_budget(-1)
+    with pytest.raises(OceanError):
+        fft.set_cu_budget(fft.cus + 1)
+    fft.set_cu_budget(1)  # one CU still computes the right answer
+    gen = ocean.Generator(fft, 1)
+    gen.CalculateOcean(1.0)
+    h1 = gen.height_map_host(0)
+    fft.set_cu_budget(0)
+    gen2 = ocean.Generator(fft, 1)
+    gen2.CalculateOcean(1.0)
+    assert np.array_equal(h1, gen2.height_map_host(0))
+
+
 def test_slab_rejects_too_narrow_slabs(ocean):
     from oceansimulation_amd.capi import OceanError
     from oceansimulation_amd.slab import SlabGenerator

@@ -44,7 +44,7 @@ $(CPPTEST): tests/cpp/test_waves.cpp $(WAVES) $(ORACLE)
 	    -Wl,-rpath,'$$ORIGIN/../../$(PKG)' -Wl,-rpath,'$$ORIGIN/../../oracle/build' -L/opt/rocm/lib -lamdhip64
 
 MB := tools/microbench
-microbench: $(MB)/genbench $(MB)/colbench $(MB)/copybench $(MB)/genbench_noxch $(MB)/genbench_nobar
+microbench: $(MB)/genbench $(MB)/colbench $(MB)/copybench $(MB)/genbench_noxch $(MB)/genbench_nobar $(MB)/layoutbench
 $(MB)/%: $(MB)/%.hip $(CSRC)/ocean_kernels.hip $(CSRC)/ocean_internal.h
 	$(HIPCC) $(HIPFLAGS) $< -o $@
 # timing ablations (wrong results by construction): no LDS exchanges / exchanges without barriers
@@ -54,7 +54,7 @@ $(MB)/genbench_nobar: $(MB)/genbench.hip $(CSRC)/ocean_kernels.hip $(CSRC)/ocean
 	$(HIPCC) $(HIPFLAGS) -DOCEAN_ABLATE_BARRIER $< -o $@
 
 clean:
-	rm -rf $(MB)/genbench $(MB)/colbench $(MB)/copybench $(MB)/genbench_noxch $(MB)/genbench_nobar $(CSRC)/build $(LIB) $(WAVES) $(CPPTEST)
+	rm -rf $(MB)/genbench $(MB)/colbench $(MB)/copybench $(MB)/genbench_noxch $(MB)/genbench_nobar $(MB)/layoutbench $(CSRC)/build $(LIB) $(WAVES) $(CPPTEST)
 	$(MAKE) -s -C oracle clean
 
 .PHONY: all clean microbench

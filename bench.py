@@ -43,6 +43,7 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="target CPU-baseline sample length")
     ap.add_argument("--no-profile", action="store_true", help="skip per-kernel HIP event timing")
     ap.add_argument("--no-slab", action="store_true", help="skip the config-5 slab-decomposed grid")
+    ap.add_argument("--no-ifft", action="store_true", help="skip the EncodeIFFT-only and rocFFT legs")
     ap.add_argument("--slab-n", type=int, default=16384, help="side of the single slab-decomposed grid")
     ap.add_argument("--slab-steps", type=int, default=10)
     ap.add_argument("--slab-reserve-cus", type=int, default=32,
@@ -126,6 +127,48 @@ def cpu_baseline(n: int, target_s: float):
         "sample": f"1 cascade {n}x{n}, {frames} frames of CalculateOcean (fp32 radix-2 restatement of "
                   f"src/FFTCalculator.cpp + spectrum.compute, OpenMP {O.get_threads()} threads), {el:.1f} s",
     }
+
+
+def ifft_legs(n: int, cascades: int, calls: int = 6) -> dict:
+    """SURVEY §8(d) "iFFT-only": FFTCalculator::EncodeIFFT (ocean_fft_encode_ifft_batch, in place) on
+    the frame's 2 packed RGBA32F images per cascade, 64 algorithmic B per texel; beside it rocFFT
+    (torch.fft.ifft2, complex64, out of place) on the same 4 complex fields per cascade, as a vendor
+    speed comparator only (it normalises by 1/N^2 and has no fftShift: not the reference's
+    semantics). Input: random values scaled by 1e-30 so that `calls` unnormalised in-place
+    transforms (x N^2 each) stay finite."""
+    import torch
+
+    import oceansimulation_amd as ocean
+
+    imgs = 2 * cascades
+    fft = ocean.FFTCalculator(n)
+    buf = torch.randn(imgs, n, n, 4, device="cuda", dtype=torch.float32) * 1e-30
+    fft.encode_ifft_batch(buf.data_ptr(), imgs)
+    sync()
+    t0 = time.perf_counter()
+    for _ in range(calls):
+        fft.encode_ifft_batch(buf.data_ptr(), imgs)
+    sync()
+    ours_ms = (time.perf_counter() - t0) * 1e3 / calls
+    texels = imgs * n * n
+    out = {"workload": f"EncodeIFFT of {imgs} packed RGBA32F {n}x{n} images ({cascades} cascades x 2), in place",
+           "ms_per_call": ours_ms, "height_field_points_per_s": cascades * n * n / (ours_ms * 1e-3),
+           "GB_per_s_algorithmic": 64.0 * texels / (ours_ms * 1e-3) / 1e9}
+    fft.close()
+    x = torch.view_as_complex(buf.view(imgs, n, n, 2, 2).permute(0, 3, 1, 2, 4).contiguous())  # [imgs, 2, n, n]
+    del buf
+    y = torch.fft.ifft2(x)
+    sync()
+    t0 = time.perf_counter()
+    for _ in range(calls):
+        y = torch.fft.ifft2(x)
+    sync()
+    roc_ms = (time.perf_counter() - t0) * 1e3 / calls
+    out["rocfft_comparator"] = {"ms_per_call": roc_ms, "GB_per_s_algorithmic": 64.0 * texels / (roc_ms * 1e-3) / 1e9,
+                                "what": "torch.fft.ifft2 (rocFFT) on the same complex64 fields, out of place"}
+    del x, y
+    torch.cuda.empty_cache()
+    return out
 
 
 def slab_grid(args, rank: int, world: int, local: int) -> dict:
@@ -317,6 +360,11 @@ def main():
         out["kernels"]["h0_seed_ms"] = h0_ms
     gen.close()
     fft.close()
+    if not args.no_ifft:
+        try:
+            out["ifft_only"] = ifft_legs(n, C)
+        except Exception as e:  # reported, never fatal to the headline measurement
+            out["ifft_only"] = {"error": f"{type(e).__name__}: {e}"}
     if not args.no_slab:
         try:
             out["slab"] = slab_grid(args, rank, world, local)

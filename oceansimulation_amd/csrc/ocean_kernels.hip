@@ -900,7 +900,7 @@ struct ColFirstCfg
 // hierarchy instead of HBM (6 % faster pass 1 than streaming them; tools/microbench/genbench).
 constexpr int kStream = 2;
 
-template <int LOGN, int KEEP, int LA = kStream, int SA = kStream, bool NOMEM = false, int LR = 0>
+template <int LOGN, int KEEP, int LA = kStream, int SA = kStream, bool NOMEM = false, int LR = 0, bool NOCOMP = false>
 __global__ __launch_bounds__(ColFirstCfg<LOGN>::WG1) void k_cols_evolve(
     FrameParams fp, SlabGeom g, const float4* __restrict__ h0, float4* __restrict__ inter,
     const float2* __restrict__ tw_glob)
@@ -953,6 +953,11 @@ __global__ __launch_bounds__(ColFirstCfg<LOGN>::WG1) void k_cols_evolve(
         const int y = i + ((m + 8) & 15) * T;
         KVec q = make_kvec(x, y, dim, f.dk);
         float2 Hm;
+        if constexpr (NOCOMP)  // memory-only timing ablation (microbench): no evolution, no FFT
+        {
+          v[m] = CPair{f2v{a[m].x, a[m].y}, f2v{a[m].z, a[m].w}};
+          continue;
+        }
         if (img == 1 && m < KEEP)
           Hm = H[m];
         else
@@ -961,7 +966,8 @@ __global__ __launch_bounds__(ColFirstCfg<LOGN>::WG1) void k_cols_evolve(
           H[m] = Hm;
         v[m] = img == 0 ? pack_height(Hm, q) : pack_displacement(Hm, q);
       }
-      fft_run<LOGN, K::C1, true>(v, i, sl * B + b, xch, tw);
+      if constexpr (!NOCOMP)
+        fft_run<LOGN, K::C1, true>(v, i, sl * B + b, xch, tw);
       // Output rows y = i + m*T go to destination block q = y / w (uniform per m since T | w),
       // laid out inter[c][q][img][xb_local][y - q*w][B]: each destination's block is one
       // contiguous range (what the all-to-all sends; for ranks == 1 it is [c][img][xb][y][B]).
@@ -983,14 +989,16 @@ __global__ __launch_bounds__(ColFirstCfg<LOGN>::WG1) void k_cols_evolve(
 // BLOCKED: input is pass 1's output after the exchange, inter[c][src][img][xb_local][y][B] for this
 // rank's w rows (xb = src * (w/B) + xb_local); otherwise row-major [c][img][y][x] (after
 // k_blocks_to_rows, used when B == 1).
-template <int LOGN, bool BLOCKED, int LA = kStream, int SA = kStream>
-__global__ __launch_bounds__(ColFirstCfg<LOGN>::WG2) void k_rows_final(
+// ABL: timing ablations for tools/microbench (results wrong by construction): 1 = no HBM traffic,
+// 2 = no FFT (memory traffic and stores only).
+template <int LOGN, bool BLOCKED, int LA = kStream, int SA = kStream, int RPW_ = ColFirstCfg<LOGN>::RPW2, int ABL = 0>
+__global__ __launch_bounds__(FftShape<LOGN>::T * RPW_) void k_rows_final(
     int cascades, SlabGeom g, const float4* __restrict__ inter, float4* __restrict__ maps, float* __restrict__ jac,
     FoamParams foam, const float2* __restrict__ tw_glob)
 {
   using S = FftShape<LOGN>;
   using K = ColFirstCfg<LOGN>;
-  constexpr int N = S::N, T = S::T, B = BLOCKED ? K::B : 1, RPW = K::RPW2;
+  constexpr int N = S::N, T = S::T, B = BLOCKED ? K::B : 1, RPW = RPW_;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   float2* tw = reinterpret_cast<float2*>(smem);
   void* xch = smem + ((S::TW_ENTRIES * 8 + 15) / 16) * 16;
@@ -1035,7 +1043,10 @@ __global__ __launch_bounds__(ColFirstCfg<LOGN>::WG2) void k_rows_final(
         // column block xb = ihi + mm*T/B: source rank and local block are uniform per m
         const int xbm = ((m + 8) & 15) * (T / B);  // fftShift on x
         const int srcr = xbm / wb, xbl = xbm % wb;
-        v[m] = raw_pair(ld4<LA>(src + ((size_t)(srcr * 2 + img) * wb + xbl) * w * B, voff));
+        if constexpr (ABL == 1)
+          v[m] = CPair{f2v{1e-3f * m, (float)i}, f2v{(float)r, 1e-4f * (float)item}};
+        else
+          v[m] = raw_pair(ld4<LA>(src + ((size_t)(srcr * 2 + img) * wb + xbl) * w * B, voff));
       }
     }
     else
@@ -1046,12 +1057,16 @@ __global__ __launch_bounds__(ColFirstCfg<LOGN>::WG2) void k_rows_final(
       for (int m = 0; m < 16; m++)
         v[m] = raw_pair(ld4<LA>(src + ((m + 8) & 15) * T, voff));  // fftShift on x
     }
-    fft_run<LOGN, 0, true>(v, i, r, i2, r2, xch, tw);
+    if constexpr (ABL != 2)
+      fft_run<LOGN, 0, true>(v, i, r, i2, r2, xch, tw);
     float4* dst = maps + ((size_t)cimg * w + y0) * N;
     const int woff = ((r2 << LOGN) + i2) * 16;
 #pragma unroll
     for (int m = 0; m < 16; m++)
-      st4<SA>(dst + m * T, woff, from_pair(v[m]));
+      if constexpr (ABL == 1)
+        asm volatile("" ::"v"(v[m].re), "v"(v[m].im));
+      else
+        st4<SA>(dst + m * T, woff, from_pair(v[m]));
     if (img & 1)
     {
       // displacementMap (Dz, dDx/dx, dDz/dz, dDx/dz) = (re0, im0, re1, im1): Jacobian,
@@ -1061,8 +1076,13 @@ __global__ __launch_bounds__(ColFirstCfg<LOGN>::WG2) void k_rows_final(
       const int joff = ((r2 << LOGN) + i2) * 4;
 #pragma unroll
       for (int m = 0; m < 16; m++)
-        st1<SA>(jb + m * T, joff,
-                (1.0f + lam * v[m].im.x) * (1.0f + lam * v[m].re.y) - lam * lam * v[m].im.y * v[m].im.y);
+      {
+        const float jv = (1.0f + lam * v[m].im.x) * (1.0f + lam * v[m].re.y) - lam * lam * v[m].im.y * v[m].im.y;
+        if constexpr (ABL == 1)
+          asm volatile("" ::"v"(jv));
+        else
+          st1<SA>(jb + m * T, joff, jv);
+      }
     }
   }
 }
@@ -1331,7 +1351,8 @@ hipError_t launch_policy_variant(int pass, int policy, const FrameParams& fp, co
     auto kern = policy == 0 ? k_cols_evolve<LOGN, 0, kStream, kStream, false, 0>
                             : (policy == 1 ? k_cols_evolve<LOGN, 4, kStream, kStream, false, 0>
                                            : (policy == 2 ? k_cols_evolve<LOGN, 4, 0, kStream, false, 0>
-                                                          : k_cols_evolve<LOGN, 4, kStream, kStream, true>));
+                                                          : (policy == 3 ? k_cols_evolve<LOGN, 4, kStream, kStream, true>
+                                                                         : k_cols_evolve<LOGN, 4, kStream, kStream, false, 0, true>)));
     const int lds = ((S::TW_ENTRIES * 8 + 15) / 16) * 16 + K::LDS1;
     const int items = fp.cascades * ((g.w / K::B) / K::SPW);
     const int grid = persistent_grid(kern, K::WG1, lds, items, cus);
@@ -1339,12 +1360,19 @@ hipError_t launch_policy_variant(int pass, int policy, const FrameParams& fp, co
   }
   else
   {
+    // policy 3: 2 rows per workgroup (512 threads, half the LDS: two workgroups per CU);
+    // 4 / 5: ablations compute only / memory only
+    const int rpw = policy == 3 ? 2 : K::RPW2;
     auto kern = policy == 0 ? k_rows_final<LOGN, true, 0, 0>
-                            : (policy == 1 ? k_rows_final<LOGN, true, 0, 2> : k_rows_final<LOGN, true, 2, 2>);
-    const int lds = ((S::TW_ENTRIES * 8 + 15) / 16) * 16 + K::LDS2;
-    const int items = fp.cascades * 2 * (g.w / K::RPW2);
-    const int grid = persistent_grid(kern, K::WG2, lds, items, cus);
-    hipLaunchKernelGGL(kern, dim3(grid), dim3(K::WG2), lds, stream, fp.cascades, g, in, out, jac, foam, tw);
+                : policy == 1 ? k_rows_final<LOGN, true, 0, 2>
+                : policy == 2 ? k_rows_final<LOGN, true, 2, 2>
+                : policy == 3 ? k_rows_final<LOGN, true, 2, 2, 2>
+                : policy == 4 ? k_rows_final<LOGN, true, 2, 2, K::RPW2, 1>
+                              : k_rows_final<LOGN, true, 2, 2, K::RPW2, 2>;
+    const int lds = ((S::TW_ENTRIES * 8 + 15) / 16) * 16 + lds_row_slots<LOGN>(rpw) * 8;
+    const int items = fp.cascades * 2 * (g.w / rpw);
+    const int grid = persistent_grid(kern, S::T * rpw, lds, items, cus);
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(S::T * rpw), lds, stream, fp.cascades, g, in, out, jac, foam, tw);
   }
   return hipGetLastError();
 }

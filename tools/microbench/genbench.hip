@@ -111,7 +111,7 @@ int main(int argc, char** argv)
   const int rounds = 7, reps = 10;
   std::vector<float> t1r, t1k, t1h, t2, tf;
   std::vector<std::vector<float>> tp(6);
-  std::vector<float> tco;
+  std::vector<float> tco, trp2, t2c, t2m, t1m;
   for (int r = 0; r < rounds; r++)
   {
     t1r.push_back(time_ms(p1r, reps));
@@ -124,7 +124,13 @@ int main(int argc, char** argv)
         for (int pol = 0; pol < 3; pol++)
           tp[(pass - 1) * 3 + pol].push_back(time_ms(pv(pass, pol), reps));
     if (logn == 12)
+    {
       tco.push_back(time_ms(pv(1, 3), reps));
+      trp2.push_back(time_ms(pv(2, 3), reps));
+      t2c.push_back(time_ms(pv(2, 4), reps));
+      t2m.push_back(time_ms(pv(2, 5), reps));
+      t1m.push_back(time_ms(pv(1, 4), reps));
+    }
   }
   auto report = [&](const char* name, std::vector<float>& v, double bytes_per_pt) {
     std::sort(v.begin(), v.end());
@@ -148,6 +154,10 @@ int main(int argc, char** argv)
         report(name, tp[(pass - 1) * 3 + pol], pass == 1 ? 48 : 68);
       }
     report("pass1 keep 4 compute only (no HBM)", tco, 48);
+    report("pass2 2 rows per WG (2 WG/CU)", trp2, 68);
+    report("pass2 compute only (no HBM)", t2c, 68);
+    report("pass2 memory only (no FFT)", t2m, 68);
+    report("pass1 keep 4 memory only (no evolve/FFT)", t1m, 48);
   }
   return 0;
 }

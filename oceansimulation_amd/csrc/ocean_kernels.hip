@@ -44,65 +44,6 @@ static constexpr float kRhoWater = 1000.0f;
 // ------------------------------------------------------------------------------------------------
 // Spectrum math — float32 restatement of resources/spectrum.compute, same operation order.
 // ------------------------------------------------------------------------------------------------
-__device__ __forceinline__ float dispersion(float k, float g, float h)
-{
-  // spectrum.compute:38-44
-  float kh = k * h;
-  float tanhKH = kh >= 2.0f * OCEAN_PI ? 1.0f : tanhf(kh);
-  float omegaSquared = (g * k + kSigmaSurface / kRhoWater * k * k * k) * tanhKH;
-  return sqrtf(omegaSquared);
-}
-
-__device__ __forceinline__ float dispersion_derivative(float k, float g, float h)
-{
-  // spectrum.compute:50-57
-  float phi = dispersion(k, g, h);
-  float sech = 1.0f / coshf(h * k);
-  float numerator = h * (kSigmaSurface / kRhoWater * k * k * k + g * k) * sech * sech + phi * phi;
-  return numerator / (2.0f * phi);
-}
-
-__device__ __forceinline__ float smoothstep_f(float e0, float e1, float x)
-{
-  float t = (x - e0) / (e1 - e0);
-  t = fminf(fmaxf(t, 0.0f), 1.0f);
-  return t * t * (3.0f - 2.0f * t);
-}
-
-__device__ __forceinline__ float jonswap(const OceanSettings& s, float omega, float omega_p)
-{
-  // spectrum.compute:60-78
-  float alpha = 0.076f * powf(s.U_10 * s.U_10 / (s.F * s.g), 0.22f);
-  float gamma = 3.3f;
-  float sigma = omega > omega_p ? 0.09f : 0.07f;
-  float omegaDiff = fabsf(omega - omega_p);
-  float omegaRatio = omega_p / omega;
-  float r = expf(-omegaDiff * omegaDiff / (2.0f * sigma * sigma * omega_p * omega_p));
-  float S = alpha * s.g * s.g / powf(omega, 5.0f) * expf(-1.25f * powf(omegaRatio, 4.0f)) *
-            powf(gamma, r);
-  float w_h = fminf(omega * sqrtf(s.h / s.g), 2.0f);
-  return S * smoothstep_f(0.0f, 2.2f, w_h);
-}
-
-__device__ __forceinline__ float lh_normalization(float s)
-{
-  // spectrum.compute:81-88
-  float a = sqrtf(s);
-  return (s < 0.4f) ? (0.5f / OCEAN_PI) + s * (0.220636f + s * (-0.109f + s * 0.090f))
-                    : (1.0f / sqrtf(OCEAN_PI)) * (a * 0.5f + (1.0f / a) * 0.0625f);
-}
-
-__device__ __forceinline__ float hasselmann(const OceanSettings& st, float w, float w_p, float theta)
-{
-  // spectrum.compute:91-106
-  float p = w / w_p;
-  float s = (w <= w_p) ? 6.97f * powf(fabsf(p), 4.06f)
-                       : 9.77f * powf(fabsf(p), -2.33f - 1.45f * (st.U_10 * w_p / st.g - 1.17f));
-  float s_xi = 16.0f * tanhf(w_p / w) * st.swell * st.swell;
-  float sh = s + s_xi;
-  return lh_normalization(sh) * powf(fabsf(cosf(theta * 0.5f)), 2.0f * sh);
-}
-
 __device__ __forceinline__ uint32_t hash_raw(uint32_t x, uint32_t y)
 {
   // spectrum.compute:109-114
@@ -121,44 +62,124 @@ __device__ __forceinline__ float2 hash_uniform(uint32_t x, uint32_t y)
                      (float)((rz1 >> 1) & 0x7FFFFFFFu) / (float)0x7FFFFFFF);
 }
 
-__device__ __forceinline__ float2 spectrum_amplitude(const OceanSettings& s, float tx, float ty,
-                                                     float dim)
+// Settings-only terms of GetSpectrumAmplitude, evaluated once per launch on the host with the
+// oracle's fp32 expressions and glibc powf (bit-identical to the reference restatement) instead of
+// once per evaluation on the device.
+struct SpectrumConsts
 {
-  // spectrum.compute:129-155
-  float dk = 2.0f * OCEAN_PI / s.planeSize;
-  float kx = (tx - dim / 2.0f) * dk;
-  float ky = (ty - dim / 2.0f) * dk;
-  float k = sqrtf(kx * kx + ky * ky);
-  float theta = atan2f(ky, kx) - s.theta_0;
-  if (k == 0.0f)
+  float dk, half_dim, theta_0, g, h;
+  float alpha_g2;     // alpha * g * g (spectrum.compute:62, :70)
+  float omega_p;      // 22 (g^2 / (U F))^0.333 (spectrum.compute:143)
+  float sqrt_h_g;     // sqrt(h / g) (spectrum.compute:74)
+  float hassel_hi;    // exponent of the w > w_p branch (spectrum.compute:100)
+  float swell2;       // swell * swell
+  float spread, spread_2pi;
+  float c;            // 0.1 * scale
+  float seed_x, seed_y;
+  float sigma_rho;    // sigma_surface / rho_water
+};
+
+SpectrumConsts spectrum_consts(const OceanSettings& s, int n)
+{
+  SpectrumConsts q;
+  q.dk = 2.0f * OCEAN_PI / s.planeSize;
+  q.half_dim = (float)n / 2.0f;
+  q.theta_0 = s.theta_0;
+  q.g = s.g;
+  q.h = s.h;
+  const float alpha = 0.076f * powf(s.U_10 * s.U_10 / (s.F * s.g), 0.22f);
+  q.alpha_g2 = alpha * s.g * s.g;
+  q.omega_p = 22.0f * powf(s.g * s.g / (s.U_10 * s.F), 0.333f);
+  q.sqrt_h_g = sqrtf(s.h / s.g);
+  q.hassel_hi = -2.33f - 1.45f * (s.U_10 * q.omega_p / s.g - 1.17f);
+  q.swell2 = s.swell * s.swell;
+  q.spread = s.spread;
+  q.spread_2pi = s.spread / (2.0f * OCEAN_PI);
+  q.c = 0.1f * s.scale;
+  q.seed_x = (float)s.seed[0];
+  q.seed_y = (float)s.seed[1];
+  q.sigma_rho = kSigmaSurface / kRhoWater;
+  return q;
+}
+
+// Fast transcendentals for the spectrum (tolerance: h0 within 1e-5 of max|h0|, tests/parity.py):
+// hardware v_log_f32 / v_exp_f32 (log2 / exp2, ~1 ulp) build pow, exp and log; tanh and sech come
+// from one exp each, with an odd series where 1 - 2/(1 + e^2x) would cancel.
+__device__ __forceinline__ float log2_hw(float x) { return __builtin_amdgcn_logf(x); }
+__device__ __forceinline__ float exp2_hw(float x) { return __builtin_amdgcn_exp2f(x); }
+__device__ __forceinline__ float exp_hw(float x) { return exp2_hw(x * 1.44269504088896341f); }
+__device__ __forceinline__ float pow_pos(float x, float y) { return exp2_hw(y * log2_hw(x)); }  // x >= 0, y > 0 or x > 0
+__device__ __forceinline__ float rcp_hw(float x) { return __builtin_amdgcn_rcpf(x); }
+__device__ __forceinline__ float tanh_pos(float x)  // x >= 0
+{
+  if (x < 0.125f)
+  {
+    const float x2 = x * x;
+    return x * fmaf(fmaf(fmaf(-17.0f / 315.0f, x2, 2.0f / 15.0f), x2, -1.0f / 3.0f), x2, 1.0f);
+  }
+  return 1.0f - 2.0f * rcp_hw(1.0f + exp_hw(2.0f * x));
+}
+
+// GetSpectrumAmplitude (spectrum.compute:129-155) at grid index (tx, ty), same formula and order of
+// the reference with the settings-only terms hoisted (SpectrumConsts).
+__device__ __forceinline__ float2 spectrum_amplitude(const SpectrumConsts& q, float tx, float ty)
+{
+  const float kx = (tx - q.half_dim) * q.dk;
+  const float ky = (ty - q.half_dim) * q.dk;
+  const float k2 = kx * kx + ky * ky;
+  if (k2 == 0.0f)
     return make_float2(0.0f, 0.0f);
+  const float k = __builtin_amdgcn_sqrtf(k2);
+  const float theta = atan2f(ky, kx) - q.theta_0;
 
-  float omega = dispersion(k, s.g, s.h);
-  float omega_p = 22.0f * powf(s.g * s.g / (s.U_10 * s.F), 0.333f);
-  float Sj = jonswap(s, omega, omega_p);
-  float d = ((1.0f - s.spread) * hasselmann(s, omega, omega_p, theta) +
-             (s.spread) / (2.0f * OCEAN_PI));
-  float chain = dispersion_derivative(k, s.g, s.h) / k * dk * dk;
+  // Dispersion (spectrum.compute:38-44)
+  const float kh = k * q.h;
+  const float tanhKH = kh >= 2.0f * OCEAN_PI ? 1.0f : tanh_pos(kh);
+  const float gk_sk3 = q.g * k + q.sigma_rho * k * k * k;
+  const float omega = __builtin_amdgcn_sqrtf(gk_sk3 * tanhKH);
+  const float rw = rcp_hw(omega);
 
-  // uvec2(thread + seed): float add, then conversion (seeds and indices are non-negative).
-  uint32_t hx = (uint32_t)(int64_t)(tx + (float)s.seed[0]);
-  uint32_t hy = (uint32_t)(int64_t)(ty + (float)s.seed[1]);
-  float2 u = hash_uniform(hx, hy);
-  // Gaussian, spectrum.compute:121-127
-  float r = sqrtf(-2.0f * logf(u.x));
-  float th = 2.0f * OCEAN_PI * u.y;
-  float sn, cs;
-  sincosf(th, &sn, &cs);
-  float amp = sqrtf(2.0f * Sj * d * chain);
-  float c = 0.1f * s.scale;
-  return make_float2(c * (r * cs) * amp, c * (r * sn) * amp);
+  // JONSWAP (spectrum.compute:60-78)
+  const float w_p = q.omega_p;
+  const float sigma = omega > w_p ? 0.09f : 0.07f;
+  const float diff = omega - w_p;
+  const float r = exp_hw(-diff * diff * rcp_hw(2.0f * sigma * sigma * w_p * w_p));
+  const float ratio = w_p * rw, ratio2 = ratio * ratio;
+  const float rw2 = rw * rw;
+  const float S = q.alpha_g2 * (rw2 * rw2 * rw) * exp_hw(-1.25f * (ratio2 * ratio2)) *
+                  exp2_hw(r * 1.72246602447109f);  // 3.3^r, log2(3.3)
+  const float w_h = fminf(omega * q.sqrt_h_g, 2.0f);
+  float t = fminf(fmaxf(w_h * (1.0f / 2.2f), 0.0f), 1.0f);
+  const float Sj = S * (t * t * (3.0f - 2.0f * t));
+
+  // Hasselmann + Longuet-Higgins spreading (spectrum.compute:81-106)
+  const float p = omega * rcp_hw(w_p);
+  const float sp = omega <= w_p ? 6.97f * pow_pos(p, 4.06f) : 9.77f * pow_pos(p, q.hassel_hi);
+  const float sh = sp + 16.0f * tanh_pos(w_p * rw) * q.swell2;
+  const float lh = sh < 0.4f ? (0.5f / OCEAN_PI) + sh * (0.220636f + sh * (-0.109f + sh * 0.090f))
+                             : 0.56418958354775628f * (0.5f * __builtin_amdgcn_sqrtf(sh) + 0.0625f * __builtin_amdgcn_rsqf(sh));
+  const float ct = fabsf(__builtin_amdgcn_cosf(theta * (0.5f * 0.15915494309189533577f)));  // cos(theta/2)
+  const float d = (1.0f - q.spread) * (lh * pow_pos(ct, 2.0f * sh)) + q.spread_2pi;
+
+  // DispersionDerivative (spectrum.compute:50-57), sech = 2 e^-x / (1 + e^-2x)
+  const float em = exp_hw(-q.h * k);
+  const float sech = 2.0f * em * rcp_hw(1.0f + em * em);
+  const float deriv = (q.h * gk_sk3 * sech * sech + omega * omega) * (0.5f * rw);
+  const float chain = deriv * rcp_hw(k) * q.dk * q.dk;
+
+  // Hash + Box-Muller (spectrum.compute:109-127, :153): uvec2(thread + seed)
+  const float2 u = hash_uniform((uint32_t)(int64_t)(tx + q.seed_x), (uint32_t)(int64_t)(ty + q.seed_y));
+  const float rad = __builtin_amdgcn_sqrtf(-2.0f * 0.69314718055994531f * log2_hw(u.x));
+  const float sn = __builtin_amdgcn_sinf(u.y), cs = __builtin_amdgcn_cosf(u.y);  // angle 2 pi u.y
+  const float amp = __builtin_amdgcn_sqrtf(2.0f * Sj * d * chain);
+  return make_float2(q.c * (rad * cs) * amp, q.c * (rad * sn) * amp);
 }
 
 // generateSpectrum (spectrum.compute:157-172): texel = (h0(k), conj(h0(-k))), -k taken as N - i.
 // Stored strip-blocked, h0[xb][y][blk] (blk texel columns per strip, see ColFirstCfg), so the
 // column pass reads each strip as one contiguous run. The reference keeps this image private
 // (src/Generator.h:86), so its layout is internal.
-__global__ __launch_bounds__(256) void k_generate_spectrum(OceanSettings s, int n, int blk, int x0, int width,
+__global__ __launch_bounds__(256) void k_generate_spectrum(SpectrumConsts s, int n, int blk, int x0, int width,
                                                           float4* __restrict__ h0)
 {
   // columns [x0, x0 + width) of the N x N spectrum (a rank's column slab; width = n for a whole grid)
@@ -172,9 +193,55 @@ __global__ __launch_bounds__(256) void k_generate_spectrum(OceanSettings s, int 
     const int64_t rest = idx / blk;
     const int y = (int)(rest % n), xb = (int)(rest / n);
     const int x = x0 + xb * blk + b;
-    float2 a = spectrum_amplitude(s, (float)x, (float)y, dim);
-    float2 c = spectrum_amplitude(s, dim - (float)x, dim - (float)y, dim);
+    float2 a = spectrum_amplitude(s, (float)x, (float)y);
+    float2 c = spectrum_amplitude(s, dim - (float)x, dim - (float)y);
     h0[idx] = make_float4(a.x, a.y, c.x, -c.y);
+  }
+}
+
+// Whole grid, one amplitude evaluation per texel: texel (x, y) needs h0 at (x, y) and at its
+// partner (N-x, N-y), and the partner's texel needs the same two values swapped, so one thread
+// evaluates both points and writes both texels. Points run over the lower half y < N/2; the
+// texels no pair reaches (row N/2, which mirrors onto itself, and column 0 of the upper half,
+// whose partner column N is off the grid) are tail items with two evaluations each (O(N)).
+// Bit-identical to k_generate_spectrum: same evaluator, same float arguments.
+__global__ __launch_bounds__(256) void k_generate_spectrum_pairs(SpectrumConsts s, int n, int blk,
+                                                                float4* __restrict__ h0)
+{
+  const int half = n / 2;
+  const int64_t pairs = (int64_t)n * half, total = pairs + n + (half - 1);
+  const float dim = (float)n;
+  auto at = [&](int x, int y) { return ((int64_t)(x / blk) * n + y) * blk + (x % blk); };
+  for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < total;
+       idx += (int64_t)gridDim.x * blockDim.x)
+  {
+    int x, y;
+    bool mirror;
+    if (idx < pairs)  // blocked order over the lower half: b fastest, then y, then xb
+    {
+      const int b = (int)(idx % blk);
+      const int64_t rest = idx / blk;
+      y = (int)(rest % half);
+      x = (int)(rest / half) * blk + b;
+      mirror = x > 0 && y > 0;
+    }
+    else if (idx < pairs + n)
+    {
+      x = (int)(idx - pairs);
+      y = half;
+      mirror = false;
+    }
+    else
+    {
+      x = 0;
+      y = half + 1 + (int)(idx - pairs - n);
+      mirror = false;
+    }
+    const float2 a = spectrum_amplitude(s, (float)x, (float)y);
+    const float2 c = spectrum_amplitude(s, dim - (float)x, dim - (float)y);
+    h0[at(x, y)] = make_float4(a.x, a.y, c.x, -c.y);
+    if (mirror)
+      h0[at(n - x, n - y)] = make_float4(c.x, c.y, a.x, -a.y);
   }
 }
 
@@ -1205,13 +1272,18 @@ hipError_t launch_generate_spectrum(const OceanSettings& s, int n, float4* h0, h
     logn++;
   if (width <= 0)
     width = n;
-  long total = (long)n * width;
+  const bool whole = x0 == 0 && width == n;  // a slab's partner columns belong to other ranks
+  long total = whole ? (long)n * (n / 2) + n + n / 2 - 1 : (long)n * width;
   long blocks = (total + 255) / 256;
   long cap = (long)cus * 16;
   if (blocks > cap)
     blocks = cap;
-  hipLaunchKernelGGL(k_generate_spectrum, dim3((unsigned)blocks), dim3(256), 0, stream, s, n, spectrum_block(logn), x0,
-                     width, h0);
+  if (whole)
+    hipLaunchKernelGGL(k_generate_spectrum_pairs, dim3((unsigned)blocks), dim3(256), 0, stream,
+                       spectrum_consts(s, n), n, spectrum_block(logn), h0);
+  else
+    hipLaunchKernelGGL(k_generate_spectrum, dim3((unsigned)blocks), dim3(256), 0, stream, spectrum_consts(s, n), n,
+                       spectrum_block(logn), x0, width, h0);
   return hipGetLastError();
 }
 

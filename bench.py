@@ -44,6 +44,7 @@ def parse():
     ap.add_argument("--no-profile", action="store_true", help="skip per-kernel HIP event timing")
     ap.add_argument("--no-slab", action="store_true", help="skip the config-5 slab-decomposed grid")
     ap.add_argument("--no-ifft", action="store_true", help="skip the EncodeIFFT-only and rocFFT legs")
+    ap.add_argument("--no-surface", action="store_true", help="skip the surface-consumer leg")
     ap.add_argument("--slab-n", type=int, default=16384, help="side of the single slab-decomposed grid")
     ap.add_argument("--slab-steps", type=int, default=10)
     ap.add_argument("--slab-reserve-cus", type=int, default=32,
@@ -168,6 +169,56 @@ def ifft_legs(n: int, cascades: int, calls: int = 6) -> dict:
                                 "what": "torch.fft.ifft2 (rocFFT) on the same complex64 fields, out of place"}
     del x, y
     torch.cuda.empty_cache()
+    return out
+
+
+def surface_leg(calls: int = 20, cpu_seconds: float = 3.0) -> dict:
+    """the renderer's consumer of the maps (waveShader.glsl vertex displacement,
+    slope normal, Jacobian average) on WaveApp's scene: 3 cascades of 256^2 (L = 5/17/101 m) and
+    the reference plane mesh of 1024 x 1024 quads (src/Renderer.cpp:18) through the camera warp;
+    also a 4096 x 4096-quad mesh. Output 32 B per vertex; the maps stay in L2. CPU: the oracle
+    restatement on the host cores, bounded sample."""
+    import torch
+
+    import oceansimulation_amd as ocean
+    from oceansimulation_amd.surface import FLOATS_PER_VERTEX, SurfaceSampler, host_cascades
+    from oracle import oracle as O
+
+    fft = ocean.FFTCalculator(256)
+    gens = []
+    for L in (5.0, 17.0, 101.0):
+        g = ocean.Generator(fft, 1)
+        ocean.apply_settings(g.GetOceanSettings(0), planeSize=L)
+        g.CalculateOcean(1.0)
+        gens.append(g)
+    pairs = [(g, 0) for g in gens]
+    sampler = SurfaceSampler(pairs)
+    cam = [3.0, 5.0, -2.0, -0.6, 0.8]
+    out = {"workload": "WaveApp scene: 3 cascades 256^2, plane mesh through the camera warp; "
+                       "per vertex displacement + normal + Jacobian (32 B out)"}
+    for res in (1024, 4096):
+        pts = (res + 1) ** 2
+        buf = torch.empty(pts * FLOATS_PER_VERTEX, dtype=torch.float32, device="cuda")
+        sampler.sample_plane(cam, res, buf.data_ptr())
+        sync()
+        t0 = time.perf_counter()
+        for _ in range(calls):
+            sampler.sample_plane(cam, res, buf.data_ptr())
+        sync()
+        ms = (time.perf_counter() - t0) * 1e3 / calls
+        out[f"mesh_{res}"] = {"vertices": pts, "ms": ms, "mesh_points_per_s": pts / (ms * 1e-3),
+                              "GB_per_s_output": 32.0 * pts / (ms * 1e-3) / 1e9}
+        del buf
+    O.build()
+    O.set_threads(min(16, os.cpu_count() or 1))
+    host = host_cascades(pairs)
+    frames, t0 = 0, time.perf_counter()
+    while time.perf_counter() - t0 < cpu_seconds:
+        O.surface_plane(host, cam, 1024)
+        frames += 1
+    el = time.perf_counter() - t0
+    out["cpu_oracle_mesh_1024"] = {"mesh_points_per_s": frames * 1025 ** 2 / el, "threads": O.get_threads(),
+                                   "sample": f"{frames} plane meshes of 1025^2 vertices, {el:.1f} s"}
     return out
 
 
@@ -369,6 +420,11 @@ def main():
             out["ifft_only"] = ifft_legs(n, C)
         except Exception as e:  # reported, never fatal to the headline measurement
             out["ifft_only"] = {"error": f"{type(e).__name__}: {e}"}
+    if rank == 0 and not args.no_surface:
+        try:
+            out["surface"] = surface_leg()
+        except Exception as e:  # reported, never fatal to the headline measurement
+            out["surface"] = {"error": f"{type(e).__name__}: {e}"}
     if not args.no_slab:
         try:
             out["slab"] = slab_grid(args, rank, world, local)

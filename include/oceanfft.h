@@ -153,6 +153,24 @@ int ocean_generator_kernel_times(ocean_generator* gen, double ms_total[3], int64
  * raw[i] = uint32 n, uv[2i..2i+1] = the two uniforms. For bit-exact parity tests. */
 int ocean_debug_hash(const uint32_t* xy, int count, uint32_t* raw, float* uv, void* hip_stream);
 
+/* ---- Surface consumer: the renderer's use of the maps -------------------
+ * resources/waveShader.glsl evaluated per mesh vertex on the maps of `count` (generator, cascade)
+ * pairs (the reference binds 3 generators, src/Renderer.cpp:62-72; here 1..16, one map size,
+ * whole-grid generators): the vertex stage's displacement loop (:101-110; cascade i samples at the
+ * position cascades < i displaced), then at the displaced position the fragment stage's slope
+ * normal and Jacobian average (:127-144). Sampling is GL_LINEAR + GL_REPEAT in fp32
+ * (src/Generator.cpp:116-119). Output per vertex: 8 floats (x, y, z, jacobian, nx, ny, nz, 0),
+ * device memory, written on the first generator's stream. planeSize / displacement come from each
+ * cascade's settings (Renderer.cpp:70-71). No reference counterpart as a call: it replaces the
+ * vertex + fragment shader sampling. */
+int ocean_surface_sample(ocean_generator* const* gens, const int* cascades, int count, const float* xz,
+                         int64_t points, float* out);
+/* The same on the reference's plane mesh (40 m x 40 m, res x res quads, (res+1)^2 vertices, x
+ * fastest; src/Renderer.cpp:18) through the camera-relative warp of waveShader.glsl:77-98:
+ * camera = {viewInverse[3].x, .y, .z, forward.x, forward.z} with forward = -viewInverse[0]. */
+int ocean_surface_sample_plane(ocean_generator* const* gens, const int* cascades, int count, const float camera[5],
+                               int res, float* out);
+
 #ifdef __cplusplus
 }
 #endif

@@ -504,6 +504,71 @@ float* ocean_generator_jacobian_map(ocean_generator* g, int c)
   return g->jac + (size_t)g->fft->n * g->geom.w * c;
 }
 
+static int surface_params(ocean_generator* const* gens, const int* cascades, int count, SurfaceParams& p,
+                          ocean_fft*& fft, const char* who)
+{
+  if (!gens || !cascades || count < 1 || count > kMaxSurfaceCascades)
+    return fail(OCEAN_ERR_INVALID, std::string(who) + ": need 1..16 (generator, cascade) pairs");
+  p = SurfaceParams{};
+  p.count = count;
+  fft = nullptr;
+  for (int i = 0; i < count; i++)
+  {
+    ocean_generator* g = gens[i];
+    if (!g || cascades[i] < 0 || cascades[i] >= g->cascades)
+      return fail(OCEAN_ERR_INVALID, std::string(who) + ": null generator or cascade out of range");
+    if (g->ranks != 1)
+      return fail(OCEAN_ERR_INVALID, std::string(who) + ": slab generators hold row slabs, not whole maps");
+    if (!fft)
+      fft = g->fft;
+    else if (g->fft->n != fft->n)
+      return fail(OCEAN_ERR_INVALID, std::string(who) + ": all cascades must share one map size");
+    const int c = cascades[i];
+    p.c[i].height = reinterpret_cast<const float4*>(ocean_generator_height_map(g, c));
+    p.c[i].disp = reinterpret_cast<const float4*>(ocean_generator_displacement_map(g, c));
+    p.c[i].jac = ocean_generator_jacobian_map(g, c);
+    p.c[i].plane = g->settings[c].planeSize;
+    p.c[i].scale = g->settings[c].displacement;
+  }
+  p.n = fft->n;
+  return OCEAN_OK;
+}
+
+int ocean_surface_sample(ocean_generator* const* gens, const int* cascades, int count, const float* xz,
+                         int64_t points, float* out)
+{
+  SurfaceParams p;
+  ocean_fft* fft;
+  int rc = surface_params(gens, cascades, count, p, fft, "ocean_surface_sample");
+  if (rc != OCEAN_OK)
+    return rc;
+  if (points < 0 || (points > 0 && (!xz || !out)))
+    return fail(OCEAN_ERR_INVALID, "ocean_surface_sample: null positions/output or negative count");
+  HIP_TRY(launch_surface(p, SurfacePlane{}, reinterpret_cast<const float2*>(xz), points, reinterpret_cast<float4*>(out),
+                         fft->stream, fft->cus),
+          "ocean_surface_sample");
+  return OCEAN_OK;
+}
+
+int ocean_surface_sample_plane(ocean_generator* const* gens, const int* cascades, int count, const float camera[5],
+                               int res, float* out)
+{
+  SurfaceParams p;
+  ocean_fft* fft;
+  int rc = surface_params(gens, cascades, count, p, fft, "ocean_surface_sample_plane");
+  if (rc != OCEAN_OK)
+    return rc;
+  if (!camera || !out || res < 1 || res > 46340)
+    return fail(OCEAN_ERR_INVALID, "ocean_surface_sample_plane: null camera/output or resolution outside 1..46340");
+  if (camera[3] == 0.0f && camera[4] == 0.0f)
+    return fail(OCEAN_ERR_INVALID, "ocean_surface_sample_plane: camera forward has no horizontal component");
+  const SurfacePlane plane{res, camera[0], camera[1], camera[2], camera[3], camera[4]};
+  const int64_t pts = (int64_t)(res + 1) * (res + 1);
+  HIP_TRY(launch_surface(p, plane, nullptr, pts, reinterpret_cast<float4*>(out), fft->stream, fft->cus),
+          "ocean_surface_sample_plane");
+  return OCEAN_OK;
+}
+
 float* ocean_generator_initial_spectrum(ocean_generator* g, int c)
 {
   if (!g || c < 0 || c >= g->cascades)

@@ -30,6 +30,30 @@ struct OceanSettings
 static_assert(sizeof(OceanSettings) == 64, "GeneratorSettings is 64 bytes");
 
 constexpr int kMaxCascades = 64;  // cascades per launch (kernel-argument tables below)
+constexpr int kMaxSurfaceCascades = 16;
+
+// Surface consumer (resources/waveShader.glsl): the maps one cascade binds, plus its planeSize and
+// displacement scale (src/Renderer.cpp:62-72).
+struct SurfaceCascade
+{
+  const float4* height;
+  const float4* disp;
+  const float* jac;
+  float plane;
+  float scale;
+};
+struct SurfaceParams
+{
+  int count;  // cascades
+  int n;      // map side (power of two)
+  SurfaceCascade c[kMaxSurfaceCascades];
+};
+// The reference plane mesh and camera (waveShader.glsl:77-98); res == 0: explicit positions.
+struct SurfacePlane
+{
+  int res;
+  float cam_x, cam_y, cam_z, fwd_x, fwd_z;
+};
 
 // Per-cascade values the evolve/row kernel needs (passed by value: no per-frame H2D copy).
 struct CascadeFrame
@@ -67,6 +91,8 @@ struct SlabGeom
 int spectrum_block(int logn);
 hipError_t launch_generate_spectrum(const OceanSettings& s, int n, float4* h0, hipStream_t stream, int cus, int x0 = 0,
                                     int width = 0);
+hipError_t launch_surface(const SurfaceParams& p, const SurfacePlane& plane, const float2* xz, int64_t count,
+                          float4* out, hipStream_t stream, int cus);
 hipError_t launch_hash(const uint32_t* xy, int count, uint32_t* raw, float2* uv, hipStream_t stream);
 // Generator frame: pass 1 (evolve + y iFFT, destination-block-ordered output), pass 2 (x iFFT +
 // maps + Jacobian). keep: evolved amplitudes kept live between the two packed images (0, 8, 16).

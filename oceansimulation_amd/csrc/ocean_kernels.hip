@@ -1187,6 +1187,114 @@ __global__ __launch_bounds__(256) void k_blocks_to_rows(int cascades, int n, int
 }
 
 // ------------------------------------------------------------------------------------------------
+// Surface consumer: resources/waveShader.glsl evaluated per mesh vertex on the
+// generator's maps. Vertex stage (:101-110): each cascade samples heightMap/displacementMap at
+// pos.xz / planeSize, the position the earlier cascades already displaced, and adds
+// (scale * Dx, h, scale * Dz). Fragment stage at the displaced position (:127-144): summed slopes
+// -> normal, averaged Jacobian. Sampling is GL_LINEAR + GL_REPEAT (src/Generator.cpp:116-119) in
+// fp32 with the specification's weights, unfused and with correctly rounded division / sqrt, so
+// the oracle restatement (oracle_surface_vertex) is matched bit for bit. Memory: the maps of a
+// scene (3 x 256^2 x 36 B) live in L2; per vertex 32 B are written.
+// ------------------------------------------------------------------------------------------------
+template <int CH>
+__device__ __forceinline__ void sample_linear_repeat(const float* __restrict__ tex, int n, float u, float v, float* out)
+{
+#pragma clang fp contract(off)
+  const float s = u * (float)n - 0.5f, t = v * (float)n - 0.5f;
+  const float fs = floorf(s), ft = floorf(t);
+  const float a = s - fs, b = t - ft;
+  const int m = n - 1;  // n is a power of two: & m is the repeat wrap, also for negative indices
+  const int i0 = (int)fs & m, j0 = (int)ft & m, i1 = (i0 + 1) & m, j1 = (j0 + 1) & m;
+  const float w00 = (1.0f - a) * (1.0f - b), w10 = a * (1.0f - b), w01 = (1.0f - a) * b, w11 = a * b;
+  const float* t00 = tex + ((size_t)j0 * n + i0) * CH;
+  const float* t10 = tex + ((size_t)j0 * n + i1) * CH;
+  const float* t01 = tex + ((size_t)j1 * n + i0) * CH;
+  const float* t11 = tex + ((size_t)j1 * n + i1) * CH;
+  if constexpr (CH == 4)
+  {
+    const float4 q00 = *reinterpret_cast<const float4*>(t00), q10 = *reinterpret_cast<const float4*>(t10);
+    const float4 q01 = *reinterpret_cast<const float4*>(t01), q11 = *reinterpret_cast<const float4*>(t11);
+    out[0] = w00 * q00.x + w10 * q10.x + w01 * q01.x + w11 * q11.x;
+    out[1] = w00 * q00.y + w10 * q10.y + w01 * q01.y + w11 * q11.y;
+    out[2] = w00 * q00.z + w10 * q10.z + w01 * q01.z + w11 * q11.z;
+    out[3] = w00 * q00.w + w10 * q10.w + w01 * q01.w + w11 * q11.w;
+  }
+  else
+    out[0] = w00 * t00[0] + w10 * t10[0] + w01 * t01[0] + w11 * t11[0];
+}
+
+__global__ __launch_bounds__(256) void k_surface(SurfaceParams p, SurfacePlane plane, const float2* __restrict__ xz,
+                                                 int64_t count, float4* __restrict__ out)
+{
+#pragma clang fp contract(off)
+  float tx = 0.0f, tz = 0.0f, cam_y = 0.0f;
+  if (plane.res > 0)
+  {
+    // turnDir = normalize(forward.xz) rotated by 45 degrees (waveShader.glsl:84-88)
+    const float fl = sqrtf(plane.fwd_x * plane.fwd_x + plane.fwd_z * plane.fwd_z);
+    const float tx0 = plane.fwd_x / fl, tz0 = plane.fwd_z / fl;
+    tx = (tx0 - tz0) * 0.70711f;
+    tz = (tx0 + tz0) * 0.70711f;
+    cam_y = fmaxf(plane.cam_y, 10.0f);
+  }
+  for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < count;
+       idx += (int64_t)gridDim.x * blockDim.x)
+  {
+    float px, pz;
+    if (plane.res > 0)
+    {
+      // plane vertex (src/Renderer.cpp:18), + (15, 0, 15), rotate, distance scale, camera offset
+      const int side = plane.res + 1;
+      const int i = (int)(idx % side), j = (int)(idx / side);
+      const float x = -20.0f + 40.0f * (float)i / (float)plane.res + 15.0f;
+      const float z = -20.0f + 40.0f * (float)j / (float)plane.res + 15.0f;
+      float rx = tx * x - tz * z, rz = x * tz + z * tx;
+      const float len = sqrtf(rx * rx + rz * rz);
+      const float k = powf(fmaxf(len, 1.0f), 1.2f) * cam_y * 0.04f;
+      px = rx * k + plane.cam_x;
+      pz = rz * k + plane.cam_z;
+    }
+    else
+    {
+      const float2 q = xz[idx];
+      px = q.x;
+      pz = q.y;
+    }
+    float py = 0.0f;
+    for (int c = 0; c < p.count; c++)
+    {
+      float d1[4], d2[4];
+      const float u = px / p.c[c].plane, v = pz / p.c[c].plane;
+      sample_linear_repeat<4>(reinterpret_cast<const float*>(p.c[c].height), p.n, u, v, d1);
+      sample_linear_repeat<4>(reinterpret_cast<const float*>(p.c[c].disp), p.n, u, v, d2);
+      px += p.c[c].scale * d1[3];
+      py += d1[0];
+      pz += p.c[c].scale * d2[0];
+    }
+    float d[4] = {0.0f, 0.0f, 0.0f, 0.0f}, jac = 0.0f;
+    for (int c = 0; c < p.count; c++)
+    {
+      float d1[4], d2[4], j;
+      const float u = px / p.c[c].plane, v = pz / p.c[c].plane;
+      sample_linear_repeat<4>(reinterpret_cast<const float*>(p.c[c].height), p.n, u, v, d1);
+      sample_linear_repeat<4>(reinterpret_cast<const float*>(p.c[c].disp), p.n, u, v, d2);
+      sample_linear_repeat<1>(p.c[c].jac, p.n, u, v, &j);
+      jac += j / (float)p.count;
+      const float f = p.c[c].scale;
+      d[0] += d1[1];
+      d[1] += d2[1] * f;
+      d[2] += d1[2];
+      d[3] += d2[2] * f;
+    }
+    const float sx = d[0] / (1.0f + d[1]), sz = d[2] / (1.0f + d[3]);
+    const float nx = -sx, ny = 1.0f, nz = -sz;
+    const float len = sqrtf(nx * nx + ny * ny + nz * nz);
+    out[2 * idx] = make_float4(px, py, pz, jac);
+    out[2 * idx + 1] = make_float4(nx / len, ny / len, nz / len, 0.0f);
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
 // Host-side launchers (dispatch on log2 N).
 // ------------------------------------------------------------------------------------------------
 template <int LOGN>
@@ -1284,6 +1392,19 @@ hipError_t launch_generate_spectrum(const OceanSettings& s, int n, float4* h0, h
   else
     hipLaunchKernelGGL(k_generate_spectrum, dim3((unsigned)blocks), dim3(256), 0, stream, spectrum_consts(s, n), n,
                        spectrum_block(logn), x0, width, h0);
+  return hipGetLastError();
+}
+
+hipError_t launch_surface(const SurfaceParams& p, const SurfacePlane& plane, const float2* xz, int64_t count,
+                          float4* out, hipStream_t stream, int cus)
+{
+  if (count <= 0)
+    return hipSuccess;
+  long blocks = (long)((count + 255) / 256);
+  const long cap = (long)cus * 8;
+  if (blocks > cap)
+    blocks = cap;
+  hipLaunchKernelGGL(k_surface, dim3((unsigned)blocks), dim3(256), 0, stream, p, plane, xz, count, out);
   return hipGetLastError();
 }
 

@@ -42,6 +42,10 @@ class SlabGenerator:
         self.row0 = rank * self.rows
         self.exchange_bytes = int(lib().ocean_generator_exchange_bytes(self._h))
 
+    @property
+    def handle(self):
+        return self._h
+
     def GetOceanSettings(self) -> OceanSettings:
         p = lib().ocean_generator_settings(self._h, 0)
         if not p:

@@ -94,6 +94,10 @@ class Generator:
         self.n = fft.GetTextureResolution()
         self.cascades = cascades
 
+    @property
+    def handle(self):
+        return self._h
+
     def GetOceanSettings(self, cascade: int = 0) -> OceanSettings:
         p = lib().ocean_generator_settings(self._h, cascade)
         if not p:

@@ -412,3 +412,99 @@ void oracle_calculate_ocean(oracle_settings* s, int n, float timestep, int updat
   oracle_encode_ifft(n, disp, work);
   oracle_compute_foam(s, n, disp, jac);
 }
+
+/* ---- Surface consumer (resources/waveShader.glsl) -------------------------------------------- */
+
+/* GL_LINEAR + GL_REPEAT on an N*N texture with `ch` channels (OpenGL 4.5 §8.14.2): texel-space
+ * s = u*N - 1/2, i0 = floor(s), alpha = frac(s); weights in the specification's order. */
+static void sample_bilinear(const float* tex, int n, int ch, float u, float v, float* out)
+{
+  float s = u * (float)n - 0.5f, t = v * (float)n - 0.5f;
+  float fs = floorf(s), ft = floorf(t);
+  float a = s - fs, b = t - ft;
+  int i0 = (int)fs, j0 = (int)ft;
+  int i0w = ((i0 % n) + n) % n, j0w = ((j0 % n) + n) % n;
+  int i1w = (i0w + 1) % n, j1w = (j0w + 1) % n;
+  float w00 = (1.0f - a) * (1.0f - b), w10 = a * (1.0f - b), w01 = (1.0f - a) * b, w11 = a * b;
+  const float* t00 = tex + ((size_t)j0w * n + i0w) * ch;
+  const float* t10 = tex + ((size_t)j0w * n + i1w) * ch;
+  const float* t01 = tex + ((size_t)j1w * n + i0w) * ch;
+  const float* t11 = tex + ((size_t)j1w * n + i1w) * ch;
+  for (int k = 0; k < ch; k++)
+    out[k] = w00 * t00[k] + w10 * t10[k] + w01 * t01[k] + w11 * t11[k];
+}
+
+void oracle_surface_vertex(const oracle_cascade_maps* c, int count, float x, float z, float out[8])
+{
+  float px = x, py = 0.0f, pz = z;
+  /* vertex stage, waveShader.glsl:101-110: each cascade samples at the position the previous
+   * cascades already displaced */
+  for (int i = 0; i < count; i++)
+  {
+    float d1[4], d2[4];
+    float u = px / c[i].planeSize, v = pz / c[i].planeSize;
+    sample_bilinear(c[i].height, c[i].n, 4, u, v, d1);
+    sample_bilinear(c[i].disp, c[i].n, 4, u, v, d2);
+    px += c[i].displacement * d1[3];
+    py += d1[0];
+    pz += c[i].displacement * d2[0];
+  }
+  /* fragment stage at the displaced position, waveShader.glsl:127-144 */
+  float d[4] = {0.0f, 0.0f, 0.0f, 0.0f}, jac = 0.0f;
+  for (int i = 0; i < count; i++)
+  {
+    float d1[4], d2[4], j;
+    float u = px / c[i].planeSize, v = pz / c[i].planeSize;
+    sample_bilinear(c[i].height, c[i].n, 4, u, v, d1);
+    sample_bilinear(c[i].disp, c[i].n, 4, u, v, d2);
+    sample_bilinear(c[i].jac, c[i].n, 1, u, v, &j);
+    jac += j / (float)count; /* the reference's "/ 3.0" for its three cascades */
+    float f = c[i].displacement;
+    d[0] += d1[1];
+    d[1] += d2[1] * f;
+    d[2] += d1[2];
+    d[3] += d2[2] * f;
+  }
+  float sx = d[0] / (1.0f + d[1]), sz = d[2] / (1.0f + d[3]);
+  float nx = -sx, ny = 1.0f, nz = -sz;
+  float len = sqrtf(nx * nx + ny * ny + nz * nz);
+  out[0] = px;
+  out[1] = py;
+  out[2] = pz;
+  out[3] = jac;
+  out[4] = nx / len;
+  out[5] = ny / len;
+  out[6] = nz / len;
+  out[7] = 0.0f;
+}
+
+void oracle_surface_plane(const oracle_cascade_maps* c, int count, const float cam[5], int res, float* out)
+{
+  /* turnDir = normalize(forward.xz), rotated by 45 degrees (waveShader.glsl:84-88) */
+  float fl = sqrtf(cam[3] * cam[3] + cam[4] * cam[4]);
+  float tx0 = cam[3] / fl, tz0 = cam[4] / fl;
+  float tx = (tx0 - tz0) * 0.70711f, tz = (tx0 + tz0) * 0.70711f;
+  float cam_y = cam[1] > 10.0f ? cam[1] : 10.0f;
+  const int side = res + 1;
+#pragma omp parallel for num_threads(g_threads) schedule(static)
+  for (int j = 0; j < side; j++)
+    for (int i = 0; i < side; i++)
+    {
+      /* plane vertex (src/Renderer.cpp:18), then pos + (15, 0, 15) (waveShader.glsl:77) */
+      float x = -20.0f + 40.0f * (float)i / (float)res + 15.0f;
+      float z = -20.0f + 40.0f * (float)j / (float)res + 15.0f;
+      float rx = tx * x - tz * z, rz = x * tz + z * tx;
+      float len = sqrtf(rx * rx + rz * rz);
+      float k = powf(len > 1.0f ? len : 1.0f, 1.2f) * cam_y * 0.04f; /* shader's left-to-right order */
+      rx = rx * k + cam[0];
+      rz = rz * k + cam[2];
+      oracle_surface_vertex(c, count, rx, rz, out + 8 * ((size_t)j * side + i));
+    }
+}
+
+void oracle_surface_points(const oracle_cascade_maps* c, int count, const float* xz, int64_t npts, float* out)
+{
+#pragma omp parallel for num_threads(g_threads) schedule(static)
+  for (int64_t p = 0; p < npts; p++)
+    oracle_surface_vertex(c, count, xz[2 * p], xz[2 * p + 1], out + 8 * p);
+}

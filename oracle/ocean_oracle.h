@@ -70,6 +70,34 @@ void oracle_compute_foam(const oracle_settings* s, int n, const float* disp, flo
 void oracle_calculate_ocean(oracle_settings* s, int n, float timestep, int update_spectrum,
                             float* h0, float* height, float* disp, float* jac, float* work);
 
+/* ---- Surface consumer (resources/waveShader.glsl), SURVEY §8f rank 3 --------------------------
+ * One cascade's maps as the renderer binds them (src/Renderer.cpp:62-72): heightMap and
+ * displacementMap RGBA32F, jacobianMap R32F, N*N row-major, sampled GL_LINEAR + GL_REPEAT
+ * (src/Generator.cpp:116-119), with the cascade's planeSize and displacement (Renderer.cpp:70-71). */
+typedef struct oracle_cascade_maps
+{
+  const float* height;
+  const float* disp;
+  const float* jac;
+  int n;
+  float planeSize;
+  float displacement;
+} oracle_cascade_maps;
+
+/* Per vertex at base position (x, 0, z): the vertex stage's displacement loop over the cascades
+ * (waveShader.glsl:101-110), then at the displaced position the fragment stage's slope normal and
+ * Jacobian average (waveShader.glsl:127-144). out[8] = (x, y, z, jacobian, nx, ny, nz, 0). */
+void oracle_surface_vertex(const oracle_cascade_maps* c, int count, float x, float z, float out[8]);
+
+/* oracle_surface_vertex over npts base positions xz[2*p], xz[2*p+1]; out: npts * 8 floats. */
+void oracle_surface_points(const oracle_cascade_maps* c, int count, const float* xz, int64_t npts, float* out);
+
+/* The reference's plane mesh (40 m x 40 m, res x res quads, (res+1)^2 vertices, x fastest; src/
+ * Renderer.cpp:18) through the camera-relative warp of waveShader.glsl:77-98 (camera position
+ * cam[0..2] = viewInverse[3].xyz, forward cam[3..4] = -viewInverse[0].xz), then
+ * oracle_surface_vertex. out: (res+1)^2 * 8 floats. */
+void oracle_surface_plane(const oracle_cascade_maps* c, int count, const float cam[5], int res, float* out);
+
 /* Threads used by the OpenMP loops (1 when built without OpenMP). */
 void oracle_set_threads(int threads);
 int oracle_get_threads(void);

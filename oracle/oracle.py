@@ -16,6 +16,19 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 _LIB_PATH = os.path.join(_HERE, "build", "liboceanoracle.so")
 
 
+class OracleCascadeMaps(ctypes.Structure):
+    """oracle_cascade_maps: one cascade's maps as the renderer binds them."""
+
+    _fields_ = [
+        ("height", ctypes.POINTER(ctypes.c_float)),
+        ("disp", ctypes.POINTER(ctypes.c_float)),
+        ("jac", ctypes.POINTER(ctypes.c_float)),
+        ("n", ctypes.c_int),
+        ("planeSize", ctypes.c_float),
+        ("displacement", ctypes.c_float),
+    ]
+
+
 class OracleSettings(ctypes.Structure):
     """Waves::GeneratorSettings (src/Generator.h:12-30), 64 bytes."""
 
@@ -62,6 +75,9 @@ def lib():
         L.oracle_encode_ifft.argtypes = [ctypes.c_int, fp, fp]
         L.oracle_compute_foam.argtypes = [sp, ctypes.c_int, fp, fp]
         L.oracle_calculate_ocean.argtypes = [sp, ctypes.c_int, ctypes.c_float, ctypes.c_int, fp, fp, fp, fp, fp]
+        cp = ctypes.POINTER(OracleCascadeMaps)
+        L.oracle_surface_points.argtypes = [cp, ctypes.c_int, fp, ctypes.c_int64, fp]
+        L.oracle_surface_plane.argtypes = [cp, ctypes.c_int, fp, ctypes.c_int, fp]
         L.oracle_set_threads.argtypes = [ctypes.c_int]
         L.oracle_get_threads.restype = ctypes.c_int
         _lib = L
@@ -126,6 +142,35 @@ def compute_foam(s: OracleSettings, disp: np.ndarray) -> np.ndarray:
     jac = np.zeros((n, n), np.float32)
     lib().oracle_compute_foam(ctypes.byref(s), n, _fp(np.ascontiguousarray(disp, np.float32)), _fp(jac))
     return jac
+
+
+def _cascade_table(cascades):
+    """cascades: [(height N*N*4, disp N*N*4, jac N*N, planeSize, displacement)] float32 arrays."""
+    keep = []
+    table = (OracleCascadeMaps * len(cascades))()
+    for i, (h, d, j, L, disp) in enumerate(cascades):
+        h, d, j = (np.ascontiguousarray(a, np.float32) for a in (h, d, j))
+        keep += [h, d, j]
+        table[i] = OracleCascadeMaps(_fp(h), _fp(d), _fp(j), h.shape[0], L, disp)
+    return table, keep
+
+
+def surface_points(cascades, xz: np.ndarray) -> np.ndarray:
+    """waveShader.glsl displacement + normal + Jacobian at base positions xz (P x 2) -> (P, 8)."""
+    table, keep = _cascade_table(cascades)
+    xz = np.ascontiguousarray(xz, np.float32)
+    out = np.zeros((xz.shape[0], 8), np.float32)
+    lib().oracle_surface_points(table, len(cascades), _fp(xz), xz.shape[0], _fp(out))
+    return out
+
+
+def surface_plane(cascades, cam, res: int) -> np.ndarray:
+    """The reference plane mesh through the camera warp -> ((res+1)^2, 8)."""
+    table, keep = _cascade_table(cascades)
+    c = np.asarray(cam, np.float32)
+    out = np.zeros(((res + 1) * (res + 1), 8), np.float32)
+    lib().oracle_surface_plane(table, len(cascades), _fp(c), res, _fp(out))
+    return out
 
 
 class OracleGenerator:

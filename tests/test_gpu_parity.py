@@ -463,3 +463,87 @@ def test_generator_16384_transpose_path_sampled(ocean):
             g = np.array([got[y, x, 2 * lane] + 1j * got[y, x, 2 * lane + 1] for (y, x) in pts])
             scale = np.sqrt(np.sum(np.abs(z) ** 2))  # rms of the output field (Parseval)
             assert np.max(np.abs(g - ref)) <= FRAME_TOL * scale * 4, (img, lane)
+
+
+# ---- surface consumer (resources/waveShader.glsl), SURVEY §8f rank 3 -------------------------
+def _scene(ocean, n, t=1.0, planes=(5.0, 17.0, 101.0)):
+    """WaveApp's three cascades (src/Waves.cpp:20-39) as three generators, as Renderer binds them."""
+    fft = ocean.FFTCalculator(n)
+    gens = []
+    for L in planes:
+        g = ocean.Generator(fft, 1)
+        ocean.apply_settings(g.GetOceanSettings(0), planeSize=L)
+        g.CalculateOcean(t)
+        gens.append(g)
+    return fft, gens
+
+
+def test_surface_points_bit_exact_vs_oracle(ocean, oracle):
+    """Vertex displacement + slope normal + Jacobian average at arbitrary positions (negative,
+    multi-period, texel centres and edges): bit-exact with the oracle restatement on the same maps."""
+    from oceansimulation_amd.surface import SurfaceSampler, host_cascades
+
+    fft, gens = _scene(ocean, 256)
+    pairs = [(g, 0) for g in gens]
+    rng = np.random.default_rng(7)
+    xz = np.concatenate([rng.uniform(-300.0, 300.0, (20000, 2)),
+                         np.stack(np.meshgrid(np.arange(-8, 8) * 5.0 / 256.0, [0.0, -5.0, 1e3]), -1).reshape(-1, 2)])
+    xz = xz.astype(np.float32)
+    got = SurfaceSampler(pairs).sample_host(xz)
+    want = oracle.surface_points(host_cascades(pairs), xz)
+    assert np.array_equal(got, want), np.max(np.abs(got - want))
+    assert np.all(np.abs(np.linalg.norm(got[:, 4:7], axis=1) - 1.0) < 1e-6)
+
+
+def test_surface_plane_mesh_vs_oracle(ocean, oracle):
+    """The reference plane mesh through the camera warp (waveShader.glsl:77-98), in two checks:
+    the warp alone (zero-amplitude cascades: scale = 0) within a few ulp of the oracle (its pow is
+    ocml vs glibc, ~1 ulp apart; at the far field, uv ~ 1e5 texels, one ulp of position moves the
+    sample visibly, so the sampled output is not compared through two different warps), then the
+    sampling on the GPU's own warped positions bit-exact against the oracle."""
+    from oceansimulation_amd.surface import SurfaceSampler, host_cascades
+
+    cam = [3.0, 5.0, -2.0, -0.6, 0.8]  # WaveRenderer's camera height (src/Renderer.cpp:15)
+    res = 128
+    fft0, flat = _scene(ocean, 256)
+    for g in flat:
+        ocean.apply_settings(g.GetOceanSettings(0), scale=0.0)
+        g.CalculateOcean(0.0, update_ocean=True)
+    flat_pairs = [(g, 0) for g in flat]
+    base = SurfaceSampler(flat_pairs).plane_host(cam, res)
+    want_base = oracle.surface_plane(host_cascades(flat_pairs), cam, res)
+    rel = np.abs(base[:, [0, 2]] - want_base[:, [0, 2]]) / np.maximum(1.0, np.abs(want_base[:, [0, 2]]))
+    assert np.max(rel) < 2e-6, np.max(rel)
+    assert np.all(base[:, 1] == 0.0) and np.allclose(base[:, 3], 1.0, atol=1e-6)  # 3 x fp32(1/3)
+
+    fft, gens = _scene(ocean, 256)
+    pairs = [(g, 0) for g in gens]
+    got = SurfaceSampler(pairs).plane_host(cam, res)
+    want = oracle.surface_points(host_cascades(pairs), base[:, [0, 2]].copy())
+    assert np.array_equal(got, want), np.max(np.abs(got - want))
+
+
+def test_surface_batched_generator_and_errors(ocean):
+    """(generator, cascade) pairs from one batched generator equal three single generators;
+    invalid requests fail loudly."""
+    from oceansimulation_amd.capi import OceanError
+    from oceansimulation_amd.slab import SlabGenerator
+    from oceansimulation_amd.surface import SurfaceSampler
+
+    fft, gens = _scene(ocean, 64)
+    gb = ocean.Generator(fft, 3)
+    for c, L in enumerate((5.0, 17.0, 101.0)):
+        ocean.apply_settings(gb.GetOceanSettings(c), planeSize=L)
+    gb.CalculateOcean(1.0)
+    xz = np.random.default_rng(1).uniform(-50, 50, (512, 2)).astype(np.float32)
+    a = SurfaceSampler([(g, 0) for g in gens]).sample_host(xz)
+    b = SurfaceSampler([(gb, c) for c in range(3)]).sample_host(xz)
+    assert np.array_equal(a, b)
+    with pytest.raises(OceanError):
+        SurfaceSampler([(gb, 3)]).sample_host(xz)
+    with pytest.raises(OceanError):
+        SurfaceSampler([(gens[0], 0), (ocean.Generator(ocean.FFTCalculator(128), 1), 0)]).sample_host(xz)
+    with pytest.raises(OceanError):
+        SurfaceSampler([(SlabGenerator(ocean.FFTCalculator(256), 0, 2), 0)]).sample_host(xz)
+    with pytest.raises(OceanError):
+        SurfaceSampler([(gb, 0)]).plane_host([0, 5, 0, 0, 0], 8)

@@ -125,3 +125,52 @@ def test_golden_fixtures_reproduce(oracle):
             ref = z[f"{name}/{key}"]
             assert ref.shape == arr.shape
             assert scalar_err(arr, ref) < 1e-6, (name, key)
+
+
+# ---- surface consumer restatement (resources/waveShader.glsl) --------------------------------
+def _flat_maps(n, h=0.0, dh=(0.0, 0.0), dx=0.0, dz=0.0, jac=1.0):
+    height = np.zeros((n, n, 4), np.float32)
+    disp = np.zeros((n, n, 4), np.float32)
+    height[..., 0], height[..., 1], height[..., 2], height[..., 3] = h, dh[0], dh[1], dx
+    disp[..., 0] = dz
+    return height, disp, np.full((n, n), jac, np.float32)
+
+
+def test_surface_constant_maps(oracle):
+    """Constant fields: displacement is the sum over cascades, the normal follows the slopes."""
+    h, d, j = _flat_maps(16, h=0.5, dh=(0.1, -0.2), dx=2.0, dz=-1.0, jac=0.8)
+    c = [(h, d, j, 10.0, 0.4), (h, d, j, 30.0, 0.4)]
+    out = oracle.surface_points(c, np.array([[1.0, 2.0], [-7.5, 100.0]], np.float32))
+    np.testing.assert_allclose(out[:, 0], [1.0 + 2 * 0.4 * 2.0, -7.5 + 2 * 0.4 * 2.0], rtol=1e-6)
+    np.testing.assert_allclose(out[:, 1], 1.0, rtol=1e-6)
+    np.testing.assert_allclose(out[:, 2], [2.0 - 0.8, 100.0 - 0.8], rtol=1e-6)
+    np.testing.assert_allclose(out[:, 3], 0.8, rtol=1e-6)
+    nrm = np.array([-0.2, 1.0, 0.4]) / np.linalg.norm([-0.2, 1.0, 0.4])  # slopes summed: (0.2, -0.4)
+    np.testing.assert_allclose(out[0, 4:7], nrm, rtol=1e-5)
+
+
+def test_surface_bilinear_texel_centres_and_repeat(oracle):
+    """GL_LINEAR + GL_REPEAT: texel centres return the texel; the field repeats every planeSize."""
+    n, L = 16, 8.0
+    rng = np.random.default_rng(3)
+    h = rng.standard_normal((n, n, 4)).astype(np.float32)
+    _, d, j = _flat_maps(n)
+    c = [(h, d, j, L, 0.0)]
+    ij = np.array([[3, 5], [0, 0], [15, 15], [7, 0]])
+    xz = ((ij + 0.5) / n * L).astype(np.float32)  # texel centres (x from i, z from j)
+    out = oracle.surface_points(c, xz)
+    np.testing.assert_allclose(out[:, 1], h[ij[:, 1], ij[:, 0], 0], rtol=1e-6, atol=1e-6)
+    shifted = oracle.surface_points(c, xz + np.float32(L) * np.array([[3, -2]], np.float32))
+    np.testing.assert_allclose(shifted[:, 1], out[:, 1], rtol=1e-5, atol=1e-5)
+
+
+def test_surface_vertex_stage_is_sequential(oracle):
+    """Cascade i samples where cascades < i already moved the vertex (waveShader.glsl:101-110)."""
+    n = 16
+    h1, d1, j1 = _flat_maps(n, dx=4.0)  # first cascade moves x by 4 * scale
+    h2 = np.zeros((n, n, 4), np.float32)
+    h2[:, :, 0] = np.arange(n, dtype=np.float32)[None, :]  # height ramps with x in cascade 2
+    _, d2, j2 = _flat_maps(n)
+    c = [(h1, d1, j1, 16.0, 1.0), (h2, d2, j2, 16.0, 1.0)]
+    out = oracle.surface_points(c, np.array([[0.5, 0.5]], np.float32))  # texel (0, 0) centre
+    assert out[0, 0] == np.float32(4.5) and out[0, 1] == np.float32(4.0)  # sampled at texel 4

@@ -1,22 +1,25 @@
 # Build for MI355X (gfx950). Outputs stay in-tree so they travel to the GPU box with gpurun.
 #   make            -> oceansimulation_amd/liboceanfft.so (C ABI), libwaves.so (C++ Waves API),
-#                      oracle/build/liboceanoracle.so (CPU checker), tests/cpp/test_waves
+#                      oracle/build/liboceanoracle.so (CPU checker), tests/cpp/test_waves,
+#                      examples/waveapp_headless (the reference app's workload, no window)
 HIPCC ?= /opt/rocm/bin/hipcc
 ARCH ?= gfx950
 JOBS ?= 8
 
 PKG := oceansimulation_amd
 CSRC := $(PKG)/csrc
-# -fno-slp-vectorize: the SLP vectoriser packs the complex butterflies into v_pk_* with op_sel
-# shuffles and pushes the column pass past 128 VGPRs (spills); scalar f32 code needs ~100.
+# -fno-slp-vectorize: the SLP vectoriser packs the interleaved float4 arithmetic into v_pk_* with
+# shuffles and pushes the column pass past 128 VGPRs (spills). The FFT gets packed math explicitly
+# instead (split-plane CPair, ocean_kernels.hip).
 HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -fno-slp-vectorize -Wall -Iinclude -I$(CSRC)
 
 LIB := $(PKG)/liboceanfft.so
 WAVES := $(PKG)/libwaves.so
 ORACLE := oracle/build/liboceanoracle.so
 CPPTEST := tests/cpp/test_waves
+APP := examples/waveapp_headless
 
-all: $(LIB) $(WAVES) $(ORACLE) $(CPPTEST)
+all: $(LIB) $(WAVES) $(ORACLE) $(CPPTEST) $(APP)
 
 $(CSRC)/build/ocean_kernels.o: $(CSRC)/ocean_kernels.hip $(CSRC)/ocean_internal.h
 	@mkdir -p $(CSRC)/build
@@ -30,8 +33,10 @@ $(LIB): $(CSRC)/build/ocean_kernels.o $(CSRC)/build/ocean_capi.o
 	$(HIPCC) --offload-arch=$(ARCH) -shared -o $@ $^ -Wl,-soname,liboceanfft.so
 
 # C++ drop-in layer (Waves::FFTCalculator / Waves::Generator / Vision::RenderDevice shim) over the C ABI.
-WAVES_SRC := $(CSRC)/waves/RenderDevice.cpp $(CSRC)/waves/FFTCalculator.cpp $(CSRC)/waves/Generator.cpp
-$(WAVES): $(WAVES_SRC) include/waves/Generator.h include/waves/FFTCalculator.h include/vision/RenderDevice.h $(LIB)
+WAVES_SRC := $(CSRC)/waves/RenderDevice.cpp $(CSRC)/waves/FFTCalculator.cpp $(CSRC)/waves/Generator.cpp \
+             $(CSRC)/waves/Surface.cpp
+$(WAVES): $(WAVES_SRC) include/waves/Generator.h include/waves/FFTCalculator.h include/waves/Surface.h \
+          include/vision/RenderDevice.h $(LIB)
 	g++ -O2 -std=c++17 -fPIC -shared -Iinclude -I/opt/rocm/include -D__HIP_PLATFORM_AMD__ -o $@ $(WAVES_SRC) \
 	    -L$(PKG) -loceanfft -Wl,-rpath,'$$ORIGIN' -L/opt/rocm/lib -lamdhip64
 
@@ -42,6 +47,11 @@ $(CPPTEST): tests/cpp/test_waves.cpp $(WAVES) $(ORACLE)
 	g++ -O2 -std=c++17 -Iinclude -Ioracle -I/opt/rocm/include -D__HIP_PLATFORM_AMD__ -o $@ $< \
 	    -L$(PKG) -lwaves -loceanfft -Loracle/build -loceanoracle \
 	    -Wl,-rpath,'$$ORIGIN/../../$(PKG)' -Wl,-rpath,'$$ORIGIN/../../oracle/build' -L/opt/rocm/lib -lamdhip64
+
+# Headless WaveApp (no oracle: its dumps are checked by tests/test_gpu_parity.py)
+$(APP): examples/waveapp_headless.cpp $(WAVES)
+	g++ -O2 -std=c++17 -Iinclude -I/opt/rocm/include -D__HIP_PLATFORM_AMD__ -o $@ $< \
+	    -L$(PKG) -lwaves -loceanfft -Wl,-rpath,'$$ORIGIN/../$(PKG)' -L/opt/rocm/lib -lamdhip64
 
 MB := tools/microbench
 microbench: $(MB)/genbench $(MB)/colbench $(MB)/copybench $(MB)/genbench_noxch $(MB)/genbench_nobar $(MB)/layoutbench
@@ -54,7 +64,7 @@ $(MB)/genbench_nobar: $(MB)/genbench.hip $(CSRC)/ocean_kernels.hip $(CSRC)/ocean
 	$(HIPCC) $(HIPFLAGS) -DOCEAN_ABLATE_BARRIER $< -o $@
 
 clean:
-	rm -rf $(MB)/genbench $(MB)/colbench $(MB)/copybench $(MB)/genbench_noxch $(MB)/genbench_nobar $(MB)/layoutbench $(CSRC)/build $(LIB) $(WAVES) $(CPPTEST)
+	rm -rf $(MB)/genbench $(MB)/colbench $(MB)/copybench $(MB)/genbench_noxch $(MB)/genbench_nobar $(MB)/layoutbench $(CSRC)/build $(LIB) $(WAVES) $(CPPTEST) $(APP)
 	$(MAKE) -s -C oracle clean
 
 .PHONY: all clean microbench

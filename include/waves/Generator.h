@@ -66,6 +66,10 @@ public:
   // src/Generator.h:53. Kernels are compiled into liboceanfft for gfx950; nothing to reload.
   void LoadShaders(bool reload = false);
 
+  // Extension (no reference counterpart): the C-ABI generator behind this object, for ABI calls
+  // such as ocean_surface_sample_plane (waves/Surface.h).
+  ocean_generator* GetHandle() const { return gen; }
+
 private:
   Vision::RenderDevice* renderDevice = nullptr;
   FFTCalculator* fftCalc = nullptr;

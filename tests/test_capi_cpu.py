@@ -112,3 +112,14 @@ def test_cpp_headers_compile_standalone(tmp_path):
     r = subprocess.run(["g++", "-std=c++17", "-fsyntax-only", f"-I{ROOT}/include", "-I/opt/rocm/include",
                         "-D__HIP_PLATFORM_AMD__", str(src)], capture_output=True, text=True)
     assert r.returncode == 0, r.stderr
+
+
+def test_waveapp_headless_rejects_bad_arguments():
+    """The headless driver parses its script before touching a device (exit 2 = usage)."""
+    import subprocess
+
+    exe = os.path.join(ROOT, "examples", "waveapp_headless")
+    assert os.path.exists(exe), "make builds examples/waveapp_headless"
+    for bad in (["--bogus", "1"], ["--edit", "3:7.U_10=1"], ["--freeze", "x"], ["--n"]):
+        r = subprocess.run([exe, *bad], capture_output=True, text=True, timeout=60)
+        assert r.returncode == 2, (bad, r.returncode, r.stderr)

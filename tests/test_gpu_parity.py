@@ -547,3 +547,52 @@ def test_surface_batched_generator_and_errors(ocean):
         SurfaceSampler([(SlabGenerator(ocean.FFTCalculator(256), 0, 2), 0)]).sample_host(xz)
     with pytest.raises(OceanError):
         SurfaceSampler([(gb, 0)]).plane_host([0, 5, 0, 0, 0], 8)
+
+
+# ---- headless WaveApp driver -------------------------------------------
+def _run_app(tmp, *args):
+    exe = os.path.join(ROOT, "examples", "waveapp_headless")
+    r = subprocess.run([exe, *args, "--dump", str(tmp)], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr
+    import json
+
+    return json.loads(r.stdout.strip().splitlines()[-1])
+
+
+def test_waveapp_headless_matches_oracle(ocean, oracle, tmp_path):
+    """WaveApp::OnUpdate driven headless: Q-freeze frames (dt = 0), a settings edit that re-seeds
+    and redoes the wavelength bookkeeping, the renderer's surface step; the dumped maps equal the
+    oracle replaying the same script, and both re-seed policies give identical maps."""
+    n, frames, mesh = 64, 20, 32
+    script = ["--n", str(n), "--frames", str(frames), "--freeze", "5:8", "--edit", "10:1.U_10=20",
+              "--mesh", str(mesh)]
+    a, b = tmp_path / "ref", tmp_path / "onedit"
+    a.mkdir()
+    b.mkdir()
+    out = _run_app(a, *script)
+    _run_app(b, *script, "--reseed", "on-edit")
+    assert out["frozen_frames"] == 3 and out["reseeded_frames"] == frames
+    primes = [5.0, 17.0, 101.0]
+    refs = []
+    for i, L in enumerate(primes):
+        s = oracle.default_settings(planeSize=L, boundWavelength=1, wavelengthMax=L / 2.0,
+                                    wavelengthMin=0.0 if i == 0 else primes[i - 1] / 2.0)
+        refs.append(oracle.OracleGenerator(n, s))
+    for f in range(frames):
+        if f == 10:
+            refs[1].settings.U_10 = 20.0
+        dt = 0.0 if 5 <= f < 8 else np.float32(1.0 / 60.0)
+        for r in refs:
+            r.calculate_ocean(dt, update_ocean=True)
+    for i in range(3):
+        h, d, j = (np.load(a / f"{k}_{i}.npy") for k in ("height", "disp", "jac"))
+        for k in ("height", "disp", "jac"):
+            assert np.array_equal(np.load(a / f"{k}_{i}.npy"), np.load(b / f"{k}_{i}.npy")), (k, i)
+        _frame_check(h, d, j, refs[i])
+        assert np.float32(out["final_time"][i]) == refs[i].settings.time
+    surf = np.load(a / "surface.npy")
+    cas = [(r.height, r.disp, r.jac, L, r.settings.displacement) for r, L in zip(refs, primes)]
+    want = oracle.surface_plane(cas, [0.0, 5.0, 0.0, -0.70711, 0.70711], mesh)
+    near = np.hypot(want[:, 0], want[:, 2]) < 60.0
+    assert near.sum() > 100
+    assert np.max(np.abs(surf[near] - want[near])) < 1e-3

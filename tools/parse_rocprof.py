@@ -17,7 +17,8 @@ src, tag = sys.argv[1], sys.argv[2]
 n = int(sys.argv[3]) if len(sys.argv) > 3 else 4096
 cascades = int(sys.argv[4]) if len(sys.argv) > 4 else 8
 pts = n * n * cascades
-ALGO = {"k_cols_evolve": 48 * pts, "k_rows_final": 68 * pts, "k_generate_spectrum": 16 * n * n}
+ALGO = {"k_cols_evolve": 48 * pts, "k_rows_final": 68 * pts, "k_generate_spectrum": 16 * n * n,
+        "k_generate_spectrum_pairs": 16 * n * n}
 
 
 def read_csv(path):

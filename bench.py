@@ -104,6 +104,25 @@ def cascade_settings(rank: int, c: int) -> dict:
     return dict(planeSize=PLANES[c % len(PLANES)], seed=(12342 + 4097 * rank, 8934 + 4097 * (c // len(PLANES))))
 
 
+def measured_traffic(kernel: str, n: int, cascades: int):
+    """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC summary of this workload
+    (tools/profile_gpu.sh: separate --pmc FETCH_SIZE and --pmc WRITE_SIZE passes over bench.py,
+    read = 2 x FETCH_SIZE, write = WRITE_SIZE, KB = 1024 B; tools/parse_rocprof.py), or None."""
+    import glob
+
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_rocprof.json")), reverse=True):
+        try:
+            with open(path) as f:
+                prof = json.load(f)
+        except (OSError, ValueError):
+            continue
+        rec = prof.get("kernels", {}).get(kernel)
+        if prof.get("n") == n and prof.get("cascades") == cascades and rec and rec.get("hbm_traffic_bytes"):
+            return {"hbm_traffic_bytes": rec["hbm_traffic_bytes"],
+                    "source": f"{os.path.relpath(path, ROOT)} (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, same workload)"}
+    return None
+
+
 def cpu_baseline(n: int, target_s: float):
     """The oracle (CPU restatement of the reference FFTCalculator/Generator) on host cores."""
     from oracle import oracle as O
@@ -404,6 +423,13 @@ def main():
             "frac": achieved / HBM_PEAK_GBS,
             "traffic": None,
         }
+        pmc = measured_traffic(dom_name.split("_pass_")[-1], n, C)
+        if pmc is not None:
+            # same unit as achieved: PMC-measured HBM bytes per launch / this run's launch duration
+            out["roofline"]["traffic"] = pmc["hbm_traffic_bytes"] / (dom["avg_ms"] * 1e-3) / 1e9
+            out["roofline"]["traffic_bytes_per_launch"] = pmc["hbm_traffic_bytes"]
+            out["roofline"]["algorithmic_bytes_per_launch"] = dom["bytes"]
+            out["roofline"]["traffic_source"] = pmc["source"]
         frame_gbs = FRAME_BYTES * per_launch_pts / ((p1_ms + p2_ms) * 1e-3) / 1e9
         out["kernels"] = {
             k: {"avg_ms": v["avg_ms"], "GB_per_s": v["bytes"] / (v["avg_ms"] * 1e-3) / 1e9,

@@ -49,18 +49,21 @@ def parse():
     ap.add_argument("--slab-steps", type=int, default=10)
     ap.add_argument("--slab-reserve-cus", type=int, default=32,
                     help="CUs left free for RCCL's copy kernels while the slab passes overlap the all-to-all")
+    ap.add_argument("--shared-gpu", action="store_true",
+                    help="rehearsal: every rank on GPU 0 with gloo collectives and host-staged exchanges "
+                         "(exercises the N > 1 paths on a one-GPU machine; not a measurement)")
     ap.add_argument("--slab-force-exchange", action="store_true",
                     help="run the RCCL exchange and the pipeline even at world size 1 (plumbing check "
                          "under torch.distributed.run --nproc-per-node 1)")
     return ap.parse_args()
 
 
-def dist_setup(force: bool = False):
+def dist_setup(force: bool = False, shared_gpu: bool = False):
     import torch
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    local = 0 if shared_gpu else int(os.environ.get("LOCAL_RANK", "0"))
     if torch.cuda.is_available():
         torch.cuda.set_device(local)
     if world > 1 or (force and "MASTER_ADDR" in os.environ):
@@ -68,7 +71,9 @@ def dist_setup(force: bool = False):
 
         from datetime import timedelta
 
-        backend = "nccl" if torch.cuda.is_available() else "gloo"
+        # --shared-gpu rehearses N ranks on one GPU: RCCL refuses two ranks per device, so gloo
+        # (CPU collectives, host-staged slab exchanges) stands in for it
+        backend = "nccl" if torch.cuda.is_available() and not shared_gpu else "gloo"
         # bounded collectives: a failing optional leg must not hang the job
         dist.init_process_group(backend=backend, timeout=timedelta(seconds=300))
     return rank, world, local
@@ -300,7 +305,9 @@ def slab_grid(args, rank: int, world: int, local: int) -> dict:
     out = {
         "config": f"single {n}x{n} grid, full payload, slab-decomposed over {world} GPU(s)",
         "ranks": world,
-        "exchange": "rccl all_to_all_single" if exchange else "none (one rank)",
+        "exchange": (("rccl all_to_all_single" if dist.get_backend() == "nccl" else
+                      f"{dist.get_backend()} all_to_all_single, host-staged (rehearsal, not a measurement)")
+                     if exchange else "none (one rank)"),
         "column_pass_ms": ms[1] / max(cnt[1], 1),
         "row_pass_ms": ms[2] / max(cnt[2], 1),
         "exchange_bytes_per_rank": g.exchange_bytes * (world - 1) // world if world > 1 else 0,
@@ -343,7 +350,7 @@ def slab_grid(args, rank: int, world: int, local: int) -> dict:
 
 def main():
     args = parse()
-    rank, world, local = dist_setup(force=args.slab_force_exchange)
+    rank, world, local = dist_setup(force=args.slab_force_exchange, shared_gpu=args.shared_gpu)
     import oceansimulation_amd as ocean
 
     n, C = args.n, args.cascades

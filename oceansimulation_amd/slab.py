@@ -109,6 +109,27 @@ def emulate_frame(slabs, sends, recvs, timestep: float, update_ocean: bool = Fal
         g.rows_pass(rcv.ptr)
 
 
+def _staged() -> bool:
+    """gloo (CPU collectives) is used only to rehearse several ranks on one GPU (bench.py
+    --shared-gpu): device buffers then go through host memory."""
+    import torch.distributed as dist
+
+    return dist.get_backend() == "gloo"
+
+
+def _all_to_all(recv, send, stream=None) -> None:
+    import torch
+    import torch.distributed as dist
+
+    if not _staged():
+        dist.all_to_all_single(recv, send)
+        return
+    host_send = send.to("cpu", non_blocking=False)
+    host_recv = torch.empty_like(host_send)
+    dist.all_to_all_single(host_recv, host_send)
+    recv.copy_(host_recv, non_blocking=False)
+
+
 class TorchExchange:
     """Equal-split all-to-all over torch.distributed (backend "nccl" = RCCL on ROCm)."""
 
@@ -119,9 +140,7 @@ class TorchExchange:
         self.recv = torch.empty(nbytes, dtype=torch.uint8, device=device)
 
     def __call__(self) -> None:
-        import torch.distributed as dist
-
-        dist.all_to_all_single(self.recv, self.send)
+        _all_to_all(self.recv, self.send)
 
 
 class SlabPipeline:
@@ -224,5 +243,8 @@ class TorchExchangeSlots:
         import torch.distributed as dist
 
         with torch.cuda.stream(stream):
+            if _staged():  # rehearsal on one GPU: host-staged and synchronous
+                _all_to_all(self.recv[slot], self.send[slot])
+                return
             work = dist.all_to_all_single(self.recv[slot], self.send[slot], async_op=True)
             work.wait()  # comm stream waits for the collective; the host does not block

@@ -66,6 +66,8 @@ struct ocean_fft
   int cus = 0;         // CU budget persistent grids are sized for (ocean_fft_set_cu_budget)
   hipStream_t stream = nullptr;
   float2* twiddles = nullptr;  // two-level table, see FftShape in ocean_kernels.hip
+  float4* work = nullptr;      // column-first EncodeIFFT work image (the reference's workImage)
+  int work_images = 0;
 };
 
 struct ocean_generator
@@ -187,6 +189,8 @@ int ocean_fft_destroy(ocean_fft* fft)
     return OCEAN_OK;
   if (fft->twiddles)
     (void)hipFree(fft->twiddles);
+  if (fft->work)
+    (void)hipFree(fft->work);
   delete fft;
   return OCEAN_OK;
 }
@@ -210,6 +214,36 @@ int ocean_fft_encode_ifft_batch(ocean_fft* fft, float* images, int n_images)
   if (!fft || !images || n_images < 1)
     return fail(OCEAN_ERR_INVALID, "ocean_fft_encode_ifft_batch: null plan/image or n_images < 1");
   auto* img = reinterpret_cast<float4*>(images);
+  if (ifft_colfirst_supported(fft->logn))
+  {
+    // column-first through a work image of up to kIfftChunk images (2 GiB at N = 4096)
+    constexpr int kIfftChunk = 8;
+    const int want = n_images < kIfftChunk ? n_images : kIfftChunk;
+    if (fft->work_images < want)
+    {
+      float4* w = nullptr;
+      if (hipMalloc(&w, (size_t)want * fft->n * fft->n * sizeof(float4)) == hipSuccess)
+      {
+        if (fft->work)
+          (void)hipFree(fft->work);
+        fft->work = w;
+        fft->work_images = want;
+      }
+      else
+        (void)hipGetLastError();  // no room for the work image: the in-place passes below
+    }
+    if (fft->work)
+    {
+      for (int first = 0; first < n_images; first += fft->work_images)
+      {
+        const int count = n_images - first < fft->work_images ? n_images - first : fft->work_images;
+        HIP_TRY(launch_ifft_colfirst(fft->logn, count, img + (size_t)first * fft->n * fft->n, fft->work, fft->twiddles,
+                                     fft->stream, fft->cus),
+                "column-first EncodeIFFT");
+      }
+      return OCEAN_OK;
+    }
+  }
   HIP_TRY(launch_rows_ifft(fft->logn, n_images, img, fft->twiddles, fft->stream, fft->cus), "row pass");
   HIP_TRY(launch_cols(fft->logn, n_images, img, fft->twiddles, fft->stream, fft->cus), "column pass");
   return OCEAN_OK;

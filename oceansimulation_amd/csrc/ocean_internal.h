@@ -91,6 +91,10 @@ struct SlabGeom
 int spectrum_block(int logn);
 hipError_t launch_generate_spectrum(const OceanSettings& s, int n, float4* h0, hipStream_t stream, int cus, int x0 = 0,
                                     int width = 0);
+// Standalone EncodeIFFT, column-first through a work image of n_images * N^2 texels (N = 4096).
+bool ifft_colfirst_supported(int logn);
+hipError_t launch_ifft_colfirst(int logn, int n_images, float4* images, float4* work, const float2* tw,
+                                hipStream_t stream, int cus);
 hipError_t launch_surface(const SurfaceParams& p, const SurfacePlane& plane, const float2* xz, int64_t count,
                           float4* out, hipStream_t stream, int cus);
 hipError_t launch_hash(const uint32_t* xy, int count, uint32_t* raw, float2* uv, hipStream_t stream);

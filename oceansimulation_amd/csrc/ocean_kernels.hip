@@ -1053,6 +1053,50 @@ __global__ __launch_bounds__(ColFirstCfg<LOGN>::WG1) void k_cols_evolve(
   }
 }
 
+// Standalone EncodeIFFT, column-first with a work image (src/FFTCalculator.cpp keeps a workImage
+// too): pass A reads the caller's row-major image in strips of B columns (64-B pieces per row,
+// the only strided access), iFFTs along y with the fftShift folded into the row index, and writes
+// the blocked split-plane work image work[img][x/B][y][B] contiguously; pass B is k_rows_final on
+// it (256-B runs in, row-major rows out, no Jacobian). Measured patterns (profiles/
+// r01_colbench_patterns.log): strided read + contiguous write 3.4 TB/s, against 2.1-2.4 TB/s for
+// the in-place column pass that reads and writes 64-B pieces.
+template <int LOGN>
+__global__ __launch_bounds__(ColFirstCfg<LOGN>::WG1) void k_cols_to_blocks(int images, const float4* __restrict__ src_images,
+                                                                          float4* __restrict__ work,
+                                                                          const float2* __restrict__ tw_glob)
+{
+  using S = FftShape<LOGN>;
+  using K = ColFirstCfg<LOGN>;
+  constexpr int N = S::N, T = S::T, B = K::B, SPW = K::SPW;
+  static_assert(SPW == 1, "one strip per item");
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  float2* tw = reinterpret_cast<float2*>(smem);
+  void* xch = smem + ((S::TW_ENTRIES * 8 + 15) / 16) * 16;
+  load_twiddles<LOGN>(tw, tw_glob);
+  const int strips = N / B;
+  const int total = images * strips;
+  // adjacent strips (the two 64-B halves of each 128-B line) on blocks b, b+8: one XCD, one L2
+  for (int item = xcd_pair_slot(blockIdx.x, gridDim.x); item < total; item += gridDim.x)
+  {
+    const int tid = opaque((int)threadIdx.x);
+    const int b = tid % B, i = (tid / B) % T;
+    const int img = item / strips, xb = item - img * strips;
+    // row y = i + mm*T of the input, column xb*B + b: uniform base per m, lane offset (i*N + b)*16
+    const float4* src = src_images + ((size_t)img << (2 * LOGN)) + (size_t)xb * B;
+    const int voff = ((i << LOGN) + b) * 16;
+    CPair v[16];
+#pragma unroll
+    for (int m = 0; m < 16; m++)
+      v[m] = to_pair(ld4<kStream>(src + ((size_t)(((m + 8) & 15) * T) << LOGN), voff));  // fftShift on y
+    fft_run<LOGN, K::C1, true>(v, i, b, xch, tw);
+    float4* dst = work + ((size_t)img << (2 * LOGN)) + (size_t)xb * N * B;
+    const int soff = (i * B + b) * 16;
+#pragma unroll
+    for (int m = 0; m < 16; m++)
+      st4<kStream>(dst + m * T * B, soff, pair_raw(v[m]));
+  }
+}
+
 // BLOCKED: input is pass 1's output after the exchange, inter[c][src][img][xb_local][y][B] for this
 // rank's w rows (xb = src * (w/B) + xb_local); otherwise row-major [c][img][y][x] (after
 // k_blocks_to_rows, used when B == 1).
@@ -1060,7 +1104,7 @@ __global__ __launch_bounds__(ColFirstCfg<LOGN>::WG1) void k_cols_evolve(
 // 2 = no FFT (memory traffic and stores only).
 template <int LOGN, bool BLOCKED, int LA = kStream, int SA = kStream, int RPW_ = ColFirstCfg<LOGN>::RPW2, int ABL = 0>
 __global__ __launch_bounds__(FftShape<LOGN>::T * RPW_) void k_rows_final(
-    int cascades, SlabGeom g, const float4* __restrict__ inter, float4* __restrict__ maps, float* __restrict__ jac,
+    int images, SlabGeom g, const float4* __restrict__ inter, float4* __restrict__ maps, float* __restrict__ jac,
     FoamParams foam, const float2* __restrict__ tw_glob)
 {
   using S = FftShape<LOGN>;
@@ -1080,7 +1124,7 @@ __global__ __launch_bounds__(FftShape<LOGN>::T * RPW_) void k_rows_final(
   const int b0 = threadIdx.x % B, r0 = (threadIdx.x / B) % RPW, ihi0 = threadIdx.x / (B * RPW);
   const int i20 = threadIdx.x % T, r20 = threadIdx.x / T;
   constexpr bool REMAP = BLOCKED && S::NSTAGE > 1;
-  const int total = cascades * 2 * blocks;
+  const int total = images * blocks;  // images = 2 per cascade (height, displacement)
   for (int item = blockIdx.x; item < total; item += gridDim.x)
   {
     int i, r;
@@ -1134,7 +1178,7 @@ __global__ __launch_bounds__(FftShape<LOGN>::T * RPW_) void k_rows_final(
         asm volatile("" ::"v"(v[m].re), "v"(v[m].im));
       else
         st4<SA>(dst + m * T, woff, from_pair(v[m]));
-    if (img & 1)
+    if (jac != nullptr && (img & 1))  // jac == nullptr: plain EncodeIFFT (launch_ifft_colfirst)
     {
       // displacementMap (Dz, dDx/dx, dDz/dz, dDx/dz) = (re0, im0, re1, im1): Jacobian,
       // spectrum.compute:246-259
@@ -1431,6 +1475,35 @@ hipError_t launch_cols_evolve(int logn, const FrameParams& fp, const SlabGeom& g
   });
 }
 
+bool ifft_colfirst_supported(int logn) { return logn == 12; }
+
+hipError_t launch_ifft_colfirst(int logn, int n_images, float4* images, float4* work, const float2* tw,
+                                hipStream_t stream, int cus)
+{
+  if (!ifft_colfirst_supported(logn))
+    return hipErrorInvalidValue;
+  constexpr int LOGN = 12;
+  using K = ColFirstCfg<LOGN>;
+  using S = FftShape<LOGN>;
+  const int tw_bytes = ((S::TW_ENTRIES * 8 + 15) / 16) * 16;
+  {
+    auto kern = k_cols_to_blocks<LOGN>;
+    const int lds = tw_bytes + K::LDS1;
+    const int grid = persistent_grid(kern, K::WG1, lds, n_images * (S::N / K::B), cus);
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(K::WG1), lds, stream, n_images, images, work, tw);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess)
+      return e;
+  }
+  auto kern = k_rows_final<LOGN, true>;
+  const int lds = tw_bytes + K::LDS2;
+  const SlabGeom g{0, S::N};
+  const int grid = persistent_grid(kern, K::WG2, lds, n_images * (S::N / K::RPW2), cus);
+  hipLaunchKernelGGL(kern, dim3(grid), dim3(K::WG2), lds, stream, n_images, g, work, images, (float*)nullptr,
+                     FoamParams{}, tw);
+  return hipGetLastError();
+}
+
 // The largest H-retention that compiles without spills for this size (see k_cols_evolve).
 int default_keep(int logn) { return logn >= 13 ? 0 : (logn == 12 ? 4 : 16); }
 
@@ -1490,13 +1563,13 @@ hipError_t launch_rows_final(int logn, int cascades, const SlabGeom& g, const fl
     {
       auto kern = k_rows_final<LOGN, false>;
       const int grid = persistent_grid(kern, K::WG2, lds, items, cus);
-      hipLaunchKernelGGL(kern, dim3(grid), dim3(K::WG2), lds, stream, cascades, g, scratch, maps, jac, foam, tw);
+      hipLaunchKernelGGL(kern, dim3(grid), dim3(K::WG2), lds, stream, 2 * cascades, g, scratch, maps, jac, foam, tw);
     }
     else
     {
       auto kern = k_rows_final<LOGN, true>;
       const int grid = persistent_grid(kern, K::WG2, lds, items, cus);
-      hipLaunchKernelGGL(kern, dim3(grid), dim3(K::WG2), lds, stream, cascades, g, inter, maps, jac, foam, tw);
+      hipLaunchKernelGGL(kern, dim3(grid), dim3(K::WG2), lds, stream, 2 * cascades, g, inter, maps, jac, foam, tw);
     }
     return hipGetLastError();
   });
@@ -1565,7 +1638,7 @@ hipError_t launch_policy_variant(int pass, int policy, const FrameParams& fp, co
     const int lds = ((S::TW_ENTRIES * 8 + 15) / 16) * 16 + lds_row_slots<LOGN>(rpw) * 8;
     const int items = fp.cascades * 2 * (g.w / rpw);
     const int grid = persistent_grid(kern, S::T * rpw, lds, items, cus);
-    hipLaunchKernelGGL(kern, dim3(grid), dim3(S::T * rpw), lds, stream, fp.cascades, g, in, out, jac, foam, tw);
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(S::T * rpw), lds, stream, 2 * fp.cascades, g, in, out, jac, foam, tw);
   }
   return hipGetLastError();
 }

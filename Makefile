@@ -21,7 +21,8 @@ APP := examples/waveapp_headless
 
 all: $(LIB) $(WAVES) $(ORACLE) $(CPPTEST) $(APP)
 
-$(CSRC)/build/ocean_kernels.o: $(CSRC)/ocean_kernels.hip $(CSRC)/ocean_internal.h
+DEVICE_H := $(wildcard $(CSRC)/device/*.h)
+$(CSRC)/build/ocean_kernels.o: $(CSRC)/ocean_kernels.hip $(CSRC)/ocean_internal.h $(DEVICE_H)
 	@mkdir -p $(CSRC)/build
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
@@ -55,12 +56,12 @@ $(APP): examples/waveapp_headless.cpp $(WAVES)
 
 MB := tools/microbench
 microbench: $(MB)/genbench $(MB)/colbench $(MB)/copybench $(MB)/genbench_noxch $(MB)/genbench_nobar $(MB)/layoutbench
-$(MB)/%: $(MB)/%.hip $(CSRC)/ocean_kernels.hip $(CSRC)/ocean_internal.h
+$(MB)/%: $(MB)/%.hip $(CSRC)/ocean_kernels.hip $(CSRC)/ocean_internal.h $(DEVICE_H)
 	$(HIPCC) $(HIPFLAGS) $< -o $@
 # timing ablations (wrong results by construction): no LDS exchanges / exchanges without barriers
-$(MB)/genbench_noxch: $(MB)/genbench.hip $(CSRC)/ocean_kernels.hip $(CSRC)/ocean_internal.h
+$(MB)/genbench_noxch: $(MB)/genbench.hip $(CSRC)/ocean_kernels.hip $(CSRC)/ocean_internal.h $(DEVICE_H)
 	$(HIPCC) $(HIPFLAGS) -DOCEAN_ABLATE_EXCHANGE $< -o $@
-$(MB)/genbench_nobar: $(MB)/genbench.hip $(CSRC)/ocean_kernels.hip $(CSRC)/ocean_internal.h
+$(MB)/genbench_nobar: $(MB)/genbench.hip $(CSRC)/ocean_kernels.hip $(CSRC)/ocean_internal.h $(DEVICE_H)
 	$(HIPCC) $(HIPFLAGS) -DOCEAN_ABLATE_BARRIER $< -o $@
 
 clean:

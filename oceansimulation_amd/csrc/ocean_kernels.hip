@@ -1,5 +1,6 @@
 // ocean_kernels.hip — gfx950 device code for the ocean hot path:
-//   h0(k) JONSWAP seeding  ->  h(k,t) evolution fused into the row iFFT  ->  column iFFT + foam.
+//   h0(k) JONSWAP seeding -> h(k,t) evolution fused into the column iFFT -> row iFFT + foam,
+//   plus the standalone EncodeIFFT, the slab transpose and the surface consumer.
 //
 // Reference semantics (paths relative to the reference root):
 //   spectrum seeding      resources/spectrum.compute:38-172   (generateSpectrum)
@@ -9,19 +10,17 @@
 //   Jacobian / foam       resources/spectrum.compute:246-259
 //
 // MI355X design (DESIGN.md has the byte accounting):
-//   * 2 HBM passes per frame. Row pass: read h0 (16 B/texel), evolve in registers, 4 complex fields
-//     transformed along x, write heightMap + displacementMap rows (32 B). Column pass: read each
-//     image's column strips (16 B), transform along y, write back in place (16 B), and for the
-//     displacement image write the Jacobian (4 B). 116 B per height-field point.
-//   * Each 1D transform is a self-sorting Stockham FFT: one radix-16 butterfly per thread per
-//     stage held in VGPRs (16 points x 1-2 complex lanes), LDS only for the exchange between
-//     stages (N = 4096 = 16^3 -> 2 exchanges). fftShift is folded into the load index; no
-//     bit-reversal pass exists.
-//   * Twiddles: exact (host-double-rounded) two-level table in LDS, w = A[e>>LB] * B[e & mask].
-//   * Column pass: a strip of C texel columns per workgroup, 4 lanes per row segment (64 B at
-//     N = 4096); strips 2m and 2m+1 are given to blocks b and b+8 (same XCD under the observed
-//     round-robin placement) so both halves of each 128-B line are consumed from one L2.
-//   * Persistent grids sized from occupancy; every loop has a plain item-count exit.
+//   * Generator frame = 2 HBM passes, column pass first (116 B per height-field point):
+//     k_cols_evolve reads the strip-blocked h0 (16 B), evolves and packs both images in registers,
+//     iFFTs along y and writes the blocked intermediate (32 B); k_rows_final reads it in 256-B runs
+//     (32 B), iFFTs along x and writes the row-major maps (32 B) and the Jacobian (4 B).
+//   * Each 1D transform is a self-sorting Stockham FFT held in VGPRs (device/fft.h): 16 points per
+//     thread, radix-16 stages, split-plane packed complex math, LDS only between stages. fftShift
+//     is folded into load indices; no bit-reversal pass exists.
+//   * Persistent grids sized from occupancy (optionally for a CU budget); every loop has a plain
+//     item-count exit.
+// Device building blocks live in device/{spectrum,memory,fft,evolve}.h; this file holds the kernels
+// and their host launchers (ocean_internal.h declares the launchers).
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
@@ -30,150 +29,13 @@
 #include <vector>
 
 #include "ocean_internal.h"
+#include "device/evolve.h"
+#include "device/fft.h"
+#include "device/memory.h"
+#include "device/spectrum.h"
 
 namespace oceanfft
 {
-
-// ------------------------------------------------------------------------------------------------
-// Constants (resources/spectrum.compute:4, :34-35; resources/fft.compute:14 rounds to the same float)
-// ------------------------------------------------------------------------------------------------
-#define OCEAN_PI 3.14159265358f
-static constexpr float kSigmaSurface = 0.072f;
-static constexpr float kRhoWater = 1000.0f;
-
-// ------------------------------------------------------------------------------------------------
-// Spectrum math — float32 restatement of resources/spectrum.compute, same operation order.
-// ------------------------------------------------------------------------------------------------
-__device__ __forceinline__ uint32_t hash_raw(uint32_t x, uint32_t y)
-{
-  // spectrum.compute:109-114
-  uint32_t h32 = y + 374761393u + x * 3266489917u;
-  h32 = 2246822519u * (h32 ^ (h32 >> 15));
-  h32 = 3266489917u * (h32 ^ (h32 >> 13));
-  return h32 ^ (h32 >> 16);
-}
-
-__device__ __forceinline__ float2 hash_uniform(uint32_t x, uint32_t y)
-{
-  // spectrum.compute:115-116
-  uint32_t n = hash_raw(x, y);
-  uint32_t rz1 = n * 48271u;
-  return make_float2((float)((n >> 1) & 0x7FFFFFFFu) / (float)0x7FFFFFFF,
-                     (float)((rz1 >> 1) & 0x7FFFFFFFu) / (float)0x7FFFFFFF);
-}
-
-// Settings-only terms of GetSpectrumAmplitude, evaluated once per launch on the host with the
-// oracle's fp32 expressions and glibc powf (bit-identical to the reference restatement) instead of
-// once per evaluation on the device.
-struct SpectrumConsts
-{
-  float dk, half_dim, theta_0, g, h;
-  float alpha_g2;     // alpha * g * g (spectrum.compute:62, :70)
-  float omega_p;      // 22 (g^2 / (U F))^0.333 (spectrum.compute:143)
-  float sqrt_h_g;     // sqrt(h / g) (spectrum.compute:74)
-  float hassel_hi;    // exponent of the w > w_p branch (spectrum.compute:100)
-  float swell2;       // swell * swell
-  float spread, spread_2pi;
-  float c;            // 0.1 * scale
-  float seed_x, seed_y;
-  float sigma_rho;    // sigma_surface / rho_water
-};
-
-SpectrumConsts spectrum_consts(const OceanSettings& s, int n)
-{
-  SpectrumConsts q;
-  q.dk = 2.0f * OCEAN_PI / s.planeSize;
-  q.half_dim = (float)n / 2.0f;
-  q.theta_0 = s.theta_0;
-  q.g = s.g;
-  q.h = s.h;
-  const float alpha = 0.076f * powf(s.U_10 * s.U_10 / (s.F * s.g), 0.22f);
-  q.alpha_g2 = alpha * s.g * s.g;
-  q.omega_p = 22.0f * powf(s.g * s.g / (s.U_10 * s.F), 0.333f);
-  q.sqrt_h_g = sqrtf(s.h / s.g);
-  q.hassel_hi = -2.33f - 1.45f * (s.U_10 * q.omega_p / s.g - 1.17f);
-  q.swell2 = s.swell * s.swell;
-  q.spread = s.spread;
-  q.spread_2pi = s.spread / (2.0f * OCEAN_PI);
-  q.c = 0.1f * s.scale;
-  q.seed_x = (float)s.seed[0];
-  q.seed_y = (float)s.seed[1];
-  q.sigma_rho = kSigmaSurface / kRhoWater;
-  return q;
-}
-
-// Fast transcendentals for the spectrum (tolerance: h0 within 1e-5 of max|h0|, tests/parity.py):
-// hardware v_log_f32 / v_exp_f32 (log2 / exp2, ~1 ulp) build pow, exp and log; tanh and sech come
-// from one exp each, with an odd series where 1 - 2/(1 + e^2x) would cancel.
-__device__ __forceinline__ float log2_hw(float x) { return __builtin_amdgcn_logf(x); }
-__device__ __forceinline__ float exp2_hw(float x) { return __builtin_amdgcn_exp2f(x); }
-__device__ __forceinline__ float exp_hw(float x) { return exp2_hw(x * 1.44269504088896341f); }
-__device__ __forceinline__ float pow_pos(float x, float y) { return exp2_hw(y * log2_hw(x)); }  // x >= 0, y > 0 or x > 0
-__device__ __forceinline__ float rcp_hw(float x) { return __builtin_amdgcn_rcpf(x); }
-__device__ __forceinline__ float tanh_pos(float x)  // x >= 0
-{
-  if (x < 0.125f)
-  {
-    const float x2 = x * x;
-    return x * fmaf(fmaf(fmaf(-17.0f / 315.0f, x2, 2.0f / 15.0f), x2, -1.0f / 3.0f), x2, 1.0f);
-  }
-  return 1.0f - 2.0f * rcp_hw(1.0f + exp_hw(2.0f * x));
-}
-
-// GetSpectrumAmplitude (spectrum.compute:129-155) at grid index (tx, ty), same formula and order of
-// the reference with the settings-only terms hoisted (SpectrumConsts).
-__device__ __forceinline__ float2 spectrum_amplitude(const SpectrumConsts& q, float tx, float ty)
-{
-  const float kx = (tx - q.half_dim) * q.dk;
-  const float ky = (ty - q.half_dim) * q.dk;
-  const float k2 = kx * kx + ky * ky;
-  if (k2 == 0.0f)
-    return make_float2(0.0f, 0.0f);
-  const float k = __builtin_amdgcn_sqrtf(k2);
-  const float theta = atan2f(ky, kx) - q.theta_0;
-
-  // Dispersion (spectrum.compute:38-44)
-  const float kh = k * q.h;
-  const float tanhKH = kh >= 2.0f * OCEAN_PI ? 1.0f : tanh_pos(kh);
-  const float gk_sk3 = q.g * k + q.sigma_rho * k * k * k;
-  const float omega = __builtin_amdgcn_sqrtf(gk_sk3 * tanhKH);
-  const float rw = rcp_hw(omega);
-
-  // JONSWAP (spectrum.compute:60-78)
-  const float w_p = q.omega_p;
-  const float sigma = omega > w_p ? 0.09f : 0.07f;
-  const float diff = omega - w_p;
-  const float r = exp_hw(-diff * diff * rcp_hw(2.0f * sigma * sigma * w_p * w_p));
-  const float ratio = w_p * rw, ratio2 = ratio * ratio;
-  const float rw2 = rw * rw;
-  const float S = q.alpha_g2 * (rw2 * rw2 * rw) * exp_hw(-1.25f * (ratio2 * ratio2)) *
-                  exp2_hw(r * 1.72246602447109f);  // 3.3^r, log2(3.3)
-  const float w_h = fminf(omega * q.sqrt_h_g, 2.0f);
-  float t = fminf(fmaxf(w_h * (1.0f / 2.2f), 0.0f), 1.0f);
-  const float Sj = S * (t * t * (3.0f - 2.0f * t));
-
-  // Hasselmann + Longuet-Higgins spreading (spectrum.compute:81-106)
-  const float p = omega * rcp_hw(w_p);
-  const float sp = omega <= w_p ? 6.97f * pow_pos(p, 4.06f) : 9.77f * pow_pos(p, q.hassel_hi);
-  const float sh = sp + 16.0f * tanh_pos(w_p * rw) * q.swell2;
-  const float lh = sh < 0.4f ? (0.5f / OCEAN_PI) + sh * (0.220636f + sh * (-0.109f + sh * 0.090f))
-                             : 0.56418958354775628f * (0.5f * __builtin_amdgcn_sqrtf(sh) + 0.0625f * __builtin_amdgcn_rsqf(sh));
-  const float ct = fabsf(__builtin_amdgcn_cosf(theta * (0.5f * 0.15915494309189533577f)));  // cos(theta/2)
-  const float d = (1.0f - q.spread) * (lh * pow_pos(ct, 2.0f * sh)) + q.spread_2pi;
-
-  // DispersionDerivative (spectrum.compute:50-57), sech = 2 e^-x / (1 + e^-2x)
-  const float em = exp_hw(-q.h * k);
-  const float sech = 2.0f * em * rcp_hw(1.0f + em * em);
-  const float deriv = (q.h * gk_sk3 * sech * sech + omega * omega) * (0.5f * rw);
-  const float chain = deriv * rcp_hw(k) * q.dk * q.dk;
-
-  // Hash + Box-Muller (spectrum.compute:109-127, :153): uvec2(thread + seed)
-  const float2 u = hash_uniform((uint32_t)(int64_t)(tx + q.seed_x), (uint32_t)(int64_t)(ty + q.seed_y));
-  const float rad = __builtin_amdgcn_sqrtf(-2.0f * 0.69314718055994531f * log2_hw(u.x));
-  const float sn = __builtin_amdgcn_sinf(u.y), cs = __builtin_amdgcn_cosf(u.y);  // angle 2 pi u.y
-  const float amp = __builtin_amdgcn_sqrtf(2.0f * Sj * d * chain);
-  return make_float2(q.c * (rad * cs) * amp, q.c * (rad * sn) * amp);
-}
 
 // generateSpectrum (spectrum.compute:157-172): texel = (h0(k), conj(h0(-k))), -k taken as N - i.
 // Stored strip-blocked, h0[xb][y][blk] (blk texel columns per strip, see ColFirstCfg), so the
@@ -255,561 +117,6 @@ __global__ void k_hash(const uint32_t* __restrict__ xy, int count, uint32_t* __r
     raw[i] = hash_raw(xy[2 * i], xy[2 * i + 1]);
     uv[i] = hash_uniform(xy[2 * i], xy[2 * i + 1]);
   }
-}
-
-// ------------------------------------------------------------------------------------------------
-// Buffer (SRD) global access: wave-uniform base in SGPRs + one 32-bit lane offset (T8 in the CDNA
-// guide). Keeps the 16 per-thread element addresses out of VGPRs. Offsets stay < 2^31 bytes.
-// ------------------------------------------------------------------------------------------------
-typedef float f4v __attribute__((ext_vector_type(4)));
-
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t srd(const void* base, int num_bytes)
-{
-  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, num_bytes, 0x00020000);
-}
-
-// Raw-buffer range checking: a load at or past num_bytes returns 0 and a store there is dropped,
-// which handles ragged row blocks without branches.
-constexpr int kAllBytes = 0x7FFFFFFF;
-
-// AUX: cache-policy bits of the buffer instruction (0 = default; 2 = nt, streaming / non-temporal).
-template <int AUX = 0>
-__device__ __forceinline__ float4 ld4(const void* base, int voff_bytes, int num_bytes = kAllBytes)
-{
-  f4v r = __builtin_amdgcn_raw_buffer_load_b128(srd(base, num_bytes), voff_bytes, 0, AUX);
-  return make_float4(r.x, r.y, r.z, r.w);
-}
-
-template <int AUX = 0>
-__device__ __forceinline__ void st4(void* base, int voff_bytes, float4 v, int num_bytes = kAllBytes)
-{
-  f4v r = {v.x, v.y, v.z, v.w};
-  __builtin_amdgcn_raw_buffer_store_b128(r, srd(base, num_bytes), voff_bytes, 0, AUX);
-}
-
-template <int AUX = 0>
-__device__ __forceinline__ void st1(void* base, int voff_bytes, float v)
-{
-  __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), srd(base, kAllBytes), voff_bytes, 0, AUX);
-}
-
-__device__ __forceinline__ int clamp_bytes(int64_t b)
-{
-  return b > kAllBytes ? kAllBytes : (b < 0 ? 0 : (int)b);
-}
-
-// ------------------------------------------------------------------------------------------------
-// Complex helpers. V is float2 (one complex lane) or float4 (two lanes: xy, zw), as in the
-// reference's packed RGBA32F images (fft.compute:83-84 transforms xy and zw independently).
-// ------------------------------------------------------------------------------------------------
-__device__ __forceinline__ float2 operator+(float2 a, float2 b) { return make_float2(a.x + b.x, a.y + b.y); }
-__device__ __forceinline__ float2 operator-(float2 a, float2 b) { return make_float2(a.x - b.x, a.y - b.y); }
-__device__ __forceinline__ float4 operator+(float4 a, float4 b)
-{
-  return make_float4(a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w);
-}
-__device__ __forceinline__ float4 operator-(float4 a, float4 b)
-{
-  return make_float4(a.x - b.x, a.y - b.y, a.z - b.z, a.w - b.w);
-}
-// multiply by +i (inverse-transform sign)
-__device__ __forceinline__ float2 mul_i(float2 a) { return make_float2(-a.y, a.x); }
-__device__ __forceinline__ float4 mul_i(float4 a) { return make_float4(-a.y, a.x, -a.w, a.z); }
-// multiply by -i
-__device__ __forceinline__ float2 mul_mi(float2 a) { return make_float2(a.y, -a.x); }
-__device__ __forceinline__ float4 mul_mi(float4 a) { return make_float4(a.y, -a.x, a.w, -a.z); }
-__device__ __forceinline__ float2 cmul(float2 a, float2 w)
-{
-  return make_float2(a.x * w.x - a.y * w.y, a.x * w.y + a.y * w.x);
-}
-__device__ __forceinline__ float4 cmul(float4 a, float2 w)
-{
-  return make_float4(a.x * w.x - a.y * w.y, a.x * w.y + a.y * w.x, a.z * w.x - a.w * w.y,
-                     a.z * w.y + a.w * w.x);
-}
-
-// Two complex lanes in split planes: re = (re0, re1), im = (im0, im1). Every FFT add/sub and
-// twiddle multiply is then one v_pk_{add,mul,fma}_f32 over both lanes (the twiddle's parts are
-// op_sel splats; multiplying by +-i is operand renaming plus a neg modifier), half the VALU issue
-// of the interleaved float4 form. The reference layout (re0, im0, re1, im1) is converted only at
-// global loads/stores of caller-visible images; the generator's intermediate stays split.
-typedef float f2v __attribute__((ext_vector_type(2)));
-struct __attribute__((aligned(16))) CPair
-{
-  f2v re, im;
-};
-__device__ __forceinline__ CPair operator+(CPair a, CPair b) { return {a.re + b.re, a.im + b.im}; }
-__device__ __forceinline__ CPair operator-(CPair a, CPair b) { return {a.re - b.re, a.im - b.im}; }
-__device__ __forceinline__ CPair mul_i(CPair a) { return {-a.im, a.re}; }
-__device__ __forceinline__ CPair mul_mi(CPair a) { return {a.im, -a.re}; }
-__device__ __forceinline__ CPair cmul(CPair a, float2 w)
-{
-  const f2v wx = {w.x, w.x}, wy = {w.y, w.y};
-  return {a.re * wx - a.im * wy, a.re * wy + a.im * wx};
-}
-// reference texel (re0, im0, re1, im1) <-> split planes
-__device__ __forceinline__ CPair to_pair(float4 t) { return {f2v{t.x, t.z}, f2v{t.y, t.w}}; }
-__device__ __forceinline__ float4 from_pair(CPair c) { return make_float4(c.re.x, c.im.x, c.re.y, c.im.y); }
-// the split texel as raw 16 bytes (re0, re1, im0, im1), for the generator's intermediate
-__device__ __forceinline__ CPair raw_pair(float4 t) { return {f2v{t.x, t.y}, f2v{t.z, t.w}}; }
-__device__ __forceinline__ float4 pair_raw(CPair c) { return make_float4(c.re.x, c.re.y, c.im.x, c.im.y); }
-// the two float2 halves a SPLIT LDS exchange moves one at a time
-__device__ __forceinline__ float2 half_of(float4 v, int h) { return h ? make_float2(v.z, v.w) : make_float2(v.x, v.y); }
-__device__ __forceinline__ float2 half_of(CPair v, int h) { return h ? make_float2(v.im.x, v.im.y) : make_float2(v.re.x, v.re.y); }
-__device__ __forceinline__ void set_half(float4& v, int h, float2 r)
-{
-  if (h)
-    v.z = r.x, v.w = r.y;
-  else
-    v.x = r.x, v.y = r.y;
-}
-__device__ __forceinline__ void set_half(CPair& v, int h, float2 r)
-{
-  if (h)
-    v.im = f2v{r.x, r.y};
-  else
-    v.re = f2v{r.x, r.y};
-}
-
-// ------------------------------------------------------------------------------------------------
-// Small inverse DFTs (sign +): X[k] = sum_n x[n] exp(+2 pi i n k / r)
-// ------------------------------------------------------------------------------------------------
-template <typename V>
-__device__ __forceinline__ void idft2(V& a0, V& a1)
-{
-  V t = a0 - a1;
-  a0 = a0 + a1;
-  a1 = t;
-}
-
-template <typename V>
-__device__ __forceinline__ void idft4(V& a0, V& a1, V& a2, V& a3)
-{
-  V s0 = a0 + a2, d0 = a0 - a2, s1 = a1 + a3, d1 = a1 - a3;
-  a0 = s0 + s1;
-  a2 = s0 - s1;
-  a1 = d0 + mul_i(d1);
-  a3 = d0 - mul_i(d1);
-}
-
-// In: v[n], n = 0..7. Out: v[k] = X[k] (natural order).
-template <typename V>
-__device__ __forceinline__ void idft8(V* v)
-{
-  const float R2 = 0.70710678118654752f;
-  // n = 2*n1 + n2: DFT4 over n1 for n2 = 0, 1
-  idft4(v[0], v[2], v[4], v[6]);
-  idft4(v[1], v[3], v[5], v[7]);
-  // Y[n2=1][k1] *= W8^k1 (inverse)
-  v[3] = cmul(v[3], make_float2(R2, R2));
-  v[5] = mul_i(v[5]);
-  v[7] = cmul(v[7], make_float2(-R2, R2));
-  // DFT2 over n2: X[k1] = Y0[k1] + Y1[k1], X[k1 + 4] = Y0[k1] - Y1[k1]
-  V y00 = v[0], y01 = v[2], y02 = v[4], y03 = v[6];
-  V y10 = v[1], y11 = v[3], y12 = v[5], y13 = v[7];
-  v[0] = y00 + y10;
-  v[4] = y00 - y10;
-  v[1] = y01 + y11;
-  v[5] = y01 - y11;
-  v[2] = y02 + y12;
-  v[6] = y02 - y12;
-  v[3] = y03 + y13;
-  v[7] = y03 - y13;
-}
-
-// In: v[n], n = 0..15. Out: v[k] = X[k] (natural order). 4 x 4 decomposition.
-template <typename V>
-__device__ __forceinline__ void idft16(V* v)
-{
-  const float C1 = 0.92387953251128674f;  // cos(pi/8)
-  const float S1 = 0.38268343236508977f;  // sin(pi/8)
-  const float R2 = 0.70710678118654752f;
-  // n = 4*n1 + n2: DFT4 over n1 for each n2 -> Y[n2][k1] at v[4*k1 + n2]
-  idft4(v[0], v[4], v[8], v[12]);
-  idft4(v[1], v[5], v[9], v[13]);
-  idft4(v[2], v[6], v[10], v[14]);
-  idft4(v[3], v[7], v[11], v[15]);
-  // twiddle Y[n2][k1] *= W16^(n2*k1), inverse sign
-  v[5] = cmul(v[5], make_float2(C1, S1));     // n2=1,k1=1: W^1
-  v[9] = cmul(v[9], make_float2(R2, R2));     // n2=1,k1=2: W^2
-  v[13] = cmul(v[13], make_float2(S1, C1));   // n2=1,k1=3: W^3
-  v[6] = cmul(v[6], make_float2(R2, R2));     // n2=2,k1=1: W^2
-  v[10] = mul_i(v[10]);                       // n2=2,k1=2: W^4
-  v[14] = cmul(v[14], make_float2(-R2, R2));  // n2=2,k1=3: W^6
-  v[7] = cmul(v[7], make_float2(S1, C1));     // n2=3,k1=1: W^3
-  v[11] = cmul(v[11], make_float2(-R2, R2));  // n2=3,k1=2: W^6
-  v[15] = cmul(v[15], make_float2(-C1, -S1)); // n2=3,k1=3: W^9
-  // DFT4 over n2 for each k1: X[k1 + 4*k2]
-  idft4(v[0], v[1], v[2], v[3]);
-  idft4(v[4], v[5], v[6], v[7]);
-  idft4(v[8], v[9], v[10], v[11]);
-  idft4(v[12], v[13], v[14], v[15]);
-  // now v[4*k1 + k2] = X[k1 + 4*k2]; transpose the 4x4 index to natural order
-  V t;
-  t = v[1], v[1] = v[4], v[4] = t;
-  t = v[2], v[2] = v[8], v[8] = t;
-  t = v[3], v[3] = v[12], v[12] = t;
-  t = v[6], v[6] = v[9], v[9] = t;
-  t = v[7], v[7] = v[13], v[13] = t;
-  t = v[11], v[11] = v[14], v[14] = t;
-}
-
-// ------------------------------------------------------------------------------------------------
-// Stockham radix-16 FFT of length N = 2^LOGN held by T = N/16 cooperating threads.
-// Thread i owns v[m] = x[i + m*T]. Stage with radix r and span p (Bainville's formulation):
-//   butterfly b, k = b mod p: inputs x[b + t*N/r], twiddle exp(+2 pi i t k / (r p)),
-//   outputs y[(b/p)*r*p + k + t*p].
-// The first stage uses radix R0 = 2^(LOGN mod 4) (or 16) with p = 1; the rest are radix 16.
-// After the last stage (p = T) thread i holds X[i + m*T] directly — no final exchange.
-// ------------------------------------------------------------------------------------------------
-template <int LOGN>
-struct FftShape
-{
-  static constexpr int N = 1 << LOGN;
-  static constexpr int T = N >> 4;
-  static constexpr int LOG_R0 = (LOGN & 3) ? (LOGN & 3) : 4;
-  static constexpr int R0 = 1 << LOG_R0;
-  static constexpr int NSTAGE = 1 + (LOGN - LOG_R0) / 4;
-  static constexpr int PADDED = N + N / 16;  // one pad slot per 16: conflict-free Stockham writes
-  static constexpr int LB = LOGN / 2;        // two-level twiddle table split
-  static constexpr int TB = 1 << LB;
-  static constexpr int TA = N >> LB;
-  static constexpr int TW_ENTRIES = TA + TB;
-};
-
-__device__ __forceinline__ int pad16(int a) { return a + (a >> 4); }
-
-// Hide a loop-invariant value from LICM: without this, hipcc hoists ~100 per-thread LDS/global
-// address computations out of the persistent loops and spills them to scratch.
-__device__ __forceinline__ int opaque(int v)
-{
-  asm volatile("" : "+v"(v));
-  return v;
-}
-
-// w = exp(+2 pi i e / N) from the two-level table (exact host-rounded entries, one cmul).
-template <int LOGN>
-__device__ __forceinline__ float2 twiddle(int e, const float2* __restrict__ tw)
-{
-  using S = FftShape<LOGN>;
-  float2 lo = tw[e & (S::TB - 1)];
-  float2 hi = tw[S::TB + (e >> S::LB)];
-  return cmul(lo, hi);
-}
-
-// v[t] *= w^t for t = 1..15, w = exp(+2 pi i e1 / N). w and w^4 come from the exact table; the
-// other powers are products of at most three table values (error <= ~3 ulp), which keeps only a
-// handful of twiddles live instead of 30 hoisted LDS reads.
-template <int LOGN, typename V>
-__device__ __forceinline__ void apply_stage_twiddles(V* v, int e1, const float2* __restrict__ tw)
-{
-  constexpr int N = 1 << LOGN;
-  const float2 w1 = twiddle<LOGN>(e1, tw);
-  const float2 w4 = twiddle<LOGN>((4 * e1) & (N - 1), tw);
-  const float2 w2 = cmul(w1, w1);
-  const float2 w3 = cmul(w2, w1);
-  v[1] = cmul(v[1], w1);
-  v[2] = cmul(v[2], w2);
-  v[3] = cmul(v[3], w3);
-  v[4] = cmul(v[4], w4);
-  v[5] = cmul(v[5], cmul(w4, w1));
-  v[6] = cmul(v[6], cmul(w4, w2));
-  v[7] = cmul(v[7], cmul(w4, w3));
-  const float2 w8 = cmul(w4, w4);
-  v[8] = cmul(v[8], w8);
-  v[9] = cmul(v[9], cmul(w8, w1));
-  v[10] = cmul(v[10], cmul(w8, w2));
-  v[11] = cmul(v[11], cmul(w8, w3));
-  const float2 w12 = cmul(w8, w4);
-  v[12] = cmul(v[12], w12);
-  v[13] = cmul(v[13], cmul(w12, w1));
-  v[14] = cmul(v[14], cmul(w12, w2));
-  v[15] = cmul(v[15], cmul(w12, w3));
-}
-
-// LDS exchange layout. Element a of the transform lives at padded index pa = a + (a >> 4) (one pad
-// slot per 16 elements: conflict-free Stockham writes). Region `reg`:
-//   row layout (CI == 0):  slot = reg * RSTRIDE + pa, RSTRIDE = PADDED + 4 (the +4 staggers regions
-//                          by 8 banks, so lanes that differ only in reg do not collide)
-//   column layout (CI > 0): slot = pa * CI + reg (CI columns interleaved)
-// Write/read indices are passed as PADDED indices in closed form (base + t*stride where the
-// stride is a multiple of 16 elements), so the per-t offsets fold into ds_* immediates instead
-// of occupying 16 address VGPRs.
-template <int CI, int PADDED>
-__device__ __forceinline__ int lds_slot(int reg, int pa)
-{
-  if constexpr (CI > 0)
-    return pa * CI + reg;
-  else
-    return reg * (PADDED + 4) + pa;
-}
-
-template <int LOGN>
-__host__ __device__ constexpr int lds_row_slots(int regions)
-{
-  return regions * (FftShape<LOGN>::PADDED + 4);
-}
-
-// Padded index of x[i + m*T] (the next stage's inputs).
-template <int LOGN>
-__device__ __forceinline__ int read_pidx(int i, int m)
-{
-  constexpr int T = FftShape<LOGN>::T;
-  if constexpr ((T & 15) == 0)
-    return pad16(i) + m * (T + T / 16);
-  else
-    return pad16(i + m * T);
-}
-
-#if defined(OCEAN_ABLATE_EXCHANGE) || defined(OCEAN_ABLATE_BARRIER)
-__device__ __forceinline__ void touch(float4& v) { asm volatile("" : "+v"(v.x), "+v"(v.y), "+v"(v.z), "+v"(v.w)); }
-__device__ __forceinline__ void touch(CPair& v) { asm volatile("" : "+v"(v.re), "+v"(v.im)); }
-#endif
-#if defined(OCEAN_ABLATE_BARRIER)  // microbench-only timing ablation (results are wrong)
-#define XSYNC() asm volatile("" ::: "memory")
-#else
-#define XSYNC() __syncthreads()
-#endif
-
-// Write the 16 stage outputs (padded indices wp(t), region reg_w), barrier, read back the next
-// stage's inputs for the thread's (possibly different) position i_r in region reg_r, barrier.
-// SPLIT: float4 data exchanged as two float2 lanes through a float2 buffer (half the LDS).
-template <int LOGN, int CI, bool SPLIT, typename V, typename WP>
-__device__ __forceinline__ void exchange(V* v, int reg_w, int i_r, int reg_r, void* lds_raw, WP wp)
-{
-  using S = FftShape<LOGN>;
-#if defined(OCEAN_ABLATE_EXCHANGE)  // microbench-only timing ablation (results are wrong)
-  for (int t = 0; t < 16; t++)
-    touch(v[t]);
-  return;
-#endif
-  if constexpr (!SPLIT)
-  {
-    V* lds = reinterpret_cast<V*>(lds_raw);
-#pragma unroll
-    for (int t = 0; t < 16; t++)
-      lds[lds_slot<CI, S::PADDED>(reg_w, wp(t))] = v[t];
-    XSYNC();
-#pragma unroll
-    for (int m = 0; m < 16; m++)
-      v[m] = lds[lds_slot<CI, S::PADDED>(reg_r, read_pidx<LOGN>(i_r, m))];
-    XSYNC();
-  }
-  else
-  {
-    static_assert(sizeof(V) == 16, "SPLIT exchange is for two-lane data");
-    float2* lds = reinterpret_cast<float2*>(lds_raw);
-#pragma unroll
-    for (int half = 0; half < 2; half++)
-    {
-#pragma unroll
-      for (int t = 0; t < 16; t++)
-        lds[lds_slot<CI, S::PADDED>(reg_w, wp(t))] = half_of(v[t], half);
-      XSYNC();
-#pragma unroll
-      for (int m = 0; m < 16; m++)
-        set_half(v[m], half, lds[lds_slot<CI, S::PADDED>(reg_r, read_pidx<LOGN>(i_r, m))]);
-      XSYNC();
-    }
-  }
-}
-
-// Full 1D inverse FFT (unnormalised) of the transforms held by the workgroup.
-// On entry thread holds v[m] = x[i + m*T] of transform `reg`; the first exchange re-deals the data
-// so that from then on (and on exit, v[m] = X[i2 + m*T]) the thread is position i2 of transform
-// reg2. Any bijection (i, reg) -> (i2, reg2) over the workgroup is valid: it lets the global loads
-// and the global stores use different lane mappings for free. Transforms with a single stage
-// (N = 16) have no exchange and require i2 == i, reg2 == reg.
-template <int LOGN, int CI, bool SPLIT, typename V>
-__device__ __forceinline__ void fft_run(V* v, int i, int reg, int i2, int reg2, void* lds,
-                                        const float2* __restrict__ tw)
-{
-  using S = FftShape<LOGN>;
-  constexpr int N = S::N, T = S::T, R0 = S::R0;
-
-  // ---- stage 0: radix R0, p = 1 (no twiddles) ----
-  if constexpr (R0 == 16)
-  {
-    idft16(v);
-    if constexpr (S::NSTAGE > 1)
-    {
-      const int base = 17 * i;  // pad16(16 i + t) = 17 i + t
-      exchange<LOGN, CI, SPLIT>(v, reg, i2, reg2, lds, [&](int t) { return base + t; });
-    }
-  }
-  else
-  {
-    constexpr int U = 16 / R0;  // butterflies per thread; butterfly u uses v[u + t*U]
-#pragma unroll
-    for (int u = 0; u < U; u++)
-    {
-      V w[R0];
-#pragma unroll
-      for (int t = 0; t < R0; t++)
-        w[t] = v[u + t * U];
-      if constexpr (R0 == 2)
-        idft2(w[0], w[1]);
-      else if constexpr (R0 == 4)
-        idft4(w[0], w[1], w[2], w[3]);
-      else
-        idft8(w);
-#pragma unroll
-      for (int t = 0; t < R0; t++)
-        v[u + t * U] = w[t];
-    }
-    // output of butterfly b = i + u*T, element t -> y[b*R0 + t]; v index q = u + t*U
-    exchange<LOGN, CI, SPLIT>(v, reg, i2, reg2, lds, [&](int q) {
-      int u = q % U, t = q / U;
-      return pad16((i + u * T) * R0 + t);
-    });
-  }
-
-  // ---- radix-16 stages (position i2 of transform reg2) ----
-  int p = R0;
-#pragma unroll
-  for (int s = 1; s < S::NSTAGE; s++)
-  {
-    const int k = i2 & (p - 1);
-    const int stride = N / (16 * p);  // twiddle exponent unit for this stage, in 2 pi / N
-    apply_stage_twiddles<LOGN>(v, k * stride, tw);
-    idft16(v);
-    if (s + 1 < S::NSTAGE)
-    {
-      const int j = (i2 / p) * 16 * p + k;
-      const int pp = p;
-      if (pp >= 16)
-      {
-        const int base = pad16(j), st = pp + pp / 16;
-        exchange<LOGN, CI, SPLIT>(v, reg2, i2, reg2, lds, [&](int t) { return base + t * st; });
-      }
-      else
-        exchange<LOGN, CI, SPLIT>(v, reg2, i2, reg2, lds, [&](int t) { return pad16(j + t * pp); });
-    }
-    p *= 16;
-  }
-}
-
-template <int LOGN, int CI, bool SPLIT, typename V>
-__device__ __forceinline__ void fft_run(V* v, int i, int reg, void* lds, const float2* __restrict__ tw)
-{
-  fft_run<LOGN, CI, SPLIT>(v, i, reg, i, reg, lds, tw);
-}
-
-template <int LOGN>
-__device__ __forceinline__ void load_twiddles(float2* tw_lds, const float2* __restrict__ tw_glob)
-{
-  using S = FftShape<LOGN>;
-  for (int e = threadIdx.x; e < S::TW_ENTRIES; e += blockDim.x)
-    tw_lds[e] = tw_glob[e];
-  __syncthreads();
-}
-
-// ------------------------------------------------------------------------------------------------
-// Evolution + packing, resources/spectrum.compute:183-240.
-// ------------------------------------------------------------------------------------------------
-struct KVec
-{
-  float kx, kz, dirx, dirz, k;
-};
-
-// Correctly rounded sqrt for the normal-range, non-negative arguments of the evolution (|k|^2 >=
-// dk^2 ~ 1e-6; 0 maps to 0): hardware v_sqrt_f32 (<= 1 ulp) plus one residual test per neighbour,
-// 9 VALU instead of hipcc's ~15 with denormal scaling. |k| and w must be bit-identical to the
-// oracle's: the phase w*t multiplies any ulp of w by t (1e2-1e4 s of simulated time).
-__device__ __forceinline__ float sqrt_rn(float x)
-{
-  const float s = __builtin_amdgcn_sqrtf(x);
-  const float sm = __int_as_float(__float_as_int(s) - 1), sp = __int_as_float(__float_as_int(s) + 1);
-  float r = s;
-  if (fmaf(-sm, s, x) <= 0.0f)
-    r = sm;
-  if (fmaf(-sp, s, x) > 0.0f)
-    r = sp;
-  return r;
-}
-
-__device__ __forceinline__ KVec make_kvec(int x, int y, float dim, float dk)
-{
-#pragma clang fp contract(off)  // the reference's unfused float expression order
-  KVec r;
-  r.kx = ((float)x - dim / 2.0f) * dk;
-  r.kz = ((float)y - dim / 2.0f) * dk;
-  // |k| (spectrum.compute:189-192) correctly rounded, since it feeds the phase; normalize(kVec)
-  // only scales the choppy terms and uses the hardware v_rsq_f32 (<= 1 ulp) instead of a
-  // correctly rounded division (~10 VALU).
-  const float len2 = r.kx * r.kx + r.kz * r.kz;
-  const float inv = len2 == 0.0f ? 0.0f : __builtin_amdgcn_rsqf(len2);
-  r.dirx = r.kx * inv;
-  r.dirz = r.kz * inv;
-  r.k = sqrt_rn(len2) + 1e-6f;
-  return r;
-}
-
-// Dispersion (spectrum.compute:38-44) for the per-frame evolution. Same formula; tanh(kh), needed
-// only when kh < 2*pi (very long waves), is evaluated as an odd series for kh < 1/8 (|err| < 1e-10)
-// and as 1 - 2/(1 + e^{2kh}) above — a few VGPRs instead of ocml tanhf's.
-__device__ __forceinline__ float dispersion_evolve(float k, float g, float h)
-{
-#pragma clang fp contract(off)  // bit-identical w in the deep-water case (tanh = 1)
-  const float kh = k * h;
-  float t = 1.0f;
-  if (kh < 2.0f * OCEAN_PI)
-  {
-    const float x2 = kh * kh;
-    t = kh < 0.125f ? kh * fmaf(fmaf(fmaf(-17.0f / 315.0f, x2, 2.0f / 15.0f), x2, -1.0f / 3.0f), x2, 1.0f)
-                    : 1.0f - 2.0f / (1.0f + expf(2.0f * kh));
-  }
-  const float omegaSquared = (g * k + kSigmaSurface / kRhoWater * k * k * k) * t;
-  return sqrt_rn(omegaSquared);
-}
-
-// sin/cos of a large fp32 phase (w*t reaches 1e3-1e7 rad). The phase is reduced to a fraction of a
-// revolution in double (exact to ~1e-16 rev for |x| < 1e7) and fed to the hardware v_sin_f32 /
-// v_cos_f32, which take revolutions (absolute error ~3e-7, the class of the reference shader's own
-// GLSL sin/cos). ~10 VALU slots instead of ~35 for a polynomial kernel with quadrant logic, and no
-// Payne-Hanek slow path (ocml's sincosf costs ~60 VGPRs that a 1024-thread workgroup lacks).
-__device__ __forceinline__ void sincos_phase(float x, float* s, float* c)
-{
-  const double rev = (double)x * 0.15915494309189533577;  // 1 / (2 pi)
-  const float f = (float)(rev - rint(rev));                // [-1/2, 1/2] revolution
-  *s = __builtin_amdgcn_sinf(f);
-  *c = __builtin_amdgcn_cosf(f);
-}
-
-// heightAmp = h0 * e^{i w t} + conj-partner * e^{-i w t}
-__device__ __forceinline__ float2 evolve(float4 a, float k, const CascadeFrame& f)
-{
-  float phase = dispersion_evolve(k, f.g, f.h) * f.time;
-  float ws, wc;
-  sincos_phase(phase, &ws, &wc);
-  float ampx = a.x * wc - a.y * ws;
-  float ampy = a.x * ws + a.y * wc;
-  float ws2 = -ws;
-  float oppx = a.z * wc - a.w * ws2;
-  float oppy = a.z * ws2 + a.w * wc;
-  return make_float2(ampx + oppx, ampy + oppy);
-}
-
-// heightMap texel = (H + i*dH/dx, dH/dz + i*Dx)   (spectrum.compute:236)
-__device__ __forceinline__ CPair pack_height(float2 H, const KVec& q)
-{
-  float hx = H.x, hy = H.y;
-  float dhdx_x = q.kx * (-hy), dhdx_y = q.kx * hx;
-  float dhdz_x = q.kz * (-hy), dhdz_y = q.kz * hx;
-  float disX_x = q.dirx * (-hy), disX_y = q.dirx * hx;
-  return {f2v{hx - dhdx_y, dhdz_x - disX_y}, f2v{hy + dhdx_x, dhdz_y + disX_x}};
-}
-
-// displacementMap texel = (Dz + i*dDx/dx, dDz/dz + i*dDx/dz)   (spectrum.compute:237)
-__device__ __forceinline__ CPair pack_displacement(float2 H, const KVec& q)
-{
-  float hx = H.x, hy = H.y;
-  float disZ_x = q.dirz * (-hy), disZ_y = q.dirz * hx;
-  float a = -q.kx * q.dirx, b = -q.kz * q.dirz, c = -q.kz * q.dirx;
-  float dDXdx_x = a * hx, dDXdx_y = a * hy;
-  float dDZdz_x = b * hx, dDZdz_y = b * hy;
-  float dDXdz_x = c * hx, dDXdz_y = c * hy;
-  return {f2v{disZ_x - dDXdx_y, dDZdz_x - dDXdz_y}, f2v{disZ_y + dDXdx_x, dDZdz_y + dDXdz_x}};
 }
 
 // ------------------------------------------------------------------------------------------------

@@ -142,11 +142,8 @@ __global__ __launch_bounds__(256 * RPW) void k_pass2pat(const float4* inter, flo
     const float4* src = inter + ((size_t)img << (2 * LOGN));
     float4 v[16];
 #pragma unroll
-    for (int m = 0; m < 16; m++)
-    {
-      const int x = ii + m * T;  // m*T multiple of B
+    for (int m = 0; m < 16; m++)  // column x = ii + m*T (m*T a multiple of B)
       v[m] = ld4(src + (size_t)(m * T / B) * N * B, (((ii / B) * N + y) * B + (ii % B)) * 16);
-    }
     float4* dst = out + ((size_t)img << (2 * LOGN)) + ((size_t)y << LOGN);
 #pragma unroll
     for (int m = 0; m < 16; m++)
@@ -258,7 +255,7 @@ __global__ __launch_bounds__(1024) void k_cols_compute_only(int n_images, float4
 {
   using S = FftShape<LOGN>;
   using K = ColCfg<LOGN>;
-  constexpr int T = S::T, C = K::C;
+  constexpr int C = K::C;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   float2* tw = reinterpret_cast<float2*>(smem);
   void* xch = smem + ((S::TW_ENTRIES * 8 + 15) / 16) * 16;
@@ -382,7 +379,6 @@ int main()
     float ms = time_ms([&] { hipLaunchKernelGGL(k, dim3(cus), dim3(1024), lds, 0, n_images, d, tw); }, 10);
     std::printf("column kernel compute+LDS only (no HBM)           : %7.3f ms\n", ms);
     // production column kernel for comparison
-    FoamParams fp{};
     ms = time_ms([&] { (void)launch_cols(LOGN, n_images, d, tw, 0, cus); }, 10);
     std::printf("column kernel (production, no foam)               : %7.3f ms  %7.1f GB/s\n", ms, bytes / ms / 1e6);
     ms = time_ms([&] { (void)launch_rows_ifft(LOGN, n_images, d, tw, 0, cus); }, 10);

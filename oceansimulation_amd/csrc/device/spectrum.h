@@ -135,7 +135,10 @@ __device__ __forceinline__ float2 spectrum_amplitude(const SpectrumConsts& q, fl
   const float sh = sp + 16.0f * tanh_pos(w_p * rw) * q.swell2;
   const float lh = sh < 0.4f ? (0.5f / OCEAN_PI) + sh * (0.220636f + sh * (-0.109f + sh * 0.090f))
                              : 0.56418958354775628f * (0.5f * __builtin_amdgcn_sqrtf(sh) + 0.0625f * __builtin_amdgcn_rsqf(sh));
-  const float ct = fabsf(__builtin_amdgcn_cosf(theta * (0.5f * 0.15915494309189533577f)));  // cos(theta/2)
+  // |cos(theta/2)|^(2 sh): near the anti-wind direction cos -> 0 and the power amplifies its relative
+  // error, so cos is ocml's accurate cosf (theta/2 is ~10-15 rad with theta_0 = 25, :135), not the
+  // hardware v_cos_f32 whose absolute error is a large relative error there.
+  const float ct = fabsf(cosf(theta * 0.5f));
   const float d = (1.0f - q.spread) * (lh * pow_pos(ct, 2.0f * sh)) + q.spread_2pi;
 
   // DispersionDerivative (spectrum.compute:50-57), sech = 2 e^-x / (1 + e^-2x)
@@ -146,8 +149,10 @@ __device__ __forceinline__ float2 spectrum_amplitude(const SpectrumConsts& q, fl
 
   // Hash + Box-Muller (spectrum.compute:109-127, :153): uvec2(thread + seed)
   const float2 u = hash_uniform((uint32_t)(int64_t)(tx + q.seed_x), (uint32_t)(int64_t)(ty + q.seed_y));
-  const float rad = __builtin_amdgcn_sqrtf(-2.0f * 0.69314718055994531f * log2_hw(u.x));
-  const float sn = __builtin_amdgcn_sinf(u.y), cs = __builtin_amdgcn_cosf(u.y);  // angle 2 pi u.y
+  // accurate logf: for u near 1 the hardware log2's absolute error is a large relative error
+  const float rad = __builtin_amdgcn_sqrtf(-2.0f * logf(u.x));
+  float sn, cs;
+  sincosf(2.0f * OCEAN_PI * u.y, &sn, &cs);
   const float amp = __builtin_amdgcn_sqrtf(2.0f * Sj * d * chain);
   return make_float2(q.c * (rad * cs) * amp, q.c * (rad * sn) * amp);
 }

@@ -71,9 +71,13 @@ def test_hash_bit_exact(ocean, oracle):
 
 
 # ---- generateSpectrum (spectrum.compute:157-172) ---------------------------------------------
-@pytest.mark.parametrize("n", [16, 64, 256, 1024])
+@pytest.mark.parametrize("n", [16, 64, 256, 1024, 4096])
 @pytest.mark.parametrize("plane", [5.0, 17.0, 40.0, 101.0])
 def test_generate_spectrum(ocean, oracle, n, plane):
+    """h0 against the oracle, also weighted by |k|: the slope and choppy-derivative channels
+    multiply h0 by up to |k| (~10^3 rad/m), so an error at small-amplitude high-k texels that
+    max|err|/max|h0| hides shows up in the maps (the anti-wind cos(theta/2)^(2s) factor once did
+    exactly that with a hardware cosine)."""
     fft = ocean.FFTCalculator(n)
     gen = ocean.Generator(fft, 1)
     ocean.apply_settings(gen.GetOceanSettings(0), planeSize=plane)
@@ -83,6 +87,9 @@ def test_generate_spectrum(ocean, oracle, n, plane):
     assert np.isfinite(got).all()
     errs = lane_err(got, ref)
     assert max(errs) <= H0_TOL, errs
+    y, x = np.meshgrid(np.arange(n), np.arange(n), indexing="ij")
+    k = np.hypot(x - n / 2, y - n / 2)[..., None]
+    assert max(lane_err(got * k, ref * k)) <= 10 * H0_TOL, (n, plane, lane_err(got * k, ref * k))
 
 
 # ---- EncodeIFFT (src/FFTCalculator.cpp:73-114) ----------------------------------------------
@@ -201,6 +208,42 @@ def test_calculate_ocean_default_t1(ocean, oracle, n):
     ref = oracle.OracleGenerator(n)
     ref.calculate_ocean(1.0)
     _frame_check(gen.height_map_host(0), gen.displacement_map_host(0), gen.jacobian_map_host(0), ref)
+
+
+@pytest.mark.parametrize("n", [16, 32, 128, 512, 4096])
+def test_calculate_ocean_every_kernel_shape(ocean, oracle, n):
+    """Full frames at the sizes whose kernels differ in shape from the ones above (first-stage
+    radix 2/4/8/16, blocks of 1-4 texels, strips per workgroup, KEEP 16/4), two frames so the
+    second reuses h0 (src/Generator.cpp:55-59)."""
+    fft = ocean.FFTCalculator(n)
+    gen = ocean.Generator(fft, 1)
+    ocean.apply_settings(gen.GetOceanSettings(0), planeSize=23.0)
+    ref = oracle.OracleGenerator(n, oracle.default_settings(planeSize=23.0))
+    for dt in (0.75, 1.0 / 60.0):
+        gen.CalculateOcean(dt)
+        ref.calculate_ocean(dt)
+    _frame_check(gen.height_map_host(0), gen.displacement_map_host(0), gen.jacobian_map_host(0), ref)
+
+
+def test_sixty_four_cascades_in_one_launch(ocean):
+    """The ABI's cascade limit (OCEAN_MAX_CASCADES = 64) in one batched generator: every cascade
+    equals the same cascade computed alone, bit for bit; 65 is rejected."""
+    from oceansimulation_amd.capi import OceanError
+
+    n = 64
+    fft = ocean.FFTCalculator(n)
+    gen = ocean.Generator(fft, 64)
+    for c in range(64):
+        ocean.apply_settings(gen.GetOceanSettings(c), planeSize=3.0 + 7.0 * c, seed=(100 + c, 7 * c))
+    gen.CalculateOcean(0.5)
+    for c in (0, 17, 63):
+        one = ocean.Generator(fft, 1)
+        ocean.apply_settings(one.GetOceanSettings(0), planeSize=3.0 + 7.0 * c, seed=(100 + c, 7 * c))
+        one.CalculateOcean(0.5)
+        assert np.array_equal(gen.height_map_host(c), one.height_map_host(0))
+        assert np.array_equal(gen.jacobian_map_host(c), one.jacobian_map_host(0))
+    with pytest.raises(OceanError):
+        ocean.Generator(fft, 65)
 
 
 def test_calculate_ocean_long_time(ocean, oracle):

@@ -225,6 +225,27 @@ def test_calculate_ocean_every_kernel_shape(ocean, oracle, n):
     _frame_check(gen.height_map_host(0), gen.displacement_map_host(0), gen.jacobian_map_host(0), ref)
 
 
+def test_calculate_ocean_8192_vs_float64(ocean, oracle):
+    """A full frame at 8192^2 (blocks of 2 texels, KEEP 0, 4-stage transforms): h0 and the packed
+    spectra from the oracle, their transform in float64 (N^2 ifft2(ifftshift), the meaning of
+    src/FFTCalculator.cpp:73-114; the oracle's own fp32 radix-2 is 6e-7 from it at 4096), foam from
+    the float64 maps (spectrum.compute:246-259)."""
+    import numpy_ref as R
+
+    n, L = 8192, 61.0
+    fft = ocean.FFTCalculator(n)
+    gen = ocean.Generator(fft, 1)
+    ocean.apply_settings(gen.GetOceanSettings(0), planeSize=L)
+    gen.CalculateOcean(1.25)
+    s = oracle.default_settings(planeSize=L)
+    s.time = 1.25
+    hp, dp = oracle.prepare_fft(s, n, oracle.generate_spectrum(s, n))
+    h64, d64 = R.encode_ifft(hp), R.encode_ifft(dp)
+    assert max(lane_err(gen.height_map_host(0), h64)) <= FRAME_TOL
+    assert max(lane_err(gen.displacement_map_host(0), d64)) <= FRAME_TOL
+    assert scalar_err(gen.jacobian_map_host(0) - 1.0, R.compute_foam(s, d64) - 1.0) <= FRAME_TOL
+
+
 def test_sixty_four_cascades_in_one_launch(ocean):
     """The ABI's cascade limit (OCEAN_MAX_CASCADES = 64) in one batched generator: every cascade
     equals the same cascade computed alone, bit for bit; 65 is rejected."""

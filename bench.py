@@ -314,6 +314,16 @@ def slab_grid(args, rank: int, world: int, local: int) -> dict:
         "serial_ms_per_frame": 1000.0 * el / per,
     }
     out["serial_exchange_and_gaps_ms"] = out["serial_ms_per_frame"] - out["column_pass_ms"] - out["row_pass_ms"]
+    if ex is not None:
+        # the all-to-all alone (no passes): the achieved per-rank exchange rate over xGMI
+        def exchange_steps():
+            for _ in range(per):
+                ex()
+
+        el = timed(exchange_steps)
+        out["exchange_only_ms"] = 1000.0 * el / per
+        moved = g.exchange_bytes * (world - 1) // world if world > 1 else g.exchange_bytes
+        out["exchange_GBps_per_rank"] = moved / (el / per) / 1e9
     del ex
     torch.cuda.empty_cache()
 

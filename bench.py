@@ -26,10 +26,19 @@ sys.path.insert(0, ROOT)
 
 PLANES = [5.0, 17.0, 101.0, 251.0, 509.0, 1021.0, 2039.0, 4093.0]
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md, chip-level parameters)
-# Algorithmic HBM bytes per height-field point:
-PASS1_BYTES = 16 + 32            # column pass: read h0 texel, write both packed images (blocked)
-PASS2_BYTES = 32 + 32 + 4        # row pass: read both images, write both maps + the Jacobian
-FRAME_BYTES = PASS1_BYTES + PASS2_BYTES  # 116 B / point
+
+
+def frame_bytes_per_point(n: int, half: bool):
+    """Algorithmic HBM bytes per height-field point of (column pass, row pass); the
+    generator reports the same through ocean_generator_frame_bytes (checked at run time).
+    Full spectrum: h0 16 + intermediate 32 | intermediate 32 + maps 32 + Jacobian 4 = 48 | 68.
+    Half spectrum (default for whole grids of 1024..4096): only the kept columns u in [0, N/2) plus
+    the 4-wide Nyquist strip, kept = (N/2 + 4)/N of the grid: h0 16 + 5 fields 40 per kept texel |
+    5 fields 40 per kept texel + maps 32 + Jacobian 4 (~28 | ~56)."""
+    if not half:
+        return 48.0, 68.0
+    kept = (n / 2 + 4) / n
+    return 16.0 * kept + 40.0 * kept, 40.0 * kept + 36.0
 
 
 def parse():
@@ -45,6 +54,8 @@ def parse():
     ap.add_argument("--no-slab", action="store_true", help="skip the config-5 slab-decomposed grid")
     ap.add_argument("--no-ifft", action="store_true", help="skip the EncodeIFFT-only and rocFFT legs")
     ap.add_argument("--no-surface", action="store_true", help="skip the surface-consumer leg")
+    ap.add_argument("--full-spectrum", action="store_true",
+                    help="time the full-spectrum frame path instead of the default half-spectrum one")
     ap.add_argument("--slab-n", type=int, default=16384, help="side of the single slab-decomposed grid")
     ap.add_argument("--slab-steps", type=int, default=10)
     ap.add_argument("--slab-reserve-cus", type=int, default=32,
@@ -368,6 +379,11 @@ def main():
     gen = ocean.Generator(fft, C)
     for c in range(C):
         ocean.apply_settings(gen.GetOceanSettings(c), **cascade_settings(rank, c))
+    if args.full_spectrum:
+        gen.set_half_spectrum(False)
+    pass_bytes = gen.frame_bytes()
+    half = pass_bytes[0] < 48.0
+    assert tuple(pass_bytes) == frame_bytes_per_point(n, half), (pass_bytes, n, half)
 
     dt = 1.0 / 60.0
     # h0 seeding, timed separately (time-independent; the reference API regenerates only on change)
@@ -418,15 +434,18 @@ def main():
             "cascades_per_gpu": C,
             "plane_sizes_m": [PLANES[c % len(PLANES)] for c in range(C)],
             "parallelism": f"cascades sharded over {world} GPU(s), no collective",
-            "frame_hbm_bytes_per_point": FRAME_BYTES,
+            "frame_path": "half spectrum" if half else "full spectrum",
+            "frame_hbm_bytes_per_point": pass_bytes[0] + pass_bytes[1],
         },
     }
     if not args.no_profile and cnt[1] > 0 and cnt[2] > 0:
         p1_ms, p2_ms = ms[1] / cnt[1], ms[2] / cnt[2]
         per_launch_pts = float(n) * n * C
         kernels = {
-            "column_pass_k_cols_evolve": {"avg_ms": p1_ms, "bytes": PASS1_BYTES * per_launch_pts},
-            "row_pass_k_rows_final": {"avg_ms": p2_ms, "bytes": PASS2_BYTES * per_launch_pts},
+            ("column_pass_k_cols_half" if half else "column_pass_k_cols_evolve"):
+                {"avg_ms": p1_ms, "bytes": pass_bytes[0] * per_launch_pts},
+            ("row_pass_k_rows_half" if half else "row_pass_k_rows_final"):
+                {"avg_ms": p2_ms, "bytes": pass_bytes[1] * per_launch_pts},
         }
         dom_name = max(kernels, key=lambda k: kernels[k]["avg_ms"])
         dom = kernels[dom_name]
@@ -447,7 +466,7 @@ def main():
             out["roofline"]["traffic_bytes_per_launch"] = pmc["hbm_traffic_bytes"]
             out["roofline"]["algorithmic_bytes_per_launch"] = dom["bytes"]
             out["roofline"]["traffic_source"] = pmc["source"]
-        frame_gbs = FRAME_BYTES * per_launch_pts / ((p1_ms + p2_ms) * 1e-3) / 1e9
+        frame_gbs = (pass_bytes[0] + pass_bytes[1]) * per_launch_pts / ((p1_ms + p2_ms) * 1e-3) / 1e9
         out["kernels"] = {
             k: {"avg_ms": v["avg_ms"], "GB_per_s": v["bytes"] / (v["avg_ms"] * 1e-3) / 1e9,
                 "frac_hbm_peak": v["bytes"] / (v["avg_ms"] * 1e-3) / 1e9 / HBM_PEAK_GBS}

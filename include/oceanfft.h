@@ -125,6 +125,17 @@ float* ocean_generator_jacobian_map(ocean_generator* gen, int cascade);
 float* ocean_generator_initial_spectrum(ocean_generator* gen, int cascade);
 int ocean_generator_spectrum_block(const ocean_generator* gen);
 
+/* Frame path of a whole-grid generator. Half spectrum (default where supported: N = 1024 .. 4096,
+ * ranks == 1): the column pass transforms only the u >= 0 half of the columns, as 5 complex fields
+ * (H, kz H, H/|k|, kz H/|k|, kz^2 H/|k|), and the row pass rebuilds the reference's 4 packed lanes
+ * from Hermitian symmetry plus the reference's Nyquist-row term (84 HBM bytes per point instead of
+ * 116). enable = 0 selects the full-spectrum path (both give the reference's results
+ * within rounding). */
+int ocean_generator_set_half_spectrum(ocean_generator* gen, int enable);
+/* Algorithmic HBM bytes per height-field point of the column pass [0] and the row pass [1] of the
+ * generator's current path (what bench.py prices the roofline with). */
+int ocean_generator_frame_bytes(const ocean_generator* gen, double per_point[2]);
+
 /* ---- slab decomposition of one grid over several GPUs ------------------------------------- */
 /* One N x N cascade split over `ranks` GPUs (power of two <= 16), this process being `rank`: the
  * column pass works on columns [rank*w, rank*w + w), the row pass on rows [rank*w, rank*w + w),

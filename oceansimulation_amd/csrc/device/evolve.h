@@ -18,6 +18,7 @@ namespace oceanfft
 struct KVec
 {
   float kx, kz, dirx, dirz, k;
+  float inv;  // 1/|k| (0 at k = 0)
 };
 
 // Correctly rounded sqrt for the normal-range, non-negative arguments of the evolution (|k|^2 >=
@@ -47,6 +48,7 @@ __device__ __forceinline__ KVec make_kvec(int x, int y, float dim, float dk)
   // correctly rounded division (~10 VALU).
   const float len2 = r.kx * r.kx + r.kz * r.kz;
   const float inv = len2 == 0.0f ? 0.0f : __builtin_amdgcn_rsqf(len2);
+  r.inv = inv;
   r.dirx = r.kx * inv;
   r.dirz = r.kz * inv;
   r.k = sqrt_rn(len2) + 1e-6f;

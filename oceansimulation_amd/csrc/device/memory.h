@@ -40,6 +40,22 @@ __device__ __forceinline__ void st4(void* base, int voff_bytes, float4 v, int nu
   __builtin_amdgcn_raw_buffer_store_b128(r, srd(base, num_bytes), voff_bytes, 0, AUX);
 }
 
+typedef unsigned int u2v __attribute__((ext_vector_type(2)));
+
+template <int AUX = 0>
+__device__ __forceinline__ float2 ld2(const void* base, int voff_bytes)
+{
+  u2v r = __builtin_amdgcn_raw_buffer_load_b64(srd(base, kAllBytes), voff_bytes, 0, AUX);
+  return make_float2(__uint_as_float(r.x), __uint_as_float(r.y));
+}
+
+template <int AUX = 0>
+__device__ __forceinline__ void st2(void* base, int voff_bytes, float2 v)
+{
+  u2v r = {__float_as_uint(v.x), __float_as_uint(v.y)};
+  __builtin_amdgcn_raw_buffer_store_b64(r, srd(base, kAllBytes), voff_bytes, 0, AUX);
+}
+
 template <int AUX = 0>
 __device__ __forceinline__ void st1(void* base, int voff_bytes, float v)
 {

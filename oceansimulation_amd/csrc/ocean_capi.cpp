@@ -83,6 +83,13 @@ struct ocean_generator
   float4* scratch = nullptr;    // [cascade][2][w][N] row-major, only when B == 1 (N = 16384)
   float4* maps = nullptr;       // [cascade][2][w][N]: heightMap, displacementMap rows (row-major)
   float* jac = nullptr;         // [cascade][w][N]
+  // half-spectrum path (ranks == 1, N = 1024 .. 4096; ocean_generator_set_half_spectrum)
+  bool half = false;
+  FrameParams frame{};    // the last column pass's per-cascade values (the row pass needs dk)
+  float4* gab = nullptr;  // [cascade][strip][N][4]: y-transformed (H, kz H) for u >= 0 + Nyquist strip
+  float4* gcd = nullptr;  // (kz H/|k|, kz^2 H/|k|)
+  float2* ge = nullptr;   // H/|k|
+  float4* spec = nullptr; // [cascade][2][N]: the Nyquist-row term R
   bool profiling = false;
   std::vector<EventPair> pending;
   std::vector<hipEvent_t> pool;
@@ -300,6 +307,21 @@ extern "C" {
 // ---------------------------------------------------------------------------------------------
 // Generator
 // ---------------------------------------------------------------------------------------------
+static hipError_t half_buffers(ocean_generator* g)
+{
+  const size_t t = half_field_texels(g->fft->logn) * g->cascades;
+  hipError_t e = hipSuccess;
+  if (!g->gab)
+    e = hipMalloc(&g->gab, t * sizeof(float4));
+  if (e == hipSuccess && !g->gcd)
+    e = hipMalloc(&g->gcd, t * sizeof(float4));
+  if (e == hipSuccess && !g->ge)
+    e = hipMalloc(&g->ge, t * sizeof(float2));
+  if (e == hipSuccess && !g->spec)
+    e = hipMalloc(&g->spec, (size_t)g->cascades * 2 * g->fft->n * sizeof(float4));
+  return e;
+}
+
 static int generator_alloc(ocean_generator** out, ocean_fft* fft, int cascades, int rank, int ranks)
 {
   auto* g = new ocean_generator();
@@ -313,9 +335,12 @@ static int generator_alloc(ocean_generator** out, ocean_fft* fft, int cascades, 
   for (auto& s : g->settings)
     ocean_default_settings(&s);
   const size_t slab = (size_t)fft->n * g->geom.w;  // texels per cascade image slab
+  g->half = ranks == 1 && half_spectrum_supported(fft->logn);
   hipError_t e = hipMalloc(&g->h0, slab * cascades * sizeof(float4));
-  if (e == hipSuccess)
+  if (e == hipSuccess && !g->half)
     e = hipMalloc(&g->inter, slab * cascades * 2 * sizeof(float4));
+  if (e == hipSuccess && g->half)
+    e = half_buffers(g);
   if (e == hipSuccess && rows_need_transpose(fft->logn))
     e = hipMalloc(&g->scratch, slab * cascades * 2 * sizeof(float4));
   if (e == hipSuccess)
@@ -388,6 +413,9 @@ int ocean_generator_destroy(ocean_generator* g)
     (void)hipFree(g->maps);
   if (g->jac)
     (void)hipFree(g->jac);
+  for (void* p : {(void*)g->gab, (void*)g->gcd, (void*)g->ge, (void*)g->spec})
+    if (p)
+      (void)hipFree(p);
   delete g;
   return OCEAN_OK;
 }
@@ -449,11 +477,19 @@ static int generator_columns(ocean_generator* g, float timestep, int update_spec
     fp.c[c].g = s.g;
     fp.c[c].h = s.h;
   }
-  HIP_TRY(timed(g, 1, [&] {
-            return launch_cols_evolve(f->logn, fp, g->geom, g->h0, out, f->twiddles, f->stream, f->cus,
-                                      default_keep(f->logn));
-          }),
-          "column pass");
+  if (g->half)
+    HIP_TRY(timed(g, 1, [&] {
+              return launch_half_columns(f->logn, fp, g->h0, g->gab, g->gcd, g->ge, g->spec, f->twiddles, f->stream,
+                                         f->cus);
+            }),
+            "column pass (half spectrum)");
+  else
+    HIP_TRY(timed(g, 1, [&] {
+              return launch_cols_evolve(f->logn, fp, g->geom, g->h0, out, f->twiddles, f->stream, f->cus,
+                                        default_keep(f->logn));
+            }),
+            "column pass");
+  g->frame = fp;
   return OCEAN_OK;
 }
 
@@ -464,11 +500,55 @@ static int generator_rows(ocean_generator* g, const float4* in)
   FoamParams foam{};
   for (int c = 0; c < g->cascades; c++)
     foam.displacement[c] = g->settings[c].displacement;
-  HIP_TRY(timed(g, 2, [&] {
-            return launch_rows_final(f->logn, g->cascades, g->geom, in, g->scratch, g->maps, g->jac, foam, f->twiddles,
-                                     f->stream, f->cus);
-          }),
-          "row pass");
+  if (g->half)
+    HIP_TRY(timed(g, 2, [&] {
+              return launch_half_rows(f->logn, g->frame, g->gab, g->gcd, g->ge, g->spec, g->maps, g->jac, foam,
+                                      f->twiddles, f->stream, f->cus);
+            }),
+            "row pass (half spectrum)");
+  else
+    HIP_TRY(timed(g, 2, [&] {
+              return launch_rows_final(f->logn, g->cascades, g->geom, in, g->scratch, g->maps, g->jac, foam,
+                                       f->twiddles, f->stream, f->cus);
+            }),
+            "row pass");
+  return OCEAN_OK;
+}
+
+int ocean_generator_set_half_spectrum(ocean_generator* g, int enable)
+{
+  if (!g)
+    return fail(OCEAN_ERR_INVALID, "ocean_generator_set_half_spectrum: null generator");
+  if (enable && (g->ranks != 1 || !half_spectrum_supported(g->fft->logn)))
+    return fail(OCEAN_ERR_INVALID, "ocean_generator_set_half_spectrum: whole grids of N = 1024 .. 4096 only");
+  hipError_t e = hipSuccess;
+  if (enable)
+    e = half_buffers(g);
+  else if (!g->inter)
+    e = hipMalloc(&g->inter, (size_t)g->fft->n * g->geom.w * g->cascades * 2 * sizeof(float4));
+  if (e != hipSuccess)
+    return fail(e == hipErrorOutOfMemory ? OCEAN_ERR_OOM : OCEAN_ERR_HIP,
+                std::string("ocean_generator_set_half_spectrum: ") + hipGetErrorString(e));
+  g->half = enable != 0;
+  return OCEAN_OK;
+}
+
+int ocean_generator_frame_bytes(const ocean_generator* g, double per_point[2])
+{
+  if (!g || !per_point)
+    return fail(OCEAN_ERR_INVALID, "ocean_generator_frame_bytes: null argument");
+  if (g->half)
+  {
+    // h0 of the kept columns (half + the Nyquist strip) + 5 complex fields out; 5 fields in, maps + Jacobian
+    const double n = g->fft->n, kept = (n / 2 + 4) / n;
+    per_point[0] = 16.0 * kept + 40.0 * kept;
+    per_point[1] = 40.0 * kept + 36.0;
+  }
+  else
+  {
+    per_point[0] = 48.0;
+    per_point[1] = 68.0;
+  }
   return OCEAN_OK;
 }
 

@@ -91,6 +91,17 @@ struct SlabGeom
 int spectrum_block(int logn);
 hipError_t launch_generate_spectrum(const OceanSettings& s, int n, float4* h0, hipStream_t stream, int cus, int x0 = 0,
                                     int width = 0);
+// Half-spectrum generator path (whole grids, N = 1024 .. 4096): pass 1 (+ the Nyquist-row term
+// into spec, 2 * cascades rows of N float4) and pass 2. Field buffers: half_field_texels(logn) per
+// cascade each for gab, gcd (float4) and ge (float2).
+bool half_spectrum_supported(int logn);
+size_t half_field_texels(int logn);
+hipError_t launch_half_columns(int logn, const FrameParams& fp, const float4* h0, float4* gab, float4* gcd, float2* ge,
+                               float4* spec, const float2* tw, hipStream_t stream, int cus);
+hipError_t launch_half_rows(int logn, const FrameParams& fp, const float4* gab, const float4* gcd, const float2* ge,
+                            const float4* rcorr, float4* maps, float* jac, const FoamParams& foam, const float2* tw,
+                            hipStream_t stream, int cus, int ablation = 0);
+hipError_t launch_rows_ifft_rows(int logn, int rows, float4* data, const float2* tw, hipStream_t stream, int cus);
 // Standalone EncodeIFFT, column-first through a work image of n_images * N^2 texels (N = 4096).
 bool ifft_colfirst_supported(int logn);
 hipError_t launch_ifft_colfirst(int logn, int n_images, float4* images, float4* work, const float2* tw,

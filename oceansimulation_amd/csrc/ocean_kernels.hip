@@ -140,7 +140,7 @@ struct RowCfg
 // Row pass of a plain EncodeIFFT on packed images [n_images][N][N] float4, in place.
 template <int LOGN>
 __global__ __launch_bounds__(RowCfg<LOGN>::WG, RowCfg<LOGN>::MIN_WAVES) void k_rows_ifft(
-    int n_images, float4* __restrict__ images, const float2* __restrict__ tw_glob)
+    int rows, float4* __restrict__ images, const float2* __restrict__ tw_glob)
 {
   using S = FftShape<LOGN>;
   using R = RowCfg<LOGN>;
@@ -151,7 +151,7 @@ __global__ __launch_bounds__(RowCfg<LOGN>::WG, RowCfg<LOGN>::MIN_WAVES) void k_r
   load_twiddles<LOGN>(tw, tw_glob);
 
   const int rho0 = threadIdx.x / T, i0 = threadIdx.x % T;
-  const int total = n_images * N;
+  const int total = rows;  // rows of N packed texels, contiguous (n_images * N for whole images)
   for (int row0 = blockIdx.x * R::RPW; row0 < total; row0 += gridDim.x * R::RPW)
   {
     const int i = opaque(i0), rho = R::RPW == 1 ? 0 : opaque(rho0);
@@ -505,6 +505,291 @@ __global__ __launch_bounds__(FftShape<LOGN>::T * RPW_) void k_rows_final(
   }
 }
 
+// ------------------------------------------------------------------------------------------------
+// Generator path, half spectrum (whole grids, B = 4, one strip per pass-1 item: N = 1024 .. 4096).
+// All eight output fields are real multipliers of the one Hermitian field H (tests/
+// half_spectrum_ref.py): lane0 = (1 - kx) A, lane1 = i B - kx C, lane2 = i (D - kx^2 C),
+// lane3 = -E - i kx D with A = H, B = kz H, C = H/|k|, D = kz H/|k|, E = kz^2 H/|k|. The kx factors
+// commute with the y transform, and H(-k) = conj(H(k)) makes each y-transformed field
+// (anti-)Hermitian in u = x - N/2, so pass 1 transforms only the columns u >= 0 and the Nyquist
+// column u = -N/2 (half the columns, half of h0 read), storing 5 complex fields (20 B per grid
+// point instead of 32); pass 2 rebuilds u < 0 as s_F conj(G_F(q, -u)). The reference's Nyquist row
+// is not Hermitian-paired (its partner is evaluated at +N/2, spectrum.compute:165); its share is the
+// rank-1 term (-1)^q R(p), R the x-transform of a one-row spectrum built by k_half_nyquist.
+// Frame bytes: h0 8 + fields 20 + 20 + maps 32 + Jacobian 4 = 84 per point (the full path: 116).
+// ------------------------------------------------------------------------------------------------
+template <int LOGN>
+struct HalfCfg
+{
+  static constexpr int N = 1 << LOGN;
+  static constexpr int B = ColFirstCfg<LOGN>::B;
+  static constexpr int STRIPS = N / (2 * B) + 1;  // u in [0, N/2), then the strip of x = 0..B-1
+  static constexpr bool SUPPORTED = B == 4 && ColFirstCfg<LOGN>::SPW == 1;
+};
+
+// Pass 1: per strip of B columns (u >= 0, or the Nyquist strip), three y-iFFT rounds of CPairs:
+// (A, B), (D, E), (C, 0), stored as gab, gde (float4) and gc (float2): pass 2 reads (A, B) + C for
+// image 0 and C + (D, E) for image 1. H is re-evolved per round from h0: keeping the 16 H (32 VGPRs)
+// next to the transform's ~107 spills in a 1024-thread workgroup.
+template <int LOGN, int LA = 0, int SA = kStream>
+__global__ __launch_bounds__(ColFirstCfg<LOGN>::WG1) void k_cols_half(FrameParams fp, const float4* __restrict__ h0,
+                                                                     float4* __restrict__ gab, float4* __restrict__ gde,
+                                                                     float2* __restrict__ gc,
+                                                                     const float2* __restrict__ tw_glob)
+{
+  using S = FftShape<LOGN>;
+  using K = ColFirstCfg<LOGN>;
+  using HC = HalfCfg<LOGN>;
+  constexpr int N = S::N, T = S::T, B = K::B, STRIPS = HC::STRIPS;
+  static_assert(HC::SUPPORTED, "half-spectrum path: B = 4, one strip per item");
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  float2* tw = reinterpret_cast<float2*>(smem);
+  void* xch = smem + ((S::TW_ENTRIES * 8 + 15) / 16) * 16;
+  load_twiddles<LOGN>(tw, tw_glob);
+
+  const int total = fp.cascades * STRIPS;
+  const float dim = (float)N;
+  for (int item = blockIdx.x; item < total; item += gridDim.x)
+  {
+    const int b = opaque((int)threadIdx.x) % B;
+    const int c = item / STRIPS, s = item - c * STRIPS;
+    const int xb = s == STRIPS - 1 ? 0 : N / (2 * B) + s;
+    const CascadeFrame f = fp.c[c];
+    const float4* src = h0 + ((size_t)c * (N / B) + xb) * N * B;
+    const size_t base = ((size_t)c * STRIPS + s) * N * B;
+    const int x = xb * B + b;
+#pragma unroll 1
+    for (int round = 0; round < 3; round++)
+    {
+      const int i = (opaque((int)threadIdx.x) / B) % T;
+      const int voff = (i * B + b) * 16;
+      float4 a[16];
+#pragma unroll
+      for (int m = 0; m < 16; m++)  // fftShift on y folded into the load
+        a[m] = ld4<LA>(src + ((m + 8) & 15) * T * B, voff);
+      CPair v[16];
+#pragma unroll
+      for (int m = 0; m < 16; m++)
+      {
+        const int y = i + ((m + 8) & 15) * T;
+        const KVec q = make_kvec(x, y, dim, f.dk);
+        const float2 H = evolve(a[m], q.k, f);
+        if (round == 0)  // (A, B) = (H, kz H)
+          v[m] = CPair{f2v{H.x, q.kz * H.x}, f2v{H.y, q.kz * H.y}};
+        else if (round == 1)  // (D, E) = (kz H / |k|, kz^2 H / |k|)
+        {
+          const float e = q.kz * q.dirz;
+          v[m] = CPair{f2v{q.dirz * H.x, e * H.x}, f2v{q.dirz * H.y, e * H.y}};
+        }
+        else  // (C, 0) = (H / |k|, 0)
+          v[m] = CPair{f2v{q.inv * H.x, 0.0f}, f2v{q.inv * H.y, 0.0f}};
+      }
+      fft_run<LOGN, K::C1, true>(v, i, b, xch, tw);
+#pragma unroll
+      for (int m = 0; m < 16; m++)
+      {
+        if (round == 0)
+          st4<SA>(gab + base + m * T * B, voff, pair_raw(v[m]));
+        else if (round == 1)
+          st4<SA>(gde + base + m * T * B, voff, pair_raw(v[m]));
+        else
+          st2<SA>(gc + base + m * T * B, (i * B + b) * 8, make_float2(v[m].re.x, v[m].im.x));
+      }
+    }
+  }
+}
+
+// The Nyquist-row term: for u = -u' (0 < u' < N/2) the pass-2 rebuild s_F conj(G_F(q, u')) misses
+// (-1)^q Delta_F(u'), Delta_F(u') = F(-N/2, -u') - s_F conj(F(-N/2, u')). Its lanes (the kx
+// factors of pass 2 applied to Delta) form one row spectrum per image, spec[c][img][x] (zero
+// outside 0 < x < N/2); pass 2 adds (-1)^q spec to the lanes it rebuilds at u < 0.
+__global__ __launch_bounds__(256) void k_half_nyquist(FrameParams fp, int n, int blk, const float4* __restrict__ h0,
+                                                      float4* __restrict__ spec)
+{
+  const int total = fp.cascades * n;
+  const float dim = (float)n;
+  for (int idx = blockIdx.x * blockDim.x + threadIdx.x; idx < total; idx += gridDim.x * blockDim.x)
+  {
+    const int c = idx / n, x = idx - c * n;
+    float4 s01 = make_float4(0.0f, 0.0f, 0.0f, 0.0f), s23 = s01;
+    if (x > 0 && x < n / 2)
+    {
+      const CascadeFrame f = fp.c[c];
+      const int xp = n - x;  // u' = n/2 - x > 0 at column n/2 + u' = n - x; its mirror is x itself
+      const float4* hc = h0 + (size_t)c * n * n;
+      const float4 ap = hc[(size_t)(xp / blk) * n * blk + (xp % blk)];  // row y = 0 (v = -n/2)
+      const float4 an = hc[(size_t)(x / blk) * n * blk + (x % blk)];
+      const KVec qp = make_kvec(xp, 0, dim, f.dk), qn = make_kvec(x, 0, dim, f.dk);
+      const float2 hp = evolve(ap, qp.k, f), hn = evolve(an, qn.k, f);
+      const float2 dm = make_float2(hn.x - hp.x, hn.y + hp.y);  // Hn - conj(Hp)
+      const float2 dq = make_float2(hn.x + hp.x, hn.y - hp.y);  // Hn + conj(Hp)
+      const float kz = qn.kz, inv = qn.inv, dirz = qn.dirz, kx = qn.kx;
+      const float2 dA = dm;                                              // s = +1
+      const float2 dB = make_float2(kz * dq.x, kz * dq.y);               // s = -1
+      const float2 dC = make_float2(inv * dm.x, inv * dm.y);             // s = +1
+      const float2 dD = make_float2(dirz * dq.x, dirz * dq.y);           // s = -1
+      const float2 dE = make_float2(kz * dirz * dm.x, kz * dirz * dm.y); // s = +1
+      const float kx2 = kx * kx;
+      s01 = make_float4((1.0f - kx) * dA.x, (1.0f - kx) * dA.y, -dB.y - kx * dC.x, dB.x - kx * dC.y);
+      s23 = make_float4(-(dD.y - kx2 * dC.y), dD.x - kx2 * dC.x, -dE.x + kx * dD.y, -dE.y - kx * dD.x);
+    }
+    spec[((size_t)c * 2 + 0) * n + x] = s01;
+    spec[((size_t)c * 2 + 1) * n + x] = s23;
+  }
+}
+
+// Pass 2: RPW rows of one image. Element m of the x transform is column x = ((m + 8) & 15) T + i,
+// u = x - N/2: m < 8 -> u = m T + i >= 0 (stored column u), m >= 8 -> u < 0. Every thread loads
+// only its 8 direct elements (and thread 0 the Nyquist column for m = 8) and computes the lanes
+// both at u (its own) and at -u, adding there the Nyquist-row term (-1)^y S(-u); the -u lanes go
+// through LDS to the thread that holds -u: element 15 - m of thread T - i (thread 0: element
+// 16 - m of itself). Each stored value is read once from HBM. Then the x-iFFT, maps + Jacobian.
+// ABL (tools/microbench timing ablations, results wrong by construction): 1 = no HBM loads,
+// 2 = no x transform, 3 = no mirror exchange through LDS.
+// RPW_ = 2 (default): 512-thread workgroups, two per CU, so one workgroup's loads overlap the
+// other's transform (the LDS mirror exchange adds a barrier the 1024-thread, one-per-CU shape cannot
+// hide: 1.92 -> 1.69 ms at 8 x 4096^2, tools/microbench/genbench).
+template <int LOGN, int LA = kStream, int SA = kStream, int ABL = 0, int RPW_ = 2>
+__global__ __launch_bounds__(FftShape<LOGN>::T * RPW_) void k_rows_half(
+    FrameParams fp, const float4* __restrict__ gab, const float4* __restrict__ gde, const float2* __restrict__ gc,
+    const float4* __restrict__ spec, float4* __restrict__ maps, float* __restrict__ jac, FoamParams foam,
+    const float2* __restrict__ tw_glob)
+{
+  using S = FftShape<LOGN>;
+  using K = ColFirstCfg<LOGN>;
+  using HC = HalfCfg<LOGN>;
+  constexpr int N = S::N, T = S::T, B = K::B, RPW = RPW_, STRIPS = HC::STRIPS, WG = T * RPW;
+  static_assert(WG * 8 * 16 <= lds_row_slots<LOGN>(RPW) * 8, "mirror exchange fits the transform's LDS");
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  float2* tw = reinterpret_cast<float2*>(smem);
+  void* xch = smem + ((S::TW_ENTRIES * 8 + 15) / 16) * 16;
+  CPair* mir = reinterpret_cast<CPair*>(xch);  // [m < 8][thread]: lanes at -u for the partner
+  load_twiddles<LOGN>(tw, tw_glob);
+
+  const int blocks = N / RPW;
+  const int b0 = threadIdx.x % B, r0 = (threadIdx.x / B) % RPW, ihi0 = threadIdx.x / (B * RPW);
+  const int i20 = threadIdx.x % T, r20 = threadIdx.x / T;
+  const int total = fp.cascades * 2 * blocks;
+  const float dim = (float)N;
+  // RPW = 2: C's row pairs are 64-B halves of 128-B lines; items 2p, 2p+1 (the same line) run
+  // together on one XCD so the line is fetched once
+  for (int item = RPW == 2 ? xcd_pair_slot(blockIdx.x, gridDim.x) : blockIdx.x; item < total; item += gridDim.x)
+  {
+    const int b = opaque(b0), ihi = opaque(ihi0), r = RPW == 1 ? 0 : opaque(r0);
+    const int i = ihi * B + b;
+    const int cimg = item / blocks, y0 = (item - cimg * blocks) * RPW;
+    const int c = cimg >> 1, img = cimg & 1;
+    const float dk = fp.c[c].dk;
+    const size_t base = (size_t)c * STRIPS * N * B;
+    const int y = y0 + r;
+    const float sgy = (y & 1) ? -1.0f : 1.0f;  // (-1)^q of the Nyquist-row term
+    const float4* sp = spec + (size_t)cimg * N;
+    const int tid = opaque((int)threadIdx.x);
+    CPair v[16];
+#pragma unroll
+    for (int m = 0; m < 8; m++)
+    {
+      const int u = m * T + i;               // >= 0, column x = N/2 + u
+      const int off = ((u / B) * N + y) * B + (u % B);
+      const float kx = (float)u * dk;        // ((float)x - N/2) dk, x - N/2 exact
+      const float4 s4 = ld4<0>(sp, (N / 2 - u) * 16);  // the -u column's Nyquist-row term (x = N/2 - u)
+      CPair own, neg;
+      if (ABL == 1)
+      {
+        own = CPair{f2v{kx, s4.x}, f2v{(float)off, sgy}};
+        neg = CPair{f2v{s4.y, kx}, f2v{sgy, (float)u}};
+      }
+      else if (img == 0)
+      {
+        const CPair p = raw_pair(ld4<LA>(gab + base, off * 16));  // (A, B)
+        const float2 cc = ld2<LA>(gc + base, off * 8);              // C
+        const float Ar = p.re.x, Ai = p.im.x, Br = p.re.y, Bi = p.im.y, Cr = cc.x, Ci = cc.y;
+        // at u: lane0 = (1 - kx) A, lane1 = i B - kx C
+        own = CPair{f2v{(1.0f - kx) * Ar, -Bi - kx * Cr}, f2v{(1.0f - kx) * Ai, Br - kx * Ci}};
+        // at -u (kx -> -kx, A -> conj A, B -> -conj B, C -> conj C): lane0 = (1 + kx) conj A,
+        // lane1 = i (-conj B) + kx conj C
+        neg = CPair{f2v{(1.0f + kx) * Ar + sgy * s4.x, -Bi + kx * Cr + sgy * s4.z},
+                    f2v{-(1.0f + kx) * Ai + sgy * s4.y, -Br - kx * Ci + sgy * s4.w}};
+      }
+      else
+      {
+        const CPair q = raw_pair(ld4<LA>(gde + base, off * 16));  // (D, E)
+        const float2 cc = ld2<LA>(gc + base, off * 8);              // C
+        const float Cr = cc.x, Ci = cc.y, Dr = q.re.x, Di = q.im.x, Er = q.re.y, Ei = q.im.y;
+        const float kx2 = kx * kx;
+        // at u: lane2 = i (D - kx^2 C), lane3 = -E - i kx D
+        own = CPair{f2v{-(Di - kx2 * Ci), -Er + kx * Di}, f2v{Dr - kx2 * Cr, -Ei - kx * Dr}};
+        // at -u (D -> -conj D, C -> conj C, E -> conj E, kx -> -kx): lane2 = i (-conj D - kx^2 conj C),
+        // lane3 = -conj E + i kx (-conj D)
+        neg = CPair{f2v{-(Di + kx2 * Ci) + sgy * s4.x, -Er - kx * Di + sgy * s4.z},
+                    f2v{-Dr - kx2 * Cr + sgy * s4.y, Ei - kx * Dr + sgy * s4.w}};
+      }
+      v[m] = own;
+      if constexpr (ABL == 3)
+        v[m + 8] = neg;
+      else
+        mir[m * WG + tid] = neg;
+    }
+    if constexpr (ABL != 3)
+      __syncthreads();
+    // own elements m >= 8 (u < 0): from the partner's mirror slots; thread 0's m = 8 is the Nyquist
+    // column (u = -N/2), read directly
+    const int tp = i == 0 ? tid : tid + (((T - i) / B - ihi) * B * RPW) + ((T - i) % B - b);
+#pragma unroll
+    for (int m = 8; m < 16; m++)
+    {
+      if (ABL == 3 || ABL == 1)
+      {
+        if (ABL == 1)
+          v[m] = mir[(i == 0 ? 16 - m : 15 - m) * WG + tp];
+      }
+      else if (i == 0 && m == 8)
+      {
+        const int off = ((N / 2 / B) * N + y) * B;  // Nyquist column: first column of the last strip
+        const float kx = -(dim / 2.0f) * dk;
+        const float2 cc = ld2<LA>(gc + base, off * 8);  // C
+        if (img == 0)
+        {
+          const CPair p = raw_pair(ld4<LA>(gab + base, off * 16));  // (A, B)
+          v[m] = CPair{f2v{(1.0f - kx) * p.re.x, -p.im.y - kx * cc.x},
+                       f2v{(1.0f - kx) * p.im.x, p.re.y - kx * cc.y}};
+        }
+        else
+        {
+          const CPair q = raw_pair(ld4<LA>(gde + base, off * 16));  // (D, E): D = (re.x, im.x)
+          const float kx2 = kx * kx;
+          v[m] = CPair{f2v{-(q.im.x - kx2 * cc.y), -q.re.y + kx * q.im.x},
+                       f2v{q.re.x - kx2 * cc.x, -q.im.y - kx * q.re.x}};
+        }
+      }
+      else
+        v[m] = mir[(i == 0 ? 16 - m : 15 - m) * WG + tp];
+    }
+    if constexpr (ABL != 3)
+      __syncthreads();  // the transform's first exchange reuses the LDS
+    const int i2 = opaque(i20), r2 = RPW == 1 ? 0 : opaque(r20);
+    if constexpr (ABL != 2)
+      fft_run<LOGN, 0, true>(v, i, r, i2, r2, xch, tw);
+    float4* dst = maps + ((size_t)cimg * N + y0) * N;
+    const int woff = ((r2 << LOGN) + i2) * 16;
+#pragma unroll
+    for (int m = 0; m < 16; m++)
+      st4<SA>(dst + m * T, woff, from_pair(v[m]));
+    if (img & 1)
+    {
+      // displacementMap (Dz, dDx/dx, dDz/dz, dDx/dz) = (re0, im0, re1, im1): Jacobian,
+      // spectrum.compute:246-259
+      const float lam = foam.displacement[c];
+      float* jb = jac + ((size_t)c * N + y0) * N;
+      const int joff = ((r2 << LOGN) + i2) * 4;
+#pragma unroll
+      for (int m = 0; m < 16; m++)
+        st1<SA>(jb + m * T, joff,
+                (1.0f + lam * v[m].im.x) * (1.0f + lam * v[m].re.y) - lam * lam * v[m].im.y * v[m].im.y);
+    }
+  }
+}
+
 // B == 1 (N = 16384: one 256-KiB column per CU) makes the blocked layout column-major, whose rows
 // the row pass could only read 16 bytes at a time. This tiled transpose (64 x 64 texels through
 // LDS, 1-KiB runs on both sides) turns inter[c][src][img][x_local][y] into row-major
@@ -782,6 +1067,73 @@ hipError_t launch_cols_evolve(int logn, const FrameParams& fp, const SlabGeom& g
   });
 }
 
+bool half_spectrum_supported(int logn) { return logn >= 10 && logn <= 12; }
+
+size_t half_field_texels(int logn)
+{
+  const size_t n = (size_t)1 << logn;
+  return (n / 8 + 1) * n * 4;  // HalfCfg: STRIPS * N * B per cascade (B = 4)
+}
+
+hipError_t launch_half_columns(int logn, const FrameParams& fp, const float4* h0, float4* gab, float4* gcd, float2* ge,
+                               float4* spec, const float2* tw, hipStream_t stream, int cus)
+{
+  return with_logn(logn, [&](auto L) -> hipError_t {
+    constexpr int LOGN = decltype(L)::value;
+    if constexpr (!HalfCfg<LOGN>::SUPPORTED)
+      return hipErrorInvalidValue;
+    else
+    {
+      using K = ColFirstCfg<LOGN>;
+      using S = FftShape<LOGN>;
+      const int n = S::N;
+      // the Nyquist-row term: one row spectrum per image, then its x-iFFT (in place)
+      long blocks = ((long)fp.cascades * n + 255) / 256;
+      if (blocks > (long)cus * 4)
+        blocks = (long)cus * 4;
+      hipLaunchKernelGGL(k_half_nyquist, dim3((unsigned)blocks), dim3(256), 0, stream, fp, n, K::B, h0, spec);
+      hipError_t e = hipGetLastError();
+      if (e != hipSuccess)
+        return e;
+      auto kern = k_cols_half<LOGN>;
+      const int lds = ((S::TW_ENTRIES * 8 + 15) / 16) * 16 + K::LDS1;
+      const int grid = persistent_grid(kern, K::WG1, lds, fp.cascades * HalfCfg<LOGN>::STRIPS, cus);
+      hipLaunchKernelGGL(kern, dim3(grid), dim3(K::WG1), lds, stream, fp, h0, gab, gcd, ge, tw);  // gcd/ge: (D, E) / C
+      return hipGetLastError();
+    }
+  });
+}
+
+hipError_t launch_half_rows(int logn, const FrameParams& fp, const float4* gab, const float4* gcd, const float2* ge,
+                            const float4* rcorr, float4* maps, float* jac, const FoamParams& foam, const float2* tw,
+                            hipStream_t stream, int cus, int ablation)
+{
+  return with_logn(logn, [&](auto L) -> hipError_t {
+    constexpr int LOGN = decltype(L)::value;
+    if constexpr (!HalfCfg<LOGN>::SUPPORTED)
+      return hipErrorInvalidValue;
+    else
+    {
+      using K = ColFirstCfg<LOGN>;
+      using S = FftShape<LOGN>;
+      // ablation (tools/microbench): 1 no HBM loads, 2 no x transform, 3 no mirror exchange,
+      // 4 / 5 ColFirstCfg's rows per workgroup (one 1024-thread workgroup per CU) / one row
+      constexpr int R4 = K::RPW2;
+      const int rpw = ablation == 4 ? R4 : ablation == 5 ? 1 : 2;
+      auto kern = ablation == 1   ? k_rows_half<LOGN, kStream, kStream, 1>
+                  : ablation == 2 ? k_rows_half<LOGN, kStream, kStream, 2>
+                  : ablation == 3 ? k_rows_half<LOGN, kStream, kStream, 3>
+                  : ablation == 4 ? k_rows_half<LOGN, kStream, kStream, 0, R4>
+                  : ablation == 5 ? k_rows_half<LOGN, kStream, kStream, 0, 1>
+                                  : k_rows_half<LOGN>;
+      const int lds = ((S::TW_ENTRIES * 8 + 15) / 16) * 16 + lds_row_slots<LOGN>(rpw) * 8;
+      const int grid = persistent_grid(kern, S::T * rpw, lds, fp.cascades * 2 * (S::N / rpw), cus);
+      hipLaunchKernelGGL(kern, dim3(grid), dim3(S::T * rpw), lds, stream, fp, gab, gcd, ge, rcorr, maps, jac, foam, tw);
+      return hipGetLastError();
+    }
+  });
+}
+
 bool ifft_colfirst_supported(int logn) { return logn == 12; }
 
 hipError_t launch_ifft_colfirst(int logn, int n_images, float4* images, float4* work, const float2* tw,
@@ -882,18 +1234,23 @@ hipError_t launch_rows_final(int logn, int cascades, const SlabGeom& g, const fl
   });
 }
 
-hipError_t launch_rows_ifft(int logn, int n_images, float4* images, const float2* tw, hipStream_t stream, int cus)
+hipError_t launch_rows_ifft_rows(int logn, int rows, float4* data, const float2* tw, hipStream_t stream, int cus)
 {
   return with_logn(logn, [&](auto L) -> hipError_t {
     constexpr int LOGN = decltype(L)::value;
     using R = RowCfg<LOGN>;
     auto kern = k_rows_ifft<LOGN>;
     int lds = lds_bytes_rows<LOGN>();
-    int items = ((n_images << LOGN) + R::RPW - 1) / R::RPW;
+    int items = (rows + R::RPW - 1) / R::RPW;
     int grid = persistent_grid(kern, R::WG, lds, items, cus);
-    hipLaunchKernelGGL(kern, dim3(grid), dim3(R::WG), lds, stream, n_images, images, tw);
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(R::WG), lds, stream, rows, data, tw);
     return hipGetLastError();
   });
+}
+
+hipError_t launch_rows_ifft(int logn, int n_images, float4* images, const float2* tw, hipStream_t stream, int cus)
+{
+  return launch_rows_ifft_rows(logn, n_images << logn, images, tw, stream, cus);
 }
 
 hipError_t launch_cols(int logn, int n_images, float4* images, const float2* tw, hipStream_t stream, int cus)

@@ -98,6 +98,16 @@ class Generator:
     def handle(self):
         return self._h
 
+    def set_half_spectrum(self, enable: bool) -> None:
+        """Select the half-spectrum (default where supported) or the full-spectrum frame path."""
+        check(lib().ocean_generator_set_half_spectrum(self._h, 1 if enable else 0), "ocean_generator_set_half_spectrum")
+
+    def frame_bytes(self):
+        """Algorithmic HBM bytes per point of the column and row pass of the current path."""
+        out = (ctypes.c_double * 2)()
+        check(lib().ocean_generator_frame_bytes(self._h, out), "ocean_generator_frame_bytes")
+        return float(out[0]), float(out[1])
+
     def GetOceanSettings(self, cascade: int = 0) -> OceanSettings:
         p = lib().ocean_generator_settings(self._h, cascade)
         if not p:

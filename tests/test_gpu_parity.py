@@ -246,6 +246,32 @@ def test_calculate_ocean_8192_vs_float64(ocean, oracle):
     assert scalar_err(gen.jacobian_map_host(0) - 1.0, R.compute_foam(s, d64) - 1.0) <= FRAME_TOL
 
 
+@pytest.mark.parametrize("n", [1024, 2048, 4096])
+def test_half_spectrum_path_matches_full_path_and_oracle(ocean, oracle, n):
+    """The half-spectrum frame (5 fields over the u >= 0 half, Hermitian rebuild, Nyquist-row
+    term) against the full-spectrum frame and the oracle, over several frames and 3 cascades."""
+    planes = [5.0, 23.0, 101.0]
+    fft = ocean.FFTCalculator(n)
+    gh, gf = ocean.Generator(fft, 3), ocean.Generator(fft, 3)
+    gf.set_half_spectrum(False)
+    assert gh.frame_bytes()[0] < 30 and gf.frame_bytes() == (48.0, 68.0)
+    refs = []
+    for c, L in enumerate(planes):
+        for g in (gh, gf):
+            ocean.apply_settings(g.GetOceanSettings(c), planeSize=L)
+        refs.append(oracle.OracleGenerator(n, oracle.default_settings(planeSize=L)))
+    for dt in (0.6, 1.0 / 60.0):
+        gh.CalculateOcean(dt)
+        gf.CalculateOcean(dt)
+        for r in refs:
+            r.calculate_ocean(dt)
+    for c in range(3):
+        for get in ("height_map_host", "displacement_map_host"):
+            a, b = getattr(gh, get)(c), getattr(gf, get)(c)
+            assert max(lane_err(a, b)) <= 1e-5, (c, get, lane_err(a, b))
+        _frame_check(gh.height_map_host(c), gh.displacement_map_host(c), gh.jacobian_map_host(c), refs[c])
+
+
 def test_sixty_four_cascades_in_one_launch(ocean):
     """The ABI's cascade limit (OCEAN_MAX_CASCADES = 64) in one batched generator: every cascade
     equals the same cascade computed alone, bit for bit; 65 is rejected."""
@@ -392,6 +418,7 @@ def test_slab_decomposition_matches_whole_grid(ocean, n, ranks):
     h, d, j = _slab_run(ocean, n, ranks, steps, settings)
     fft = ocean.FFTCalculator(n)
     gen = ocean.Generator(fft, 1)
+    gen.set_half_spectrum(False)  # slabs run the full-spectrum kernels (whole grids 1024..4096 default to half)
     ocean.apply_settings(gen.GetOceanSettings(0), **settings)
     for dt in steps:
         gen.CalculateOcean(dt)
@@ -403,6 +430,7 @@ def test_slab_decomposition_matches_whole_grid(ocean, n, ranks):
 def _whole_grid_frames(ocean, n, steps, settings):
     fft = ocean.FFTCalculator(n)
     gen = ocean.Generator(fft, 1)
+    gen.set_half_spectrum(False)  # the kernels the slabs run
     ocean.apply_settings(gen.GetOceanSettings(0), **settings)
     frames = []
     for dt in steps:

@@ -16,7 +16,11 @@ def _bench():
 
 def test_bench_byte_accounting():
     b = _bench()
-    assert b.PASS1_BYTES == 48 and b.PASS2_BYTES == 68 and b.FRAME_BYTES == 116
+    assert b.frame_bytes_per_point(4096, False) == (48.0, 68.0)
+    p1, p2 = b.frame_bytes_per_point(4096, True)
+    kept = (2048 + 4) / 4096
+    assert p1 == 16.0 * kept + 40.0 * kept and p2 == 40.0 * kept + 36.0
+    assert 84.0 < p1 + p2 < 84.1  # 8 + 20 | 20 + 36 per grid point, plus the Nyquist strip
 
 
 def test_bench_cascade_sharding_is_disjoint():

@@ -92,6 +92,20 @@ int main(int argc, char** argv)
   float4* scratch = nullptr;
   if (rows_need_transpose(logn))
     CHECK(hipMalloc(&scratch, tex * C * 2 * sizeof(float4)));
+  // half-spectrum path buffers (N = 1024 .. 4096)
+  float4 *gab = nullptr, *gcd = nullptr, *spec = nullptr;
+  float2* ge = nullptr;
+  const bool half = half_spectrum_supported(logn);
+  if (half)
+  {
+    const size_t ht = half_field_texels(logn) * C;
+    CHECK(hipMalloc(&gab, ht * sizeof(float4)));
+    CHECK(hipMalloc(&gcd, ht * sizeof(float4)));
+    CHECK(hipMalloc(&ge, ht * sizeof(float2)));
+    CHECK(hipMalloc(&spec, (size_t)C * 2 * n * sizeof(float4)));
+  }
+  auto h1 = [&] { return launch_half_columns(logn, fp, h0, gab, gcd, ge, spec, tw, 0, cus); };
+  auto h2 = [&] { return launch_half_rows(logn, fp, gab, gcd, ge, spec, maps, jac, foam, tw, 0, cus); };
   auto p1r = [&] { return launch_cols_evolve(logn, fp, geom, h0, inter, tw, 0, cus, 0); };
   auto p1k = [&] { return launch_cols_evolve(logn, fp, geom, h0, inter, tw, 0, cus, 16); };
   auto p1h = [&] { return launch_cols_evolve(logn, fp, geom, h0, inter, tw, 0, cus, default_keep(logn)); };
@@ -111,7 +125,7 @@ int main(int argc, char** argv)
   const int rounds = 7, reps = 10;
   std::vector<float> t1r, t1k, t1h, t2, tf;
   std::vector<std::vector<float>> tp(6);
-  std::vector<float> tco, trp2, t2c, t2m, t1m;
+  std::vector<float> tco, trp2, t2c, t2m, t1m, th1, th2;
   for (int r = 0; r < rounds; r++)
   {
     t1r.push_back(time_ms(p1r, reps));
@@ -130,6 +144,8 @@ int main(int argc, char** argv)
       t2c.push_back(time_ms(pv(2, 4), reps));
       t2m.push_back(time_ms(pv(2, 5), reps));
       t1m.push_back(time_ms(pv(1, 4), reps));
+      th1.push_back(time_ms(h1, reps));
+      th2.push_back(time_ms(h2, reps));
     }
   }
   auto report = [&](const char* name, std::vector<float>& v, double bytes_per_pt) {
@@ -158,6 +174,18 @@ int main(int argc, char** argv)
     report("pass2 compute only (no HBM)", t2c, 68);
     report("pass2 memory only (no FFT)", t2m, 68);
     report("pass1 keep 4 memory only (no evolve/FFT)", t1m, 48);
+    report("half pass1 (Nyquist term + k_cols_half)", th1, 28);
+    report("half pass2 k_rows_half (2 rows/WG)", th2, 56);
+    for (int a = 1; a <= 5; a++)
+    {
+      static const char* names[] = {"", "half pass2 no HBM loads", "half pass2 no FFT", "half pass2 no mirror exchange",
+                                    "half pass2 4 rows per WG (1 WG/CU)", "half pass2 1 row per WG (4 WG/CU)"};
+      auto ha = [&] { return launch_half_rows(logn, fp, gab, gcd, ge, spec, maps, jac, foam, tw, 0, cus, a); };
+      std::vector<float> ta;
+      for (int r = 0; r < rounds; r++)
+        ta.push_back(time_ms(ha, reps));
+      report(names[a], ta, 56);
+    }
   }
   return 0;
 }

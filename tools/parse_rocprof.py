@@ -17,8 +17,10 @@ src, tag = sys.argv[1], sys.argv[2]
 n = int(sys.argv[3]) if len(sys.argv) > 3 else 4096
 cascades = int(sys.argv[4]) if len(sys.argv) > 4 else 8
 pts = n * n * cascades
+kept = (n // 2 + 4) / n  # half-spectrum path: columns u in [0, N/2) plus the 4-wide Nyquist strip
 ALGO = {"k_cols_evolve": 48 * pts, "k_rows_final": 68 * pts, "k_generate_spectrum": 16 * n * n,
-        "k_generate_spectrum_pairs": 16 * n * n}
+        "k_generate_spectrum_pairs": 16 * n * n,
+        "k_cols_half": int((16 + 40) * kept * pts), "k_rows_half": int((40 * kept + 36) * pts)}
 
 
 def read_csv(path):

@@ -86,6 +86,7 @@ struct ocean_generator
   // half-spectrum path (ranks == 1, N = 1024 .. 4096; ocean_generator_set_half_spectrum)
   bool half = false;
   FrameParams frame{};    // the last column pass's per-cascade values (the row pass needs dk)
+  float2* hs = nullptr;    // pass-1 H scratch, half_hs_bytes(logn, device CUs)
   float4* gab = nullptr;  // [cascade][strip][N][4]: y-transformed (H, kz H) for u >= 0 + Nyquist strip
   float4* gcd = nullptr;  // (kz H/|k|, kz^2 H/|k|)
   float2* ge = nullptr;   // H/|k|
@@ -319,6 +320,8 @@ static hipError_t half_buffers(ocean_generator* g)
     e = hipMalloc(&g->ge, t * sizeof(float2));
   if (e == hipSuccess && !g->spec)
     e = hipMalloc(&g->spec, (size_t)g->cascades * 2 * g->fft->n * sizeof(float4));
+  if (e == hipSuccess && !g->hs)  // pass 1's H scratch: one slice per resident block (1 per CU)
+    e = hipMalloc(&g->hs, half_hs_bytes(g->fft->logn, g->fft->device_cus));
   return e;
 }
 
@@ -413,7 +416,7 @@ int ocean_generator_destroy(ocean_generator* g)
     (void)hipFree(g->maps);
   if (g->jac)
     (void)hipFree(g->jac);
-  for (void* p : {(void*)g->gab, (void*)g->gcd, (void*)g->ge, (void*)g->spec})
+  for (void* p : {(void*)g->gab, (void*)g->gcd, (void*)g->ge, (void*)g->spec, (void*)g->hs})
     if (p)
       (void)hipFree(p);
   delete g;
@@ -480,7 +483,7 @@ static int generator_columns(ocean_generator* g, float timestep, int update_spec
   if (g->half)
     HIP_TRY(timed(g, 1, [&] {
               return launch_half_columns(f->logn, fp, g->h0, g->gab, g->gcd, g->ge, g->spec, f->twiddles, f->stream,
-                                         f->cus);
+                                         f->cus, g->hs, f->device_cus);
             }),
             "column pass (half spectrum)");
   else

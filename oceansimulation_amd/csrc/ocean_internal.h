@@ -96,8 +96,12 @@ hipError_t launch_generate_spectrum(const OceanSettings& s, int n, float4* h0, h
 // cascade each for gab, gcd (float4) and ge (float2).
 bool half_spectrum_supported(int logn);
 size_t half_field_texels(int logn);
+// hs (optional): H scratch of half_hs_bytes(logn, hs_blocks) bytes; pass 1 then evolves each texel
+// once (grid capped at hs_blocks) instead of once per field round.
+size_t half_hs_bytes(int logn, int blocks);
 hipError_t launch_half_columns(int logn, const FrameParams& fp, const float4* h0, float4* gab, float4* gcd, float2* ge,
-                               float4* spec, const float2* tw, hipStream_t stream, int cus);
+                               float4* spec, const float2* tw, hipStream_t stream, int cus, float2* hs = nullptr,
+                               int hs_blocks = 0);
 hipError_t launch_half_rows(int logn, const FrameParams& fp, const float4* gab, const float4* gcd, const float2* ge,
                             const float4* rcorr, float4* maps, float* jac, const FoamParams& foam, const float2* tw,
                             hipStream_t stream, int cus, int ablation = 0);

@@ -531,11 +531,15 @@ struct HalfCfg
 // (A, B), (D, E), (C, 0), stored as gab, gde (float4) and gc (float2): pass 2 reads (A, B) + C for
 // image 0 and C + (D, E) for image 1. H is re-evolved per round from h0: keeping the 16 H (32 VGPRs)
 // next to the transform's ~107 spills in a 1024-thread workgroup.
-template <int LOGN, int LA = 0, int SA = kStream>
+// HS (H scratch): round 0 evolves H once and parks it in a per-workgroup scratch slice (8 B per
+// texel, [m][thread], L2/MALL-resident); rounds 1 and 2 load it back (nt: served by L2, never a
+// stale L1 line from the previous item) instead of re-reading h0 (16 B) and re-evolving.
+template <int LOGN, int LA = 0, int SA = kStream, bool HS = false>
 __global__ __launch_bounds__(ColFirstCfg<LOGN>::WG1) void k_cols_half(FrameParams fp, const float4* __restrict__ h0,
                                                                      float4* __restrict__ gab, float4* __restrict__ gde,
                                                                      float2* __restrict__ gc,
-                                                                     const float2* __restrict__ tw_glob)
+                                                                     const float2* __restrict__ tw_glob,
+                                                                     float2* __restrict__ hs)
 {
   using S = FftShape<LOGN>;
   using K = ColFirstCfg<LOGN>;
@@ -558,22 +562,12 @@ __global__ __launch_bounds__(ColFirstCfg<LOGN>::WG1) void k_cols_half(FrameParam
     const float4* src = h0 + ((size_t)c * (N / B) + xb) * N * B;
     const size_t base = ((size_t)c * STRIPS + s) * N * B;
     const int x = xb * B + b;
-#pragma unroll 1
-    for (int round = 0; round < 3; round++)
-    {
+    // one field round: (A, B), (D, E) or (C, 0) of the 16 texels, y-iFFT, store
+    auto run_round = [&](int round) __attribute__((always_inline)) {
       const int i = (opaque((int)threadIdx.x) / B) % T;
       const int voff = (i * B + b) * 16;
-      float4 a[16];
-#pragma unroll
-      for (int m = 0; m < 16; m++)  // fftShift on y folded into the load
-        a[m] = ld4<LA>(src + ((m + 8) & 15) * T * B, voff);
       CPair v[16];
-#pragma unroll
-      for (int m = 0; m < 16; m++)
-      {
-        const int y = i + ((m + 8) & 15) * T;
-        const KVec q = make_kvec(x, y, dim, f.dk);
-        const float2 H = evolve(a[m], q.k, f);
+      auto pack = [&](int m, float2 H, const KVec& q) __attribute__((always_inline)) {
         if (round == 0)  // (A, B) = (H, kz H)
           v[m] = CPair{f2v{H.x, q.kz * H.x}, f2v{H.y, q.kz * H.y}};
         else if (round == 1)  // (D, E) = (kz H / |k|, kz^2 H / |k|)
@@ -583,6 +577,36 @@ __global__ __launch_bounds__(ColFirstCfg<LOGN>::WG1) void k_cols_half(FrameParam
         }
         else  // (C, 0) = (H / |k|, 0)
           v[m] = CPair{f2v{q.inv * H.x, 0.0f}, f2v{q.inv * H.y, 0.0f}};
+      };
+      if (!HS || round == 0)
+      {
+        float2* hsb = hs + (size_t)blockIdx.x * 16 * K::WG1;
+        const int hoff = opaque((int)threadIdx.x) * 8;
+        float4 a[16];
+#pragma unroll
+        for (int m = 0; m < 16; m++)  // fftShift on y folded into the load
+          a[m] = ld4<LA>(src + ((m + 8) & 15) * T * B, voff);
+#pragma unroll
+        for (int m = 0; m < 16; m++)
+        {
+          const int y = i + ((m + 8) & 15) * T;
+          const KVec q = make_kvec(x, y, dim, f.dk);
+          const float2 H = evolve(a[m], q.k, f);
+          if (HS)
+            st2<0>(hsb + m * K::WG1, hoff, H);
+          pack(m, H, q);
+        }
+      }
+      else
+      {
+        const float2* hsb = hs + (size_t)blockIdx.x * 16 * K::WG1;
+        const int hoff = opaque((int)threadIdx.x) * 8;
+#pragma unroll
+        for (int m = 0; m < 16; m++)
+        {
+          const int y = i + ((m + 8) & 15) * T;
+          pack(m, ld2<kStream>(hsb + m * K::WG1, hoff), make_kvec(x, y, dim, f.dk));
+        }
       }
       fft_run<LOGN, K::C1, true>(v, i, b, xch, tw);
 #pragma unroll
@@ -595,6 +619,18 @@ __global__ __launch_bounds__(ColFirstCfg<LOGN>::WG1) void k_cols_half(FrameParam
         else
           st2<SA>(gc + base + m * T * B, (i * B + b) * 8, make_float2(v[m].re.x, v[m].im.x));
       }
+    };
+    if constexpr (HS)
+    {
+#pragma unroll
+      for (int round = 0; round < 3; round++)  // specialised per round: 113 VGPRs, no spills
+        run_round(round);
+    }
+    else
+    {
+#pragma unroll 1
+      for (int round = 0; round < 3; round++)
+        run_round(round);
     }
   }
 }
@@ -649,7 +685,9 @@ __global__ __launch_bounds__(256) void k_half_nyquist(FrameParams fp, int n, int
 // RPW_ = 2 (default): 512-thread workgroups, two per CU, so one workgroup's loads overlap the
 // other's transform (the LDS mirror exchange adds a barrier the 1024-thread, one-per-CU shape cannot
 // hide: 1.92 -> 1.69 ms at 8 x 4096^2, tools/microbench/genbench).
-template <int LOGN, int LA = kStream, int SA = kStream, int ABL = 0, int RPW_ = 2>
+// BOTH: one item = both images of its rows (image 0, then image 1), so C is loaded once and kept
+// in VGPRs (16) for image 1 instead of being fetched again by a second item.
+template <int LOGN, int LA = kStream, int SA = kStream, int ABL = 0, int RPW_ = 2, bool BOTH = false>
 __global__ __launch_bounds__(FftShape<LOGN>::T * RPW_) void k_rows_half(
     FrameParams fp, const float4* __restrict__ gab, const float4* __restrict__ gde, const float2* __restrict__ gc,
     const float4* __restrict__ spec, float4* __restrict__ maps, float* __restrict__ jac, FoamParams foam,
@@ -669,16 +707,22 @@ __global__ __launch_bounds__(FftShape<LOGN>::T * RPW_) void k_rows_half(
   const int blocks = N / RPW;
   const int b0 = threadIdx.x % B, r0 = (threadIdx.x / B) % RPW, ihi0 = threadIdx.x / (B * RPW);
   const int i20 = threadIdx.x % T, r20 = threadIdx.x / T;
-  const int total = fp.cascades * 2 * blocks;
+  const int total = fp.cascades * (BOTH ? 1 : 2) * blocks;
   const float dim = (float)N;
   // RPW = 2: C's row pairs are 64-B halves of 128-B lines; items 2p, 2p+1 (the same line) run
   // together on one XCD so the line is fetched once
   for (int item = RPW == 2 ? xcd_pair_slot(blockIdx.x, gridDim.x) : blockIdx.x; item < total; item += gridDim.x)
   {
+    const int cimg0 = item / blocks, y0 = (item - cimg0 * blocks) * RPW;
+    float2 ckeep[8];  // BOTH: image 0's C loads, reused by image 1
+    float2 cnyq;
+#pragma unroll
+    for (int pass = 0; pass < (BOTH ? 2 : 1); pass++)
+    {
+    const int cimg = BOTH ? cimg0 * 2 + pass : cimg0;
     const int b = opaque(b0), ihi = opaque(ihi0), r = RPW == 1 ? 0 : opaque(r0);
     const int i = ihi * B + b;
-    const int cimg = item / blocks, y0 = (item - cimg * blocks) * RPW;
-    const int c = cimg >> 1, img = cimg & 1;
+    const int c = cimg >> 1, img = BOTH ? pass : (cimg & 1);
     const float dk = fp.c[c].dk;
     const size_t base = (size_t)c * STRIPS * N * B;
     const int y = y0 + r;
@@ -703,6 +747,8 @@ __global__ __launch_bounds__(FftShape<LOGN>::T * RPW_) void k_rows_half(
       {
         const CPair p = raw_pair(ld4<LA>(gab + base, off * 16));  // (A, B)
         const float2 cc = ld2<LA>(gc + base, off * 8);              // C
+        if (BOTH)
+          ckeep[m] = cc;
         const float Ar = p.re.x, Ai = p.im.x, Br = p.re.y, Bi = p.im.y, Cr = cc.x, Ci = cc.y;
         // at u: lane0 = (1 - kx) A, lane1 = i B - kx C
         own = CPair{f2v{(1.0f - kx) * Ar, -Bi - kx * Cr}, f2v{(1.0f - kx) * Ai, Br - kx * Ci}};
@@ -714,7 +760,7 @@ __global__ __launch_bounds__(FftShape<LOGN>::T * RPW_) void k_rows_half(
       else
       {
         const CPair q = raw_pair(ld4<LA>(gde + base, off * 16));  // (D, E)
-        const float2 cc = ld2<LA>(gc + base, off * 8);              // C
+        const float2 cc = BOTH ? ckeep[m] : ld2<LA>(gc + base, off * 8);  // C
         const float Cr = cc.x, Ci = cc.y, Dr = q.re.x, Di = q.im.x, Er = q.re.y, Ei = q.im.y;
         const float kx2 = kx * kx;
         // at u: lane2 = i (D - kx^2 C), lane3 = -E - i kx D
@@ -747,7 +793,13 @@ __global__ __launch_bounds__(FftShape<LOGN>::T * RPW_) void k_rows_half(
       {
         const int off = ((N / 2 / B) * N + y) * B;  // Nyquist column: first column of the last strip
         const float kx = -(dim / 2.0f) * dk;
-        const float2 cc = ld2<LA>(gc + base, off * 8);  // C
+        float2 cc;
+        if (BOTH && img == 1)
+          cc = cnyq;
+        else
+          cc = ld2<LA>(gc + base, off * 8);  // C
+        if (BOTH && img == 0)
+          cnyq = cc;
         if (img == 0)
         {
           const CPair p = raw_pair(ld4<LA>(gab + base, off * 16));  // (A, B)
@@ -786,6 +838,7 @@ __global__ __launch_bounds__(FftShape<LOGN>::T * RPW_) void k_rows_half(
       for (int m = 0; m < 16; m++)
         st1<SA>(jb + m * T, joff,
                 (1.0f + lam * v[m].im.x) * (1.0f + lam * v[m].re.y) - lam * lam * v[m].im.y * v[m].im.y);
+    }
     }
   }
 }
@@ -1075,8 +1128,13 @@ size_t half_field_texels(int logn)
   return (n / 8 + 1) * n * 4;  // HalfCfg: STRIPS * N * B per cascade (B = 4)
 }
 
+size_t half_hs_bytes(int logn, int blocks)
+{
+  return half_spectrum_supported(logn) ? (size_t)blocks * 16 * 1024 * sizeof(float2) : 0;  // WG1 <= 1024
+}
+
 hipError_t launch_half_columns(int logn, const FrameParams& fp, const float4* h0, float4* gab, float4* gcd, float2* ge,
-                               float4* spec, const float2* tw, hipStream_t stream, int cus)
+                               float4* spec, const float2* tw, hipStream_t stream, int cus, float2* hs, int hs_blocks)
 {
   return with_logn(logn, [&](auto L) -> hipError_t {
     constexpr int LOGN = decltype(L)::value;
@@ -1095,10 +1153,15 @@ hipError_t launch_half_columns(int logn, const FrameParams& fp, const float4* h0
       hipError_t e = hipGetLastError();
       if (e != hipSuccess)
         return e;
-      auto kern = k_cols_half<LOGN>;
+      // hs: per-block H scratch (half_hs_bytes): H evolved once instead of once per round
+      auto kern = hs ? k_cols_half<LOGN, 0, kStream, true> : k_cols_half<LOGN>;
       const int lds = ((S::TW_ENTRIES * 8 + 15) / 16) * 16 + K::LDS1;
-      const int grid = persistent_grid(kern, K::WG1, lds, fp.cascades * HalfCfg<LOGN>::STRIPS, cus);
-      hipLaunchKernelGGL(kern, dim3(grid), dim3(K::WG1), lds, stream, fp, h0, gab, gcd, ge, tw);  // gcd/ge: (D, E) / C
+      int grid = persistent_grid(kern, K::WG1, lds, fp.cascades * HalfCfg<LOGN>::STRIPS, cus);
+      if (hs && grid > hs_blocks)
+        grid = hs_blocks;
+      if (grid < 1)
+        return hipErrorInvalidValue;
+      hipLaunchKernelGGL(kern, dim3(grid), dim3(K::WG1), lds, stream, fp, h0, gab, gcd, ge, tw, hs);  // gcd/ge: (D, E) / C
       return hipGetLastError();
     }
   });
@@ -1118,16 +1181,20 @@ hipError_t launch_half_rows(int logn, const FrameParams& fp, const float4* gab, 
       using S = FftShape<LOGN>;
       // ablation (tools/microbench): 1 no HBM loads, 2 no x transform, 3 no mirror exchange,
       // 4 / 5 ColFirstCfg's rows per workgroup (one 1024-thread workgroup per CU) / one row
+      // 0 (production): one item per row block for both images (C loaded once); 6: one image per
+      // item (C loaded by both items of a row block)
       constexpr int R4 = K::RPW2;
       const int rpw = ablation == 4 ? R4 : ablation == 5 ? 1 : 2;
-      auto kern = ablation == 1   ? k_rows_half<LOGN, kStream, kStream, 1>
+      const int per_item = ablation == 0 ? 1 : 2;
+      auto kern = ablation == 0   ? k_rows_half<LOGN, kStream, kStream, 0, 2, true>
+                  : ablation == 6 ? k_rows_half<LOGN>
+                  : ablation == 1 ? k_rows_half<LOGN, kStream, kStream, 1>
                   : ablation == 2 ? k_rows_half<LOGN, kStream, kStream, 2>
                   : ablation == 3 ? k_rows_half<LOGN, kStream, kStream, 3>
                   : ablation == 4 ? k_rows_half<LOGN, kStream, kStream, 0, R4>
-                  : ablation == 5 ? k_rows_half<LOGN, kStream, kStream, 0, 1>
-                                  : k_rows_half<LOGN>;
+                                  : k_rows_half<LOGN, kStream, kStream, 0, 1>;
       const int lds = ((S::TW_ENTRIES * 8 + 15) / 16) * 16 + lds_row_slots<LOGN>(rpw) * 8;
-      const int grid = persistent_grid(kern, S::T * rpw, lds, fp.cascades * 2 * (S::N / rpw), cus);
+      const int grid = persistent_grid(kern, S::T * rpw, lds, fp.cascades * per_item * (S::N / rpw), cus);
       hipLaunchKernelGGL(kern, dim3(grid), dim3(S::T * rpw), lds, stream, fp, gab, gcd, ge, rcorr, maps, jac, foam, tw);
       return hipGetLastError();
     }

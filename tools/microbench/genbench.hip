@@ -175,7 +175,7 @@ int main(int argc, char** argv)
     report("pass2 memory only (no FFT)", t2m, 68);
     report("pass1 keep 4 memory only (no evolve/FFT)", t1m, 48);
     report("half pass1 (Nyquist term + k_cols_half)", th1, 28);
-    report("half pass2 k_rows_half (2 rows/WG)", th2, 56);
+    report("half pass2 k_rows_half (both images per item)", th2, 56);
     for (int a = 1; a <= 5; a++)
     {
       static const char* names[] = {"", "half pass2 no HBM loads", "half pass2 no FFT", "half pass2 no mirror exchange",

@@ -1,0 +1,190 @@
+// halfbench.hip — interleaved A/B timing of half-spectrum frame-pass variants (8 cascades x 4096^2),
+// with a bit-identity check of every variant's output against the baseline variant.
+// Build: see Makefile target `microbench`. Usage: halfbench [logn] [cascades]
+#include "../../oceansimulation_amd/csrc/ocean_kernels.hip"
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <vector>
+
+using namespace oceanfft;
+
+#define CHECK(x)                                                                                   \
+  do                                                                                               \
+  {                                                                                                \
+    hipError_t e = (x);                                                                            \
+    if (e != hipSuccess)                                                                           \
+    {                                                                                              \
+      std::printf("HIP error %s at %s:%d\n", hipGetErrorString(e), __FILE__, __LINE__);            \
+      std::exit(1);                                                                                \
+    }                                                                                              \
+  } while (0)
+
+template <typename F>
+static float time_ms(F&& launch, int reps)
+{
+  hipEvent_t a, b;
+  CHECK(hipEventCreate(&a));
+  CHECK(hipEventCreate(&b));
+  CHECK(hipEventRecord(a));
+  for (int r = 0; r < reps; r++)
+    CHECK(launch());
+  CHECK(hipEventRecord(b));
+  CHECK(hipEventSynchronize(b));
+  float ms;
+  CHECK(hipEventElapsedTime(&ms, a, b));
+  CHECK(hipEventDestroy(a));
+  CHECK(hipEventDestroy(b));
+  return ms / reps;
+}
+
+static std::vector<unsigned char> snap(const void* d, size_t bytes)
+{
+  std::vector<unsigned char> h(bytes);
+  CHECK(hipMemcpy(h.data(), d, bytes, hipMemcpyDeviceToHost));
+  return h;
+}
+
+int main(int argc, char** argv)
+{
+  const int logn = argc > 1 ? std::atoi(argv[1]) : 12;
+  const int C = argc > 2 ? std::atoi(argv[2]) : 8;
+  const int n = 1 << logn;
+  if (!half_spectrum_supported(logn))
+  {
+    std::printf("half path: N = 1024 .. 4096 only\n");
+    return 1;
+  }
+  int cus = 0;
+  CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0));
+  const size_t tex = (size_t)n * n;
+  float4 *h0, *maps, *gab, *gcd, *spec;
+  float2 *ge, *tw, *hs;
+  float* jac;
+  const size_t ht = half_field_texels(logn) * C;
+  CHECK(hipMalloc(&h0, tex * C * sizeof(float4)));
+  CHECK(hipMalloc(&maps, tex * C * 2 * sizeof(float4)));
+  CHECK(hipMalloc(&jac, tex * C * sizeof(float)));
+  CHECK(hipMalloc(&gab, ht * sizeof(float4)));
+  CHECK(hipMalloc(&gcd, ht * sizeof(float4)));
+  CHECK(hipMalloc(&ge, ht * sizeof(float2)));
+  CHECK(hipMalloc(&spec, (size_t)C * 2 * n * sizeof(float4)));
+  CHECK(hipMalloc(&hs, half_hs_bytes(logn, cus)));
+  int lb = logn / 2, tb = 1 << lb, ta = 1 << (logn - lb);
+  std::vector<float2> tab(tb + ta);
+  for (int e = 0; e < tb; e++)
+    tab[e] = make_float2((float)std::cos(2 * M_PI * e / n), (float)std::sin(2 * M_PI * e / n));
+  for (int e = 0; e < ta; e++)
+    tab[tb + e] = make_float2((float)std::cos(2 * M_PI * e * tb / n), (float)std::sin(2 * M_PI * e * tb / n));
+  CHECK(hipMalloc(&tw, tab.size() * sizeof(float2)));
+  CHECK(hipMemcpy(tw, tab.data(), tab.size() * sizeof(float2), hipMemcpyHostToDevice));
+
+  static const float planes[] = {5, 17, 101, 251, 509, 1021, 2039, 4093};
+  FrameParams fp{};
+  FoamParams foam{};
+  fp.cascades = C;
+  for (int c = 0; c < C; c++)
+  {
+    OceanSettings s{};
+    s.seed[0] = 12342;
+    s.seed[1] = 8934;
+    s.U_10 = 40;
+    s.theta_0 = 25;
+    s.F = 800000;
+    s.g = 9.8f;
+    s.swell = 0.5f;
+    s.h = 100;
+    s.displacement = 0.4f;
+    s.planeSize = planes[c % 8];
+    s.scale = 1;
+    s.spread = 0.2f;
+    CHECK(launch_generate_spectrum(s, n, h0 + tex * c, 0, cus));
+    fp.c[c] = {2.0f * 3.14159265358f / s.planeSize, 37.5f, s.g, s.h};
+    foam.displacement[c] = s.displacement;
+  }
+  CHECK(hipDeviceSynchronize());
+  const double pts = (double)tex * C;
+
+  auto c0 = [&] { return launch_half_columns(logn, fp, h0, gab, gcd, ge, spec, tw, 0, cus); };
+  auto c1 = [&] { return launch_half_columns(logn, fp, h0, gab, gcd, ge, spec, tw, 0, cus, hs, cus); };
+  auto r0 = [&] { return launch_half_rows(logn, fp, gab, gcd, ge, spec, maps, jac, foam, tw, 0, cus, 6); };
+  auto r1 = [&] { return launch_half_rows(logn, fp, gab, gcd, ge, spec, maps, jac, foam, tw, 0, cus); };
+
+  // bit identity: baseline frame, then each variant on the same inputs (float compare, NaN-aware)
+  const size_t mb = tex * C * 2 * sizeof(float4), jb = tex * C * sizeof(float);
+  auto diff = [](const std::vector<unsigned char>& a, const std::vector<unsigned char>& b) {
+    const float* x = reinterpret_cast<const float*>(a.data());
+    const float* y = reinterpret_cast<const float*>(b.data());
+    size_t bad = 0, first = (size_t)-1;
+    double worst = 0;
+    for (size_t k = 0; k < a.size() / 4; k++)
+      if (std::memcmp(x + k, y + k, 4) != 0)
+      {
+        if (first == (size_t)-1)
+          first = k;
+        bad++;
+        worst = std::max(worst, (double)std::fabs(x[k] - y[k]));
+      }
+    if (bad)
+      std::printf("    %zu of %zu floats differ (first at %zu: %g vs %g), max |diff| %g\n", bad, a.size() / 4, first,
+                  x[first], y[first], worst);
+    return bad == 0;
+  };
+  CHECK(c0());
+  CHECK(hipDeviceSynchronize());
+  auto ref_ab = snap(gab, ht * sizeof(float4)), ref_de = snap(gcd, ht * sizeof(float4)), ref_c = snap(ge, ht * sizeof(float2));
+  CHECK(r0());
+  CHECK(hipDeviceSynchronize());
+  auto ref_m = snap(maps, mb), ref_j = snap(jac, jb);
+  CHECK(hipMemset(maps, 0, mb));
+  CHECK(hipMemset(jac, 0, jb));
+  CHECK(r1());
+  CHECK(hipDeviceSynchronize());
+  std::printf("rows (both images) vs baseline on the same fields:\n");
+  const bool same_rows = (int)diff(snap(maps, mb), ref_m) & (int)diff(snap(jac, jb), ref_j);
+  CHECK(c0());
+  CHECK(hipDeviceSynchronize());
+  std::printf("cols baseline run twice:\n");
+  const bool det = (int)diff(snap(gab, ht * sizeof(float4)), ref_ab) & (int)diff(snap(gcd, ht * sizeof(float4)), ref_de) &
+                   (int)diff(snap(ge, ht * sizeof(float2)), ref_c);
+  CHECK(hipMemset(gab, 0, ht * sizeof(float4)));
+  CHECK(hipMemset(gcd, 0, ht * sizeof(float4)));
+  CHECK(hipMemset(ge, 0, ht * sizeof(float2)));
+  CHECK(c1());
+  CHECK(hipDeviceSynchronize());
+  std::printf("cols (HS) vs baseline: gab, gde, gc\n");
+  const bool same_cols = (int)diff(snap(gab, ht * sizeof(float4)), ref_ab) & (int)diff(snap(gcd, ht * sizeof(float4)), ref_de) &
+                         (int)diff(snap(ge, ht * sizeof(float2)), ref_c);
+  std::printf("N=%d cascades=%d CUs=%d  bit-identical: cols deterministic=%s cols(HS)=%s rows(both images)=%s\n", n, C,
+              cus, det ? "yes" : "NO", same_cols ? "yes" : "NO", same_rows ? "yes" : "NO");
+
+  auto f00 = [&] { hipError_t e = c0(); return e == hipSuccess ? r0() : e; };
+  auto f11 = [&] { hipError_t e = c1(); return e == hipSuccess ? r1() : e; };
+  const int rounds = 7, reps = 10;
+  std::vector<std::vector<float>> t(6);
+  for (int r = 0; r < rounds; r++)
+  {
+    t[0].push_back(time_ms(c0, reps));
+    t[1].push_back(time_ms(c1, reps));
+    t[2].push_back(time_ms(r0, reps));
+    t[3].push_back(time_ms(r1, reps));
+    t[4].push_back(time_ms(f00, reps));
+    t[5].push_back(time_ms(f11, reps));
+  }
+  const double kept = (n / 2.0 + 4) / n;
+  const double b1 = 56 * kept, b2 = 40 * kept + 36;
+  const char* names[] = {"cols: re-evolve per round", "cols: H scratch (HS)", "rows: one image per item",
+                         "rows: both images per item", "frame: baseline", "frame: HS + both images"};
+  const double bpp[] = {b1, b1, b2, b2, b1 + b2, b1 + b2};
+  for (int k = 0; k < 6; k++)
+  {
+    std::sort(t[k].begin(), t[k].end());
+    const double med = t[k][t[k].size() / 2];
+    std::printf("%-30s median %7.3f ms  min %7.3f ms  %7.1f GB/s algorithmic (%.1f B/pt)  %.3e pts/s\n", names[k],
+                med, t[k][0], bpp[k] * pts / med / 1e6, bpp[k], pts / med * 1e3);
+  }
+  return 0;
+}

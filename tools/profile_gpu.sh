@@ -7,7 +7,7 @@
 set -u
 cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
 ARGS=${BENCH_ARGS:-"--steps 20 --warmup 3 --no-cpu-baseline --no-slab --no-ifft --no-surface"}
-KRE=${KERNEL_REGEX:-"k_cols_evolve|k_rows_final|k_rows_ifft|k_cols|k_generate_spectrum"}
+KRE=${KERNEL_REGEX:-"k_cols_evolve|k_rows_final|k_rows_ifft|k_rows_half|k_cols|k_generate_spectrum|k_half_nyquist"}
 mkdir -p gpurun_out
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -T -d gpurun_out/prof_trace -o trace --output-format csv \
   -- python3 bench.py $ARGS > gpurun_out/prof_trace.log 2>&1 || { echo "trace pass failed rc=$?"; tail -20 gpurun_out/prof_trace.log; exit 1; }

@@ -278,6 +278,8 @@ def slab_grid(args, rank: int, world: int, local: int) -> dict:
     device = torch.device("cuda", local)
     fft = ocean.FFTCalculator(n)
     g = SlabGenerator(fft, rank, world)
+    if args.full_spectrum:
+        g.set_half_spectrum(False)
 
     def timed(run_steps):
         sync()
@@ -323,6 +325,9 @@ def slab_grid(args, rank: int, world: int, local: int) -> dict:
                      if exchange else "none (one rank)"),
         "column_pass_ms": ms[1] / max(cnt[1], 1),
         "row_pass_ms": ms[2] / max(cnt[2], 1),
+        "frame_path": "full spectrum" if args.full_spectrum else "half spectrum, strip-dealt (fields moved to "
+                      "row-major after the exchange)",
+        "frame_hbm_bytes_per_point": sum(g.frame_bytes()),
         "exchange_bytes_per_rank": g.exchange_bytes * (world - 1) // world if world > 1 else 0,
         "serial_ms_per_frame": 1000.0 * el / per,
     }

@@ -7,6 +7,7 @@
 
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -91,6 +92,15 @@ struct ocean_generator
   float4* gcd = nullptr;  // (kz H/|k|, kz^2 H/|k|)
   float2* ge = nullptr;   // H/|k|
   float4* spec = nullptr; // [cascade][2][N]: the Nyquist-row term R
+  // strip-dealt half-spectrum path (slabs of N >= 1024, whole grids of N = 8192 / 16384)
+  bool hslab = false;
+  bool slab = false;  // created by ocean_generator_create_slab (also with ranks == 1)
+  HalfSlab hsl{};
+  float4* h0row = nullptr;                            // slabs: [cascade][N], row y = 0 of every column
+  float4* rm_ab = nullptr;                            // row-major fields [cascade][w][kp] after the exchange
+  float4* rm_de = nullptr;
+  float2* rm_c = nullptr;
+  unsigned char* xbuf = nullptr;                      // internal exchange buffer (ranks == 1, or null send/recv)
   bool profiling = false;
   std::vector<EventPair> pending;
   std::vector<hipEvent_t> pool;
@@ -325,7 +335,59 @@ static hipError_t half_buffers(ocean_generator* g)
   return e;
 }
 
-static int generator_alloc(ocean_generator** out, ocean_fft* fft, int cascades, int rank, int ranks)
+// The strip-dealt path's geometry: STRIPS kept strips dealt S = ceil(STRIPS / ranks) per rank.
+static HalfSlab half_slab_geom(int logn, int rank, int ranks)
+{
+  const int strips = half_strips(logn);
+  HalfSlab h{};
+  h.S = (strips + ranks - 1) / ranks;
+  h.strip0 = rank * h.S;
+  h.nstrips = std::max(0, std::min(h.S, strips - h.strip0));
+  h.w = (1 << logn) / ranks;
+  return h;
+}
+
+static size_t h0_texels(const ocean_generator* g)
+{
+  const size_t full = (size_t)g->fft->n * g->geom.w;  // the full path's column slab (whole grid: N^2)
+  if (g->ranks == 1)
+    return full;
+  const size_t strips = (size_t)g->hsl.nstrips * spectrum_block(g->fft->logn) * g->fft->n;
+  return std::max(full, strips);
+}
+
+static hipError_t hslab_buffers(ocean_generator* g)
+{
+  const int logn = g->fft->logn, C = g->cascades;
+  const size_t rt = half_slab_row_texels(logn, C, g->hsl.w);
+  hipError_t e = hipSuccess;
+  if (!g->rm_ab)
+    e = hipMalloc(&g->rm_ab, rt * sizeof(float4));
+  if (e == hipSuccess && !g->rm_de)
+    e = hipMalloc(&g->rm_de, rt * sizeof(float4));
+  if (e == hipSuccess && !g->rm_c)
+    e = hipMalloc(&g->rm_c, rt * sizeof(float2));
+  if (e == hipSuccess && !g->xbuf)
+    e = hipMalloc(&g->xbuf, (size_t)g->ranks * half_slab_block_bytes(logn, C, g->hsl));
+  if (e == hipSuccess && !g->hs)
+    e = hipMalloc(&g->hs, half_hs_bytes(logn, g->fft->device_cus));
+  if (e == hipSuccess && g->ranks > 1 && !g->h0row)
+    e = hipMalloc(&g->h0row, (size_t)C * g->fft->n * sizeof(float4));
+  return e;
+}
+
+static hipError_t full_buffers(ocean_generator* g)
+{
+  const size_t slab = (size_t)g->fft->n * g->geom.w * g->cascades;
+  hipError_t e = hipSuccess;
+  if (!g->inter)
+    e = hipMalloc(&g->inter, slab * 2 * sizeof(float4));
+  if (e == hipSuccess && rows_need_transpose(g->fft->logn) && !g->scratch)
+    e = hipMalloc(&g->scratch, slab * 2 * sizeof(float4));
+  return e;
+}
+
+static int generator_alloc(ocean_generator** out, ocean_fft* fft, int cascades, int rank, int ranks, bool is_slab)
 {
   auto* g = new ocean_generator();
   g->fft = fft;
@@ -339,20 +401,25 @@ static int generator_alloc(ocean_generator** out, ocean_fft* fft, int cascades, 
     ocean_default_settings(&s);
   const size_t slab = (size_t)fft->n * g->geom.w;  // texels per cascade image slab
   g->half = ranks == 1 && half_spectrum_supported(fft->logn);
-  hipError_t e = hipMalloc(&g->h0, slab * cascades * sizeof(float4));
-  if (e == hipSuccess && !g->half)
-    e = hipMalloc(&g->inter, slab * cascades * 2 * sizeof(float4));
+  // slabs of N >= 1024 and whole grids above the blocked half path's sizes: strip-dealt half spectrum
+  g->slab = is_slab;
+  g->half = g->half && !is_slab;
+  g->hslab = !g->half && half_slab_supported(fft->logn) && (is_slab || fft->logn > 12);
+  g->hsl = half_slab_geom(fft->logn, rank, ranks);
+  hipError_t e = hipMalloc(&g->h0, h0_texels(g) * cascades * sizeof(float4));
+  if (e == hipSuccess && !g->half && !g->hslab)
+    e = full_buffers(g);
   if (e == hipSuccess && g->half)
     e = half_buffers(g);
-  if (e == hipSuccess && rows_need_transpose(fft->logn))
-    e = hipMalloc(&g->scratch, slab * cascades * 2 * sizeof(float4));
+  if (e == hipSuccess && g->hslab)
+    e = hslab_buffers(g);
   if (e == hipSuccess)
     e = hipMalloc(&g->maps, slab * cascades * 2 * sizeof(float4));
   if (e == hipSuccess)
     e = hipMalloc(&g->jac, slab * cascades * sizeof(float));
   // Textures start zeroed like the reference's (Data = nullptr) images.
   if (e == hipSuccess)
-    e = hipMemsetAsync(g->h0, 0, slab * cascades * sizeof(float4), fft->stream);
+    e = hipMemsetAsync(g->h0, 0, h0_texels(g) * cascades * sizeof(float4), fft->stream);
   if (e == hipSuccess)
     e = hipMemsetAsync(g->maps, 0, slab * cascades * 2 * sizeof(float4), fft->stream);
   if (e == hipSuccess)
@@ -374,7 +441,7 @@ int ocean_generator_create(ocean_generator** out, ocean_fft* fft, int cascades)
   *out = nullptr;
   if (cascades < 1 || cascades > OCEAN_MAX_CASCADES)
     return fail(OCEAN_ERR_INVALID, "ocean_generator_create: cascades must be in [1, 64]");
-  return generator_alloc(out, fft, cascades, 0, 1);
+  return generator_alloc(out, fft, cascades, 0, 1, false);
 }
 
 int ocean_generator_create_slab(ocean_generator** out, ocean_fft* fft, int rank, int ranks)
@@ -390,7 +457,7 @@ int ocean_generator_create_slab(ocean_generator** out, ocean_fft* fft, int rank,
     return fail(OCEAN_ERR_INVALID, "ocean_generator_create_slab: N / ranks = " + std::to_string(w) +
                                        " is below this size's minimum slab width " +
                                        std::to_string(slab_min_width(fft->logn)));
-  return generator_alloc(out, fft, 1, rank, ranks);
+  return generator_alloc(out, fft, 1, rank, ranks, true);
 }
 
 int ocean_generator_destroy(ocean_generator* g)
@@ -416,7 +483,8 @@ int ocean_generator_destroy(ocean_generator* g)
     (void)hipFree(g->maps);
   if (g->jac)
     (void)hipFree(g->jac);
-  for (void* p : {(void*)g->gab, (void*)g->gcd, (void*)g->ge, (void*)g->spec, (void*)g->hs})
+  for (void* p : {(void*)g->gab, (void*)g->gcd, (void*)g->ge, (void*)g->spec, (void*)g->hs, (void*)g->h0row,
+                  (void*)g->rm_ab, (void*)g->rm_de, (void*)g->rm_c, (void*)g->xbuf})
     if (p)
       (void)hipFree(p);
   delete g;
@@ -441,11 +509,32 @@ int ocean_generator_generate_spectrum(ocean_generator* g)
   if (!g)
     return fail(OCEAN_ERR_INVALID, "ocean_generator_generate_spectrum: null generator");
   ocean_fft* f = g->fft;
-  const size_t slab = (size_t)f->n * g->geom.w;
+  const size_t slab = h0_texels(g);
   for (int c = 0; c < g->cascades; c++)
   {
     OceanSettings s;
     std::memcpy(&s, &g->settings[c], sizeof(s));
+    if (g->hslab && g->ranks > 1)
+    {
+      // this rank's strips: the regular ones are columns N/2 + strip*B .. (contiguous), the last
+      // global strip is the Nyquist strip x = 0..B-1; plus row 0 of every column (Nyquist-row term)
+      const int B = spectrum_block(f->logn), strips = half_strips(f->logn);
+      const HalfSlab& h = g->hsl;
+      const int nreg = std::max(0, std::min(h.nstrips, strips - 1 - h.strip0));
+      float4* base = g->h0 + (size_t)c * h.nstrips * f->n * B;
+      HIP_TRY(timed(g, 0, [&] {
+                hipError_t e = hipSuccess;
+                if (nreg > 0)
+                  e = launch_generate_spectrum(s, f->n, base, f->stream, f->cus, f->n / 2 + h.strip0 * B, nreg * B);
+                if (e == hipSuccess && nreg < h.nstrips)
+                  e = launch_generate_spectrum(s, f->n, base + (size_t)nreg * f->n * B, f->stream, f->cus, 0, B);
+                if (e == hipSuccess)
+                  e = launch_generate_spectrum_row(s, f->n, g->h0row + (size_t)c * f->n, f->stream);
+                return e;
+              }),
+              "generateSpectrum");
+      continue;
+    }
     HIP_TRY(timed(g, 0, [&] {
               return launch_generate_spectrum(s, f->n, g->h0 + slab * c, f->stream, f->cus, g->geom.x0, g->geom.w);
             }),
@@ -480,7 +569,14 @@ static int generator_columns(ocean_generator* g, float timestep, int update_spec
     fp.c[c].g = s.g;
     fp.c[c].h = s.h;
   }
-  if (g->half)
+  if (g->hslab)
+    HIP_TRY(timed(g, 1, [&] {
+              return launch_half_slab_columns(f->logn, fp, g->hsl, g->ranks, g->h0, g->ranks == 1, g->h0row,
+                                              out ? (void*)out : (void*)g->xbuf, f->twiddles, f->stream, f->cus,
+                                              g->hs, f->device_cus);
+            }),
+            "column pass (half spectrum, strip-dealt)");
+  else if (g->half)
     HIP_TRY(timed(g, 1, [&] {
               return launch_half_columns(f->logn, fp, g->h0, g->gab, g->gcd, g->ge, g->spec, f->twiddles, f->stream,
                                          f->cus, g->hs, f->device_cus);
@@ -503,7 +599,14 @@ static int generator_rows(ocean_generator* g, const float4* in)
   FoamParams foam{};
   for (int c = 0; c < g->cascades; c++)
     foam.displacement[c] = g->settings[c].displacement;
-  if (g->half)
+  if (g->hslab)
+    HIP_TRY(timed(g, 2, [&] {
+              return launch_half_slab_rows(f->logn, g->frame, g->hsl, in ? (const void*)in : (const void*)g->xbuf,
+                                           g->rm_ab, g->rm_de, g->rm_c, g->maps, g->jac, foam, f->twiddles,
+                                           f->stream, f->cus);
+            }),
+            "row pass (half spectrum, strip-dealt)");
+  else if (g->half)
     HIP_TRY(timed(g, 2, [&] {
               return launch_half_rows(f->logn, g->frame, g->gab, g->gcd, g->ge, g->spec, g->maps, g->jac, foam,
                                       f->twiddles, f->stream, f->cus);
@@ -522,17 +625,26 @@ int ocean_generator_set_half_spectrum(ocean_generator* g, int enable)
 {
   if (!g)
     return fail(OCEAN_ERR_INVALID, "ocean_generator_set_half_spectrum: null generator");
-  if (enable && (g->ranks != 1 || !half_spectrum_supported(g->fft->logn)))
-    return fail(OCEAN_ERR_INVALID, "ocean_generator_set_half_spectrum: whole grids of N = 1024 .. 4096 only");
+  const int logn = g->fft->logn;
+  const bool blocked = !g->slab && half_spectrum_supported(logn);
+  const bool dealt = !blocked && half_slab_supported(logn) && (g->slab || logn > 12);
+  if (enable && !blocked && !dealt)
+    return fail(OCEAN_ERR_INVALID, "ocean_generator_set_half_spectrum: N = 1024 .. 16384 only");
   hipError_t e = hipSuccess;
-  if (enable)
+  if (!enable)
+    e = full_buffers(g);
+  else if (blocked)
     e = half_buffers(g);
-  else if (!g->inter)
-    e = hipMalloc(&g->inter, (size_t)g->fft->n * g->geom.w * g->cascades * 2 * sizeof(float4));
+  else
+    e = hslab_buffers(g);
   if (e != hipSuccess)
     return fail(e == hipErrorOutOfMemory ? OCEAN_ERR_OOM : OCEAN_ERR_HIP,
                 std::string("ocean_generator_set_half_spectrum: ") + hipGetErrorString(e));
-  g->half = enable != 0;
+  const bool was_dealt_slab = g->hslab && g->ranks > 1;
+  g->half = enable && blocked;
+  g->hslab = enable && dealt;
+  if (was_dealt_slab != (g->hslab && g->ranks > 1))
+    g->update_spectrum = true;  // a slab's h0 layout changes (strips <-> column slab)
   return OCEAN_OK;
 }
 
@@ -540,17 +652,18 @@ int ocean_generator_frame_bytes(const ocean_generator* g, double per_point[2])
 {
   if (!g || !per_point)
     return fail(OCEAN_ERR_INVALID, "ocean_generator_frame_bytes: null argument");
-  if (g->half)
+  if (g->half || g->hslab)
   {
-    // h0 of the kept columns (half + the Nyquist strip) + 5 complex fields out; 5 fields in, maps + Jacobian
-    const double n = g->fft->n, kept = (n / 2 + 4) / n;
+    // h0 of the kept columns (half + the Nyquist strip) + 5 complex fields out; 5 fields in, maps +
+    // Jacobian; the strip-dealt path also moves the received fields to row-major (40 in + 40 out)
+    const double n = g->fft->n, kept = (n / 2 + spectrum_block(g->fft->logn)) / n;
     per_point[0] = 16.0 * kept + 40.0 * kept;
-    per_point[1] = 40.0 * kept + 36.0;
+    per_point[1] = 40.0 * kept + 36.0 + (g->hslab ? 80.0 * kept : 0.0);
   }
   else
   {
     per_point[0] = 48.0;
-    per_point[1] = 68.0;
+    per_point[1] = 68.0 + (rows_need_transpose(g->fft->logn) ? 64.0 : 0.0);  // B = 1: the tiled transpose
   }
   return OCEAN_OK;
 }
@@ -562,27 +675,33 @@ int ocean_generator_calculate(ocean_generator* g, float timestep, int update_spe
   if (g->ranks != 1)
     return fail(OCEAN_ERR_INVALID, "ocean_generator_calculate: slab generators step with "
                                    "ocean_generator_slab_columns / exchange / ocean_generator_slab_rows");
-  int rc = generator_columns(g, timestep, update_spectrum, g->inter);
-  return rc != OCEAN_OK ? rc : generator_rows(g, g->inter);
+  float4* buf = g->hslab ? nullptr : g->inter;  // null: the strip-dealt path's own exchange buffer
+  int rc = generator_columns(g, timestep, update_spectrum, buf);
+  return rc != OCEAN_OK ? rc : generator_rows(g, buf);
 }
 
 size_t ocean_generator_exchange_bytes(const ocean_generator* g)
 {
-  return g ? (size_t)g->cascades * 2 * g->fft->n * g->geom.w * sizeof(float4) : 0;
+  if (!g)
+    return 0;
+  if (g->hslab)
+    return (size_t)g->ranks * half_slab_block_bytes(g->fft->logn, g->cascades, g->hsl);
+  return (size_t)g->cascades * 2 * g->fft->n * g->geom.w * sizeof(float4);
 }
 
 int ocean_generator_slab_columns(ocean_generator* g, float timestep, int update_spectrum, float* send)
 {
   if (!g)
     return fail(OCEAN_ERR_INVALID, "ocean_generator_slab_columns: null generator");
-  return generator_columns(g, timestep, update_spectrum, send ? reinterpret_cast<float4*>(send) : g->inter);
+  return generator_columns(g, timestep, update_spectrum,
+                           send ? reinterpret_cast<float4*>(send) : (g->hslab ? nullptr : g->inter));
 }
 
 int ocean_generator_slab_rows(ocean_generator* g, const float* recv)
 {
   if (!g)
     return fail(OCEAN_ERR_INVALID, "ocean_generator_slab_rows: null generator");
-  return generator_rows(g, recv ? reinterpret_cast<const float4*>(recv) : g->inter);
+  return generator_rows(g, recv ? reinterpret_cast<const float4*>(recv) : (g->hslab ? nullptr : g->inter));
 }
 
 int ocean_generator_slab_info(const ocean_generator* g, int* rank, int* ranks, int* row0, int* rows)
@@ -690,7 +809,7 @@ float* ocean_generator_initial_spectrum(ocean_generator* g, int c)
 {
   if (!g || c < 0 || c >= g->cascades)
     return nullptr;
-  return reinterpret_cast<float*>(g->h0 + (size_t)g->fft->n * g->geom.w * c);
+  return reinterpret_cast<float*>(g->h0 + h0_texels(g) * c);
 }
 
 int ocean_generator_spectrum_block(const ocean_generator* g)

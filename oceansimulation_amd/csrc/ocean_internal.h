@@ -86,6 +86,19 @@ struct SlabGeom
   int w;
 };
 
+// Half-spectrum strip-dealt layout (slabs of any N >= 1024, and whole grids of N = 8192 / 16384).
+// The STRIPS = N / (2B) + 1 kept strips (columns u >= 0, then the Nyquist strip x = 0..B-1) are
+// dealt S per rank, rank r taking [r S, min(r S + S, STRIPS)). Pass 1 writes block q (rows
+// [q w, q w + w)) of its output as three parts of C * S * w * B elements: gab float4 | gde float4 |
+// gc float2, element ((c S + sl) w + yl) B + b; then the frame's Nyquist-row term [c][2][N] float4.
+struct HalfSlab
+{
+  int strip0;   // first global strip of this rank
+  int nstrips;  // strips this rank transforms (<= S)
+  int S;        // strip slots per block
+  int w;        // rows per block = rows of this rank's row pass
+};
+
 // h0 is stored strip-blocked [xb][y][blk]; blk = spectrum_block(log2 N). x0/width select a column
 // slab (width <= 0: the whole grid).
 int spectrum_block(int logn);
@@ -98,13 +111,29 @@ bool half_spectrum_supported(int logn);
 size_t half_field_texels(int logn);
 // hs (optional): H scratch of half_hs_bytes(logn, hs_blocks) bytes; pass 1 then evolves each texel
 // once (grid capped at hs_blocks) instead of once per field round.
-size_t half_hs_bytes(int logn, int blocks);
+size_t half_hs_bytes(int logn, int blocks);  // also the strip-dealt path's
 hipError_t launch_half_columns(int logn, const FrameParams& fp, const float4* h0, float4* gab, float4* gcd, float2* ge,
                                float4* spec, const float2* tw, hipStream_t stream, int cus, float2* hs = nullptr,
                                int hs_blocks = 0);
 hipError_t launch_half_rows(int logn, const FrameParams& fp, const float4* gab, const float4* gcd, const float2* ge,
                             const float4* rcorr, float4* maps, float* jac, const FoamParams& foam, const float2* tw,
                             hipStream_t stream, int cus, int ablation = 0);
+// Strip-dealt half-spectrum path (HalfSlab): N = 1024 .. 16384. Columns: the Nyquist-row term (from
+// h0 when h0_full, i.e. the whole grid's blocked h0, else from h0row = row 0 of every column) into
+// every destination block of `send`, and pass 1 of the rank's strips into the blocks (ranks *
+// half_slab_block_bytes). Rows: the received blocks -> row-major fields rm_ab / rm_de / rm_c
+// (half_slab_row_texels each), then pass 2 over the rank's w rows with block 0's Nyquist-row term.
+bool half_slab_supported(int logn);
+int half_strips(int logn);
+size_t half_slab_block_bytes(int logn, int cascades, const HalfSlab& h);
+size_t half_slab_row_texels(int logn, int cascades, int w);
+hipError_t launch_generate_spectrum_row(const OceanSettings& s, int n, float4* row, hipStream_t stream);
+hipError_t launch_half_slab_columns(int logn, const FrameParams& fp, const HalfSlab& hsl, int ranks, const float4* h0,
+                                    bool h0_full, const float4* h0row, void* send, const float2* tw,
+                                    hipStream_t stream, int cus, float2* hs, int hs_blocks);
+hipError_t launch_half_slab_rows(int logn, const FrameParams& fp, const HalfSlab& hsl, const void* recv, float4* rm_ab,
+                                 float4* rm_de, float2* rm_c, float4* maps, float* jac, const FoamParams& foam,
+                                 const float2* tw, hipStream_t stream, int cus);
 hipError_t launch_rows_ifft_rows(int logn, int rows, float4* data, const float2* tw, hipStream_t stream, int cus);
 // Standalone EncodeIFFT, column-first through a work image of n_images * N^2 texels (N = 4096).
 bool ifft_colfirst_supported(int logn);

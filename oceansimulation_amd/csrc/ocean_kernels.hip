@@ -42,10 +42,11 @@ namespace oceanfft
 // column pass reads each strip as one contiguous run. The reference keeps this image private
 // (src/Generator.h:86), so its layout is internal.
 __global__ __launch_bounds__(256) void k_generate_spectrum(SpectrumConsts s, int n, int blk, int x0, int width,
-                                                          float4* __restrict__ h0)
+                                                          float4* __restrict__ h0, int rows)
 {
-  // columns [x0, x0 + width) of the N x N spectrum (a rank's column slab; width = n for a whole grid)
-  const int64_t total = (int64_t)width * n;
+  // columns [x0, x0 + width) of rows [0, rows) of the N x N spectrum (a rank's column slab; width =
+  // n for a whole grid; rows = 1: the row y = 0 a slab's Nyquist-row term needs, [x])
+  const int64_t total = (int64_t)width * rows;
   const float dim = (float)n;
   for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < total;
        idx += (int64_t)gridDim.x * blockDim.x)
@@ -53,7 +54,7 @@ __global__ __launch_bounds__(256) void k_generate_spectrum(SpectrumConsts s, int
     // idx enumerates the blocked layout: b fastest, then y, then xb
     const int b = (int)(idx % blk);
     const int64_t rest = idx / blk;
-    const int y = (int)(rest % n), xb = (int)(rest / n);
+    const int y = (int)(rest % rows), xb = (int)(rest / rows);
     const int x = x0 + xb * blk + b;
     float2 a = spectrum_amplitude(s, (float)x, (float)y);
     float2 c = spectrum_amplitude(s, dim - (float)x, dim - (float)y);
@@ -524,7 +525,8 @@ struct HalfCfg
   static constexpr int N = 1 << LOGN;
   static constexpr int B = ColFirstCfg<LOGN>::B;
   static constexpr int STRIPS = N / (2 * B) + 1;  // u in [0, N/2), then the strip of x = 0..B-1
-  static constexpr bool SUPPORTED = B == 4 && ColFirstCfg<LOGN>::SPW == 1;
+  static constexpr bool SUPPORTED = B == 4 && ColFirstCfg<LOGN>::SPW == 1;  // blocked whole-grid path
+  static constexpr bool SLAB_SUPPORTED = ColFirstCfg<LOGN>::SPW == 1;      // strip-dealt path, any B
 };
 
 // Pass 1: per strip of B columns (u >= 0, or the Nyquist strip), three y-iFFT rounds of CPairs:
@@ -534,32 +536,41 @@ struct HalfCfg
 // HS (H scratch): round 0 evolves H once and parks it in a per-workgroup scratch slice (8 B per
 // texel, [m][thread], L2/MALL-resident); rounds 1 and 2 load it back (nt: served by L2, never a
 // stale L1 line from the previous item) instead of re-reading h0 (16 B) and re-evolving.
-template <int LOGN, int LA = 0, int SA = kStream, bool HS = false>
+// SLAB (strip-dealt layout, HalfSlab): this rank transforms global strips [strip0, strip0 +
+// nstrips) and writes its output in destination-block order into `send` (block q = rows
+// [q w, q w + w): gab | gde | gc parts of C * S * w * B elements, element ((c S + sl) w + yl) B + b),
+// so one equal-split all-to-all hands every rank the rows of its row pass. h0 is the whole grid's
+// blocked image when h0_full, else the rank's strips in order ([c][sl][N][B]).
+template <int LOGN, int LA = 0, int SA = kStream, bool HS = false, bool SLAB = false>
 __global__ __launch_bounds__(ColFirstCfg<LOGN>::WG1) void k_cols_half(FrameParams fp, const float4* __restrict__ h0,
                                                                      float4* __restrict__ gab, float4* __restrict__ gde,
                                                                      float2* __restrict__ gc,
                                                                      const float2* __restrict__ tw_glob,
-                                                                     float2* __restrict__ hs)
+                                                                     float2* __restrict__ hs, HalfSlab hsl,
+                                                                     unsigned char* __restrict__ send, int h0_full)
 {
   using S = FftShape<LOGN>;
   using K = ColFirstCfg<LOGN>;
   using HC = HalfCfg<LOGN>;
   constexpr int N = S::N, T = S::T, B = K::B, STRIPS = HC::STRIPS;
-  static_assert(HC::SUPPORTED, "half-spectrum path: B = 4, one strip per item");
+  static_assert(SLAB ? HC::SLAB_SUPPORTED : HC::SUPPORTED, "half-spectrum path: one strip per item (B = 4 unless SLAB)");
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   float2* tw = reinterpret_cast<float2*>(smem);
   void* xch = smem + ((S::TW_ENTRIES * 8 + 15) / 16) * 16;
   load_twiddles<LOGN>(tw, tw_glob);
 
-  const int total = fp.cascades * STRIPS;
+  const int nstrips = SLAB ? hsl.nstrips : STRIPS;
+  const int total = fp.cascades * nstrips;
   const float dim = (float)N;
   for (int item = blockIdx.x; item < total; item += gridDim.x)
   {
     const int b = opaque((int)threadIdx.x) % B;
-    const int c = item / STRIPS, s = item - c * STRIPS;
-    const int xb = s == STRIPS - 1 ? 0 : N / (2 * B) + s;
+    const int c = item / nstrips, s = item - c * nstrips;  // s: the rank's strip index
+    const int sg = SLAB ? hsl.strip0 + s : s;               // global strip
+    const int xb = sg == STRIPS - 1 ? 0 : N / (2 * B) + sg;
     const CascadeFrame f = fp.c[c];
-    const float4* src = h0 + ((size_t)c * (N / B) + xb) * N * B;
+    const float4* src = (!SLAB || h0_full) ? h0 + ((size_t)c * (N / B) + xb) * N * B
+                                           : h0 + ((size_t)c * nstrips + s) * N * B;
     const size_t base = ((size_t)c * STRIPS + s) * N * B;
     const int x = xb * B + b;
     // one field round: (A, B), (D, E) or (C, 0) of the 16 texels, y-iFFT, store
@@ -612,7 +623,22 @@ __global__ __launch_bounds__(ColFirstCfg<LOGN>::WG1) void k_cols_half(FrameParam
 #pragma unroll
       for (int m = 0; m < 16; m++)
       {
-        if (round == 0)
+        if constexpr (SLAB)
+        {
+          // row y = m T + i lies in block q = m T / w (w is a multiple of T), at yl = m T % w + i
+          const size_t part = (size_t)fp.cascades * hsl.S * hsl.w * B;  // elements per part
+          const int q = (m * T) / hsl.w, yl0 = (m * T) % hsl.w;
+          const size_t el = (((size_t)c * hsl.S + s) * hsl.w + yl0) * B;
+          // block = the three parts, then the Nyquist-row term [c][2][N] (half_slab_block_bytes)
+          unsigned char* blk = send + (size_t)q * (part * 40 + (size_t)fp.cascades * 2 * N * 16);
+          if (round == 0)
+            st4<SA>(blk + el * 16, voff, pair_raw(v[m]));
+          else if (round == 1)
+            st4<SA>(blk + part * 16 + el * 16, voff, pair_raw(v[m]));
+          else
+            st2<SA>(blk + part * 32 + el * 8, (i * B + b) * 8, make_float2(v[m].re.x, v[m].im.x));
+        }
+        else if (round == 0)
           st4<SA>(gab + base + m * T * B, voff, pair_raw(v[m]));
         else if (round == 1)
           st4<SA>(gde + base + m * T * B, voff, pair_raw(v[m]));
@@ -639,8 +665,13 @@ __global__ __launch_bounds__(ColFirstCfg<LOGN>::WG1) void k_cols_half(FrameParam
 // (-1)^q Delta_F(u'), Delta_F(u') = F(-N/2, -u') - s_F conj(F(-N/2, u')). Its lanes (the kx
 // factors of pass 2 applied to Delta) form one row spectrum per image, spec[c][img][x] (zero
 // outside 0 < x < N/2); pass 2 adds (-1)^q spec to the lanes it rebuilds at u < 0.
+// h0row (slabs, whose h0 holds only their strips): the row y = 0 texels of every column, [c][x].
+// copies / copy_stride: the strip-dealt path writes the term into every destination block of the
+// exchange buffer, so each frame's row pass reads the term of its own frame (the pipeline keeps two
+// frames in flight).
 __global__ __launch_bounds__(256) void k_half_nyquist(FrameParams fp, int n, int blk, const float4* __restrict__ h0,
-                                                      float4* __restrict__ spec)
+                                                      float4* __restrict__ spec, const float4* __restrict__ h0row,
+                                                      int copies, size_t copy_stride)
 {
   const int total = fp.cascades * n;
   const float dim = (float)n;
@@ -653,8 +684,8 @@ __global__ __launch_bounds__(256) void k_half_nyquist(FrameParams fp, int n, int
       const CascadeFrame f = fp.c[c];
       const int xp = n - x;  // u' = n/2 - x > 0 at column n/2 + u' = n - x; its mirror is x itself
       const float4* hc = h0 + (size_t)c * n * n;
-      const float4 ap = hc[(size_t)(xp / blk) * n * blk + (xp % blk)];  // row y = 0 (v = -n/2)
-      const float4 an = hc[(size_t)(x / blk) * n * blk + (x % blk)];
+      const float4 ap = h0row ? h0row[(size_t)c * n + xp] : hc[(size_t)(xp / blk) * n * blk + (xp % blk)];  // row y = 0 (v = -n/2)
+      const float4 an = h0row ? h0row[(size_t)c * n + x] : hc[(size_t)(x / blk) * n * blk + (x % blk)];
       const KVec qp = make_kvec(xp, 0, dim, f.dk), qn = make_kvec(x, 0, dim, f.dk);
       const float2 hp = evolve(ap, qp.k, f), hn = evolve(an, qn.k, f);
       const float2 dm = make_float2(hn.x - hp.x, hn.y + hp.y);  // Hn - conj(Hp)
@@ -669,8 +700,12 @@ __global__ __launch_bounds__(256) void k_half_nyquist(FrameParams fp, int n, int
       s01 = make_float4((1.0f - kx) * dA.x, (1.0f - kx) * dA.y, -dB.y - kx * dC.x, dB.x - kx * dC.y);
       s23 = make_float4(-(dD.y - kx2 * dC.y), dD.x - kx2 * dC.x, -dE.x + kx * dD.y, -dE.y - kx * dD.x);
     }
-    spec[((size_t)c * 2 + 0) * n + x] = s01;
-    spec[((size_t)c * 2 + 1) * n + x] = s23;
+    for (int k = 0; k < copies; k++)
+    {
+      float4* sp = reinterpret_cast<float4*>(reinterpret_cast<unsigned char*>(spec) + k * copy_stride);
+      sp[((size_t)c * 2 + 0) * n + x] = s01;
+      sp[((size_t)c * 2 + 1) * n + x] = s23;
+    }
   }
 }
 
@@ -687,11 +722,13 @@ __global__ __launch_bounds__(256) void k_half_nyquist(FrameParams fp, int n, int
 // hide: 1.92 -> 1.69 ms at 8 x 4096^2, tools/microbench/genbench).
 // BOTH: one item = both images of its rows (image 0, then image 1), so C is loaded once and kept
 // in VGPRs (16) for image 1 instead of being fetched again by a second item.
-template <int LOGN, int LA = kStream, int SA = kStream, int ABL = 0, int RPW_ = 2, bool BOTH = false>
+// RM (strip-dealt path, after k_half_to_rows): the fields are row-major [c][rows][kp], column u' = u
+// for u in [0, N/2] (u' = N/2: the Nyquist column), and the pass covers `rows` rows (a slab's w).
+template <int LOGN, int LA = kStream, int SA = kStream, int ABL = 0, int RPW_ = 2, bool BOTH = false, bool RM = false>
 __global__ __launch_bounds__(FftShape<LOGN>::T * RPW_) void k_rows_half(
     FrameParams fp, const float4* __restrict__ gab, const float4* __restrict__ gde, const float2* __restrict__ gc,
     const float4* __restrict__ spec, float4* __restrict__ maps, float* __restrict__ jac, FoamParams foam,
-    const float2* __restrict__ tw_glob)
+    const float2* __restrict__ tw_glob, int rows, int kp)
 {
   using S = FftShape<LOGN>;
   using K = ColFirstCfg<LOGN>;
@@ -704,7 +741,7 @@ __global__ __launch_bounds__(FftShape<LOGN>::T * RPW_) void k_rows_half(
   CPair* mir = reinterpret_cast<CPair*>(xch);  // [m < 8][thread]: lanes at -u for the partner
   load_twiddles<LOGN>(tw, tw_glob);
 
-  const int blocks = N / RPW;
+  const int blocks = (RM ? rows : N) / RPW;
   const int b0 = threadIdx.x % B, r0 = (threadIdx.x / B) % RPW, ihi0 = threadIdx.x / (B * RPW);
   const int i20 = threadIdx.x % T, r20 = threadIdx.x / T;
   const int total = fp.cascades * (BOTH ? 1 : 2) * blocks;
@@ -724,7 +761,8 @@ __global__ __launch_bounds__(FftShape<LOGN>::T * RPW_) void k_rows_half(
     const int i = ihi * B + b;
     const int c = cimg >> 1, img = BOTH ? pass : (cimg & 1);
     const float dk = fp.c[c].dk;
-    const size_t base = (size_t)c * STRIPS * N * B;
+    // RM: the item's first row; element (r, u) at r kp + u
+    const size_t base = RM ? ((size_t)c * rows + y0) * kp : (size_t)c * STRIPS * N * B;
     const int y = y0 + r;
     const float sgy = (y & 1) ? -1.0f : 1.0f;  // (-1)^q of the Nyquist-row term
     const float4* sp = spec + (size_t)cimg * N;
@@ -734,7 +772,7 @@ __global__ __launch_bounds__(FftShape<LOGN>::T * RPW_) void k_rows_half(
     for (int m = 0; m < 8; m++)
     {
       const int u = m * T + i;               // >= 0, column x = N/2 + u
-      const int off = ((u / B) * N + y) * B + (u % B);
+      const int off = RM ? r * kp + u : ((u / B) * N + y) * B + (u % B);
       const float kx = (float)u * dk;        // ((float)x - N/2) dk, x - N/2 exact
       const float4 s4 = ld4<0>(sp, (N / 2 - u) * 16);  // the -u column's Nyquist-row term (x = N/2 - u)
       CPair own, neg;
@@ -791,7 +829,7 @@ __global__ __launch_bounds__(FftShape<LOGN>::T * RPW_) void k_rows_half(
       }
       else if (i == 0 && m == 8)
       {
-        const int off = ((N / 2 / B) * N + y) * B;  // Nyquist column: first column of the last strip
+        const int off = RM ? r * kp + N / 2 : ((N / 2 / B) * N + y) * B;  // Nyquist column: first column of the last strip
         const float kx = -(dim / 2.0f) * dk;
         float2 cc;
         if (BOTH && img == 1)
@@ -822,7 +860,7 @@ __global__ __launch_bounds__(FftShape<LOGN>::T * RPW_) void k_rows_half(
     const int i2 = opaque(i20), r2 = RPW == 1 ? 0 : opaque(r20);
     if constexpr (ABL != 2)
       fft_run<LOGN, 0, true>(v, i, r, i2, r2, xch, tw);
-    float4* dst = maps + ((size_t)cimg * N + y0) * N;
+    float4* dst = maps + ((size_t)cimg * (RM ? rows : N) + y0) * N;
     const int woff = ((r2 << LOGN) + i2) * 16;
 #pragma unroll
     for (int m = 0; m < 16; m++)
@@ -832,7 +870,7 @@ __global__ __launch_bounds__(FftShape<LOGN>::T * RPW_) void k_rows_half(
       // displacementMap (Dz, dDx/dx, dDz/dz, dDx/dz) = (re0, im0, re1, im1): Jacobian,
       // spectrum.compute:246-259
       const float lam = foam.displacement[c];
-      float* jb = jac + ((size_t)c * N + y0) * N;
+      float* jb = jac + ((size_t)c * (RM ? rows : N) + y0) * N;
       const int joff = ((r2 << LOGN) + i2) * 4;
 #pragma unroll
       for (int m = 0; m < 16; m++)
@@ -840,6 +878,47 @@ __global__ __launch_bounds__(FftShape<LOGN>::T * RPW_) void k_rows_half(
                 (1.0f + lam * v[m].im.x) * (1.0f + lam * v[m].re.y) - lam * lam * v[m].im.y * v[m].im.y);
     }
     }
+  }
+}
+
+// Strip-dealt half-spectrum fields -> row-major (HalfSlab blocks -> [c][yl][kp], kp = STRIPS * B):
+// the received blocks hold, per source rank r, its strips' w rows as [sl][yl][B] runs; the row pass
+// wants each row's kept columns u' = strip * B + b contiguous. 64 columns x 64 rows per tile through
+// LDS: reads are 64 B-texel runs (one per strip), writes 64-texel row runs. E = float4 (gab, gde) or
+// float2 (gc); part_byte_off = the part's offset inside a block.
+template <typename E>
+__global__ __launch_bounds__(256) void k_half_to_rows(int cascades, int n, int B, HalfSlab hsl,
+                                                      const unsigned char* __restrict__ in, size_t part_byte_off,
+                                                      size_t block_bytes, E* __restrict__ out)
+{
+  __shared__ E tile[64][65];
+  const int strips = n / (2 * B) + 1, kp = strips * B;
+  const int tiles_u = (kp + 63) / 64, tiles_y = hsl.w / 64;
+  const int total = cascades * tiles_u * tiles_y;
+  for (int item = blockIdx.x; item < total; item += gridDim.x)
+  {
+    const int c = item / (tiles_u * tiles_y), t = item % (tiles_u * tiles_y);
+    const int tu = t % tiles_u, ty = t / tiles_u;
+    // read: b fastest, then row, then strip (runs of 64 B texels per strip)
+    for (int k = 0; k < 16; k++)
+    {
+      const int L = k * 256 + threadIdx.x, b = L % B, row = (L / B) & 63, sti = L / (64 * B);
+      const int up = tu * 64 + sti * B + b, strip = up / B;
+      if (up < kp)
+      {
+        const int r = strip / hsl.S, sl = strip % hsl.S;
+        const E* src = reinterpret_cast<const E*>(in + (size_t)r * block_bytes + part_byte_off);
+        tile[sti * B + b][row] = src[(((size_t)c * hsl.S + sl) * hsl.w + ty * 64 + row) * B + b];
+      }
+    }
+    __syncthreads();
+    for (int k = 0; k < 16; k++)
+    {
+      const int L = k * 256 + threadIdx.x, row = L >> 6, col = L & 63;
+      if (tu * 64 + col < kp)
+        out[((size_t)c * hsl.w + ty * 64 + row) * kp + tu * 64 + col] = tile[col][row];
+    }
+    __syncthreads();
   }
 }
 
@@ -1080,7 +1159,7 @@ hipError_t launch_generate_spectrum(const OceanSettings& s, int n, float4* h0, h
                        spectrum_consts(s, n), n, spectrum_block(logn), h0);
   else
     hipLaunchKernelGGL(k_generate_spectrum, dim3((unsigned)blocks), dim3(256), 0, stream, spectrum_consts(s, n), n,
-                       spectrum_block(logn), x0, width, h0);
+                       spectrum_block(logn), x0, width, h0, n);
   return hipGetLastError();
 }
 
@@ -1128,9 +1207,10 @@ size_t half_field_texels(int logn)
   return (n / 8 + 1) * n * 4;  // HalfCfg: STRIPS * N * B per cascade (B = 4)
 }
 
+bool half_slab_supported(int logn);
 size_t half_hs_bytes(int logn, int blocks)
 {
-  return half_spectrum_supported(logn) ? (size_t)blocks * 16 * 1024 * sizeof(float2) : 0;  // WG1 <= 1024
+  return half_slab_supported(logn) ? (size_t)blocks * 16 * 1024 * sizeof(float2) : 0;  // WG1 <= 1024
 }
 
 hipError_t launch_half_columns(int logn, const FrameParams& fp, const float4* h0, float4* gab, float4* gcd, float2* ge,
@@ -1149,7 +1229,8 @@ hipError_t launch_half_columns(int logn, const FrameParams& fp, const float4* h0
       long blocks = ((long)fp.cascades * n + 255) / 256;
       if (blocks > (long)cus * 4)
         blocks = (long)cus * 4;
-      hipLaunchKernelGGL(k_half_nyquist, dim3((unsigned)blocks), dim3(256), 0, stream, fp, n, K::B, h0, spec);
+      hipLaunchKernelGGL(k_half_nyquist, dim3((unsigned)blocks), dim3(256), 0, stream, fp, n, K::B, h0, spec,
+                         (const float4*)nullptr, 1, (size_t)0);
       hipError_t e = hipGetLastError();
       if (e != hipSuccess)
         return e;
@@ -1161,7 +1242,8 @@ hipError_t launch_half_columns(int logn, const FrameParams& fp, const float4* h0
         grid = hs_blocks;
       if (grid < 1)
         return hipErrorInvalidValue;
-      hipLaunchKernelGGL(kern, dim3(grid), dim3(K::WG1), lds, stream, fp, h0, gab, gcd, ge, tw, hs);  // gcd/ge: (D, E) / C
+      hipLaunchKernelGGL(kern, dim3(grid), dim3(K::WG1), lds, stream, fp, h0, gab, gcd, ge, tw, hs, HalfSlab{},
+                         (unsigned char*)nullptr, 1);  // gcd/ge: (D, E) / C
       return hipGetLastError();
     }
   });
@@ -1195,7 +1277,112 @@ hipError_t launch_half_rows(int logn, const FrameParams& fp, const float4* gab, 
                                   : k_rows_half<LOGN, kStream, kStream, 0, 1>;
       const int lds = ((S::TW_ENTRIES * 8 + 15) / 16) * 16 + lds_row_slots<LOGN>(rpw) * 8;
       const int grid = persistent_grid(kern, S::T * rpw, lds, fp.cascades * per_item * (S::N / rpw), cus);
-      hipLaunchKernelGGL(kern, dim3(grid), dim3(S::T * rpw), lds, stream, fp, gab, gcd, ge, rcorr, maps, jac, foam, tw);
+      hipLaunchKernelGGL(kern, dim3(grid), dim3(S::T * rpw), lds, stream, fp, gab, gcd, ge, rcorr, maps, jac, foam, tw,
+                         S::N, 0);
+      return hipGetLastError();
+    }
+  });
+}
+
+// ---- strip-dealt half-spectrum path (slabs, and whole grids of N = 8192 / 16384) ----
+bool half_slab_supported(int logn) { return logn >= 10 && logn <= 14; }
+
+int half_strips(int logn) { return (1 << logn) / (2 * spectrum_block(logn)) + 1; }
+
+// block = gab | gde | gc parts (40 B per element) | the Nyquist-row term [c][2][N] float4
+static size_t half_slab_spec_offset(int logn, int cascades, const HalfSlab& h)
+{
+  return (size_t)40 * cascades * h.S * h.w * spectrum_block(logn);
+}
+
+size_t half_slab_block_bytes(int logn, int cascades, const HalfSlab& h)
+{
+  return half_slab_spec_offset(logn, cascades, h) + (size_t)cascades * 2 * (1 << logn) * sizeof(float4);
+}
+
+size_t half_slab_row_texels(int logn, int cascades, int w)
+{
+  return (size_t)cascades * w * half_strips(logn) * spectrum_block(logn);
+}
+
+hipError_t launch_generate_spectrum_row(const OceanSettings& s, int n, float4* row, hipStream_t stream)
+{
+  // the slab kernel over one row: the same evaluator in the same code, so bit-identical texels
+  hipLaunchKernelGGL(k_generate_spectrum, dim3((n + 255) / 256), dim3(256), 0, stream, spectrum_consts(s, n), n, 1, 0,
+                     n, row, 1);
+  return hipGetLastError();
+}
+
+hipError_t launch_half_slab_columns(int logn, const FrameParams& fp, const HalfSlab& hsl, int ranks, const float4* h0,
+                                    bool h0_full, const float4* h0row, void* send, const float2* tw,
+                                    hipStream_t stream, int cus, float2* hs, int hs_blocks)
+{
+  return with_logn(logn, [&](auto L) -> hipError_t {
+    constexpr int LOGN = decltype(L)::value;
+    if constexpr (!HalfCfg<LOGN>::SLAB_SUPPORTED)
+      return hipErrorInvalidValue;
+    else
+    {
+      using K = ColFirstCfg<LOGN>;
+      using S = FftShape<LOGN>;
+      const int n = S::N;
+      if (hsl.w % S::T != 0 || !hs)
+        return hipErrorInvalidValue;
+      long blocks = ((long)fp.cascades * n + 255) / 256;
+      if (blocks > (long)cus * 4)
+        blocks = (long)cus * 4;
+      const size_t blk = half_slab_block_bytes(LOGN, fp.cascades, hsl);
+      float4* spec = reinterpret_cast<float4*>((unsigned char*)send + half_slab_spec_offset(LOGN, fp.cascades, hsl));
+      hipLaunchKernelGGL(k_half_nyquist, dim3((unsigned)blocks), dim3(256), 0, stream, fp, n, K::B, h0, spec,
+                         h0_full ? (const float4*)nullptr : h0row, ranks, blk);
+      hipError_t e = hipGetLastError();
+      if (e != hipSuccess || hsl.nstrips < 1)  // a rank past the last strip only builds the Nyquist-row term
+        return e;
+      auto kern = k_cols_half<LOGN, 0, kStream, true, true>;
+      const int lds = ((S::TW_ENTRIES * 8 + 15) / 16) * 16 + K::LDS1;
+      int grid = persistent_grid(kern, K::WG1, lds, fp.cascades * hsl.nstrips, cus);
+      if (grid > hs_blocks)
+        grid = hs_blocks;
+      hipLaunchKernelGGL(kern, dim3(grid), dim3(K::WG1), lds, stream, fp, h0, (float4*)nullptr, (float4*)nullptr,
+                         (float2*)nullptr, tw, hs, hsl, (unsigned char*)send, h0_full ? 1 : 0);
+      return hipGetLastError();
+    }
+  });
+}
+
+hipError_t launch_half_slab_rows(int logn, const FrameParams& fp, const HalfSlab& hsl, const void* recv, float4* rm_ab,
+                                 float4* rm_de, float2* rm_c, float4* maps, float* jac, const FoamParams& foam,
+                                 const float2* tw, hipStream_t stream, int cus)
+{
+  return with_logn(logn, [&](auto L) -> hipError_t {
+    constexpr int LOGN = decltype(L)::value;
+    if constexpr (!HalfCfg<LOGN>::SLAB_SUPPORTED)
+      return hipErrorInvalidValue;
+    else
+    {
+      using S = FftShape<LOGN>;
+      const int n = S::N, B = spectrum_block(LOGN), C = fp.cascades;
+      if (hsl.w % 64 != 0)
+        return hipErrorInvalidValue;
+      const size_t part = (size_t)C * hsl.S * hsl.w * B, blk = half_slab_block_bytes(LOGN, C, hsl);
+      const float4* spec = reinterpret_cast<const float4*>((const unsigned char*)recv +
+                                                           half_slab_spec_offset(LOGN, C, hsl));  // block 0's copy
+      const int kp = half_strips(LOGN) * B;
+      const int tiles = C * ((kp + 63) / 64) * (hsl.w / 64);
+      const int tgrid = tiles < cus * 4 ? tiles : cus * 4;
+      const unsigned char* in = (const unsigned char*)recv;
+      hipLaunchKernelGGL(k_half_to_rows<float4>, dim3(tgrid), dim3(256), 0, stream, C, n, B, hsl, in, (size_t)0, blk, rm_ab);
+      hipLaunchKernelGGL(k_half_to_rows<float4>, dim3(tgrid), dim3(256), 0, stream, C, n, B, hsl, in, part * 16, blk, rm_de);
+      hipLaunchKernelGGL(k_half_to_rows<float2>, dim3(tgrid), dim3(256), 0, stream, C, n, B, hsl, in, part * 32, blk, rm_c);
+      hipError_t e = hipGetLastError();
+      if (e != hipSuccess)
+        return e;
+      constexpr int RPW = S::T >= 1024 ? 1 : 2;
+      auto kern = k_rows_half<LOGN, kStream, kStream, 0, RPW, true, true>;
+      const int lds = ((S::TW_ENTRIES * 8 + 15) / 16) * 16 + lds_row_slots<LOGN>(RPW) * 8;
+      const int grid = persistent_grid(kern, S::T * RPW, lds, C * (hsl.w / RPW), cus);
+      hipLaunchKernelGGL(kern, dim3(grid), dim3(S::T * RPW), lds, stream, fp, rm_ab, rm_de, rm_c, spec, maps, jac, foam,
+                         tw, hsl.w, kp);
       return hipGetLastError();
     }
   });

@@ -40,7 +40,22 @@ class SlabGenerator:
         self.rank, self.ranks = rank, ranks
         self.rows = self.n // ranks
         self.row0 = rank * self.rows
-        self.exchange_bytes = int(lib().ocean_generator_exchange_bytes(self._h))
+
+    @property
+    def exchange_bytes(self) -> int:
+        """Bytes of this rank's send (and receive) buffer: ranks equal blocks."""
+        return int(lib().ocean_generator_exchange_bytes(self._h))
+
+    def set_half_spectrum(self, enable: bool) -> None:
+        """Strip-dealt half-spectrum path (default for N >= 1024) or the full-spectrum path; the
+        exchange size changes with it and h0 is re-seeded at the next frame."""
+        check(lib().ocean_generator_set_half_spectrum(self._h, 1 if enable else 0), "ocean_generator_set_half_spectrum")
+
+    def frame_bytes(self):
+        """Algorithmic HBM bytes per point of the column pass and the row pass (transposes included)."""
+        b = (ctypes.c_double * 2)()
+        check(lib().ocean_generator_frame_bytes(self._h, b), "ocean_generator_frame_bytes")
+        return b[0], b[1]
 
     @property
     def handle(self):

@@ -225,16 +225,19 @@ def test_calculate_ocean_every_kernel_shape(ocean, oracle, n):
     _frame_check(gen.height_map_host(0), gen.displacement_map_host(0), gen.jacobian_map_host(0), ref)
 
 
-def test_calculate_ocean_8192_vs_float64(ocean, oracle):
-    """A full frame at 8192^2 (blocks of 2 texels, KEEP 0, 4-stage transforms): h0 and the packed
-    spectra from the oracle, their transform in float64 (N^2 ifft2(ifftshift), the meaning of
-    src/FFTCalculator.cpp:73-114; the oracle's own fp32 radix-2 is 6e-7 from it at 4096), foam from
-    the float64 maps (spectrum.compute:246-259)."""
+@pytest.mark.parametrize("half", [True, False])
+def test_calculate_ocean_8192_vs_float64(ocean, oracle, half):
+    """A full frame at 8192^2 (blocks of 2 texels, 4-stage transforms; half: the strip-dealt
+    half-spectrum path with its transposes, else the full-spectrum path with KEEP 0): h0 and the
+    packed spectra from the oracle, their transform in float64 (N^2 ifft2(ifftshift), the meaning
+    of src/FFTCalculator.cpp:73-114; the oracle's own fp32 radix-2 is 6e-7 from it at 4096), foam
+    from the float64 maps (spectrum.compute:246-259)."""
     import numpy_ref as R
 
     n, L = 8192, 61.0
     fft = ocean.FFTCalculator(n)
     gen = ocean.Generator(fft, 1)
+    gen.set_half_spectrum(half)
     ocean.apply_settings(gen.GetOceanSettings(0), planeSize=L)
     gen.CalculateOcean(1.25)
     s = oracle.default_settings(planeSize=L)
@@ -409,16 +412,20 @@ def _slab_run(ocean, n, ranks, steps, settings):
     return h, d, j
 
 
-@pytest.mark.parametrize("n,ranks", [(512, 2), (256, 2), (256, 4), (1024, 8), (4096, 4), (2048, 16)])
+@pytest.mark.parametrize("n,ranks", [(512, 2), (256, 2), (256, 4), (1024, 1), (1024, 8), (4096, 4), (2048, 16),
+                                     (1024, 16)])
 def test_slab_decomposition_matches_whole_grid(ocean, n, ranks):
     """Rank-split column pass + all-to-all + rank-split row pass == the single-GPU generator,
-    bit for bit (the same kernels compute every column and every row)."""
+    bit for bit. N >= 1024: the strip-dealt half-spectrum path (strips dealt over the ranks, the
+    fields moved to row-major after the exchange) against the whole grid's blocked half-spectrum
+    path; (1024, 16) leaves the last rank without strips. N < 1024: the full-spectrum kernels."""
     settings = dict(planeSize=17.0)
     steps = [0.25, 1.0 / 60.0]
     h, d, j = _slab_run(ocean, n, ranks, steps, settings)
     fft = ocean.FFTCalculator(n)
     gen = ocean.Generator(fft, 1)
-    gen.set_half_spectrum(False)  # slabs run the full-spectrum kernels (whole grids 1024..4096 default to half)
+    if n < 1024:
+        gen.set_half_spectrum(False)  # what slabs below 1024 run
     ocean.apply_settings(gen.GetOceanSettings(0), **settings)
     for dt in steps:
         gen.CalculateOcean(dt)
@@ -430,7 +437,8 @@ def test_slab_decomposition_matches_whole_grid(ocean, n, ranks):
 def _whole_grid_frames(ocean, n, steps, settings):
     fft = ocean.FFTCalculator(n)
     gen = ocean.Generator(fft, 1)
-    gen.set_half_spectrum(False)  # the kernels the slabs run
+    if n < 1024:
+        gen.set_half_spectrum(False)  # the formulation the slabs run
     ocean.apply_settings(gen.GetOceanSettings(0), **settings)
     frames = []
     for dt in steps:
@@ -516,8 +524,9 @@ def test_slab_rejects_too_narrow_slabs(ocean):
         SlabGenerator(ocean.FFTCalculator(256), 0, 3)  # not a power of two
 
 
-def test_slab_small_grid_vs_oracle(ocean, oracle):
-    n, ranks = 256, 4
+@pytest.mark.parametrize("n,ranks", [(256, 4), (1024, 4)])
+def test_slab_small_grid_vs_oracle(ocean, oracle, n, ranks):
+    """Slab frames (full spectrum at 256, strip-dealt half spectrum at 1024) against the oracle."""
     h, d, j = _slab_run(ocean, n, ranks, [1.0], dict(planeSize=5.0))
     ref = oracle.OracleGenerator(n, oracle.default_settings(planeSize=5.0))
     ref.calculate_ocean(1.0)
@@ -538,7 +547,8 @@ def _sampled_idft(field, pts):
 
 @pytest.mark.slow
 def test_generator_16384_transpose_path_sampled(ocean):
-    """N = 16384 (B = 1: column pass + tiled transpose + row pass): sampled outputs against a
+    """N = 16384 (B = 1: the strip-dealt half-spectrum path on one GPU: column pass of the kept
+    strips, tiled transposes of the five fields to row-major, row pass): sampled outputs against a
     float64 direct 2D iDFT of the GPU's own h0, evolved in float64."""
     n = 16384
     fft = ocean.FFTCalculator(n)

@@ -883,40 +883,59 @@ __global__ __launch_bounds__(FftShape<LOGN>::T * RPW_) void k_rows_half(
 
 // Strip-dealt half-spectrum fields -> row-major (HalfSlab blocks -> [c][yl][kp], kp = STRIPS * B):
 // the received blocks hold, per source rank r, its strips' w rows as [sl][yl][B] runs; the row pass
-// wants each row's kept columns u' = strip * B + b contiguous. 64 columns x 64 rows per tile through
-// LDS: reads are 64 B-texel runs (one per strip), writes 64-texel row runs. E = float4 (gab, gde) or
-// float2 (gc); part_byte_off = the part's offset inside a block.
-template <typename E>
-__global__ __launch_bounds__(256) void k_half_to_rows(int cascades, int n, int B, HalfSlab hsl,
+// wants each row's kept columns u' = strip * B + b contiguous. 128 columns x 32 rows per tile
+// through LDS: reads are 32 B-texel runs (one per strip), writes 128-texel row runs. E = float4
+// (gab, gde) or float2 (gc); part_byte_off = the part's offset inside a block.
+template <typename E, int B>
+__global__ __launch_bounds__(256) void k_half_to_rows(int cascades, int n, HalfSlab hsl,
                                                       const unsigned char* __restrict__ in, size_t part_byte_off,
                                                       size_t block_bytes, E* __restrict__ out)
 {
-  __shared__ E tile[64][65];
+  // 128 columns x 32 rows: 2-KiB row runs on the write side, 32 B-texel runs per strip on the read
+  // side (4.5 TB/s for float4 at N = 16384, against 4.0 for 64 x 64; tools/microbench/transbench)
+  constexpr int TU = 128, TY = 32;
+  __shared__ E tile[TU][TY + 1];
   const int strips = n / (2 * B) + 1, kp = strips * B;
-  const int tiles_u = (kp + 63) / 64, tiles_y = hsl.w / 64;
-  const int total = cascades * tiles_u * tiles_y;
+  // tiles never straddle two source blocks: (c, source rank r, column tile within r's strips, row tile)
+  const int ranks = (strips + hsl.S - 1) / hsl.S;
+  const int tiles_r = (hsl.S * B + TU - 1) / TU, tiles_y = hsl.w / TY;
+  const int total = cascades * ranks * tiles_r * tiles_y;
   for (int item = blockIdx.x; item < total; item += gridDim.x)
   {
-    const int c = item / (tiles_u * tiles_y), t = item % (tiles_u * tiles_y);
-    const int tu = t % tiles_u, ty = t / tiles_u;
-    // read: b fastest, then row, then strip (runs of 64 B texels per strip)
+    int t = item;
+    const int tr = t % tiles_r;
+    t /= tiles_r;
+    const int r = t % ranks;
+    t /= ranks;
+    const int ty = t % tiles_y, c = t / tiles_y;
+    const int u0 = r * hsl.S * B + tr * TU;  // the tile's first column u'
+    const int ulim = min(kp, (r + 1) * hsl.S * B);
+    const E* src = reinterpret_cast<const E*>(in + (size_t)r * block_bytes + part_byte_off) +
+                   (((size_t)c * hsl.S + tr * (TU / B)) * hsl.w + ty * TY) * B;
+    // read: b fastest, then row, then strip; all 16 loads are issued before the first LDS write
+    E v[16];
+#pragma unroll
     for (int k = 0; k < 16; k++)
     {
-      const int L = k * 256 + threadIdx.x, b = L % B, row = (L / B) & 63, sti = L / (64 * B);
-      const int up = tu * 64 + sti * B + b, strip = up / B;
-      if (up < kp)
-      {
-        const int r = strip / hsl.S, sl = strip % hsl.S;
-        const E* src = reinterpret_cast<const E*>(in + (size_t)r * block_bytes + part_byte_off);
-        tile[sti * B + b][row] = src[(((size_t)c * hsl.S + sl) * hsl.w + ty * 64 + row) * B + b];
-      }
+      const int L = k * 256 + threadIdx.x, b = L % B, row = (L / B) % TY, sti = L / (TY * B);
+      // unconditional loads (a guarded load per element serialises them): columns past the rank's
+      // strips read the tile's first element instead, and are not stored
+      const bool in_range = u0 + sti * B + b < ulim;
+      v[k] = src[in_range ? ((size_t)sti * hsl.w + row) * B + b : 0];
+    }
+#pragma unroll
+    for (int k = 0; k < 16; k++)
+    {
+      const int L = k * 256 + threadIdx.x, b = L % B, row = (L / B) % TY, sti = L / (TY * B);
+      tile[sti * B + b][row] = v[k];
     }
     __syncthreads();
+#pragma unroll
     for (int k = 0; k < 16; k++)
     {
-      const int L = k * 256 + threadIdx.x, row = L >> 6, col = L & 63;
-      if (tu * 64 + col < kp)
-        out[((size_t)c * hsl.w + ty * 64 + row) * kp + tu * 64 + col] = tile[col][row];
+      const int L = k * 256 + threadIdx.x, row = L / TU, col = L % TU;
+      if (u0 + col < ulim)
+        out[((size_t)c * hsl.w + ty * TY + row) * kp + u0 + col] = tile[col][row];
     }
     __syncthreads();
   }
@@ -1362,18 +1381,19 @@ hipError_t launch_half_slab_rows(int logn, const FrameParams& fp, const HalfSlab
     {
       using S = FftShape<LOGN>;
       const int n = S::N, B = spectrum_block(LOGN), C = fp.cascades;
-      if (hsl.w % 64 != 0)
+      if (hsl.w % 32 != 0)
         return hipErrorInvalidValue;
       const size_t part = (size_t)C * hsl.S * hsl.w * B, blk = half_slab_block_bytes(LOGN, C, hsl);
       const float4* spec = reinterpret_cast<const float4*>((const unsigned char*)recv +
                                                            half_slab_spec_offset(LOGN, C, hsl));  // block 0's copy
       const int kp = half_strips(LOGN) * B;
-      const int tiles = C * ((kp + 63) / 64) * (hsl.w / 64);
+      const int tiles = C * ((half_strips(LOGN) + hsl.S - 1) / hsl.S) * ((hsl.S * B + 127) / 128) * (hsl.w / 32);
       const int tgrid = tiles < cus * 4 ? tiles : cus * 4;
       const unsigned char* in = (const unsigned char*)recv;
-      hipLaunchKernelGGL(k_half_to_rows<float4>, dim3(tgrid), dim3(256), 0, stream, C, n, B, hsl, in, (size_t)0, blk, rm_ab);
-      hipLaunchKernelGGL(k_half_to_rows<float4>, dim3(tgrid), dim3(256), 0, stream, C, n, B, hsl, in, part * 16, blk, rm_de);
-      hipLaunchKernelGGL(k_half_to_rows<float2>, dim3(tgrid), dim3(256), 0, stream, C, n, B, hsl, in, part * 32, blk, rm_c);
+      constexpr int KB = ColFirstCfg<LOGN>::B;
+      hipLaunchKernelGGL((k_half_to_rows<float4, KB>), dim3(tgrid), dim3(256), 0, stream, C, n, hsl, in, (size_t)0, blk, rm_ab);
+      hipLaunchKernelGGL((k_half_to_rows<float4, KB>), dim3(tgrid), dim3(256), 0, stream, C, n, hsl, in, part * 16, blk, rm_de);
+      hipLaunchKernelGGL((k_half_to_rows<float2, KB>), dim3(tgrid), dim3(256), 0, stream, C, n, hsl, in, part * 32, blk, rm_c);
       hipError_t e = hipGetLastError();
       if (e != hipSuccess)
         return e;

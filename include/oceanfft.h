@@ -121,16 +121,21 @@ float* ocean_generator_displacement_map(ocean_generator* gen, int cascade);
 float* ocean_generator_jacobian_map(ocean_generator* gen, int cascade);
 /* The initialSpectrum image (private in the reference, src/Generator.h:86): (h0(k), conj(h0(-k)))
  * per texel, stored strip-blocked: texel (x, y) at index ((x / B) * N + y) * B + (x % B) with
- * B = ocean_generator_spectrum_block(gen), so the column pass streams it contiguously. */
+ * B = ocean_generator_spectrum_block(gen), so the column pass streams it contiguously. Slab
+ * generators hold only their own columns: the column slab (full spectrum), or their kept strips in
+ * order, each N * B texels (half spectrum; the Nyquist strip x = 0 .. B-1 last). */
 float* ocean_generator_initial_spectrum(ocean_generator* gen, int cascade);
 int ocean_generator_spectrum_block(const ocean_generator* gen);
 
-/* Frame path of a whole-grid generator. Half spectrum (default where supported: N = 1024 .. 4096,
- * ranks == 1): the column pass transforms only the u >= 0 half of the columns, as 5 complex fields
- * (H, kz H, H/|k|, kz H/|k|, kz^2 H/|k|), and the row pass rebuilds the reference's 4 packed lanes
- * from Hermitian symmetry plus the reference's Nyquist-row term (84 HBM bytes per point instead of
- * 116). enable = 0 selects the full-spectrum path (both give the reference's results
- * within rounding). */
+/* Frame path. Half spectrum (default for N = 1024 .. 16384): the column pass transforms only the
+ * u >= 0 half of the columns, as 5 complex fields (H, kz H, H/|k|, kz H/|k|, kz^2 H/|k|), and the
+ * row pass rebuilds the reference's 4 packed lanes from Hermitian symmetry plus the reference's
+ * Nyquist-row term. Whole grids of 1024 .. 4096 use the blocked layout (84 HBM bytes
+ * per point instead of 116); slab generators, and whole grids of 8192 / 16384, deal the kept
+ * strips over the ranks and move the received fields to row-major before the row pass (124 bytes
+ * per point; exchange 20 bytes per point instead of 32). enable = 0 selects the full-spectrum path
+ * (both give the reference's results within rounding). On a slab generator the switch changes
+ * ocean_generator_exchange_bytes and re-seeds h0 at the next frame. */
 int ocean_generator_set_half_spectrum(ocean_generator* gen, int enable);
 /* Algorithmic HBM bytes per height-field point of the column pass [0] and the row pass [1] of the
  * generator's current path (what bench.py prices the roofline with). */
@@ -139,7 +144,9 @@ int ocean_generator_frame_bytes(const ocean_generator* gen, double per_point[2])
 /* ---- slab decomposition of one grid over several GPUs ------------------------------------- */
 /* One N x N cascade split over `ranks` GPUs (power of two <= 16), this process being `rank`: the
  * column pass works on columns [rank*w, rank*w + w), the row pass on rows [rank*w, rank*w + w),
- * w = N / ranks (the reference runs everything on one device). A frame is:
+ * w = N / ranks (the reference runs everything on one device). With the half spectrum
+ * (default for N >= 1024) the column pass works on the rank's share of the kept strips instead of
+ * the column slab. A frame is:
  *   ocean_generator_slab_columns(gen, dt, update, send)  time += dt, h0 if needed, evolve + y iFFT
  *   all-to-all with equal splits of ocean_generator_exchange_bytes(gen) / ranks bytes: the block at
  *     send + q * bytes/ranks goes to rank q and arrives at recv + rank_src * bytes/ranks (RCCL)

@@ -158,6 +158,12 @@ size_t ocean_generator_exchange_bytes(const ocean_generator* gen);
 int ocean_generator_slab_columns(ocean_generator* gen, float timestep, int update_spectrum, float* send);
 int ocean_generator_slab_rows(ocean_generator* gen, const float* recv);
 int ocean_generator_slab_info(const ocean_generator* gen, int* rank, int* ranks, int* row0, int* rows);
+/* Host-only geometry of a one-cascade slab generator (no device needed): out = {first kept strip,
+ * strips this rank transforms, strip slots per block, rows per block (N / ranks), exchange block
+ * bytes, exchange bytes} for the half-spectrum path (half != 0: the STRIPS = N / (2B) + 1 kept
+ * strips dealt ceil(STRIPS / ranks) per rank), or {first column, columns, 0, rows, block bytes,
+ * exchange bytes} for the full-spectrum path. */
+int ocean_slab_layout(size_t texture_size, int rank, int ranks, int half, int64_t out[6]);
 
 /* ---- instrumentation (bench) ------------------------------------------------------------- */
 /* When enabled, each kernel launch of the generator is bracketed by HIP events on its stream. */

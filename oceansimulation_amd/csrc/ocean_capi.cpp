@@ -704,6 +704,33 @@ int ocean_generator_slab_rows(ocean_generator* g, const float* recv)
   return generator_rows(g, recv ? reinterpret_cast<const float4*>(recv) : (g->hslab ? nullptr : g->inter));
 }
 
+int ocean_slab_layout(size_t texture_size, int rank, int ranks, int half, int64_t out[6])
+{
+  int logn = 0;
+  while (logn < 15 && ((size_t)1 << logn) < texture_size)
+    logn++;
+  if (!out || ((size_t)1 << logn) != texture_size || logn < 4 || logn > 14 || ranks < 1 || ranks > 16 ||
+      (ranks & (ranks - 1)) != 0 || rank < 0 || rank >= ranks)
+    return fail(OCEAN_ERR_INVALID, "ocean_slab_layout: N a power of two in [16, 16384], ranks a power of two <= 16");
+  if (half && !half_slab_supported(logn))
+    return fail(OCEAN_ERR_INVALID, "ocean_slab_layout: the half-spectrum path needs N >= 1024");
+  const int n = 1 << logn, w = n / ranks;
+  if (half)
+  {
+    const HalfSlab h = half_slab_geom(logn, rank, ranks);
+    const int64_t blk = (int64_t)half_slab_block_bytes(logn, 1, h);
+    const int64_t v[6] = {h.strip0, h.nstrips, h.S, h.w, blk, blk * ranks};
+    std::memcpy(out, v, sizeof(v));
+  }
+  else
+  {
+    const int64_t blk = (int64_t)2 * w * w * sizeof(float4);
+    const int64_t v[6] = {(int64_t)rank * w, w, 0, w, blk, blk * ranks};
+    std::memcpy(out, v, sizeof(v));
+  }
+  return OCEAN_OK;
+}
+
 int ocean_generator_slab_info(const ocean_generator* g, int* rank, int* ranks, int* row0, int* rows)
 {
   if (!g)

@@ -107,6 +107,14 @@ class SlabGenerator:
             pass
 
 
+def slab_layout(n: int, rank: int, ranks: int, half: bool = True):
+    """ocean_slab_layout: (first strip, strips, strip slots per block, rows, block bytes, exchange
+    bytes) of a one-cascade slab generator; host-only, no device needed."""
+    out = (ctypes.c_int64 * 6)()
+    check(lib().ocean_slab_layout(n, rank, ranks, 1 if half else 0, out), "ocean_slab_layout")
+    return tuple(int(v) for v in out)
+
+
 def block_moves(ranks: int, nbytes: int):
     """(src_rank, src_offset, dst_rank, dst_offset, size) of the equal-split all-to-all."""
     blk = nbytes // ranks

@@ -123,3 +123,51 @@ def test_waveapp_headless_rejects_bad_arguments():
     for bad in (["--bogus", "1"], ["--edit", "3:7.U_10=1"], ["--freeze", "x"], ["--n"]):
         r = subprocess.run([exe, *bad], capture_output=True, text=True, timeout=60)
         assert r.returncode == 2, (bad, r.returncode, r.stderr)
+
+
+def _half_slab_restated(n, rank, ranks):
+    """DESIGN.md §3 strip dealing, restated: B = 4 / 2 / 1 texels per strip at N <= 4096 / 8192 /
+    16384; STRIPS = N/(2B) + 1 kept strips (u >= 0, then the Nyquist strip), ceil(STRIPS/ranks) per
+    rank; a block = gab | gde | gc parts (40 B per element) + the Nyquist-row term (2N float4)."""
+    b = 4 if n <= 4096 else (2 if n == 8192 else 1)
+    strips = n // (2 * b) + 1
+    s = -(-strips // ranks)
+    strip0 = rank * s
+    nstrips = max(0, min(s, strips - strip0))
+    w = n // ranks
+    blk = 40 * s * w * b + 2 * n * 16
+    return strip0, nstrips, s, w, blk, blk * ranks
+
+
+@pytest.mark.parametrize("n", [1024, 2048, 4096, 8192, 16384])
+@pytest.mark.parametrize("ranks", [1, 2, 4, 8, 16])
+def test_half_slab_layout_deals_every_strip_once(capi, n, ranks):
+    """The strip-dealt path's geometry (host logic, no device): the ABI's layout equals the
+    restatement, every kept strip is transformed by exactly one rank, and the blocks tile the
+    exchange buffer."""
+    from oceansimulation_amd.slab import slab_layout
+
+    seen = []
+    for r in range(ranks):
+        lay = slab_layout(n, r, ranks, half=True)
+        assert lay == _half_slab_restated(n, r, ranks)
+        seen.extend(range(lay[0], lay[0] + lay[1]))
+        assert lay[3] % 32 == 0  # whole transpose row tiles
+    b = 4 if n <= 4096 else (2 if n == 8192 else 1)
+    assert seen == list(range(n // (2 * b) + 1))
+    full = slab_layout(n, 0, ranks, half=False)
+    assert full[5] == 32 * n * (n // ranks)  # the full spectrum's 32 B per point
+    assert slab_layout(n, 0, ranks)[5] < 0.7 * full[5]  # half spectrum: ~20 B per point + slot padding + the term
+
+
+def test_slab_layout_rejects_bad_geometry(capi):
+    from oceansimulation_amd.capi import OceanError
+    from oceansimulation_amd.slab import slab_layout
+
+    with pytest.raises(OceanError):
+        slab_layout(1000, 0, 2)
+    with pytest.raises(OceanError):
+        slab_layout(4096, 0, 3)
+    with pytest.raises(OceanError):
+        slab_layout(512, 0, 2, half=True)
+    assert slab_layout(512, 1, 2, half=False)[:2] == (256, 256)

@@ -190,6 +190,17 @@ struct ColCfg
 // Block -> work-slot map that gives blocks b and b+8 (same XCD under round-robin placement)
 // adjacent strips, so both 64-B halves of a 128-B line meet in one L2. Speed only; any placement
 // is correct.
+// Generalisation: GROUP consecutive work slots on blocks b, b+8, ..., b+8(GROUP-1) (one XCD).
+template <int GROUP>
+__device__ __forceinline__ int xcd_group_slot(int b, int G)
+{
+  if (G % (8 * GROUP) != 0)
+    return b;
+  const int xcd = b & 7, j = b >> 3;
+  const int grp = xcd * (G / (8 * GROUP)) + j / GROUP;
+  return GROUP * grp + j % GROUP;
+}
+
 __device__ __forceinline__ int xcd_pair_slot(int b, int G)
 {
   if ((G & 15) != 0)
@@ -368,7 +379,10 @@ __global__ __launch_bounds__(ColFirstCfg<LOGN>::WG1) void k_cols_evolve(
 // it (256-B runs in, row-major rows out, no Jacobian). Measured patterns (profiles/
 // r01_colbench_patterns.log): strided read + contiguous write 3.4 TB/s, against 2.1-2.4 TB/s for
 // the in-place column pass that reads and writes 64-B pieces.
-template <int LOGN>
+// LA: default-policy loads. Each 128-B line is read half by this block and half by the block of
+// the adjacent strip (same XCD, same time); streamed (nt) loads lost the line before the partner's
+// read: 1.38 -> 1.12 ms per 8 images (tools/microbench/ifftbench; grouping 4 or 8 strips: no gain).
+template <int LOGN, int LA = 0, int GROUP = 2>
 __global__ __launch_bounds__(ColFirstCfg<LOGN>::WG1) void k_cols_to_blocks(int images, const float4* __restrict__ src_images,
                                                                           float4* __restrict__ work,
                                                                           const float2* __restrict__ tw_glob)
@@ -384,7 +398,7 @@ __global__ __launch_bounds__(ColFirstCfg<LOGN>::WG1) void k_cols_to_blocks(int i
   const int strips = N / B;
   const int total = images * strips;
   // adjacent strips (the two 64-B halves of each 128-B line) on blocks b, b+8: one XCD, one L2
-  for (int item = xcd_pair_slot(blockIdx.x, gridDim.x); item < total; item += gridDim.x)
+  for (int item = xcd_group_slot<GROUP>(blockIdx.x, gridDim.x); item < total; item += gridDim.x)
   {
     const int tid = opaque((int)threadIdx.x);
     const int b = tid % B, i = (tid / B) % T;
@@ -395,7 +409,7 @@ __global__ __launch_bounds__(ColFirstCfg<LOGN>::WG1) void k_cols_to_blocks(int i
     CPair v[16];
 #pragma unroll
     for (int m = 0; m < 16; m++)
-      v[m] = to_pair(ld4<kStream>(src + ((size_t)(((m + 8) & 15) * T) << LOGN), voff));  // fftShift on y
+      v[m] = to_pair(ld4<LA>(src + ((size_t)(((m + 8) & 15) * T) << LOGN), voff));  // fftShift on y
     fft_run<LOGN, K::C1, true>(v, i, b, xch, tw);
     float4* dst = work + ((size_t)img << (2 * LOGN)) + (size_t)xb * N * B;
     const int soff = (i * B + b) * 16;
@@ -1286,8 +1300,12 @@ hipError_t launch_half_rows(int logn, const FrameParams& fp, const float4* gab, 
       // item (C loaded by both items of a row block)
       constexpr int R4 = K::RPW2;
       const int rpw = ablation == 4 ? R4 : ablation == 5 ? 1 : 2;
-      const int per_item = ablation == 0 ? 1 : 2;
-      auto kern = ablation == 0   ? k_rows_half<LOGN, kStream, kStream, 0, 2, true>
+      const int per_item = (ablation == 0 || ablation == 7) ? 1 : 2;
+      // production loads use the default policy: C's 128-B lines are shared by the paired items
+      // (xcd_pair_slot) and streamed loads lost them before the partner's read (-5 %,
+      // tools/microbench/halfbench); 7: streamed loads
+      auto kern = ablation == 0   ? k_rows_half<LOGN, 0, kStream, 0, 2, true>
+                  : ablation == 7 ? k_rows_half<LOGN, kStream, kStream, 0, 2, true>
                   : ablation == 6 ? k_rows_half<LOGN>
                   : ablation == 1 ? k_rows_half<LOGN, kStream, kStream, 1>
                   : ablation == 2 ? k_rows_half<LOGN, kStream, kStream, 2>

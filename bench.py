@@ -120,14 +120,14 @@ def cascade_settings(rank: int, c: int) -> dict:
     return dict(planeSize=PLANES[c % len(PLANES)], seed=(12342 + 4097 * rank, 8934 + 4097 * (c // len(PLANES))))
 
 
-TRAFFIC_PROFILES = ["r01_hs_rocprof.json", "r01_rocprof.json"]
+TRAFFIC_PROFILES = ["r01_v3_rocprof.json", "r01_hs_rocprof.json", "r01_rocprof.json"]
 
 
 def measured_traffic(kernel: str, n: int, cascades: int):
     """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC summary of this workload
     (tools/profile_gpu.sh: separate --pmc FETCH_SIZE and --pmc WRITE_SIZE passes over bench.py,
     read = 2 x FETCH_SIZE, write = WRITE_SIZE, KB = 1024 B; tools/parse_rocprof.py), or None."""
-    # newest collection first: the current kernels (r01_hs), then the full-spectrum path's (r01)
+    # newest collection first: the current kernels (r01_v3), then older ones (r01_hs; r01: full spectrum)
     for path in [os.path.join(ROOT, "profiles", p) for p in TRAFFIC_PROFILES]:
         try:
             with open(path) as f:

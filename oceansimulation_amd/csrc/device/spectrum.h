@@ -151,8 +151,10 @@ __device__ __forceinline__ float2 spectrum_amplitude(const SpectrumConsts& q, fl
   const float2 u = hash_uniform((uint32_t)(int64_t)(tx + q.seed_x), (uint32_t)(int64_t)(ty + q.seed_y));
   // accurate logf: for u near 1 the hardware log2's absolute error is a large relative error
   const float rad = __builtin_amdgcn_sqrtf(-2.0f * logf(u.x));
-  float sn, cs;
-  sincosf(2.0f * OCEAN_PI * u.y, &sn, &cs);
+  // sin/cos(2 pi u.y) with u.y in [0, 1): the hardware v_sin_f32 / v_cos_f32 take revolutions, so
+  // u.y goes in unreduced (absolute error ~3e-7, the size of the fp32 rounding of the reference's
+  // own argument 2 pi u.y, whose ulp is up to 4.8e-7)
+  const float sn = __builtin_amdgcn_sinf(u.y), cs = __builtin_amdgcn_cosf(u.y);
   const float amp = __builtin_amdgcn_sqrtf(2.0f * Sj * d * chain);
   return make_float2(q.c * (rad * cs) * amp, q.c * (rad * sn) * amp);
 }

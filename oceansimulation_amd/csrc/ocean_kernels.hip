@@ -68,36 +68,39 @@ __global__ __launch_bounds__(256) void k_generate_spectrum(SpectrumConsts s, int
 // texels no pair reaches (row N/2, which mirrors onto itself, and column 0 of the upper half,
 // whose partner column N is off the grid) are tail items with two evaluations each (O(N)).
 // Bit-identical to k_generate_spectrum: same evaluator, same float arguments.
-__global__ __launch_bounds__(256) void k_generate_spectrum_pairs(SpectrumConsts s, int n, int blk,
+// Index math in 32 bits with shifts (n, blk powers of two; pairs + tail < 2^31 up to n = 16384):
+// the 64-bit divisions by runtime n / blk cost ~100 VALU per point.
+__global__ __launch_bounds__(256) void k_generate_spectrum_pairs(SpectrumConsts s, int logn, int lblk,
                                                                 float4* __restrict__ h0)
 {
-  const int half = n / 2;
-  const int64_t pairs = (int64_t)n * half, total = pairs + n + (half - 1);
+  const int n = 1 << logn, half = n >> 1, blk = 1 << lblk;
+  const int pairs = n * half, total = pairs + n + (half - 1);
   const float dim = (float)n;
-  auto at = [&](int x, int y) { return ((int64_t)(x / blk) * n + y) * blk + (x % blk); };
-  for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < total;
-       idx += (int64_t)gridDim.x * blockDim.x)
+  auto at = [&](int x, int y) {
+    return ((size_t)(((x >> lblk) << logn) + y) << lblk) + (x & (blk - 1));
+  };
+  for (int idx = blockIdx.x * blockDim.x + threadIdx.x; idx < total; idx += gridDim.x * blockDim.x)
   {
     int x, y;
     bool mirror;
     if (idx < pairs)  // blocked order over the lower half: b fastest, then y, then xb
     {
-      const int b = (int)(idx % blk);
-      const int64_t rest = idx / blk;
-      y = (int)(rest % half);
-      x = (int)(rest / half) * blk + b;
+      const int b = idx & (blk - 1);
+      const int rest = idx >> lblk;
+      y = rest & (half - 1);
+      x = ((rest >> (logn - 1)) << lblk) + b;
       mirror = x > 0 && y > 0;
     }
     else if (idx < pairs + n)
     {
-      x = (int)(idx - pairs);
+      x = idx - pairs;
       y = half;
       mirror = false;
     }
     else
     {
       x = 0;
-      y = half + 1 + (int)(idx - pairs - n);
+      y = half + 1 + (idx - pairs - n);
       mirror = false;
     }
     const float2 a = spectrum_amplitude(s, (float)x, (float)y);
@@ -1188,8 +1191,13 @@ hipError_t launch_generate_spectrum(const OceanSettings& s, int n, float4* h0, h
   if (blocks > cap)
     blocks = cap;
   if (whole)
+  {
+    int lblk = 0;
+    while ((1 << lblk) < spectrum_block(logn))
+      lblk++;
     hipLaunchKernelGGL(k_generate_spectrum_pairs, dim3((unsigned)blocks), dim3(256), 0, stream,
-                       spectrum_consts(s, n), n, spectrum_block(logn), h0);
+                       spectrum_consts(s, n), logn, lblk, h0);
+  }
   else
     hipLaunchKernelGGL(k_generate_spectrum, dim3((unsigned)blocks), dim3(256), 0, stream, spectrum_consts(s, n), n,
                        spectrum_block(logn), x0, width, h0, n);

@@ -89,6 +89,7 @@ __device__ __forceinline__ void sincos_phase(float x, float* s, float* c)
 // heightAmp = h0 * e^{i w t} + conj-partner * e^{-i w t}
 __device__ __forceinline__ float2 evolve(float4 a, float k, const CascadeFrame& f)
 {
+#pragma clang fp contract(off)  // rounds identically wherever it is inlined (rolled or unrolled loops)
   float phase = dispersion_evolve(k, f.g, f.h) * f.time;
   float ws, wc;
   sincos_phase(phase, &ws, &wc);

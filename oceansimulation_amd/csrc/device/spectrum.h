@@ -101,6 +101,9 @@ __device__ __forceinline__ float tanh_pos(float x)  // x >= 0
 // the reference with the settings-only terms hoisted (SpectrumConsts).
 __device__ __forceinline__ float2 spectrum_amplitude(const SpectrumConsts& q, float tx, float ty)
 {
+  // No FMA contraction: the same expression then rounds the same way in every kernel it is inlined
+  // into (the pairs kernel, the slab kernel, the fused re-seed column pass), as in the oracle.
+#pragma clang fp contract(off)
   const float kx = (tx - q.half_dim) * q.dk;
   const float ky = (ty - q.half_dim) * q.dk;
   const float k2 = kx * kx + ky * ky;

@@ -101,6 +101,11 @@ struct ocean_generator
   float4* rm_de = nullptr;
   float2* rm_c = nullptr;
   unsigned char* xbuf = nullptr;                      // internal exchange buffer (ranks == 1, or null send/recv)
+  // fused re-seed frames (blocked half path): h0 evaluated inside pass 1, the h0 image left stale
+  void* seedc = nullptr;                 // device: one seed_consts record per cascade
+  std::vector<unsigned char> seedc_host; // what seedc holds
+  bool h0_stale = false;                 // the h0 image is not written yet (materialise_h0)
+  std::vector<ocean_settings> seed_settings;  // the settings the last fused re-seed evaluated
   bool profiling = false;
   std::vector<EventPair> pending;
   std::vector<hipEvent_t> pool;
@@ -483,7 +488,7 @@ int ocean_generator_destroy(ocean_generator* g)
     (void)hipFree(g->maps);
   if (g->jac)
     (void)hipFree(g->jac);
-  for (void* p : {(void*)g->gab, (void*)g->gcd, (void*)g->ge, (void*)g->spec, (void*)g->hs, (void*)g->h0row,
+  for (void* p : {(void*)g->gab, (void*)g->gcd, (void*)g->ge, (void*)g->spec, (void*)g->hs, (void*)g->h0row, g->seedc,
                   (void*)g->rm_ab, (void*)g->rm_de, (void*)g->rm_c, (void*)g->xbuf})
     if (p)
       (void)hipFree(p);
@@ -504,16 +509,17 @@ ocean_settings* ocean_generator_settings(ocean_generator* g, int c)
 }
 
 
-int ocean_generator_generate_spectrum(ocean_generator* g)
+// generateSpectrum with the given per-cascade settings (the current ones, or those a fused re-seed
+// frame evaluated h0 with, when that h0 image is materialised later)
+static int generate_spectrum_with(ocean_generator* g, const std::vector<ocean_settings>& settings)
 {
-  if (!g)
-    return fail(OCEAN_ERR_INVALID, "ocean_generator_generate_spectrum: null generator");
+  g->h0_stale = false;
   ocean_fft* f = g->fft;
   const size_t slab = h0_texels(g);
   for (int c = 0; c < g->cascades; c++)
   {
     OceanSettings s;
-    std::memcpy(&s, &g->settings[c], sizeof(s));
+    std::memcpy(&s, &settings[c], sizeof(s));
     if (g->hslab && g->ranks > 1)
     {
       // this rank's strips: the regular ones are columns N/2 + strip*B .. (contiguous), the last
@@ -543,6 +549,19 @@ int ocean_generator_generate_spectrum(ocean_generator* g)
   return OCEAN_OK;
 }
 
+int ocean_generator_generate_spectrum(ocean_generator* g)
+{
+  if (!g)
+    return fail(OCEAN_ERR_INVALID, "ocean_generator_generate_spectrum: null generator");
+  return generate_spectrum_with(g, g->settings);
+}
+
+// After fused re-seed frames: write the h0 image those frames evaluated (their settings snapshot).
+static int materialise_h0(ocean_generator* g)
+{
+  return g->h0_stale ? generate_spectrum_with(g, g->seed_settings) : OCEAN_OK;
+}
+
 // First half of CalculateOcean: time += dt (src/Generator.cpp:50), h0 if requested (:55-59),
 // prepareFFT fused with the y direction of both EncodeIFFTs (:63-72). Output in destination-block
 // order into `out` (the internal buffer when null).
@@ -551,10 +570,47 @@ static int generator_columns(ocean_generator* g, float timestep, int update_spec
   ocean_fft* f = g->fft;
   for (auto& s : g->settings)
     s.time += timestep;
+  const void* seed = nullptr;
   if (g->update_spectrum || update_spectrum)
   {
+    // The generator's first seeding writes the h0 image. Explicit re-seeds (the reference app's
+    // every-frame CalculateOcean(dt, true)) are fused into pass 1 on the blocked half path; the
+    // inlined ocml functions round the same amplitude within an ulp of the seeding kernels' (frames
+    // agree to ~1e-7 of max, test_fused_reseed_frames), so the first frame keeps the kernels that
+    // slabs and batches are compared with bit-exactly.
+    const bool fused = update_spectrum && !g->update_spectrum && g->half && g->hs;
     g->update_spectrum = false;
-    int rc = ocean_generator_generate_spectrum(g);
+    if (fused)
+    {
+      // fused re-seed (src/Generator.cpp:55-59 followed by :63-72): pass 1 evaluates h0 itself
+      std::vector<unsigned char> host((size_t)g->cascades * seed_consts_bytes());
+      for (int c = 0; c < g->cascades; c++)
+      {
+        OceanSettings os;
+        std::memcpy(&os, &g->settings[c], sizeof(os));
+        seed_consts(os, f->n, host.data() + (size_t)c * seed_consts_bytes());
+      }
+      if (!g->seedc)
+        HIP_TRY(hipMalloc(&g->seedc, (size_t)kMaxCascades * seed_consts_bytes()), "seed constants");
+      if (host != g->seedc_host)  // pageable source: staged before the call returns
+      {
+        HIP_TRY(hipMemcpyAsync(g->seedc, host.data(), host.size(), hipMemcpyHostToDevice, f->stream), "seed constants");
+        g->seedc_host.swap(host);
+      }
+      seed = g->seedc;
+      g->h0_stale = true;
+      g->seed_settings = g->settings;
+    }
+    else
+    {
+      int rc = ocean_generator_generate_spectrum(g);
+      if (rc != OCEAN_OK)
+        return rc;
+    }
+  }
+  else
+  {
+    int rc = materialise_h0(g);  // the next frames read the h0 image
     if (rc != OCEAN_OK)
       return rc;
   }
@@ -579,7 +635,7 @@ static int generator_columns(ocean_generator* g, float timestep, int update_spec
   else if (g->half)
     HIP_TRY(timed(g, 1, [&] {
               return launch_half_columns(f->logn, fp, g->h0, g->gab, g->gcd, g->ge, g->spec, f->twiddles, f->stream,
-                                         f->cus, g->hs, f->device_cus);
+                                         f->cus, g->hs, f->device_cus, seed);
             }),
             "column pass (half spectrum)");
   else
@@ -835,6 +891,8 @@ int ocean_surface_sample_plane(ocean_generator* const* gens, const int* cascades
 float* ocean_generator_initial_spectrum(ocean_generator* g, int c)
 {
   if (!g || c < 0 || c >= g->cascades)
+    return nullptr;
+  if (materialise_h0(g) != OCEAN_OK)  // after fused re-seed frames
     return nullptr;
   return reinterpret_cast<float*>(g->h0 + h0_texels(g) * c);
 }

@@ -112,9 +112,14 @@ size_t half_field_texels(int logn);
 // hs (optional): H scratch of half_hs_bytes(logn, hs_blocks) bytes; pass 1 then evolves each texel
 // once (grid capped at hs_blocks) instead of once per field round.
 size_t half_hs_bytes(int logn, int blocks);  // also the strip-dealt path's
+// seed_consts (optional, device array of one seed_consts_bytes() record per cascade, needs hs): the
+// fused re-seed frame — pass 1 evaluates h0 itself and neither reads nor writes the h0 image.
 hipError_t launch_half_columns(int logn, const FrameParams& fp, const float4* h0, float4* gab, float4* gcd, float2* ge,
                                float4* spec, const float2* tw, hipStream_t stream, int cus, float2* hs = nullptr,
-                               int hs_blocks = 0);
+                               int hs_blocks = 0, const void* seed_consts = nullptr);
+// generateSpectrum's settings-only constants (host, the oracle's fp32 expressions), as a device record
+size_t seed_consts_bytes();
+void seed_consts(const OceanSettings& s, int n, void* out);
 hipError_t launch_half_rows(int logn, const FrameParams& fp, const float4* gab, const float4* gcd, const float2* ge,
                             const float4* rcorr, float4* maps, float* jac, const FoamParams& foam, const float2* tw,
                             hipStream_t stream, int cus, int ablation = 0);

@@ -536,6 +536,15 @@ __global__ __launch_bounds__(FftShape<LOGN>::T * RPW_) void k_rows_final(
 // rank-1 term (-1)^q R(p), R the x-transform of a one-row spectrum built by k_half_nyquist.
 // Frame bytes: h0 8 + fields 20 + 20 + maps 32 + Jacobian 4 = 84 per point (the full path: 116).
 // ------------------------------------------------------------------------------------------------
+// One h0 texel evaluated in place: (h0(k), conj(h0(-k))), -k at index N - i
+// (spectrum.compute:160-168), with the evaluator and arguments of k_generate_spectrum(_pairs).
+__device__ __forceinline__ float4 seed_texel(const SpectrumConsts& q, int x, int y, float dim)
+{
+  const float2 a = spectrum_amplitude(q, (float)x, (float)y);
+  const float2 c = spectrum_amplitude(q, dim - (float)x, dim - (float)y);
+  return make_float4(a.x, a.y, c.x, -c.y);
+}
+
 template <int LOGN>
 struct HalfCfg
 {
@@ -558,13 +567,17 @@ struct HalfCfg
 // [q w, q w + w): gab | gde | gc parts of C * S * w * B elements, element ((c S + sl) w + yl) B + b),
 // so one equal-split all-to-all hands every rank the rows of its row pass. h0 is the whole grid's
 // blocked image when h0_full, else the rank's strips in order ([c][sl][N][B]).
-template <int LOGN, int LA = 0, int SA = kStream, bool HS = false, bool SLAB = false>
+// SEED (the fused re-seed frame, CalculateOcean(dt, true) on whole grids): round 0 evaluates each
+// texel's two amplitudes (seed[c], the host's settings constants) instead of loading h0, so h0 is
+// neither written nor read this frame (HS only).
+template <int LOGN, int LA = 0, int SA = kStream, bool HS = false, bool SLAB = false, bool SEED = false>
 __global__ __launch_bounds__(ColFirstCfg<LOGN>::WG1) void k_cols_half(FrameParams fp, const float4* __restrict__ h0,
                                                                      float4* __restrict__ gab, float4* __restrict__ gde,
                                                                      float2* __restrict__ gc,
                                                                      const float2* __restrict__ tw_glob,
                                                                      float2* __restrict__ hs, HalfSlab hsl,
-                                                                     unsigned char* __restrict__ send, int h0_full)
+                                                                     unsigned char* __restrict__ send, int h0_full,
+                                                                     const SpectrumConsts* __restrict__ seed)
 {
   using S = FftShape<LOGN>;
   using K = ColFirstCfg<LOGN>;
@@ -606,7 +619,30 @@ __global__ __launch_bounds__(ColFirstCfg<LOGN>::WG1) void k_cols_half(FrameParam
         else  // (C, 0) = (H / |k|, 0)
           v[m] = CPair{f2v{q.inv * H.x, 0.0f}, f2v{q.inv * H.y, 0.0f}};
       };
-      if (!HS || round == 0)
+      if (SEED && round == 0)
+      {
+        static_assert(!SEED || HS, "the fused seed keeps H in the scratch");
+        float2* hsb = hs + (size_t)blockIdx.x * 16 * K::WG1;
+        const int hoff = opaque((int)threadIdx.x) * 8;
+        const SpectrumConsts q = seed[c];
+        // the evaluator is too large to unroll 16 times: a rolled loop parks each H in the scratch,
+        // then the round reads them back like rounds 1 and 2 (its own stores, from L2)
+#pragma unroll 1
+        for (int m = 0; m < 16; m++)
+        {
+          const int y = i + ((m + 8) & 15) * T;
+          const float2 H = evolve(seed_texel(q, x, y, dim), make_kvec(x, y, dim, f.dk).k, f);
+          st2<0>(hsb + m * K::WG1, hoff, H);
+        }
+        __threadfence_block();  // this thread's scratch stores are complete before it reads them back
+#pragma unroll
+        for (int m = 0; m < 16; m++)
+        {
+          const int y = i + ((m + 8) & 15) * T;
+          pack(m, ld2<kStream>(hsb + m * K::WG1, hoff), make_kvec(x, y, dim, f.dk));
+        }
+      }
+      else if (!HS || round == 0)
       {
         float2* hsb = hs + (size_t)blockIdx.x * 16 * K::WG1;
         const int hoff = opaque((int)threadIdx.x) * 8;
@@ -686,9 +722,11 @@ __global__ __launch_bounds__(ColFirstCfg<LOGN>::WG1) void k_cols_half(FrameParam
 // copies / copy_stride: the strip-dealt path writes the term into every destination block of the
 // exchange buffer, so each frame's row pass reads the term of its own frame (the pipeline keeps two
 // frames in flight).
+// seed (the fused re-seed frame, h0 not materialised): the two row-0 texels are evaluated here.
 __global__ __launch_bounds__(256) void k_half_nyquist(FrameParams fp, int n, int blk, const float4* __restrict__ h0,
                                                       float4* __restrict__ spec, const float4* __restrict__ h0row,
-                                                      int copies, size_t copy_stride)
+                                                      int copies, size_t copy_stride,
+                                                      const SpectrumConsts* __restrict__ seed)
 {
   const int total = fp.cascades * n;
   const float dim = (float)n;
@@ -701,8 +739,17 @@ __global__ __launch_bounds__(256) void k_half_nyquist(FrameParams fp, int n, int
       const CascadeFrame f = fp.c[c];
       const int xp = n - x;  // u' = n/2 - x > 0 at column n/2 + u' = n - x; its mirror is x itself
       const float4* hc = h0 + (size_t)c * n * n;
-      const float4 ap = h0row ? h0row[(size_t)c * n + xp] : hc[(size_t)(xp / blk) * n * blk + (xp % blk)];  // row y = 0 (v = -n/2)
-      const float4 an = h0row ? h0row[(size_t)c * n + x] : hc[(size_t)(x / blk) * n * blk + (x % blk)];
+      float4 ap, an;  // row y = 0 (v = -n/2)
+      if (seed)
+      {
+        ap = seed_texel(seed[c], xp, 0, dim);
+        an = seed_texel(seed[c], x, 0, dim);
+      }
+      else
+      {
+        ap = h0row ? h0row[(size_t)c * n + xp] : hc[(size_t)(xp / blk) * n * blk + (xp % blk)];
+        an = h0row ? h0row[(size_t)c * n + x] : hc[(size_t)(x / blk) * n * blk + (x % blk)];
+      }
       const KVec qp = make_kvec(xp, 0, dim, f.dk), qn = make_kvec(x, 0, dim, f.dk);
       const float2 hp = evolve(ap, qp.k, f), hn = evolve(an, qn.k, f);
       const float2 dm = make_float2(hn.x - hp.x, hn.y + hp.y);  // Hn - conj(Hp)
@@ -1170,6 +1217,10 @@ static int persistent_grid(K kernel, int wg, int lds, int items, int cus)
   return g < 1 ? 1 : (int)g;
 }
 
+size_t seed_consts_bytes() { return sizeof(SpectrumConsts); }
+
+void seed_consts(const OceanSettings& s, int n, void* out) { *static_cast<SpectrumConsts*>(out) = spectrum_consts(s, n); }
+
 int spectrum_block(int logn)
 {
   int t = 1 << (logn - 4);
@@ -1255,8 +1306,10 @@ size_t half_hs_bytes(int logn, int blocks)
 }
 
 hipError_t launch_half_columns(int logn, const FrameParams& fp, const float4* h0, float4* gab, float4* gcd, float2* ge,
-                               float4* spec, const float2* tw, hipStream_t stream, int cus, float2* hs, int hs_blocks)
+                               float4* spec, const float2* tw, hipStream_t stream, int cus, float2* hs, int hs_blocks,
+                               const void* seed_consts)
 {
+  const SpectrumConsts* seed = static_cast<const SpectrumConsts*>(seed_consts);
   return with_logn(logn, [&](auto L) -> hipError_t {
     constexpr int LOGN = decltype(L)::value;
     if constexpr (!HalfCfg<LOGN>::SUPPORTED)
@@ -1271,12 +1324,15 @@ hipError_t launch_half_columns(int logn, const FrameParams& fp, const float4* h0
       if (blocks > (long)cus * 4)
         blocks = (long)cus * 4;
       hipLaunchKernelGGL(k_half_nyquist, dim3((unsigned)blocks), dim3(256), 0, stream, fp, n, K::B, h0, spec,
-                         (const float4*)nullptr, 1, (size_t)0);
+                         (const float4*)nullptr, 1, (size_t)0, seed);
       hipError_t e = hipGetLastError();
       if (e != hipSuccess)
         return e;
       // hs: per-block H scratch (half_hs_bytes): H evolved once instead of once per round
-      auto kern = hs ? k_cols_half<LOGN, 0, kStream, true> : k_cols_half<LOGN>;
+      if (seed && !hs)
+        return hipErrorInvalidValue;
+      auto kern = seed ? k_cols_half<LOGN, 0, kStream, true, false, true>
+                       : (hs ? k_cols_half<LOGN, 0, kStream, true> : k_cols_half<LOGN>);
       const int lds = ((S::TW_ENTRIES * 8 + 15) / 16) * 16 + K::LDS1;
       int grid = persistent_grid(kern, K::WG1, lds, fp.cascades * HalfCfg<LOGN>::STRIPS, cus);
       if (hs && grid > hs_blocks)
@@ -1284,7 +1340,7 @@ hipError_t launch_half_columns(int logn, const FrameParams& fp, const float4* h0
       if (grid < 1)
         return hipErrorInvalidValue;
       hipLaunchKernelGGL(kern, dim3(grid), dim3(K::WG1), lds, stream, fp, h0, gab, gcd, ge, tw, hs, HalfSlab{},
-                         (unsigned char*)nullptr, 1);  // gcd/ge: (D, E) / C
+                         (unsigned char*)nullptr, 1, seed);  // gcd/ge: (D, E) / C
       return hipGetLastError();
     }
   });
@@ -1379,7 +1435,7 @@ hipError_t launch_half_slab_columns(int logn, const FrameParams& fp, const HalfS
       const size_t blk = half_slab_block_bytes(LOGN, fp.cascades, hsl);
       float4* spec = reinterpret_cast<float4*>((unsigned char*)send + half_slab_spec_offset(LOGN, fp.cascades, hsl));
       hipLaunchKernelGGL(k_half_nyquist, dim3((unsigned)blocks), dim3(256), 0, stream, fp, n, K::B, h0, spec,
-                         h0_full ? (const float4*)nullptr : h0row, ranks, blk);
+                         h0_full ? (const float4*)nullptr : h0row, ranks, blk, (const SpectrumConsts*)nullptr);
       hipError_t e = hipGetLastError();
       if (e != hipSuccess || hsl.nstrips < 1)  // a rank past the last strip only builds the Nyquist-row term
         return e;
@@ -1389,7 +1445,8 @@ hipError_t launch_half_slab_columns(int logn, const FrameParams& fp, const HalfS
       if (grid > hs_blocks)
         grid = hs_blocks;
       hipLaunchKernelGGL(kern, dim3(grid), dim3(K::WG1), lds, stream, fp, h0, (float4*)nullptr, (float4*)nullptr,
-                         (float2*)nullptr, tw, hs, hsl, (unsigned char*)send, h0_full ? 1 : 0);
+                         (float2*)nullptr, tw, hs, hsl, (unsigned char*)send, h0_full ? 1 : 0,
+                         (const SpectrumConsts*)nullptr);
       return hipGetLastError();
     }
   });

@@ -55,17 +55,19 @@ $(APP): examples/waveapp_headless.cpp $(WAVES)
 	    -L$(PKG) -lwaves -loceanfft -Wl,-rpath,'$$ORIGIN/../$(PKG)' -L/opt/rocm/lib -lamdhip64
 
 MB := tools/microbench
-microbench: $(MB)/ifftbench $(MB)/transbench $(MB)/scatterbench $(MB)/halfbench $(MB)/genbench $(MB)/colbench $(MB)/copybench $(MB)/genbench_noxch $(MB)/genbench_nobar $(MB)/layoutbench
+microbench: $(MB)/halfbench_nohs $(MB)/ifftbench $(MB)/transbench $(MB)/scatterbench $(MB)/halfbench $(MB)/genbench $(MB)/colbench $(MB)/copybench $(MB)/genbench_noxch $(MB)/genbench_nobar $(MB)/layoutbench
 $(MB)/%: $(MB)/%.hip $(CSRC)/ocean_kernels.hip $(CSRC)/ocean_internal.h $(DEVICE_H)
 	$(HIPCC) $(HIPFLAGS) $< -o $@
 # timing ablations (wrong results by construction): no LDS exchanges / exchanges without barriers
 $(MB)/genbench_noxch: $(MB)/genbench.hip $(CSRC)/ocean_kernels.hip $(CSRC)/ocean_internal.h $(DEVICE_H)
 	$(HIPCC) $(HIPFLAGS) -DOCEAN_ABLATE_EXCHANGE $< -o $@
+$(MB)/halfbench_nohs: $(MB)/halfbench.hip $(CSRC)/ocean_kernels.hip $(CSRC)/ocean_internal.h $(DEVICE_H)
+	$(HIPCC) $(HIPFLAGS) -DOCEAN_ABLATE_HS $< -o $@
 $(MB)/genbench_nobar: $(MB)/genbench.hip $(CSRC)/ocean_kernels.hip $(CSRC)/ocean_internal.h $(DEVICE_H)
 	$(HIPCC) $(HIPFLAGS) -DOCEAN_ABLATE_BARRIER $< -o $@
 
 clean:
-	rm -rf $(MB)/ifftbench $(MB)/transbench $(MB)/scatterbench $(MB)/halfbench $(MB)/genbench $(MB)/colbench $(MB)/copybench $(MB)/genbench_noxch $(MB)/genbench_nobar $(MB)/layoutbench $(CSRC)/build $(LIB) $(WAVES) $(CPPTEST) $(APP)
+	rm -rf $(MB)/halfbench_nohs $(MB)/ifftbench $(MB)/transbench $(MB)/scatterbench $(MB)/halfbench $(MB)/genbench $(MB)/colbench $(MB)/copybench $(MB)/genbench_noxch $(MB)/genbench_nobar $(MB)/layoutbench $(CSRC)/build $(LIB) $(WAVES) $(CPPTEST) $(APP)
 	$(MAKE) -s -C oracle clean
 
 .PHONY: all clean microbench

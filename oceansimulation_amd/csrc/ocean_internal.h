@@ -116,7 +116,7 @@ size_t half_hs_bytes(int logn, int blocks);  // also the strip-dealt path's
 // fused re-seed frame — pass 1 evaluates h0 itself and neither reads nor writes the h0 image.
 hipError_t launch_half_columns(int logn, const FrameParams& fp, const float4* h0, float4* gab, float4* gcd, float2* ge,
                                float4* spec, const float2* tw, hipStream_t stream, int cus, float2* hs = nullptr,
-                               int hs_blocks = 0, const void* seed_consts = nullptr);
+                               int hs_blocks = 0, const void* seed_consts = nullptr, int variant = 0);
 // generateSpectrum's settings-only constants (host, the oracle's fp32 expressions), as a device record
 size_t seed_consts_bytes();
 void seed_consts(const OceanSettings& s, int n, void* out);

@@ -555,6 +555,19 @@ struct HalfCfg
   static constexpr bool SLAB_SUPPORTED = ColFirstCfg<LOGN>::SPW == 1;      // strip-dealt path, any B
 };
 
+// Whole-grid half-spectrum field layout, texel offset of (row y, strip, column b of the strip) in a
+// cascade. RG = 1: strips [strip][y][B], a strip one contiguous run (pass 1 stores 1-KiB wave runs,
+// pass 2 reads one RPW * B-texel piece per strip). RG > 1: row groups [y / RG][strip][y % RG][B], so a
+// pass-2 item of RG rows reads one contiguous run and pass 1 stores RG * B-texel pieces. The offset is
+// linear in (y, strip) for y a multiple of RG: offset(y0 + i, s, b) = offset(y0, s) + offset(i, 0, b).
+constexpr int kHalfRG = 1, kHalfRGC = 1;  // production layout
+template <int LOGN, int RG>
+__device__ __forceinline__ int half_group_offset(int y, int strip, int b = 0)
+{
+  constexpr int N = HalfCfg<LOGN>::N, B = HalfCfg<LOGN>::B, STRIPS = HalfCfg<LOGN>::STRIPS;
+  return RG == 1 ? (strip * N + y) * B + b : (((y / RG) * STRIPS + strip) * RG + (y % RG)) * B + b;
+}
+
 // Pass 1: per strip of B columns (u >= 0, or the Nyquist strip), three y-iFFT rounds of CPairs:
 // (A, B), (D, E), (C, 0), stored as gab, gde (float4) and gc (float2): pass 2 reads (A, B) + C for
 // image 0 and C + (D, E) for image 1. H is re-evolved per round from h0: keeping the 16 H (32 VGPRs)
@@ -570,7 +583,9 @@ struct HalfCfg
 // SEED (the fused re-seed frame, CalculateOcean(dt, true) on whole grids): round 0 evaluates each
 // texel's two amplitudes (seed[c], the host's settings constants) instead of loading h0, so h0 is
 // neither written nor read this frame (HS only).
-template <int LOGN, int LA = 0, int SA = kStream, bool HS = false, bool SLAB = false, bool SEED = false>
+// RG / RGC (whole grids): rows per group of the gab/gde and the gc layout (half_group_offset).
+template <int LOGN, int LA = 0, int SA = kStream, bool HS = false, bool SLAB = false, bool SEED = false, int RG = 1,
+          int RGC = 1>
 __global__ __launch_bounds__(ColFirstCfg<LOGN>::WG1) void k_cols_half(FrameParams fp, const float4* __restrict__ h0,
                                                                      float4* __restrict__ gab, float4* __restrict__ gde,
                                                                      float2* __restrict__ gc,
@@ -601,7 +616,11 @@ __global__ __launch_bounds__(ColFirstCfg<LOGN>::WG1) void k_cols_half(FrameParam
     const CascadeFrame f = fp.c[c];
     const float4* src = (!SLAB || h0_full) ? h0 + ((size_t)c * (N / B) + xb) * N * B
                                            : h0 + ((size_t)c * nstrips + s) * N * B;
-    const size_t base = ((size_t)c * STRIPS + s) * N * B;
+    // the strip's first texel in the cascade's fields (whole grids); + half_group_offset(m T, 0) per m
+    const size_t gbase = RG == 1 ? ((size_t)c * STRIPS + s) * N * B
+                                 : (size_t)c * STRIPS * N * B + half_group_offset<LOGN, RG>(0, s);
+    const size_t cgbase = RGC == 1 ? ((size_t)c * STRIPS + s) * N * B
+                                   : (size_t)c * STRIPS * N * B + half_group_offset<LOGN, RGC>(0, s);
     const int x = xb * B + b;
     // one field round: (A, B), (D, E) or (C, 0) of the 16 texels, y-iFFT, store
     auto run_round = [&](int round) __attribute__((always_inline)) {
@@ -656,8 +675,13 @@ __global__ __launch_bounds__(ColFirstCfg<LOGN>::WG1) void k_cols_half(FrameParam
           const int y = i + ((m + 8) & 15) * T;
           const KVec q = make_kvec(x, y, dim, f.dk);
           const float2 H = evolve(a[m], q.k, f);
+#ifndef OCEAN_ABLATE_HS
           if (HS)
             st2<0>(hsb + m * K::WG1, hoff, H);
+#else
+          (void)hsb;
+          (void)hoff;
+#endif
           pack(m, H, q);
         }
       }
@@ -669,7 +693,12 @@ __global__ __launch_bounds__(ColFirstCfg<LOGN>::WG1) void k_cols_half(FrameParam
         for (int m = 0; m < 16; m++)
         {
           const int y = i + ((m + 8) & 15) * T;
+#ifdef OCEAN_ABLATE_HS  // timing ablation (tools/microbench): no scratch read-back, wrong results
+          (void)hsb;
+          pack(m, make_float2((float)hoff, (float)m), make_kvec(x, y, dim, f.dk));
+#else
           pack(m, ld2<kStream>(hsb + m * K::WG1, hoff), make_kvec(x, y, dim, f.dk));
+#endif
         }
       }
       fft_run<LOGN, K::C1, true>(v, i, b, xch, tw);
@@ -691,12 +720,24 @@ __global__ __launch_bounds__(ColFirstCfg<LOGN>::WG1) void k_cols_half(FrameParam
           else
             st2<SA>(blk + part * 32 + el * 8, (i * B + b) * 8, make_float2(v[m].re.x, v[m].im.x));
         }
+        else if constexpr (RG == 1 && RGC == 1)
+        {
+          if (round == 0)
+            st4<SA>(gab + gbase + m * T * B, voff, pair_raw(v[m]));
+          else if (round == 1)
+            st4<SA>(gde + gbase + m * T * B, voff, pair_raw(v[m]));
+          else
+            st2<SA>(gc + gbase + m * T * B, (i * B + b) * 8, make_float2(v[m].re.x, v[m].im.x));
+        }
         else if (round == 0)
-          st4<SA>(gab + base + m * T * B, voff, pair_raw(v[m]));
+          st4<SA>(gab + gbase + half_group_offset<LOGN, RG>(m * T, 0), half_group_offset<LOGN, RG>(i, 0, b) * 16,
+                  pair_raw(v[m]));
         else if (round == 1)
-          st4<SA>(gde + base + m * T * B, voff, pair_raw(v[m]));
+          st4<SA>(gde + gbase + half_group_offset<LOGN, RG>(m * T, 0), half_group_offset<LOGN, RG>(i, 0, b) * 16,
+                  pair_raw(v[m]));
         else
-          st2<SA>(gc + base + m * T * B, (i * B + b) * 8, make_float2(v[m].re.x, v[m].im.x));
+          st2<SA>(gc + cgbase + half_group_offset<LOGN, RGC>(m * T, 0), half_group_offset<LOGN, RGC>(i, 0, b) * 8,
+                  make_float2(v[m].re.x, v[m].im.x));
       }
     };
     if constexpr (HS)
@@ -788,7 +829,9 @@ __global__ __launch_bounds__(256) void k_half_nyquist(FrameParams fp, int n, int
 // in VGPRs (16) for image 1 instead of being fetched again by a second item.
 // RM (strip-dealt path, after k_half_to_rows): the fields are row-major [c][rows][kp], column u' = u
 // for u in [0, N/2] (u' = N/2: the Nyquist column), and the pass covers `rows` rows (a slab's w).
-template <int LOGN, int LA = kStream, int SA = kStream, int ABL = 0, int RPW_ = 2, bool BOTH = false, bool RM = false>
+// RG / RGC (whole grids): the field layout pass 1 wrote (half_group_offset).
+template <int LOGN, int LA = kStream, int SA = kStream, int ABL = 0, int RPW_ = 2, bool BOTH = false, bool RM = false,
+          int RG = 1, int RGC = 1>
 __global__ __launch_bounds__(FftShape<LOGN>::T * RPW_) void k_rows_half(
     FrameParams fp, const float4* __restrict__ gab, const float4* __restrict__ gde, const float2* __restrict__ gc,
     const float4* __restrict__ spec, float4* __restrict__ maps, float* __restrict__ jac, FoamParams foam,
@@ -836,7 +879,8 @@ __global__ __launch_bounds__(FftShape<LOGN>::T * RPW_) void k_rows_half(
     for (int m = 0; m < 8; m++)
     {
       const int u = m * T + i;               // >= 0, column x = N/2 + u
-      const int off = RM ? r * kp + u : ((u / B) * N + y) * B + (u % B);
+      const int off = RM ? r * kp + u : half_group_offset<LOGN, RG>(y, u / B, u % B);
+      const int offc = RM ? off : half_group_offset<LOGN, RGC>(y, u / B, u % B);
       const float kx = (float)u * dk;        // ((float)x - N/2) dk, x - N/2 exact
       const float4 s4 = ld4<0>(sp, (N / 2 - u) * 16);  // the -u column's Nyquist-row term (x = N/2 - u)
       CPair own, neg;
@@ -848,7 +892,7 @@ __global__ __launch_bounds__(FftShape<LOGN>::T * RPW_) void k_rows_half(
       else if (img == 0)
       {
         const CPair p = raw_pair(ld4<LA>(gab + base, off * 16));  // (A, B)
-        const float2 cc = ld2<LA>(gc + base, off * 8);              // C
+        const float2 cc = ld2<LA>(gc + base, offc * 8);             // C
         if (BOTH)
           ckeep[m] = cc;
         const float Ar = p.re.x, Ai = p.im.x, Br = p.re.y, Bi = p.im.y, Cr = cc.x, Ci = cc.y;
@@ -862,7 +906,7 @@ __global__ __launch_bounds__(FftShape<LOGN>::T * RPW_) void k_rows_half(
       else
       {
         const CPair q = raw_pair(ld4<LA>(gde + base, off * 16));  // (D, E)
-        const float2 cc = BOTH ? ckeep[m] : ld2<LA>(gc + base, off * 8);  // C
+        const float2 cc = BOTH ? ckeep[m] : ld2<LA>(gc + base, offc * 8);  // C
         const float Cr = cc.x, Ci = cc.y, Dr = q.re.x, Di = q.im.x, Er = q.re.y, Ei = q.im.y;
         const float kx2 = kx * kx;
         // at u: lane2 = i (D - kx^2 C), lane3 = -E - i kx D
@@ -893,13 +937,15 @@ __global__ __launch_bounds__(FftShape<LOGN>::T * RPW_) void k_rows_half(
       }
       else if (i == 0 && m == 8)
       {
-        const int off = RM ? r * kp + N / 2 : ((N / 2 / B) * N + y) * B;  // Nyquist column: first column of the last strip
+        // Nyquist column: first column of the last strip
+        const int off = RM ? r * kp + N / 2 : half_group_offset<LOGN, RG>(y, N / 2 / B);
+        const int offc = RM ? off : half_group_offset<LOGN, RGC>(y, N / 2 / B);
         const float kx = -(dim / 2.0f) * dk;
         float2 cc;
         if (BOTH && img == 1)
           cc = cnyq;
         else
-          cc = ld2<LA>(gc + base, off * 8);  // C
+          cc = ld2<LA>(gc + base, offc * 8);  // C
         if (BOTH && img == 0)
           cnyq = cc;
         if (img == 0)
@@ -1307,7 +1353,7 @@ size_t half_hs_bytes(int logn, int blocks)
 
 hipError_t launch_half_columns(int logn, const FrameParams& fp, const float4* h0, float4* gab, float4* gcd, float2* ge,
                                float4* spec, const float2* tw, hipStream_t stream, int cus, float2* hs, int hs_blocks,
-                               const void* seed_consts)
+                               const void* seed_consts, int variant)
 {
   const SpectrumConsts* seed = static_cast<const SpectrumConsts*>(seed_consts);
   return with_logn(logn, [&](auto L) -> hipError_t {
@@ -1331,8 +1377,20 @@ hipError_t launch_half_columns(int logn, const FrameParams& fp, const float4* h0
       // hs: per-block H scratch (half_hs_bytes): H evolved once instead of once per round
       if (seed && !hs)
         return hipErrorInvalidValue;
-      auto kern = seed ? k_cols_half<LOGN, 0, kStream, true, false, true>
-                       : (hs ? k_cols_half<LOGN, 0, kStream, true> : k_cols_half<LOGN>);
+      // HS: h0 is read once per item, streamed (nt), which leaves the XCD's L2 to the H scratch
+      // (0.972 -> 0.935 ms, tools/microbench/halfbench). variant (halfbench): 1 = default-policy h0
+      // loads, 2 = sc1 field stores (dropped from L2: slower), 3 = sc1 + nt stores
+      // 4..6: field layouts with row groups (RG, RGC) = (2, 2), (2, 4), (4, 4) (launch_half_rows 8..10)
+      constexpr int RG = kHalfRG, RGC = kHalfRGC;
+      auto kern = seed ? k_cols_half<LOGN, 0, kStream, true, false, true, RG, RGC>
+                       : !hs ? k_cols_half<LOGN, 0, kStream, false, false, false, RG, RGC>
+                       : variant == 1 ? k_cols_half<LOGN, 0, kStream, true, false, false, RG, RGC>
+                       : variant == 2 ? k_cols_half<LOGN, kStream, 16, true, false, false, RG, RGC>
+                       : variant == 3 ? k_cols_half<LOGN, kStream, 18, true, false, false, RG, RGC>
+                       : variant == 4 ? k_cols_half<LOGN, kStream, kStream, true, false, false, 2, 2>
+                       : variant == 5 ? k_cols_half<LOGN, kStream, kStream, true, false, false, 2, 4>
+                       : variant == 6 ? k_cols_half<LOGN, kStream, kStream, true, false, false, 4, 4>
+                                      : k_cols_half<LOGN, kStream, kStream, true, false, false, RG, RGC>;
       const int lds = ((S::TW_ENTRIES * 8 + 15) / 16) * 16 + K::LDS1;
       int grid = persistent_grid(kern, K::WG1, lds, fp.cascades * HalfCfg<LOGN>::STRIPS, cus);
       if (hs && grid > hs_blocks)
@@ -1364,13 +1422,18 @@ hipError_t launch_half_rows(int logn, const FrameParams& fp, const float4* gab, 
       // item (C loaded by both items of a row block)
       constexpr int R4 = K::RPW2;
       const int rpw = ablation == 4 ? R4 : ablation == 5 ? 1 : 2;
-      const int per_item = (ablation == 0 || ablation == 7) ? 1 : 2;
+      const int per_item = (ablation == 0 || ablation >= 7) ? 1 : 2;
       // production loads use the default policy: C's 128-B lines are shared by the paired items
       // (xcd_pair_slot) and streamed loads lost them before the partner's read (-5 %,
       // tools/microbench/halfbench); 7: streamed loads
-      auto kern = ablation == 0   ? k_rows_half<LOGN, 0, kStream, 0, 2, true>
-                  : ablation == 7 ? k_rows_half<LOGN, kStream, kStream, 0, 2, true>
-                  : ablation == 6 ? k_rows_half<LOGN>
+      // 8..10: the field layouts of launch_half_columns' variants 4..6
+      constexpr int RG = kHalfRG, RGC = kHalfRGC;
+      auto kern = ablation == 0   ? k_rows_half<LOGN, 0, kStream, 0, 2, true, false, RG, RGC>
+                  : ablation == 8 ? k_rows_half<LOGN, 0, kStream, 0, 2, true, false, 2, 2>
+                  : ablation == 9 ? k_rows_half<LOGN, 0, kStream, 0, 2, true, false, 2, 4>
+                  : ablation == 10 ? k_rows_half<LOGN, 0, kStream, 0, 2, true, false, 4, 4>
+                  : ablation == 7 ? k_rows_half<LOGN, kStream, kStream, 0, 2, true, false, RG, RGC>
+                  : ablation == 6 ? k_rows_half<LOGN, kStream, kStream, 0, 2, false, false, RG, RGC>
                   : ablation == 1 ? k_rows_half<LOGN, kStream, kStream, 1>
                   : ablation == 2 ? k_rows_half<LOGN, kStream, kStream, 2>
                   : ablation == 3 ? k_rows_half<LOGN, kStream, kStream, 3>
@@ -1439,7 +1502,7 @@ hipError_t launch_half_slab_columns(int logn, const FrameParams& fp, const HalfS
       hipError_t e = hipGetLastError();
       if (e != hipSuccess || hsl.nstrips < 1)  // a rank past the last strip only builds the Nyquist-row term
         return e;
-      auto kern = k_cols_half<LOGN, 0, kStream, true, true>;
+      auto kern = k_cols_half<LOGN, kStream, kStream, true, true>;
       const int lds = ((S::TW_ENTRIES * 8 + 15) / 16) * 16 + K::LDS1;
       int grid = persistent_grid(kern, K::WG1, lds, fp.cascades * hsl.nstrips, cus);
       if (grid > hs_blocks)

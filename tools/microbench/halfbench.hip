@@ -164,6 +164,60 @@ int main(int argc, char** argv)
 
   auto f00 = [&] { hipError_t e = c0(); return e == hipSuccess ? r0() : e; };
   auto f11 = [&] { hipError_t e = c1(); return e == hipSuccess ? r1() : e; };
+  {
+    // pass-1 cache-policy variants (HS): same results, timing only
+    const char* vn[] = {"cols HS: production (nt h0 loads, nt stores)", "cols HS: default-policy h0 loads",
+                        "cols HS: sc1 stores", "cols HS: sc1+nt stores"};
+    std::vector<std::vector<float>> tv(4);
+    for (int r = 0; r < 7; r++)
+      for (int v = 0; v < 4; v++)
+        tv[v].push_back(time_ms([&] { return launch_half_columns(logn, fp, h0, gab, gcd, ge, spec, tw, 0, cus, hs, cus,
+                                                                 nullptr, v); }, 10));
+    for (int v = 0; v < 4; v++)
+    {
+      std::sort(tv[v].begin(), tv[v].end());
+      std::printf("%-46s median %7.3f ms\n", vn[v], tv[v][3]);
+    }
+  }
+  {
+    // field layouts (row groups RG for gab/gde, RGC for gc; half_group_offset): pass 1 variant 4..6
+    // with pass 2 variant 8..10. Only the intermediate layout changes, so the frame must be
+    // bit-identical to the production frame.
+    CHECK(f11());
+    CHECK(hipDeviceSynchronize());
+    auto pm = snap(maps, mb), pj = snap(jac, jb);
+    const char* ln[] = {"production layout (RG 1, RGC 1)", "layout RG 2, RGC 2", "layout RG 2, RGC 4", "layout RG 4, RGC 4"};
+    const int cv[] = {0, 4, 5, 6}, rv[] = {0, 8, 9, 10};
+    bool same[4] = {true, true, true, true};
+    for (int v = 1; v < 4; v++)
+    {
+      CHECK(hipMemset(maps, 0, mb));
+      CHECK(hipMemset(jac, 0, jb));
+      CHECK(launch_half_columns(logn, fp, h0, gab, gcd, ge, spec, tw, 0, cus, hs, cus, nullptr, cv[v]));
+      CHECK(launch_half_rows(logn, fp, gab, gcd, ge, spec, maps, jac, foam, tw, 0, cus, rv[v]));
+      CHECK(hipDeviceSynchronize());
+      std::printf("%s vs production frame:\n", ln[v]);
+      same[v] = (int)diff(snap(maps, mb), pm) & (int)diff(snap(jac, jb), pj);
+    }
+    std::vector<std::vector<float>> tc(4), tr(4), tf(4);
+    for (int r = 0; r < 7; r++)
+      for (int v = 0; v < 4; v++)
+      {
+        auto cl = [&] { return launch_half_columns(logn, fp, h0, gab, gcd, ge, spec, tw, 0, cus, hs, cus, nullptr, cv[v]); };
+        auto rl = [&] { return launch_half_rows(logn, fp, gab, gcd, ge, spec, maps, jac, foam, tw, 0, cus, rv[v]); };
+        tc[v].push_back(time_ms(cl, 10));
+        tr[v].push_back(time_ms(rl, 10));
+        tf[v].push_back(time_ms([&] { hipError_t e = cl(); return e == hipSuccess ? rl() : e; }, 10));
+      }
+    for (int v = 0; v < 4; v++)
+    {
+      std::sort(tc[v].begin(), tc[v].end());
+      std::sort(tr[v].begin(), tr[v].end());
+      std::sort(tf[v].begin(), tf[v].end());
+      std::printf("%-34s cols %7.3f  rows %7.3f  frame %7.3f ms (median)  bit-identical %s\n", ln[v], tc[v][3], tr[v][3],
+                  tf[v][3], same[v] ? "yes" : "NO");
+    }
+  }
   const int rounds = 7, reps = 10;
   std::vector<std::vector<float>> t(7);
   for (int r = 0; r < rounds; r++)

@@ -560,7 +560,11 @@ struct HalfCfg
 // pass 2 reads one RPW * B-texel piece per strip). RG > 1: row groups [y / RG][strip][y % RG][B], so a
 // pass-2 item of RG rows reads one contiguous run and pass 1 stores RG * B-texel pieces. The offset is
 // linear in (y, strip) for y a multiple of RG: offset(y0 + i, s, b) = offset(y0, s) + offset(i, 0, b).
-constexpr int kHalfRG = 1, kHalfRGC = 1;  // production layout
+// Production: RG = 2, RGC = 4. A pass-2 item (2 rows) reads whole 128-B lines of gab/gde in one
+// contiguous run per image, and gc's 128-B lines are shared by the two items paired on one XCD
+// (xcd_pair_slot); pass 1 stores 128-B pieces. Against strips (RG = 1): pass 2 1.637 -> 1.506 ms,
+// pass 1 0.934 -> 0.960 ms, frame 2.581 -> 2.477 ms at 8 x 4096^2 (tools/microbench/halfbench).
+constexpr int kHalfRG = 2, kHalfRGC = 4;
 template <int LOGN, int RG>
 __device__ __forceinline__ int half_group_offset(int y, int strip, int b = 0)
 {
@@ -1380,7 +1384,7 @@ hipError_t launch_half_columns(int logn, const FrameParams& fp, const float4* h0
       // HS: h0 is read once per item, streamed (nt), which leaves the XCD's L2 to the H scratch
       // (0.972 -> 0.935 ms, tools/microbench/halfbench). variant (halfbench): 1 = default-policy h0
       // loads, 2 = sc1 field stores (dropped from L2: slower), 3 = sc1 + nt stores
-      // 4..6: field layouts with row groups (RG, RGC) = (2, 2), (2, 4), (4, 4) (launch_half_rows 8..10)
+      // 4..7: field layouts with row groups (RG, RGC) = (2, 2), (2, 4), (4, 4), (1, 1) (launch_half_rows 8..11)
       constexpr int RG = kHalfRG, RGC = kHalfRGC;
       auto kern = seed ? k_cols_half<LOGN, 0, kStream, true, false, true, RG, RGC>
                        : !hs ? k_cols_half<LOGN, 0, kStream, false, false, false, RG, RGC>
@@ -1390,6 +1394,7 @@ hipError_t launch_half_columns(int logn, const FrameParams& fp, const float4* h0
                        : variant == 4 ? k_cols_half<LOGN, kStream, kStream, true, false, false, 2, 2>
                        : variant == 5 ? k_cols_half<LOGN, kStream, kStream, true, false, false, 2, 4>
                        : variant == 6 ? k_cols_half<LOGN, kStream, kStream, true, false, false, 4, 4>
+                       : variant == 7 ? k_cols_half<LOGN, kStream, kStream, true, false, false, 1, 1>
                                       : k_cols_half<LOGN, kStream, kStream, true, false, false, RG, RGC>;
       const int lds = ((S::TW_ENTRIES * 8 + 15) / 16) * 16 + K::LDS1;
       int grid = persistent_grid(kern, K::WG1, lds, fp.cascades * HalfCfg<LOGN>::STRIPS, cus);
@@ -1426,12 +1431,13 @@ hipError_t launch_half_rows(int logn, const FrameParams& fp, const float4* gab, 
       // production loads use the default policy: C's 128-B lines are shared by the paired items
       // (xcd_pair_slot) and streamed loads lost them before the partner's read (-5 %,
       // tools/microbench/halfbench); 7: streamed loads
-      // 8..10: the field layouts of launch_half_columns' variants 4..6
+      // 8..11: the field layouts of launch_half_columns' variants 4..7
       constexpr int RG = kHalfRG, RGC = kHalfRGC;
       auto kern = ablation == 0   ? k_rows_half<LOGN, 0, kStream, 0, 2, true, false, RG, RGC>
                   : ablation == 8 ? k_rows_half<LOGN, 0, kStream, 0, 2, true, false, 2, 2>
                   : ablation == 9 ? k_rows_half<LOGN, 0, kStream, 0, 2, true, false, 2, 4>
                   : ablation == 10 ? k_rows_half<LOGN, 0, kStream, 0, 2, true, false, 4, 4>
+                  : ablation == 11 ? k_rows_half<LOGN, 0, kStream, 0, 2, true, false, 1, 1>
                   : ablation == 7 ? k_rows_half<LOGN, kStream, kStream, 0, 2, true, false, RG, RGC>
                   : ablation == 6 ? k_rows_half<LOGN, kStream, kStream, 0, 2, false, false, RG, RGC>
                   : ablation == 1 ? k_rows_half<LOGN, kStream, kStream, 1>

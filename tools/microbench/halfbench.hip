@@ -180,14 +180,15 @@ int main(int argc, char** argv)
     }
   }
   {
-    // field layouts (row groups RG for gab/gde, RGC for gc; half_group_offset): pass 1 variant 4..6
-    // with pass 2 variant 8..10. Only the intermediate layout changes, so the frame must be
+    // field layouts (row groups RG for gab/gde, RGC for gc; half_group_offset): pass 1 variant 7, 4, 6
+    // with pass 2 variant 11, 8, 10. Only the intermediate layout changes, so the frame must be
     // bit-identical to the production frame.
     CHECK(f11());
     CHECK(hipDeviceSynchronize());
     auto pm = snap(maps, mb), pj = snap(jac, jb);
-    const char* ln[] = {"production layout (RG 1, RGC 1)", "layout RG 2, RGC 2", "layout RG 2, RGC 4", "layout RG 4, RGC 4"};
-    const int cv[] = {0, 4, 5, 6}, rv[] = {0, 8, 9, 10};
+    const char* ln[] = {"production layout (RG 2, RGC 4)", "layout RG 1, RGC 1 (strips)", "layout RG 2, RGC 2",
+                        "layout RG 4, RGC 4"};
+    const int cv[] = {0, 7, 4, 6}, rv[] = {0, 11, 8, 10};
     bool same[4] = {true, true, true, true};
     for (int v = 1; v < 4; v++)
     {

@@ -54,6 +54,7 @@ def parse():
     ap.add_argument("--no-slab", action="store_true", help="skip the config-5 slab-decomposed grid")
     ap.add_argument("--no-ifft", action="store_true", help="skip the EncodeIFFT-only and rocFFT legs")
     ap.add_argument("--no-surface", action="store_true", help="skip the surface-consumer leg")
+    ap.add_argument("--no-reseed", action="store_true", help="skip the re-seed-every-frame leg")
     ap.add_argument("--full-spectrum", action="store_true",
                     help="time the full-spectrum frame path instead of the default half-spectrum one")
     ap.add_argument("--slab-n", type=int, default=16384, help="side of the single slab-decomposed grid")
@@ -120,14 +121,14 @@ def cascade_settings(rank: int, c: int) -> dict:
     return dict(planeSize=PLANES[c % len(PLANES)], seed=(12342 + 4097 * rank, 8934 + 4097 * (c // len(PLANES))))
 
 
-TRAFFIC_PROFILES = ["r01_v3_rocprof.json", "r01_hs_rocprof.json", "r01_rocprof.json"]
+TRAFFIC_PROFILES = ["r01_v4_rocprof.json", "r01_v3_rocprof.json", "r01_hs_rocprof.json", "r01_rocprof.json"]
 
 
 def measured_traffic(kernel: str, n: int, cascades: int):
     """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC summary of this workload
     (tools/profile_gpu.sh: separate --pmc FETCH_SIZE and --pmc WRITE_SIZE passes over bench.py,
     read = 2 x FETCH_SIZE, write = WRITE_SIZE, KB = 1024 B; tools/parse_rocprof.py), or None."""
-    # newest collection first: the current kernels (r01_v3), then older ones (r01_hs; r01: full spectrum)
+    # newest collection first: the current kernels (r01_v4), then older ones (r01_v3, r01_hs; r01: full spectrum)
     for path in [os.path.join(ROOT, "profiles", p) for p in TRAFFIC_PROFILES]:
         try:
             with open(path) as f:
@@ -422,16 +423,18 @@ def main():
     # The reference application's own loop re-seeds h0 on every frame (src/Waves.cpp:91-94, where
     # `updateSpectrum = false` is commented out): CalculateOcean(dt, true). Timed as its own leg.
     gen.set_profiling(False)
-    sync()
-    barrier(world)
-    sync()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        gen.CalculateOcean(dt, True)
-    sync()
-    barrier(world)
-    sync()
-    el_reseed = max_over_ranks(time.perf_counter() - t0, world)
+    el_reseed = None
+    if not args.no_reseed:
+        sync()
+        barrier(world)
+        sync()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            gen.CalculateOcean(dt, True)
+        sync()
+        barrier(world)
+        sync()
+        el_reseed = max_over_ranks(time.perf_counter() - t0, world)
 
     points = float(n) * n * C * args.steps * world
     value = points / el_max
@@ -459,12 +462,13 @@ def main():
             "frame_hbm_bytes_per_point": pass_bytes[0] + pass_bytes[1],
         },
     }
-    out["reseed_every_frame"] = {
-        "what": "the reference app's loop: CalculateOcean(dt, updateOcean=true) each frame, h0 re-seeded "
-                "(src/Waves.cpp:91-94)",
-        "ms_per_step": 1000.0 * el_reseed / args.steps,
-        "points_per_s": float(n) * n * C * args.steps * world / el_reseed,
-    }
+    if el_reseed is not None:
+        out["reseed_every_frame"] = {
+            "what": "the reference app's loop: CalculateOcean(dt, updateOcean=true) each frame, h0 re-seeded "
+                    "(src/Waves.cpp:91-94)",
+            "ms_per_step": 1000.0 * el_reseed / args.steps,
+            "points_per_s": float(n) * n * C * args.steps * world / el_reseed,
+        }
     if not args.no_profile and cnt[1] > 0 and cnt[2] > 0:
         p1_ms, p2_ms = ms[1] / cnt[1], ms[2] / cnt[2]
         per_launch_pts = float(n) * n * C

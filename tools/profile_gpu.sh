@@ -6,7 +6,7 @@
 # Counters are never combined with tracing domains (pool rule), and each step has its own limit.
 set -u
 cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
-ARGS=${BENCH_ARGS:-"--steps 20 --warmup 3 --no-cpu-baseline --no-slab --no-ifft --no-surface"}
+ARGS=${BENCH_ARGS:-"--steps 20 --warmup 3 --no-cpu-baseline --no-slab --no-ifft --no-surface --no-reseed"}
 KRE=${KERNEL_REGEX:-"k_cols_evolve|k_rows_final|k_rows_ifft|k_rows_half|k_cols|k_generate_spectrum|k_half_nyquist"}
 mkdir -p gpurun_out
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -T -d gpurun_out/prof_trace -o trace --output-format csv \

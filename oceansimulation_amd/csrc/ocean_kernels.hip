@@ -565,11 +565,12 @@ struct HalfCfg
 // (xcd_pair_slot); pass 1 stores 128-B pieces. Against strips (RG = 1): pass 2 1.637 -> 1.506 ms,
 // pass 1 0.934 -> 0.960 ms, frame 2.581 -> 2.477 ms at 8 x 4096^2 (tools/microbench/halfbench).
 constexpr int kHalfRG = 2, kHalfRGC = 4;
-template <int LOGN, int RG>
+// FB: columns per field strip (4 = the h0 strip; 2 = k_cols_half2's half strips, FS = 2 STRIPS).
+template <int LOGN, int RG, int FB = 4>
 __device__ __forceinline__ int half_group_offset(int y, int strip, int b = 0)
 {
-  constexpr int N = HalfCfg<LOGN>::N, B = HalfCfg<LOGN>::B, STRIPS = HalfCfg<LOGN>::STRIPS;
-  return RG == 1 ? (strip * N + y) * B + b : (((y / RG) * STRIPS + strip) * RG + (y % RG)) * B + b;
+  constexpr int N = HalfCfg<LOGN>::N, FS = HalfCfg<LOGN>::STRIPS * HalfCfg<LOGN>::B / FB;
+  return RG == 1 ? (strip * N + y) * FB + b : (((y / RG) * FS + strip) * RG + (y % RG)) * FB + b;
 }
 
 // Pass 1: per strip of B columns (u >= 0, or the Nyquist strip), three y-iFFT rounds of CPairs:
@@ -759,6 +760,111 @@ __global__ __launch_bounds__(ColFirstCfg<LOGN>::WG1) void k_cols_half(FrameParam
   }
 }
 
+// Pass 1 on half strips (whole grids): a 2T-thread workgroup (512 at N = 4096, 256 VGPRs, one per
+// CU) transforms 2 columns per item, so the thread's 16 evolved amplitudes H stay in VGPRs (32)
+// across the three rounds: no H scratch (k_cols_half<HS> moves 24 B per kept texel through it).
+// Field strips are FB = 2 columns wide (half_group_offset<.., 2>): with RG rows per group, one store
+// instruction of a wave (32 rows x 2 columns) writes whole 128-B lines when RG * 2 * 16 B = 128 B
+// (gab, gde: RG = 4; gc: RGC = 8). The two halves of an h0 strip (items 2p, 2p + 1) run together
+// on one XCD (xcd_pair_slot), so each 64-B h0 row is fetched once for both (default-policy loads).
+// The Nyquist strip's second half (columns 2, 3: u < 0) is not needed and is skipped. The exchange
+// moves whole CPairs (2 x PADDED x 16 B = 139 KiB of LDS at N = 4096).
+// A/B only (launch_half_columns variants 12..14 with launch_half_rows 12..14; halfbench,
+// profiles/r01_halfbench_halfstrips.log): pass 1 takes 0.81 ms against 0.96, but pass 2 then reads
+// half lines (a 2-row item holds half of each 4-row x 2-column line): 1.64 ms against 1.52, frame
+// 2.447 against 2.486 ms. Half-line stores (RG = 2, paired workgroups, default policy) lose the pass-1
+// gain instead (0.96 ms). Production keeps 4-column items with the H scratch.
+// The field CPair of a round: (A, B), (D, E) or (C, 0) from H (k_cols_half's pack).
+template <int LOGN>
+__device__ __forceinline__ CPair half_round_pack(int round, float2 H, const KVec& q)
+{
+  if (round == 0)  // (A, B) = (H, kz H)
+    return CPair{f2v{H.x, q.kz * H.x}, f2v{H.y, q.kz * H.y}};
+  if (round == 1)  // (D, E) = (kz H / |k|, kz^2 H / |k|)
+  {
+    const float e = q.kz * q.dirz;
+    return CPair{f2v{q.dirz * H.x, e * H.x}, f2v{q.dirz * H.y, e * H.y}};
+  }
+  return CPair{f2v{q.inv * H.x, 0.0f}, f2v{q.inv * H.y, 0.0f}};  // (C, 0) = (H / |k|, 0)
+}
+
+// SAC: gc's store policy (default: SA).
+template <int LOGN, int LA = 0, int SA = kStream, int RG = 4, int RGC = 8, int SAC = SA>
+__global__ __launch_bounds__(2 * FftShape<LOGN>::T) void k_cols_half2(FrameParams fp, const float4* __restrict__ h0,
+                                                                      float4* __restrict__ gab, float4* __restrict__ gde,
+                                                                      float2* __restrict__ gc,
+                                                                      const float2* __restrict__ tw_glob)
+{
+  using S = FftShape<LOGN>;
+  using K = ColFirstCfg<LOGN>;
+  using HC = HalfCfg<LOGN>;
+  constexpr int N = S::N, T = S::T, B = K::B, STRIPS = HC::STRIPS, FS = 2 * STRIPS;
+  static_assert(HC::SUPPORTED && B == 4, "half strips of 4-column h0 strips");
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  float2* tw = reinterpret_cast<float2*>(smem);
+  void* xch = smem + ((S::TW_ENTRIES * 8 + 15) / 16) * 16;
+  load_twiddles<LOGN>(tw, tw_glob);
+
+  const int total = fp.cascades * FS;
+  const float dim = (float)N;
+  for (int item = xcd_pair_slot(blockIdx.x, gridDim.x); item < total; item += gridDim.x)
+  {
+    const int c = item / FS, fs = item - c * FS, s = fs >> 1, h = fs & 1;
+    if (s == STRIPS - 1 && h == 1)
+      continue;  // Nyquist strip, columns 2 and 3 (u < 0): unused (uniform per workgroup)
+    const int xb = s == STRIPS - 1 ? 0 : N / (2 * B) + s;
+    const CascadeFrame f = fp.c[c];
+    const float4* src = h0 + ((size_t)c * (N / B) + xb) * N * B;
+    const size_t cbase = (size_t)c * STRIPS * N * B;
+    const size_t gbase = cbase + half_group_offset<LOGN, RG, 2>(0, fs);
+    const size_t cgbase = cbase + half_group_offset<LOGN, RGC, 2>(0, fs);
+    float2 H[16];
+    {
+      const int tid = opaque((int)threadIdx.x);
+      const int b2 = tid % 2, i = (tid / 2) % T, x = xb * B + 2 * h + b2;
+      const int voff = (i * B + 2 * h + b2) * 16;
+      float4 a[16];
+#pragma unroll
+      for (int m = 0; m < 16; m++)  // fftShift on y folded into the load
+        a[m] = ld4<LA>(src + ((m + 8) & 15) * T * B, voff);
+#pragma unroll
+      for (int m = 0; m < 16; m++)
+      {
+        const int y = i + ((m + 8) & 15) * T;
+        H[m] = evolve(a[m], make_kvec(x, y, dim, f.dk).k, f);
+      }
+    }
+#pragma unroll
+    for (int round = 0; round < 3; round++)
+    {
+      // k-vectors recomputed per round (opaque: CSE would keep 48 of them live)
+      const int tr = opaque((int)threadIdx.x);
+      const int br = tr % 2, ir = (tr / 2) % T, xr = xb * B + 2 * h + br;
+      CPair v[16];
+#pragma unroll
+      for (int m = 0; m < 16; m++)
+      {
+        const int y = ir + ((m + 8) & 15) * T;
+        v[m] = half_round_pack<LOGN>(round, H[m], make_kvec(xr, y, dim, f.dk));
+      }
+      fft_run<LOGN, 2, false>(v, ir, br, xch, tw);
+#pragma unroll
+      for (int m = 0; m < 16; m++)
+      {
+        if (round == 0)
+          st4<SA>(gab + gbase + half_group_offset<LOGN, RG, 2>(m * T, 0), half_group_offset<LOGN, RG, 2>(ir, 0, br) * 16,
+                  pair_raw(v[m]));
+        else if (round == 1)
+          st4<SA>(gde + gbase + half_group_offset<LOGN, RG, 2>(m * T, 0), half_group_offset<LOGN, RG, 2>(ir, 0, br) * 16,
+                  pair_raw(v[m]));
+        else
+          st2<SAC>(gc + cgbase + half_group_offset<LOGN, RGC, 2>(m * T, 0), half_group_offset<LOGN, RGC, 2>(ir, 0, br) * 8,
+                  make_float2(v[m].re.x, v[m].im.x));
+      }
+    }
+  }
+}
+
 // The Nyquist-row term: for u = -u' (0 < u' < N/2) the pass-2 rebuild s_F conj(G_F(q, u')) misses
 // (-1)^q Delta_F(u'), Delta_F(u') = F(-N/2, -u') - s_F conj(F(-N/2, u')). Its lanes (the kx
 // factors of pass 2 applied to Delta) form one row spectrum per image, spec[c][img][x] (zero
@@ -834,8 +940,10 @@ __global__ __launch_bounds__(256) void k_half_nyquist(FrameParams fp, int n, int
 // RM (strip-dealt path, after k_half_to_rows): the fields are row-major [c][rows][kp], column u' = u
 // for u in [0, N/2] (u' = N/2: the Nyquist column), and the pass covers `rows` rows (a slab's w).
 // RG / RGC (whole grids): the field layout pass 1 wrote (half_group_offset).
+// FB: the field strips' width (half_group_offset); GRP: consecutive items run together on one XCD
+// (2: pairs, xcd_pair_slot; 4: FB = 2 with RGC = 8, where four items share each gc line).
 template <int LOGN, int LA = kStream, int SA = kStream, int ABL = 0, int RPW_ = 2, bool BOTH = false, bool RM = false,
-          int RG = 1, int RGC = 1>
+          int RG = 1, int RGC = 1, int FB = 4, int GRP = 2>
 __global__ __launch_bounds__(FftShape<LOGN>::T * RPW_) void k_rows_half(
     FrameParams fp, const float4* __restrict__ gab, const float4* __restrict__ gde, const float2* __restrict__ gc,
     const float4* __restrict__ spec, float4* __restrict__ maps, float* __restrict__ jac, FoamParams foam,
@@ -859,7 +967,9 @@ __global__ __launch_bounds__(FftShape<LOGN>::T * RPW_) void k_rows_half(
   const float dim = (float)N;
   // RPW = 2: C's row pairs are 64-B halves of 128-B lines; items 2p, 2p+1 (the same line) run
   // together on one XCD so the line is fetched once
-  for (int item = RPW == 2 ? xcd_pair_slot(blockIdx.x, gridDim.x) : blockIdx.x; item < total; item += gridDim.x)
+  for (int item = RPW != 2 ? blockIdx.x : GRP == 4 ? xcd_group_slot<4>(blockIdx.x, gridDim.x)
+                                                    : xcd_pair_slot(blockIdx.x, gridDim.x);
+       item < total; item += gridDim.x)
   {
     const int cimg0 = item / blocks, y0 = (item - cimg0 * blocks) * RPW;
     float2 ckeep[8];  // BOTH: image 0's C loads, reused by image 1
@@ -883,8 +993,8 @@ __global__ __launch_bounds__(FftShape<LOGN>::T * RPW_) void k_rows_half(
     for (int m = 0; m < 8; m++)
     {
       const int u = m * T + i;               // >= 0, column x = N/2 + u
-      const int off = RM ? r * kp + u : half_group_offset<LOGN, RG>(y, u / B, u % B);
-      const int offc = RM ? off : half_group_offset<LOGN, RGC>(y, u / B, u % B);
+      const int off = RM ? r * kp + u : half_group_offset<LOGN, RG, FB>(y, u / FB, u % FB);
+      const int offc = RM ? off : half_group_offset<LOGN, RGC, FB>(y, u / FB, u % FB);
       const float kx = (float)u * dk;        // ((float)x - N/2) dk, x - N/2 exact
       const float4 s4 = ld4<0>(sp, (N / 2 - u) * 16);  // the -u column's Nyquist-row term (x = N/2 - u)
       CPair own, neg;
@@ -942,8 +1052,8 @@ __global__ __launch_bounds__(FftShape<LOGN>::T * RPW_) void k_rows_half(
       else if (i == 0 && m == 8)
       {
         // Nyquist column: first column of the last strip
-        const int off = RM ? r * kp + N / 2 : half_group_offset<LOGN, RG>(y, N / 2 / B);
-        const int offc = RM ? off : half_group_offset<LOGN, RGC>(y, N / 2 / B);
+        const int off = RM ? r * kp + N / 2 : half_group_offset<LOGN, RG, FB>(y, N / 2 / FB);
+        const int offc = RM ? off : half_group_offset<LOGN, RGC, FB>(y, N / 2 / FB);
         const float kx = -(dim / 2.0f) * dk;
         float2 cc;
         if (BOTH && img == 1)
@@ -1396,6 +1506,16 @@ hipError_t launch_half_columns(int logn, const FrameParams& fp, const float4* h0
                        : variant == 6 ? k_cols_half<LOGN, kStream, kStream, true, false, false, 4, 4>
                        : variant == 7 ? k_cols_half<LOGN, kStream, kStream, true, false, false, 1, 1>
                                       : k_cols_half<LOGN, kStream, kStream, true, false, false, RG, RGC>;
+      if (variant >= 12 && variant <= 14 && !seed)  // half-strip items (k_cols_half2): H in VGPRs
+      {
+        auto hk = variant == 12   ? k_cols_half2<LOGN, 0, kStream, 4, 8>
+                  : variant == 13 ? k_cols_half2<LOGN, 0, 0, 2, 4>
+                                  : k_cols_half2<LOGN, 0, kStream, 4, 4, 0>;
+        const int hlds = ((S::TW_ENTRIES * 8 + 15) / 16) * 16 + 2 * S::PADDED * 16;
+        const int hg = persistent_grid(hk, 2 * S::T, hlds, fp.cascades * 2 * HalfCfg<LOGN>::STRIPS, cus);
+        hipLaunchKernelGGL(hk, dim3(hg), dim3(2 * S::T), hlds, stream, fp, h0, gab, gcd, ge, tw);
+        return hipGetLastError();
+      }
       const int lds = ((S::TW_ENTRIES * 8 + 15) / 16) * 16 + K::LDS1;
       int grid = persistent_grid(kern, K::WG1, lds, fp.cascades * HalfCfg<LOGN>::STRIPS, cus);
       if (hs && grid > hs_blocks)
@@ -1438,6 +1558,9 @@ hipError_t launch_half_rows(int logn, const FrameParams& fp, const float4* gab, 
                   : ablation == 9 ? k_rows_half<LOGN, 0, kStream, 0, 2, true, false, 2, 4>
                   : ablation == 10 ? k_rows_half<LOGN, 0, kStream, 0, 2, true, false, 4, 4>
                   : ablation == 11 ? k_rows_half<LOGN, 0, kStream, 0, 2, true, false, 1, 1>
+                  : ablation == 12 ? k_rows_half<LOGN, 0, kStream, 0, 2, true, false, 4, 8, 2, 4>
+                  : ablation == 13 ? k_rows_half<LOGN, 0, kStream, 0, 2, true, false, 2, 4, 2, 2>
+                  : ablation == 14 ? k_rows_half<LOGN, 0, kStream, 0, 2, true, false, 4, 4, 2, 2>
                   : ablation == 7 ? k_rows_half<LOGN, kStream, kStream, 0, 2, true, false, RG, RGC>
                   : ablation == 6 ? k_rows_half<LOGN, kStream, kStream, 0, 2, false, false, RG, RGC>
                   : ablation == 1 ? k_rows_half<LOGN, kStream, kStream, 1>

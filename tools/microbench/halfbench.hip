@@ -187,10 +187,11 @@ int main(int argc, char** argv)
     CHECK(hipDeviceSynchronize());
     auto pm = snap(maps, mb), pj = snap(jac, jb);
     const char* ln[] = {"production layout (RG 2, RGC 4)", "layout RG 1, RGC 1 (strips)", "layout RG 2, RGC 2",
-                        "layout RG 4, RGC 4"};
-    const int cv[] = {0, 7, 4, 6}, rv[] = {0, 11, 8, 10};
-    bool same[4] = {true, true, true, true};
-    for (int v = 1; v < 4; v++)
+                        "layout RG 4, RGC 4", "half strips RG 4, RGC 8 (cols2)", "half strips RG 2, RGC 4, dflt st",
+                        "half strips RG 4, RGC 4, gc dflt st"};
+    const int NV = 7, cv[] = {0, 7, 4, 6, 12, 13, 14}, rv[] = {0, 11, 8, 10, 12, 13, 14};
+    bool same[7] = {true, true, true, true, true, true, true};
+    for (int v = 1; v < NV; v++)
     {
       CHECK(hipMemset(maps, 0, mb));
       CHECK(hipMemset(jac, 0, jb));
@@ -200,9 +201,9 @@ int main(int argc, char** argv)
       std::printf("%s vs production frame:\n", ln[v]);
       same[v] = (int)diff(snap(maps, mb), pm) & (int)diff(snap(jac, jb), pj);
     }
-    std::vector<std::vector<float>> tc(4), tr(4), tf(4);
+    std::vector<std::vector<float>> tc(NV), tr(NV), tf(NV);
     for (int r = 0; r < 7; r++)
-      for (int v = 0; v < 4; v++)
+      for (int v = 0; v < NV; v++)
       {
         auto cl = [&] { return launch_half_columns(logn, fp, h0, gab, gcd, ge, spec, tw, 0, cus, hs, cus, nullptr, cv[v]); };
         auto rl = [&] { return launch_half_rows(logn, fp, gab, gcd, ge, spec, maps, jac, foam, tw, 0, cus, rv[v]); };
@@ -210,7 +211,7 @@ int main(int argc, char** argv)
         tr[v].push_back(time_ms(rl, 10));
         tf[v].push_back(time_ms([&] { hipError_t e = cl(); return e == hipSuccess ? rl() : e; }, 10));
       }
-    for (int v = 0; v < 4; v++)
+    for (int v = 0; v < NV; v++)
     {
       std::sort(tc[v].begin(), tc[v].end());
       std::sort(tr[v].begin(), tr[v].end());

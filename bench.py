@@ -55,6 +55,9 @@ def parse():
     ap.add_argument("--no-ifft", action="store_true", help="skip the EncodeIFFT-only and rocFFT legs")
     ap.add_argument("--no-surface", action="store_true", help="skip the surface-consumer leg")
     ap.add_argument("--no-reseed", action="store_true", help="skip the re-seed-every-frame leg")
+    ap.add_argument("--legs-timeout", type=float, default=300.0,
+                    help="seconds allowed for the optional legs after the headline measurement; past it the "
+                         "line is printed without the unfinished legs and every rank exits")
     ap.add_argument("--full-spectrum", action="store_true",
                     help="time the full-spectrum frame path instead of the default half-spectrum one")
     ap.add_argument("--slab-n", type=int, default=16384, help="side of the single slab-decomposed grid")
@@ -140,6 +143,51 @@ def measured_traffic(kernel: str, n: int, cascades: int):
             return {"hbm_traffic_bytes": rec["hbm_traffic_bytes"],
                     "source": f"{os.path.relpath(path, ROOT)} (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, same workload)"}
     return None
+
+
+class _LegsWatchdog:
+    """The optional legs run after the headline measurement. If they have not finished within the
+    deadline (e.g. a collective that never completes on a misconfigured node), rank 0 prints the line
+    it has, with "legs_timeout" naming what was cut, and every rank exits, so the headline number is
+    never lost behind an optional leg."""
+
+    def __init__(self, out: dict, rank: int, seconds: float):
+        import threading
+
+        self.out, self.rank = out, rank
+        self.lock = threading.Lock()
+        self.done = False
+        self.timer = threading.Timer(seconds, self._expire)
+        self.timer.daemon = True
+        self.seconds = seconds
+
+    def _expire(self):
+        with self.lock:
+            if self.done:
+                return
+            self.done = True
+            if self.rank == 0:
+                line = {k: v for k, v in list(self.out.items())}
+                line["legs_timeout"] = f"optional legs unfinished after {self.seconds:.0f} s; headline unaffected"
+                print(json.dumps(line), flush=True)
+            sys.stdout.flush()
+            os._exit(0)
+
+    def finish(self) -> bool:
+        """True if the legs finished first (the caller prints); False if the watchdog already has."""
+        with self.lock:
+            if self.done:
+                return False
+            self.done = True
+        self.timer.cancel()
+        return True
+
+
+def start_legs_watchdog(out: dict, rank: int, seconds: float) -> _LegsWatchdog:
+    w = _LegsWatchdog(out, rank, seconds)
+    if seconds > 0:
+        w.timer.start()
+    return w
 
 
 def cpu_baseline(n: int, target_s: float):
@@ -508,6 +556,7 @@ def main():
         out["kernels"]["h0_seed_ms"] = h0_ms
     gen.close()
     fft.close()
+    watchdog = start_legs_watchdog(out, rank, args.legs_timeout)
     if not args.no_ifft:
         try:
             out["ifft_only"] = ifft_legs(n, C)
@@ -525,6 +574,8 @@ def main():
             out["slab"] = {"error": f"{type(e).__name__}: {e}"}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(n, args.cpu_seconds)
+    if not watchdog.finish():
+        return  # the watchdog printed the line and is ending the process
     if rank == 0:
         print(json.dumps(out), flush=True)
     import torch.distributed as dist

@@ -58,3 +58,31 @@ def test_python_mirror_settings_helpers():
     assert s.planeSize == 17.0 and (s.seed[0], s.seed[1]) == (1, 2) and s.U_10 == 40.0
     ocean.apply_settings(s, time=2.5)
     assert s.time == 2.5
+
+
+def test_bench_legs_watchdog_prints_headline_and_exits():
+    """bench.py's optional legs run under a deadline: past it, rank 0 prints the headline line it
+    has (with "legs_timeout") and the process exits 0, so a stuck optional leg never loses the
+    measurement; legs that finish first cancel it and the caller prints."""
+    import json
+    import os
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    code = ("import sys, time; sys.path.insert(0, %r); import bench\n"
+            "out = {'metric': 'm', 'value': 1.0}\n"
+            "w = bench.start_legs_watchdog(out, 0, 0.2)\n"
+            "time.sleep(5)\n"
+            "print('not reached')\n") % root
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=60)
+    assert r.returncode == 0, r.stderr
+    lines = [l for l in r.stdout.splitlines() if l.strip()]
+    assert len(lines) == 1, r.stdout
+    line = json.loads(lines[0])
+    assert line["value"] == 1.0 and "legs_timeout" in line
+    code = ("import sys; sys.path.insert(0, %r); import bench\n"
+            "w = bench.start_legs_watchdog({'value': 2.0}, 0, 30.0)\n"
+            "print('finished', w.finish())\n") % root
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=60)
+    assert r.returncode == 0 and r.stdout.strip() == "finished True", (r.stdout, r.stderr)

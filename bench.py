@@ -10,14 +10,20 @@ Workload (BASELINE.json configs[3], per GPU): 8 independent 4096^2 cascades, def
 sizes 5/17/101/251/509/1021/2039/4093 m (extending src/Waves.cpp:27). Ranks own disjoint cascade
 sets (seed offset 4097*rank: non-overlapping noise tiles) — weak scaling, no data-path collective.
 
-Launch: python bench.py [--gpus N --steps K --warmup W]; N > 1 via torch.distributed.run, one rank
-per GPU (RCCL only for the barrier and the max-over-ranks timing reduction).
+Launch: python bench.py [--gpus N --steps K --warmup W], one rank per GPU. Under torch.distributed.run
+(WORLD_SIZE set) the process is one rank. Started directly with --gpus N > 1, it first checks that N
+GPUs are visible, then starts `python -m torch.distributed.run --nproc-per-node N bench.py ...` as a
+child process (before anything touches the GPU; no exec) and exits with the child's status; rank 0
+of the child job prints the one JSON line. RCCL carries the barrier, the max-over-ranks timing
+reduction and the config-5 slab all-to-all; the independent cascades use no collective.
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -41,7 +47,10 @@ def frame_bytes_per_point(n: int, half: bool):
     return 16.0 * kept + 40.0 * kept, 40.0 * kept + 36.0
 
 
-def parse():
+METRIC = "height-field points/sec (N² iFFT) at 1/2/4/8 MI355X; % HBM roofline"
+
+
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
@@ -70,16 +79,69 @@ def parse():
     ap.add_argument("--slab-force-exchange", action="store_true",
                     help="run the RCCL exchange and the pipeline even at world size 1 (plumbing check "
                          "under torch.distributed.run --nproc-per-node 1)")
-    return ap.parse_args()
+    ap.add_argument("--plumbing-check", action="store_true",
+                    help="launcher/rank plumbing only (no GPU work): every rank joins the process group, "
+                         "runs the barrier + max-over-ranks protocol, and rank 0 prints a line naming n_gpus")
+    return ap.parse_args(argv)
 
 
-def dist_setup(force: bool = False, shared_gpu: bool = False):
+LEGS_TIMEOUT_RC = 3  # exit status when the optional legs overran their deadline (headline still printed)
+
+
+def _free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def visible_gpus() -> int:
+    """GPUs this process could use, counted without initialising the HIP runtime (on this image
+    torch.cuda.device_count() does not initialise it), so a child may still be started."""
+    import torch
+
+    return torch.cuda.device_count()
+
+
+def launch_ranks(args, argv) -> int:
+    """`--gpus N` (N > 1) started without a launcher: run N ranks as a child job of
+    torch.distributed.run on 127.0.0.1 and return its exit status. Nothing in this process touches
+    the GPU (no exec after a HIP call: the child is a separate process). Fails loudly when fewer
+    than N GPUs are visible, unless --shared-gpu/--plumbing-check (rehearsals that need no N GPUs)."""
+    if not (args.shared_gpu or args.plumbing_check):
+        have = visible_gpus()
+        if have < args.gpus:
+            print(f"bench.py: --gpus {args.gpus} requested but only {have} GPU(s) are visible; refusing to "
+                  f"report a {args.gpus}-GPU number (use --shared-gpu to rehearse ranks on one GPU)",
+                  file=sys.stderr, flush=True)
+            return 2
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}", os.path.abspath(__file__)] + list(argv)
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # dmabuf IPC, required by RCCL on this host driver
+    return subprocess.run(cmd, env=env).returncode
+
+
+def plumbing_check(args, rank: int, world: int) -> None:
+    """No GPU work: the rank protocol the timed legs use (barrier, max over ranks) and the line shape."""
+    barrier(world)
+    el = max_over_ranks(0.001 * (rank + 1), world)
+    barrier(world)
+    if rank == 0:
+        print(json.dumps({"metric": METRIC, "plumbing": True, "n_gpus": world, "gpus_requested": args.gpus,
+                          "max_over_ranks_s": el}), flush=True)
+
+
+def dist_setup(force: bool = False, shared_gpu: bool = False, plumbing: bool = False):
     import torch
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = 0 if shared_gpu else int(os.environ.get("LOCAL_RANK", "0"))
-    if torch.cuda.is_available():
+    if plumbing:
+        shared_gpu = True  # gloo, no device work
+    elif torch.cuda.is_available():
         torch.cuda.set_device(local)
     if world > 1 or (force and "MASTER_ADDR" in os.environ):
         import torch.distributed as dist
@@ -148,8 +210,8 @@ def measured_traffic(kernel: str, n: int, cascades: int):
 class _LegsWatchdog:
     """The optional legs run after the headline measurement. If they have not finished within the
     deadline (e.g. a collective that never completes on a misconfigured node), rank 0 prints the line
-    it has, with "legs_timeout" naming what was cut, and every rank exits, so the headline number is
-    never lost behind an optional leg."""
+    it has, with "legs_timeout" naming what was cut, and every rank exits with LEGS_TIMEOUT_RC, so the
+    headline number is never lost behind an optional leg and the run still reads as failed."""
 
     def __init__(self, out: dict, rank: int, seconds: float):
         import threading
@@ -171,7 +233,9 @@ class _LegsWatchdog:
                 line["legs_timeout"] = f"optional legs unfinished after {self.seconds:.0f} s; headline unaffected"
                 print(json.dumps(line), flush=True)
             sys.stdout.flush()
-            os._exit(0)
+            sys.stderr.write(f"bench.py: optional legs overran {self.seconds:.0f} s; exiting {LEGS_TIMEOUT_RC}\n")
+            sys.stderr.flush()
+            os._exit(LEGS_TIMEOUT_RC)
 
     def finish(self) -> bool:
         """True if the legs finished first (the caller prints); False if the watchdog already has."""
@@ -190,12 +254,30 @@ def start_legs_watchdog(out: dict, rank: int, seconds: float) -> _LegsWatchdog:
     return w
 
 
+def host_cores():
+    """(threads to use, CPUs the machine has, CPUs this process may run on). The threads are the
+    process's CPU share: OMP_NUM_THREADS when the host sets it (the GPU box sets it to its share of
+    a machine whose os.cpu_count() is many times larger), else the affinity mask."""
+    machine = os.cpu_count() or 1
+    try:
+        affinity = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        affinity = machine
+    try:
+        share = int(os.environ.get("OMP_NUM_THREADS", "0"))
+    except ValueError:
+        share = 0
+    threads = min(share, affinity) if share > 0 else affinity
+    return max(1, threads), machine, affinity
+
+
 def cpu_baseline(n: int, target_s: float):
-    """The oracle (CPU restatement of the reference FFTCalculator/Generator) on host cores."""
+    """The oracle (CPU restatement of the reference FFTCalculator/Generator) on the host cores this
+    process has (host_cores())."""
     from oracle import oracle as O
 
     O.build()
-    threads = min(16, os.cpu_count() or 1)
+    threads, machine, affinity = host_cores()
     O.set_threads(threads)
     g = O.OracleGenerator(n, O.default_settings(planeSize=PLANES[0]))
     g.calculate_ocean(1.0 / 60.0)  # seeds h0 (excluded, like the GPU warm-up)
@@ -210,6 +292,10 @@ def cpu_baseline(n: int, target_s: float):
         "value": n * n * frames / el,
         "unit": "height-field points/s",
         "cores": O.get_threads(),
+        "host_cpus": machine,
+        "affinity_cpus": affinity,
+        "cores_note": "cores = OpenMP threads used = this process's CPU share (OMP_NUM_THREADS, else the "
+                      "affinity mask); host_cpus = os.cpu_count() of the whole machine",
         "kind": "port",
         "sample": f"1 cascade {n}x{n}, {frames} frames of CalculateOcean (fp32 radix-2 restatement of "
                   f"src/FFTCalculator.cpp + spectrum.compute, OpenMP {O.get_threads()} threads), {el:.1f} s",
@@ -296,7 +382,7 @@ def surface_leg(calls: int = 20, cpu_seconds: float = 3.0) -> dict:
                               "GB_per_s_output": 32.0 * pts / (ms * 1e-3) / 1e9}
         del buf
     O.build()
-    O.set_threads(min(16, os.cpu_count() or 1))
+    O.set_threads(host_cores()[0])
     host = host_cascades(pairs)
     frames, t0 = 0, time.perf_counter()
     while time.perf_counter() - t0 < cpu_seconds:
@@ -425,8 +511,19 @@ def slab_grid(args, rank: int, world: int, local: int) -> dict:
     return out
 
 
-def main():
-    args = parse()
+def main(argv=None):
+    argv = sys.argv[1:] if argv is None else argv
+    args = parse(argv)
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        return launch_ranks(args, argv)
+    if "WORLD_SIZE" in os.environ and int(os.environ["WORLD_SIZE"]) != args.gpus:
+        print(f"bench.py: WORLD_SIZE={os.environ['WORLD_SIZE']} but --gpus {args.gpus}", file=sys.stderr, flush=True)
+        return 2
+    if args.plumbing_check:
+        rank, world, _ = dist_setup(plumbing=True)
+        plumbing_check(args, rank, world)
+        _teardown()
+        return 0
     rank, world, local = dist_setup(force=args.slab_force_exchange, shared_gpu=args.shared_gpu)
     import oceansimulation_amd as ocean
 
@@ -487,7 +584,7 @@ def main():
     points = float(n) * n * C * args.steps * world
     value = points / el_max
     out = {
-        "metric": "height-field points/sec (N² iFFT) at 1/2/4/8 MI355X; % HBM roofline",
+        "metric": METRIC,
         "value": value,
         "unit": "height-field points/s",
         "n_gpus": world,
@@ -575,9 +672,14 @@ def main():
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(n, args.cpu_seconds)
     if not watchdog.finish():
-        return  # the watchdog printed the line and is ending the process
+        return LEGS_TIMEOUT_RC  # the watchdog printed the line and is ending the process
     if rank == 0:
         print(json.dumps(out), flush=True)
+    _teardown()
+    return 0
+
+
+def _teardown():
     import torch.distributed as dist
 
     if dist.is_available() and dist.is_initialized():
@@ -586,4 +688,4 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

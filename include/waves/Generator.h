@@ -5,6 +5,8 @@
 
 #include <cstddef>
 #include <cstdint>
+#include <type_traits>
+#include <utility>
 
 #include "oceanfft.h"
 #include "vision/RenderDevice.h"
@@ -13,11 +15,31 @@
 namespace Waves
 {
 
-// glm::ivec2 stand-in with the same layout (the reference's only glm use in the settings).
+// glm::ivec2 stand-in with the same layout (the reference's only glm use in the settings,
+// src/Generator.h:14). It converts to and from any {x, y} vector type, so reference code that
+// writes `settings.seed = glm::ivec2(a, b)` (or reads it back into one) compiles unchanged.
 struct IVec2
 {
-  int32_t x, y;
+  int32_t x = 0, y = 0;
+
+  constexpr IVec2() = default;
+  constexpr IVec2(int32_t x_, int32_t y_) : x(x_), y(y_) {}
+  template <class V, class = decltype(std::declval<const V&>().x + std::declval<const V&>().y),
+            class = std::enable_if_t<!std::is_same<std::decay_t<V>, IVec2>::value>>
+  constexpr IVec2(const V& v) : x(static_cast<int32_t>(v.x)), y(static_cast<int32_t>(v.y))
+  {
+  }
+  template <class V, class = decltype(V{int32_t{}, int32_t{}})>
+  constexpr explicit operator V() const
+  {
+    return V{x, y};
+  }
+  int32_t& operator[](int i) { return i == 0 ? x : y; }
+  const int32_t& operator[](int i) const { return i == 0 ? x : y; }
+  friend constexpr bool operator==(const IVec2& a, const IVec2& b) { return a.x == b.x && a.y == b.y; }
+  friend constexpr bool operator!=(const IVec2& a, const IVec2& b) { return !(a == b); }
 };
+static_assert(sizeof(IVec2) == 8 && std::is_trivially_copyable<IVec2>::value, "IVec2 must match glm::ivec2");
 
 // src/Generator.h:12-30 — identical defaults and 64-byte layout.
 struct GeneratorSettings

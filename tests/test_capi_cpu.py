@@ -114,6 +114,30 @@ def test_cpp_headers_compile_standalone(tmp_path):
     assert r.returncode == 0, r.stderr
 
 
+def test_seed_assigns_from_glm_ivec2_shaped_types(tmp_path):
+    """Reference code sets the seed as a glm::ivec2 (src/Generator.h:14): the drop-in's seed type
+    converts from and to any {x, y} vector type, keeping the 64-byte layout. glm itself is absent
+    here, so the test declares a vector type of the same shape."""
+    src = tmp_path / "seed.cpp"
+    src.write_text(
+        '#include "waves/Generator.h"\n'
+        "namespace glm { struct ivec2 { int x, y; ivec2() : x(0), y(0) {} ivec2(int a, int b) : x(a), y(b) {} }; }\n"
+        "int main() {\n"
+        "  Waves::GeneratorSettings s;\n"
+        "  if (s.seed.x != 12342 || s.seed.y != 8934) return 1;\n"
+        "  s.seed = glm::ivec2(7, 9);\n"
+        "  glm::ivec2 back = glm::ivec2(s.seed);\n"
+        "  Waves::GeneratorSettings t = s;\n"
+        "  static_assert(sizeof(Waves::GeneratorSettings) == 64, \"layout\");\n"
+        "  return (back.x == 7 && back.y == 9 && t.seed == s.seed && s.seed[1] == 9) ? 0 : 2;\n"
+        "}\n")
+    exe = tmp_path / "seed"
+    r = subprocess.run(["g++", "-std=c++17", f"-I{ROOT}/include", "-I/opt/rocm/include", "-D__HIP_PLATFORM_AMD__",
+                        str(src), "-o", str(exe)], capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
+    assert subprocess.run([str(exe)]).returncode == 0
+
+
 def test_waveapp_headless_rejects_bad_arguments():
     """The headless driver parses its script before touching a device (exit 2 = usage)."""
     import subprocess

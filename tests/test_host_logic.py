@@ -76,7 +76,7 @@ def test_bench_legs_watchdog_prints_headline_and_exits():
             "time.sleep(5)\n"
             "print('not reached')\n") % root
     r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=60)
-    assert r.returncode == 0, r.stderr
+    assert r.returncode == _bench().LEGS_TIMEOUT_RC == 3, (r.returncode, r.stderr)
     lines = [l for l in r.stdout.splitlines() if l.strip()]
     assert len(lines) == 1, r.stdout
     line = json.loads(lines[0])
@@ -86,3 +86,47 @@ def test_bench_legs_watchdog_prints_headline_and_exits():
             "print('finished', w.finish())\n") % root
     r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=60)
     assert r.returncode == 0 and r.stdout.strip() == "finished True", (r.stdout, r.stderr)
+
+
+def _run_bench(args, timeout=240):
+    import subprocess
+    import sys
+
+    env = dict(os.environ)
+    env.pop("WORLD_SIZE", None)
+    env.pop("RANK", None)
+    env.pop("LOCAL_RANK", None)
+    return subprocess.run([sys.executable, os.path.join(ROOT, "bench.py")] + args, capture_output=True, text=True,
+                          timeout=timeout, env=env, cwd=ROOT)
+
+
+def test_bench_gpus_n_launches_n_ranks():
+    """`bench.py --gpus 2` without a launcher starts torch.distributed.run as a child (gloo here: no
+    GPU work with --plumbing-check) and rank 0's single line reports n_gpus = 2."""
+    import json
+
+    r = _run_bench(["--gpus", "2", "--plumbing-check"])
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [l for l in r.stdout.splitlines() if l.strip().startswith("{")]
+    assert len(lines) == 1, r.stdout
+    line = json.loads(lines[0])
+    assert line["n_gpus"] == 2 and line["gpus_requested"] == 2 and line["plumbing"] is True
+    assert abs(line["max_over_ranks_s"] - 0.002) < 1e-12  # the slower rank's time, not rank 0's
+
+
+def test_bench_gpus_n_fails_loudly_without_n_gpus():
+    """Asking for more GPUs than are visible must fail (rc 2), never report a 1-GPU number."""
+    r = _run_bench(["--gpus", "2"], timeout=120)
+    assert r.returncode == 2, (r.returncode, r.stdout, r.stderr[-2000:])
+    assert "GPU(s) are visible" in r.stderr
+    assert not [l for l in r.stdout.splitlines() if l.strip().startswith("{")]
+
+
+def test_bench_cpu_baseline_core_accounting(monkeypatch):
+    b = _bench()
+    monkeypatch.setenv("OMP_NUM_THREADS", "3")
+    threads, machine, affinity = b.host_cores()
+    assert threads == min(3, affinity) and machine == os.cpu_count()
+    monkeypatch.delenv("OMP_NUM_THREADS")
+    threads, _, affinity = b.host_cores()
+    assert threads == affinity

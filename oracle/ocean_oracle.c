@@ -220,6 +220,27 @@ void oracle_generate_spectrum(const oracle_settings* s, int n, float* h0)
   }
 }
 
+/* resources/spectrum.compute:157-172 at `count` texels (x, y) of an N x N image (the same
+   per-texel body as oracle_generate_spectrum): sampled checks at sizes where the whole image
+   would take the oracle minutes (N = 16384). xy: count int32 pairs; h0: count float4. */
+void oracle_spectrum_texels(const oracle_settings* s, int n, int64_t count, const int32_t* xy, float* h0)
+{
+  const float dim = (float)n;
+#pragma omp parallel for num_threads(g_threads) schedule(static)
+  for (int64_t i = 0; i < count; i++)
+  {
+    float a[2], b[2];
+    float x = (float)xy[2 * i], y = (float)xy[2 * i + 1];
+    oracle_spectrum_amplitude(s, x, y, dim, dim, a);
+    oracle_spectrum_amplitude(s, dim - x, dim - y, dim, dim, b);
+    float* o = h0 + 4 * i;
+    o[0] = a[0];
+    o[1] = a[1];
+    o[2] = b[0];
+    o[3] = -b[1];
+  }
+}
+
 /* resources/spectrum.compute:183-240 */
 void oracle_prepare_fft(const oracle_settings* s, int n, const float* h0, float* height, float* disp)
 {

@@ -55,6 +55,9 @@ void oracle_spectrum_amplitude(const oracle_settings* s, float tx, float ty, flo
 /* resources/spectrum.compute:157-172 over the whole N x N image. h0: N*N float4 (row-major, x fastest). */
 void oracle_generate_spectrum(const oracle_settings* s, int n, float* h0);
 
+/* The same texels as oracle_generate_spectrum at `count` indices (x, y) (int32 pairs); h0: count float4. */
+void oracle_spectrum_texels(const oracle_settings* s, int n, int64_t count, const int32_t* xy, float* h0);
+
 /* resources/spectrum.compute:183-240. height, disp: N*N float4 each. */
 void oracle_prepare_fft(const oracle_settings* s, int n, const float* h0, float* height, float* disp);
 

@@ -71,6 +71,7 @@ def lib():
         L.oracle_default_settings.argtypes = [sp]
         L.oracle_hash.argtypes = [ctypes.c_uint32, ctypes.c_uint32, fp, ctypes.POINTER(ctypes.c_uint32)]
         L.oracle_generate_spectrum.argtypes = [sp, ctypes.c_int, fp]
+        L.oracle_spectrum_texels.argtypes = [sp, ctypes.c_int, ctypes.c_int64, ctypes.POINTER(ctypes.c_int32), fp]
         L.oracle_prepare_fft.argtypes = [sp, ctypes.c_int, fp, fp, fp]
         L.oracle_encode_ifft.argtypes = [ctypes.c_int, fp, fp]
         L.oracle_compute_foam.argtypes = [sp, ctypes.c_int, fp, fp]
@@ -119,6 +120,15 @@ def generate_spectrum(s: OracleSettings, n: int) -> np.ndarray:
     h0 = np.zeros((n, n, 4), np.float32)
     lib().oracle_generate_spectrum(ctypes.byref(s), n, _fp(h0))
     return h0
+
+
+def spectrum_texels(s: OracleSettings, n: int, xy: np.ndarray) -> np.ndarray:
+    """generateSpectrum's texels at the (x, y) index pairs `xy` ([count, 2]) of an N x N image."""
+    xy = np.ascontiguousarray(xy, np.int32)
+    out = np.zeros((len(xy), 4), np.float32)
+    lib().oracle_spectrum_texels(ctypes.byref(s), n, len(xy), xy.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)),
+                                 _fp(out))
+    return out
 
 
 def prepare_fft(s: OracleSettings, n: int, h0: np.ndarray):

@@ -1,0 +1,202 @@
+"""GPU parity at the BASELINE.json configurations themselves (configs[3] and configs[4] geometry),
+and bench.py's multi-rank launch on a one-GPU box.
+
+- configs[3]: the 8 x 4096^2 batch bench.py times (same plane sizes and seeds, the persistent
+  xcd-paired item mapping of an 8-cascade launch) against the oracle, and bit-exact against the
+  same cascades run one per generator.
+- configs[4]: the single 16384^2 grid split over 8 ranks (strip-dealt half spectrum, equal-split
+  all-to-all emulated by device copies in one process) against the whole-grid generator, bit for
+  bit, compared on the device (17 GB of maps never leave HBM); h0 at 16384 against the oracle on
+  sampled texels (the whole image would take the CPU oracle minutes).
+All compute goes through the C ABI (liboceanfft.so); the oracle is only the checker.
+"""
+import importlib.util
+import json
+import os
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+from parity import FRAME_TOL, H0_TOL, lane_err, scalar_err
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.fixture(scope="module")
+def ocean():
+    import oceansimulation_amd as o
+    from oceansimulation_amd import capi
+
+    assert capi.lib().ocean_device_count() > 0, "no GPU visible to liboceanfft.so"
+    return o
+
+
+def _bench():
+    spec = importlib.util.spec_from_file_location("bench", os.path.join(ROOT, "bench.py"))
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    return mod
+
+
+def _dev_equal(ptr_a: int, ptr_b: int, nbytes: int) -> bool:
+    """Bit-exact comparison of two device ranges without host copies (torch shares the HIP
+    runtime with liboceanfft.so, see conftest.py)."""
+    import torch
+
+    from oceansimulation_amd import hip
+
+    a = torch.empty(nbytes, dtype=torch.uint8, device="cuda")
+    b = torch.empty_like(a)
+    hip.copy_d2d(a.data_ptr(), ptr_a, nbytes)
+    hip.copy_d2d(b.data_ptr(), ptr_b, nbytes)
+    eq = bool(torch.equal(a, b))
+    del a, b
+    return eq
+
+
+# ---- configs[3]: 8 independent 4096^2 cascades, as bench.py times them ---------------------------
+def test_headline_batch_vs_oracle(ocean, oracle):
+    """bench.py's step (rank 0's 8 cascades of 4096^2, plane sizes 5..4093 m) against the oracle
+    after three frames (the first seeds h0): cascades 0, 3 and 7 at FRAME_TOL; and every cascade of
+    the 8-cascade launch bit-exact against the same cascade in a one-cascade generator, so the
+    many-cascade item mapping is exercised (src/Generator.cpp:45-83)."""
+    b = _bench()
+    n, C = 4096, 8
+    steps = [1.0 / 60.0] * 3
+    fft = ocean.FFTCalculator(n)
+    gen = ocean.Generator(fft, C)
+    for c in range(C):
+        ocean.apply_settings(gen.GetOceanSettings(c), **b.cascade_settings(0, c))
+    for dt in steps:
+        gen.CalculateOcean(dt)
+    fft.synchronize()
+    for c in (0, 3, 7):
+        s = b.cascade_settings(0, c)
+        ref = oracle.OracleGenerator(n, oracle.default_settings(**s))
+        for dt in steps:
+            ref.calculate_ocean(dt)
+        e = lane_err(gen.height_map_host(c), ref.height) + lane_err(gen.displacement_map_host(c), ref.disp)
+        ej = scalar_err(gen.jacobian_map_host(c) - 1.0, ref.jac - 1.0)
+        assert max(e) <= FRAME_TOL and ej <= FRAME_TOL, (c, e, ej)
+        del ref
+    for c in range(C):
+        one = ocean.Generator(fft, 1)
+        ocean.apply_settings(one.GetOceanSettings(0), **b.cascade_settings(0, c))
+        for dt in steps:
+            one.CalculateOcean(dt)
+        fft.synchronize()
+        for get, tex in ((ocean.Generator.GetHeightMap, 16), (ocean.Generator.GetDisplacementMap, 16),
+                         (ocean.Generator.GetJacobianMap, 4)):
+            assert _dev_equal(get(gen, c), get(one, 0), tex * n * n), (c, get.__name__)
+        one.close()
+    gen.close()
+    fft.close()
+
+
+# ---- configs[4]: one 16384^2 grid, 8 ranks -------------------------------------------------------
+def test_h0_16384_sampled_vs_oracle(ocean, oracle):
+    """generateSpectrum at N = 16384 (spectrum.compute:157-172) against the oracle on ~20k texels:
+    rows and columns 0, N/2 - 1, N/2, N/2 + 1 and N - 1 (k = 0, the Nyquist row/column and their
+    partners N - i), the 96 x 96 block around k = 0 (where the spectrum peaks for the default
+    fetch), and random texels; plain and |k|-weighted like test_generate_spectrum."""
+    n = 16384
+    fft = ocean.FFTCalculator(n)
+    gen = ocean.Generator(fft, 1)
+    gen.GenerateSpectrum()
+    fft.synchronize()
+    from oceansimulation_amd import capi, hip
+
+    bsz = int(capi.lib().ocean_generator_spectrum_block(gen.handle))
+    blocked = hip.to_host(gen.GetInitialSpectrum(0), (n // bsz, n, bsz, 4))  # [x/B][y][x%B]
+    rng = np.random.default_rng(16384)
+    lines = np.array([0, n // 2 - 1, n // 2, n // 2 + 1, n - 1])
+    pts = []
+    for v in lines:
+        r = rng.integers(0, n, 1024)
+        pts += [np.stack([r, np.full_like(r, v)], 1), np.stack([np.full_like(r, v), r], 1)]
+    c = np.arange(n // 2 - 48, n // 2 + 48)
+    yy, xx = np.meshgrid(c, c, indexing="ij")
+    pts.append(np.stack([xx.ravel(), yy.ravel()], 1))
+    pts.append(rng.integers(0, n, (4096, 2)))
+    for v in lines:
+        pts.append(np.stack([lines, np.full_like(lines, v)], 1))
+    xy = np.concatenate(pts).astype(np.int32)
+    got = blocked[xy[:, 0] // bsz, xy[:, 1], xy[:, 0] % bsz]
+    del blocked
+    ref = oracle.spectrum_texels(oracle.default_settings(), n, xy)
+    assert np.isfinite(got).all()
+    errs = lane_err(got, ref)
+    assert max(errs) <= H0_TOL, errs
+    k = np.hypot(xy[:, 0] - n / 2, xy[:, 1] - n / 2)[:, None]
+    assert max(lane_err(got * k, ref * k)) <= 10 * H0_TOL, lane_err(got * k, ref * k)
+    kzero = (xy[:, 0] == n // 2) & (xy[:, 1] == n // 2)
+    assert kzero.any() and not got[kzero, :2].any()  # spectrum.compute:137-138
+    gen.close()
+    fft.close()
+
+
+@pytest.mark.slow
+def test_config5_geometry_16384_eight_ranks_bit_exact(ocean):
+    """BASELINE configs[4] geometry on one GPU: 8 SlabGenerators over the single 16384^2 grid
+    (default settings), each seeding its dealt strips, column pass into destination-block order,
+    the equal-split all-to-all as device copies, transposes + row pass on its 2048 rows; the
+    stitched maps and Jacobian must equal the whole-grid generator's bit for bit, frame after
+    frame (the first seeds h0)."""
+    from oceansimulation_amd import capi, hip
+    from oceansimulation_amd.hip import DeviceBuffer
+    from oceansimulation_amd.slab import SlabGenerator, emulate_frame
+
+    n, P = 16384, 8
+    steps = [0.25, 1.0 / 60.0, 2.0]
+    fft = ocean.FFTCalculator(n)
+    whole = ocean.Generator(fft, 1)
+    slabs = [SlabGenerator(fft, r, P) for r in range(P)]
+    sends = [DeviceBuffer(g.exchange_bytes) for g in slabs]
+    recvs = [DeviceBuffer(g.exchange_bytes) for g in slabs]
+    L = capi.lib()
+    w = n // P
+    for k, dt in enumerate(steps):
+        emulate_frame(slabs, sends, recvs, dt, update_ocean=(k == 0))
+        whole.CalculateOcean(dt)
+        hip.synchronize()
+        for r, g in enumerate(slabs):
+            for get, tex in ((L.ocean_generator_height_map, 16), (L.ocean_generator_displacement_map, 16),
+                             (L.ocean_generator_jacobian_map, 4)):
+                slab_ptr = int(get(g.handle, 0))
+                whole_ptr = int(get(whole.handle, 0)) + r * w * n * tex
+                assert _dev_equal(slab_ptr, whole_ptr, w * n * tex), (k, r, get.__name__)
+    for buf in sends + recvs:
+        buf.free()
+    for g in slabs:
+        g.close()
+    whole.close()
+    fft.close()
+
+
+# ---- bench.py --gpus N on a one-GPU box ---------------------------------------------------------
+def test_bench_gpus_two_shared_gpu_reports_two_ranks(tmp_path):
+    """`bench.py --gpus 2 --shared-gpu` (no launcher) starts 2 ranks under torch.distributed.run,
+    both on GPU 0 with gloo standing in for RCCL; rank 0 prints one line with n_gpus = 2 and a
+    2-rank slab leg. Small sizes: this checks the launch path, not a measurement. Without
+    --shared-gpu, --gpus 2 on a one-GPU box must refuse (rc 2)."""
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    args = ["--gpus", "2", "--shared-gpu", "--n", "1024", "--cascades", "2", "--slab-n", "2048", "--steps", "3",
+            "--warmup", "1", "--slab-steps", "2", "--no-cpu-baseline", "--no-surface", "--no-ifft", "--no-reseed"]
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py")] + args, capture_output=True, text=True,
+                       timeout=300, env=env, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-4000:]
+    lines = [l for l in r.stdout.splitlines() if l.strip().startswith("{")]
+    assert len(lines) == 1, r.stdout
+    line = json.loads(lines[0])
+    assert line["n_gpus"] == 2 and line["value"] > 0
+    assert line["slab"]["ranks"] == 2 and "all_to_all_single" in line["slab"]["exchange"]
+    import torch
+
+    if torch.cuda.device_count() < 2:
+        r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2"], capture_output=True,
+                           text=True, timeout=120, env=env, cwd=ROOT)
+        assert r.returncode == 2 and "GPU(s) are visible" in r.stderr, (r.returncode, r.stderr[-2000:])

@@ -174,3 +174,18 @@ def test_surface_vertex_stage_is_sequential(oracle):
     c = [(h1, d1, j1, 16.0, 1.0), (h2, d2, j2, 16.0, 1.0)]
     out = oracle.surface_points(c, np.array([[0.5, 0.5]], np.float32))  # texel (0, 0) centre
     assert out[0, 0] == np.float32(4.5) and out[0, 1] == np.float32(4.0)  # sampled at texel 4
+
+
+def test_spectrum_texels_equal_whole_image(oracle):
+    """The sampled h0 entry point (used at N = 16384, where the whole image would take minutes) is
+    the whole-image generateSpectrum body, bit for bit, including the k = 0 and Nyquist texels."""
+    import numpy as np
+
+    n = 64
+    s = oracle.default_settings(planeSize=17.0)
+    full = oracle.generate_spectrum(s, n)
+    y, x = np.meshgrid(np.arange(n), np.arange(n), indexing="ij")
+    xy = np.stack([x.ravel(), y.ravel()], axis=1)
+    assert np.array_equal(oracle.spectrum_texels(s, n, xy).reshape(n, n, 4), full)
+    assert np.array_equal(oracle.spectrum_texels(s, n, xy[[0, n * n // 2 + n // 2]]),
+                          full.reshape(-1, 4)[[0, n * n // 2 + n // 2]])

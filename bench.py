@@ -85,6 +85,7 @@ def parse(argv=None):
     return ap.parse_args(argv)
 
 
+ARGV_ENV = "OCEAN_BENCH_ARGV"  # launch_ranks -> its ranks: the original argument list (JSON)
 LEGS_TIMEOUT_RC = 3  # exit status when the optional legs overran their deadline (headline still printed)
 
 
@@ -116,9 +117,12 @@ def launch_ranks(args, argv) -> int:
                   f"report a {args.gpus}-GPU number (use --shared-gpu to rehearse ranks on one GPU)",
                   file=sys.stderr, flush=True)
             return 2
+    # the ranks' arguments travel in the environment: torchrun's own parser would take abbreviations
+    # of its options (e.g. --n for --nnodes) out of a script argument list
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
-           "--master-addr=127.0.0.1", f"--master-port={_free_port()}", os.path.abspath(__file__)] + list(argv)
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}", os.path.abspath(__file__)]
     env = dict(os.environ)
+    env[ARGV_ENV] = json.dumps(list(argv))
     env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # dmabuf IPC, required by RCCL on this host driver
     return subprocess.run(cmd, env=env).returncode
 
@@ -512,7 +516,10 @@ def slab_grid(args, rank: int, world: int, local: int) -> dict:
 
 
 def main(argv=None):
-    argv = sys.argv[1:] if argv is None else argv
+    if argv is None:
+        argv = sys.argv[1:]
+        if "WORLD_SIZE" in os.environ and ARGV_ENV in os.environ and not argv:
+            argv = json.loads(os.environ[ARGV_ENV])  # a rank started by launch_ranks
     args = parse(argv)
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
         return launch_ranks(args, argv)

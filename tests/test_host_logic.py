@@ -105,7 +105,7 @@ def test_bench_gpus_n_launches_n_ranks():
     GPU work with --plumbing-check) and rank 0's single line reports n_gpus = 2."""
     import json
 
-    r = _run_bench(["--gpus", "2", "--plumbing-check"])
+    r = _run_bench(["--gpus", "2", "--plumbing-check", "--n", "1024"])
     assert r.returncode == 0, r.stderr[-3000:]
     lines = [l for l in r.stdout.splitlines() if l.strip().startswith("{")]
     assert len(lines) == 1, r.stdout

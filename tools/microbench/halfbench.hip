@@ -162,6 +162,35 @@ int main(int argc, char** argv)
   std::printf("N=%d cascades=%d CUs=%d  bit-identical: cols deterministic=%s cols(HS)=%s rows(both images)=%s\n", n, C,
               cus, det ? "yes" : "NO", same_cols ? "yes" : "NO", same_rows ? "yes" : "NO");
 
+  {
+    // persistent grids (resident blocks x CUs, item loop) against one-shot grids (one block per
+    // item: launchers called with a huge CU count), same kernels, same results. The H-scratch
+    // column pass needs one scratch slice per resident block, so its no-scratch forms stand in.
+    const int BIG = 1 << 20;
+    auto rp = [&] { return launch_half_rows(logn, fp, gab, gcd, ge, spec, maps, jac, foam, tw, 0, cus); };
+    auto ro = [&] { return launch_half_rows(logn, fp, gab, gcd, ge, spec, maps, jac, foam, tw, 0, BIG); };
+    auto wp = [&] { return launch_half_columns(logn, fp, h0, gab, gcd, ge, spec, tw, 0, cus, nullptr, 0, nullptr, 0); };
+    auto wo = [&] { return launch_half_columns(logn, fp, h0, gab, gcd, ge, spec, tw, 0, BIG, nullptr, 0, nullptr, 0); };
+    auto hp = [&] { return launch_half_columns(logn, fp, h0, gab, gcd, ge, spec, tw, 0, cus, nullptr, 0, nullptr, 12); };
+    auto ho = [&] { return launch_half_columns(logn, fp, h0, gab, gcd, ge, spec, tw, 0, BIG, nullptr, 0, nullptr, 12); };
+    const char* nm[] = {"rows persistent", "rows one-shot", "cols re-evolve persistent", "cols re-evolve one-shot",
+                        "cols half2 persistent", "cols half2 one-shot"};
+    std::vector<std::vector<float>> tt(6);
+    for (int r = 0; r < 7; r++)
+    {
+      tt[0].push_back(time_ms(rp, 10));
+      tt[1].push_back(time_ms(ro, 10));
+      tt[2].push_back(time_ms(wp, 10));
+      tt[3].push_back(time_ms(wo, 10));
+      tt[4].push_back(time_ms(hp, 10));
+      tt[5].push_back(time_ms(ho, 10));
+    }
+    for (int k = 0; k < 6; k++)
+    {
+      std::sort(tt[k].begin(), tt[k].end());
+      std::printf("%-28s median %7.3f ms\n", nm[k], tt[k][3]);
+    }
+  }
   auto f00 = [&] { hipError_t e = c0(); return e == hipSuccess ? r0() : e; };
   auto f11 = [&] { hipError_t e = c1(); return e == hipSuccess ? r1() : e; };
   {

@@ -1107,17 +1107,46 @@ __global__ __launch_bounds__(FftShape<LOGN>::T * RPW_) void k_rows_half(
 
 // Strip-dealt half-spectrum fields -> row-major (HalfSlab blocks -> [c][yl][kp], kp = STRIPS * B):
 // the received blocks hold, per source rank r, its strips' w rows as [sl][yl][B] runs; the row pass
-// wants each row's kept columns u' = strip * B + b contiguous. 128 columns x 32 rows per tile
-// through LDS: reads are 32 B-texel runs (one per strip), writes 128-texel row runs. E = float4
-// (gab, gde) or float2 (gc); part_byte_off = the part's offset inside a block.
+// wants each row's kept columns u' = strip * B + b contiguous. 256 columns x 16 rows per tile
+// through LDS: reads are 16 B-texel runs (one per strip), writes 256-texel (4 KiB for float4) row
+// runs, both non-temporal. Measured at N = 16384, float4 (tools/microbench/transbench,
+// profiles/r02_transbench.log): 0.955 -> 0.870 ms per part against the earlier 128 x 32 tile with
+// default-policy access; the write run length sets the rate (64 x 64: 4.0 TB/s, 128 x 32: 4.5,
+// 256 x 16 with nt: 5.0), and strip-stride padding changes nothing.
+// E = float4 (gab, gde) or float2 (gc); part_byte_off = the part's offset inside a block.
+template <typename E>
+__device__ __forceinline__ E ld_nt(const E* p)
+{
+  if constexpr (sizeof(E) == 16)
+  {
+    const f4v t = __builtin_nontemporal_load(reinterpret_cast<const f4v*>(p));
+    return E{t.x, t.y, t.z, t.w};
+  }
+  else
+  {
+    const f2v t = __builtin_nontemporal_load(reinterpret_cast<const f2v*>(p));
+    return E{t.x, t.y};
+  }
+}
+
+template <typename E>
+__device__ __forceinline__ void st_nt(E* p, E v)
+{
+  if constexpr (sizeof(E) == 16)
+    __builtin_nontemporal_store(f4v{v.x, v.y, v.z, v.w}, reinterpret_cast<f4v*>(p));
+  else
+    __builtin_nontemporal_store(f2v{v.x, v.y}, reinterpret_cast<f2v*>(p));
+}
+
+constexpr int kHalfToRowsTU = 256, kHalfToRowsTY = 16;
+
 template <typename E, int B>
 __global__ __launch_bounds__(256) void k_half_to_rows(int cascades, int n, HalfSlab hsl,
                                                       const unsigned char* __restrict__ in, size_t part_byte_off,
                                                       size_t block_bytes, E* __restrict__ out)
 {
-  // 128 columns x 32 rows: 2-KiB row runs on the write side, 32 B-texel runs per strip on the read
-  // side (4.5 TB/s for float4 at N = 16384, against 4.0 for 64 x 64; tools/microbench/transbench)
-  constexpr int TU = 128, TY = 32;
+  constexpr int TU = kHalfToRowsTU, TY = kHalfToRowsTY, PER = TU * TY / 256;
+  static_assert(PER == 16 && TU % B == 0, "16 elements per thread");
   __shared__ E tile[TU][TY + 1];
   const int strips = n / (2 * B) + 1, kp = strips * B;
   // tiles never straddle two source blocks: (c, source rank r, column tile within r's strips, row tile)
@@ -1136,30 +1165,30 @@ __global__ __launch_bounds__(256) void k_half_to_rows(int cascades, int n, HalfS
     const int ulim = min(kp, (r + 1) * hsl.S * B);
     const E* src = reinterpret_cast<const E*>(in + (size_t)r * block_bytes + part_byte_off) +
                    (((size_t)c * hsl.S + tr * (TU / B)) * hsl.w + ty * TY) * B;
-    // read: b fastest, then row, then strip; all 16 loads are issued before the first LDS write
-    E v[16];
+    // read: b fastest, then row, then strip; all loads are issued before the first LDS write
+    E v[PER];
 #pragma unroll
-    for (int k = 0; k < 16; k++)
+    for (int k = 0; k < PER; k++)
     {
       const int L = k * 256 + threadIdx.x, b = L % B, row = (L / B) % TY, sti = L / (TY * B);
       // unconditional loads (a guarded load per element serialises them): columns past the rank's
       // strips read the tile's first element instead, and are not stored
       const bool in_range = u0 + sti * B + b < ulim;
-      v[k] = src[in_range ? ((size_t)sti * hsl.w + row) * B + b : 0];
+      v[k] = ld_nt(src + (in_range ? ((size_t)sti * hsl.w + row) * B + b : 0));
     }
 #pragma unroll
-    for (int k = 0; k < 16; k++)
+    for (int k = 0; k < PER; k++)
     {
       const int L = k * 256 + threadIdx.x, b = L % B, row = (L / B) % TY, sti = L / (TY * B);
       tile[sti * B + b][row] = v[k];
     }
     __syncthreads();
 #pragma unroll
-    for (int k = 0; k < 16; k++)
+    for (int k = 0; k < PER; k++)
     {
       const int L = k * 256 + threadIdx.x, row = L / TU, col = L % TU;
       if (u0 + col < ulim)
-        out[((size_t)c * hsl.w + ty * TY + row) * kp + u0 + col] = tile[col][row];
+        st_nt(out + ((size_t)c * hsl.w + ty * TY + row) * kp + u0 + col, tile[col][row]);
     }
     __syncthreads();
   }
@@ -1656,13 +1685,14 @@ hipError_t launch_half_slab_rows(int logn, const FrameParams& fp, const HalfSlab
     {
       using S = FftShape<LOGN>;
       const int n = S::N, B = spectrum_block(LOGN), C = fp.cascades;
-      if (hsl.w % 32 != 0)
+      if (hsl.w % kHalfToRowsTY != 0)
         return hipErrorInvalidValue;
       const size_t part = (size_t)C * hsl.S * hsl.w * B, blk = half_slab_block_bytes(LOGN, C, hsl);
       const float4* spec = reinterpret_cast<const float4*>((const unsigned char*)recv +
                                                            half_slab_spec_offset(LOGN, C, hsl));  // block 0's copy
       const int kp = half_strips(LOGN) * B;
-      const int tiles = C * ((half_strips(LOGN) + hsl.S - 1) / hsl.S) * ((hsl.S * B + 127) / 128) * (hsl.w / 32);
+      const int tiles = C * ((half_strips(LOGN) + hsl.S - 1) / hsl.S) *
+                        ((hsl.S * B + kHalfToRowsTU - 1) / kHalfToRowsTU) * (hsl.w / kHalfToRowsTY);
       const int tgrid = tiles < cus * 4 ? tiles : cus * 4;
       const unsigned char* in = (const unsigned char*)recv;
       constexpr int KB = ColFirstCfg<LOGN>::B;

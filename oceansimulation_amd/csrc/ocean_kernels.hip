@@ -1370,9 +1370,36 @@ static hipError_t with_logn(int logn, F&& f)
   }
 }
 
-// Persistent grid: resident blocks per CU x CUs, capped by the work item count. The occupancy
-// query and the dynamic-LDS attribute are set once per kernel instantiation (host API calls cost
-// microseconds; a frame is two launches).
+// Grid sizing. With the whole device available (cus >= the device's CUs) every kernel with an item
+// loop gets a one-shot grid, one block per work item: the hardware dispatcher then hands items out
+// in order, so the blocks in flight at any time work on neighbouring items (adjacent strips share
+// 128-B lines in L2, rows stream through neighbouring DRAM pages). Measured against persistent grids
+// (resident blocks x CUs, same kernels; tools/microbench/gridbench, profiles/r02_gridbench.log):
+// row pass 1.513 -> 1.453 ms, EncodeIFFT strided pass 1.115 -> 0.927 ms, 16384 column pass 6.69 ->
+// 5.56 ms. Under a CU budget (ocean_fft_set_cu_budget: CUs left free for RCCL's copy kernels in
+// the slab pipeline) grids stay persistent, so at most `cus` CUs' worth of blocks exist. Kernels
+// with per-block scratch (the H scratch of the half-spectrum column pass) cap the grid themselves.
+// The occupancy query and the dynamic-LDS attribute are set once per kernel instantiation (host API
+// calls cost microseconds; a frame is two launches).
+static int device_cu_count()
+{
+  static const int n = [] {
+    int dev = 0, c = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+      return 0;
+    return c;
+  }();
+  return n;
+}
+
+static bool g_force_persistent = false;  // tools/microbench A/B only (they include this file)
+
+static bool one_shot_grids(int cus)
+{
+  const int d = device_cu_count();
+  return !g_force_persistent && d > 0 && cus >= d;
+}
+
 struct LaunchCacheEntry
 {
   const void* kernel;
@@ -1400,6 +1427,8 @@ static int persistent_grid(K kernel, int wg, int lds, int items, int cus)
       cache.push_back({(const void*)kernel, lds, per_cu});
     }
   }
+  if (one_shot_grids(cus))
+    return items < 1 ? 1 : items;
   long g = (long)per_cu * cus;
   if (g > items)
     g = items;
@@ -1693,7 +1722,7 @@ hipError_t launch_half_slab_rows(int logn, const FrameParams& fp, const HalfSlab
       const int kp = half_strips(LOGN) * B;
       const int tiles = C * ((half_strips(LOGN) + hsl.S - 1) / hsl.S) *
                         ((hsl.S * B + kHalfToRowsTU - 1) / kHalfToRowsTU) * (hsl.w / kHalfToRowsTY);
-      const int tgrid = tiles < cus * 4 ? tiles : cus * 4;
+      const int tgrid = (one_shot_grids(cus) || tiles < cus * 4) ? tiles : cus * 4;
       const unsigned char* in = (const unsigned char*)recv;
       constexpr int KB = ColFirstCfg<LOGN>::B;
       hipLaunchKernelGGL((k_half_to_rows<float4, KB>), dim3(tgrid), dim3(256), 0, stream, C, n, hsl, in, (size_t)0, blk, rm_ab);

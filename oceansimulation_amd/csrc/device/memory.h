@@ -62,6 +62,38 @@ __device__ __forceinline__ void st1(void* base, int voff_bytes, float v)
   __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), srd(base, kAllBytes), voff_bytes, 0, AUX);
 }
 
+// The same with a wave-uniform byte offset in the instruction's SGPR soffset field: call sites that
+// touch 16 pieces of one buffer per item (m * stride) keep ONE descriptor (4 SGPRs) and pass the
+// piece offset as soffset, instead of building 16 descriptors. k_cols_half built ~50 per item and
+// spilled SGPRs to VGPR lanes (476 v_readlane/v_writelane per item at 112 SGPRs).
+template <int AUX = 0>
+__device__ __forceinline__ float4 ld4s(const void* base, int voff_bytes, int soff_bytes)
+{
+  f4v r = __builtin_amdgcn_raw_buffer_load_b128(srd(base, kAllBytes), voff_bytes + soff_bytes, 0, AUX);
+  return make_float4(r.x, r.y, r.z, r.w);
+}
+
+template <int AUX = 0>
+__device__ __forceinline__ void st4s(void* base, int voff_bytes, int soff_bytes, float4 v)
+{
+  f4v r = {v.x, v.y, v.z, v.w};
+  __builtin_amdgcn_raw_buffer_store_b128(r, srd(base, kAllBytes), voff_bytes + soff_bytes, 0, AUX);
+}
+
+template <int AUX = 0>
+__device__ __forceinline__ float2 ld2s(const void* base, int voff_bytes, int soff_bytes)
+{
+  u2v r = __builtin_amdgcn_raw_buffer_load_b64(srd(base, kAllBytes), voff_bytes + soff_bytes, 0, AUX);
+  return make_float2(__uint_as_float(r.x), __uint_as_float(r.y));
+}
+
+template <int AUX = 0>
+__device__ __forceinline__ void st2s(void* base, int voff_bytes, int soff_bytes, float2 v)
+{
+  u2v r = {__float_as_uint(v.x), __float_as_uint(v.y)};
+  __builtin_amdgcn_raw_buffer_store_b64(r, srd(base, kAllBytes), voff_bytes + soff_bytes, 0, AUX);
+}
+
 __device__ __forceinline__ int clamp_bytes(int64_t b)
 {
   return b > kAllBytes ? kAllBytes : (b < 0 ? 0 : (int)b);
@@ -73,6 +105,13 @@ __device__ __forceinline__ int clamp_bytes(int64_t b)
 __device__ __forceinline__ int opaque(int v)
 {
   asm volatile("" : "+v"(v));
+  return v;
+}
+
+// The same for a wave-uniform 64-bit value kept in SGPRs: computed where it is used, not hoisted.
+__device__ __forceinline__ size_t sopaque(size_t v)
+{
+  asm volatile("" : "+s"(v));
   return v;
 }
 

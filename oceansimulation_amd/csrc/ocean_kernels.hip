@@ -331,7 +331,7 @@ __global__ __launch_bounds__(ColFirstCfg<LOGN>::WG1) void k_cols_evolve(
           if constexpr (NOMEM)  // compute-only timing variant (microbench): no HBM reads
             a[m] = make_float4(1e-3f * m, 2e-3f * (float)i, 1e-3f * (float)b, 1e-4f * (float)item);
           else if (m < KEEP)  // read once per frame
-            a[m] = ld4<LA>(src + ((m + 8) & 15) * T * B, voff);  // fftShift on y folded into the load
+            a[m] = ld4s<LA>(src, voff, ((m + 8) & 15) * T * B * 16);  // fftShift on y folded into the load
           else  // read twice (re-evolved for the second image): policy LR
             a[m] = ld4<LR>(src + ((m + 8) & 15) * T * B, voff);
         }
@@ -589,9 +589,12 @@ __device__ __forceinline__ int half_group_offset(int y, int strip, int b = 0)
 // texel's two amplitudes (seed[c], the host's settings constants) instead of loading h0, so h0 is
 // neither written nor read this frame (HS only).
 // RG / RGC (whole grids): rows per group of the gab/gde and the gc layout (half_group_offset).
+// CPI: columns per item (B = the whole strip; B / 2: half strips, T * CPI threads, two workgroups
+// per CU so one's loads and stores overlap the other's transform; the strip's two halves are items
+// 2p, 2p + 1 on one XCD, whose loads share h0 lines and whose half-line stores meet in L2).
 template <int LOGN, int LA = 0, int SA = kStream, bool HS = false, bool SLAB = false, bool SEED = false, int RG = 1,
-          int RGC = 1>
-__global__ __launch_bounds__(ColFirstCfg<LOGN>::WG1) void k_cols_half(FrameParams fp, const float4* __restrict__ h0,
+          int RGC = 1, int CPI = ColFirstCfg<LOGN>::B>
+__global__ __launch_bounds__(FftShape<LOGN>::T * CPI, CPI < ColFirstCfg<LOGN>::B ? 4 : 1) void k_cols_half(FrameParams fp, const float4* __restrict__ h0,
                                                                      float4* __restrict__ gab, float4* __restrict__ gde,
                                                                      float2* __restrict__ gc,
                                                                      const float2* __restrict__ tw_glob,
@@ -602,21 +605,25 @@ __global__ __launch_bounds__(ColFirstCfg<LOGN>::WG1) void k_cols_half(FrameParam
   using S = FftShape<LOGN>;
   using K = ColFirstCfg<LOGN>;
   using HC = HalfCfg<LOGN>;
-  constexpr int N = S::N, T = S::T, B = K::B, STRIPS = HC::STRIPS;
+  constexpr int N = S::N, T = S::T, B = K::B, STRIPS = HC::STRIPS, WG = T * CPI, HALVES = B / CPI;
   static_assert(SLAB ? HC::SLAB_SUPPORTED : HC::SUPPORTED, "half-spectrum path: one strip per item (B = 4 unless SLAB)");
+  static_assert(CPI * HALVES == B && HALVES <= 2 && (HALVES == 1 || (!SLAB && !SEED)), "whole or half strips");
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   float2* tw = reinterpret_cast<float2*>(smem);
   void* xch = smem + ((S::TW_ENTRIES * 8 + 15) / 16) * 16;
   load_twiddles<LOGN>(tw, tw_glob);
 
   const int nstrips = SLAB ? hsl.nstrips : STRIPS;
-  const int total = fp.cascades * nstrips;
+  const int total = fp.cascades * nstrips * HALVES;
   const float dim = (float)N;
-  for (int item = blockIdx.x; item < total; item += gridDim.x)
+  for (int item = HALVES > 1 ? xcd_pair_slot(blockIdx.x, gridDim.x) : blockIdx.x; item < total; item += gridDim.x)
   {
-    const int b = opaque((int)threadIdx.x) % B;
-    const int c = item / nstrips, s = item - c * nstrips;  // s: the rank's strip index
-    const int sg = SLAB ? hsl.strip0 + s : s;               // global strip
+    const int hh = HALVES > 1 ? item % HALVES : 0, si = HALVES > 1 ? item / HALVES : item;
+    const int c = si / nstrips, s = si - c * nstrips;  // s: the rank's strip index
+    const int sg = SLAB ? hsl.strip0 + s : s;           // global strip
+    if (HALVES > 1 && sg == STRIPS - 1 && hh != 0)
+      continue;  // Nyquist strip: only column 0 (u = -N/2) is kept (uniform per workgroup)
+    const int b = opaque((int)threadIdx.x) % CPI + hh * CPI;  // column within the strip
     const int xb = sg == STRIPS - 1 ? 0 : N / (2 * B) + sg;
     const CascadeFrame f = fp.c[c];
     const float4* src = (!SLAB || h0_full) ? h0 + ((size_t)c * (N / B) + xb) * N * B
@@ -629,7 +636,7 @@ __global__ __launch_bounds__(ColFirstCfg<LOGN>::WG1) void k_cols_half(FrameParam
     const int x = xb * B + b;
     // one field round: (A, B), (D, E) or (C, 0) of the 16 texels, y-iFFT, store
     auto run_round = [&](int round) __attribute__((always_inline)) {
-      const int i = (opaque((int)threadIdx.x) / B) % T;
+      const int i = (opaque((int)threadIdx.x) / CPI) % T;
       const int voff = (i * B + b) * 16;
       CPair v[16];
       auto pack = [&](int m, float2 H, const KVec& q) __attribute__((always_inline)) {
@@ -646,7 +653,7 @@ __global__ __launch_bounds__(ColFirstCfg<LOGN>::WG1) void k_cols_half(FrameParam
       if (SEED && round == 0)
       {
         static_assert(!SEED || HS, "the fused seed keeps H in the scratch");
-        float2* hsb = hs + (size_t)blockIdx.x * 16 * K::WG1;
+        float2* hsb = hs + (size_t)blockIdx.x * 16 * WG;
         const int hoff = opaque((int)threadIdx.x) * 8;
         const SpectrumConsts q = seed[c];
         // the evaluator is too large to unroll 16 times: a rolled loop parks each H in the scratch,
@@ -656,24 +663,24 @@ __global__ __launch_bounds__(ColFirstCfg<LOGN>::WG1) void k_cols_half(FrameParam
         {
           const int y = i + ((m + 8) & 15) * T;
           const float2 H = evolve(seed_texel(q, x, y, dim), make_kvec(x, y, dim, f.dk).k, f);
-          st2<0>(hsb + m * K::WG1, hoff, H);
+          st2s<0>(hsb, hoff, m * WG * 8, H);
         }
         __threadfence_block();  // this thread's scratch stores are complete before it reads them back
 #pragma unroll
         for (int m = 0; m < 16; m++)
         {
           const int y = i + ((m + 8) & 15) * T;
-          pack(m, ld2<kStream>(hsb + m * K::WG1, hoff), make_kvec(x, y, dim, f.dk));
+          pack(m, ld2s<kStream>(hsb, hoff, m * WG * 8), make_kvec(x, y, dim, f.dk));
         }
       }
       else if (!HS || round == 0)
       {
-        float2* hsb = hs + (size_t)blockIdx.x * 16 * K::WG1;
+        float2* hsb = hs + (size_t)blockIdx.x * 16 * WG;
         const int hoff = opaque((int)threadIdx.x) * 8;
         float4 a[16];
 #pragma unroll
         for (int m = 0; m < 16; m++)  // fftShift on y folded into the load
-          a[m] = ld4<LA>(src + ((m + 8) & 15) * T * B, voff);
+          a[m] = ld4s<LA>(src, voff, ((m + 8) & 15) * T * B * 16);
 #pragma unroll
         for (int m = 0; m < 16; m++)
         {
@@ -682,7 +689,7 @@ __global__ __launch_bounds__(ColFirstCfg<LOGN>::WG1) void k_cols_half(FrameParam
           const float2 H = evolve(a[m], q.k, f);
 #ifndef OCEAN_ABLATE_HS
           if (HS)
-            st2<0>(hsb + m * K::WG1, hoff, H);
+            st2s<0>(hsb, hoff, m * WG * 8, H);
 #else
           (void)hsb;
           (void)hoff;
@@ -692,7 +699,7 @@ __global__ __launch_bounds__(ColFirstCfg<LOGN>::WG1) void k_cols_half(FrameParam
       }
       else
       {
-        const float2* hsb = hs + (size_t)blockIdx.x * 16 * K::WG1;
+        const float2* hsb = hs + (size_t)blockIdx.x * 16 * WG;
         const int hoff = opaque((int)threadIdx.x) * 8;
 #pragma unroll
         for (int m = 0; m < 16; m++)
@@ -702,11 +709,11 @@ __global__ __launch_bounds__(ColFirstCfg<LOGN>::WG1) void k_cols_half(FrameParam
           (void)hsb;
           pack(m, make_float2((float)hoff, (float)m), make_kvec(x, y, dim, f.dk));
 #else
-          pack(m, ld2<kStream>(hsb + m * K::WG1, hoff), make_kvec(x, y, dim, f.dk));
+          pack(m, ld2s<kStream>(hsb, hoff, m * WG * 8), make_kvec(x, y, dim, f.dk));
 #endif
         }
       }
-      fft_run<LOGN, K::C1, true>(v, i, b, xch, tw);
+      fft_run<LOGN, CPI, true>(v, i, HALVES > 1 ? opaque((int)threadIdx.x) % CPI : b, xch, tw);
 #pragma unroll
       for (int m = 0; m < 16; m++)
       {
@@ -716,8 +723,9 @@ __global__ __launch_bounds__(ColFirstCfg<LOGN>::WG1) void k_cols_half(FrameParam
           const size_t part = (size_t)fp.cascades * hsl.S * hsl.w * B;  // elements per part
           const int q = (m * T) / hsl.w, yl0 = (m * T) % hsl.w;
           const size_t el = (((size_t)c * hsl.S + s) * hsl.w + yl0) * B;
-          // block = the three parts, then the Nyquist-row term [c][2][N] (half_slab_block_bytes)
-          unsigned char* blk = send + (size_t)q * (part * 40 + (size_t)fp.cascades * 2 * N * 16);
+          // block = the three parts, then the Nyquist-row term [c][2][N] (half_slab_block_bytes).
+          // The block base is built at its store (sopaque): hoisted, the 16 descriptors spilled SGPRs.
+          unsigned char* blk = send + sopaque((size_t)q * (part * 40 + (size_t)fp.cascades * 2 * N * 16));
           if (round == 0)
             st4<SA>(blk + el * 16, voff, pair_raw(v[m]));
           else if (round == 1)
@@ -728,21 +736,21 @@ __global__ __launch_bounds__(ColFirstCfg<LOGN>::WG1) void k_cols_half(FrameParam
         else if constexpr (RG == 1 && RGC == 1)
         {
           if (round == 0)
-            st4<SA>(gab + gbase + m * T * B, voff, pair_raw(v[m]));
+            st4s<SA>(gab + gbase, voff, m * T * B * 16, pair_raw(v[m]));
           else if (round == 1)
-            st4<SA>(gde + gbase + m * T * B, voff, pair_raw(v[m]));
+            st4s<SA>(gde + gbase, voff, m * T * B * 16, pair_raw(v[m]));
           else
-            st2<SA>(gc + gbase + m * T * B, (i * B + b) * 8, make_float2(v[m].re.x, v[m].im.x));
+            st2s<SA>(gc + gbase, (i * B + b) * 8, m * T * B * 8, make_float2(v[m].re.x, v[m].im.x));
         }
-        else if (round == 0)
-          st4<SA>(gab + gbase + half_group_offset<LOGN, RG>(m * T, 0), half_group_offset<LOGN, RG>(i, 0, b) * 16,
-                  pair_raw(v[m]));
+        else if (round == 0)  // one descriptor per field; the row group of m T in soffset
+          st4s<SA>(gab + gbase, half_group_offset<LOGN, RG>(i, 0, b) * 16, half_group_offset<LOGN, RG>(m * T, 0) * 16,
+                   pair_raw(v[m]));
         else if (round == 1)
-          st4<SA>(gde + gbase + half_group_offset<LOGN, RG>(m * T, 0), half_group_offset<LOGN, RG>(i, 0, b) * 16,
-                  pair_raw(v[m]));
+          st4s<SA>(gde + gbase, half_group_offset<LOGN, RG>(i, 0, b) * 16, half_group_offset<LOGN, RG>(m * T, 0) * 16,
+                   pair_raw(v[m]));
         else
-          st2<SA>(gc + cgbase + half_group_offset<LOGN, RGC>(m * T, 0), half_group_offset<LOGN, RGC>(i, 0, b) * 8,
-                  make_float2(v[m].re.x, v[m].im.x));
+          st2s<SA>(gc + cgbase, half_group_offset<LOGN, RGC>(i, 0, b) * 8, half_group_offset<LOGN, RGC>(m * T, 0) * 8,
+                   make_float2(v[m].re.x, v[m].im.x));
       }
     };
     if constexpr (HS)
@@ -1572,6 +1580,22 @@ hipError_t launch_half_columns(int logn, const FrameParams& fp, const float4* h0
         const int hlds = ((S::TW_ENTRIES * 8 + 15) / 16) * 16 + 2 * S::PADDED * 16;
         const int hg = persistent_grid(hk, 2 * S::T, hlds, fp.cascades * 2 * HalfCfg<LOGN>::STRIPS, cus);
         hipLaunchKernelGGL(hk, dim3(hg), dim3(2 * S::T), hlds, stream, fp, h0, gab, gcd, ge, tw);
+        return hipGetLastError();
+      }
+      if (variant == 20 && hs && !seed)  // half-strip items, two workgroups per CU (HS slices of half size)
+      {
+        auto hk = k_cols_half<LOGN, 0, 0, true, false, false, RG, RGC, K::B / 2>;
+        const int wg = S::T * (K::B / 2);
+        const int hlds = ((S::TW_ENTRIES * 8 + 15) / 16) * 16 + (K::B / 2) * S::PADDED * 8;
+        int hg = persistent_grid(hk, wg, hlds, fp.cascades * HalfCfg<LOGN>::STRIPS * 2, cus);
+        const int slices = hs_blocks * (K::WG1 / wg);
+        if (hg > slices)
+          hg = slices;
+        hg &= ~15;  // xcd_pair_slot needs a multiple of 16 blocks
+        if (hg < 16)
+          return hipErrorInvalidValue;
+        hipLaunchKernelGGL(hk, dim3(hg), dim3(wg), hlds, stream, fp, h0, gab, gcd, ge, tw, hs, HalfSlab{},
+                           (unsigned char*)nullptr, 1, seed);
         return hipGetLastError();
       }
       const int lds = ((S::TW_ENTRIES * 8 + 15) / 16) * 16 + K::LDS1;

@@ -1,6 +1,6 @@
 // halfbench.hip — interleaved A/B timing of half-spectrum frame-pass variants (8 cascades x 4096^2),
 // with a bit-identity check of every variant's output against the baseline variant.
-// Build: see Makefile target `microbench`. Usage: halfbench [logn] [cascades]
+// Build: see Makefile target `microbench`. Usage: halfbench [logn] [cascades] [quick]
 #include "../../oceansimulation_amd/csrc/ocean_kernels.hip"
 
 #include <algorithm>
@@ -162,6 +162,42 @@ int main(int argc, char** argv)
   std::printf("N=%d cascades=%d CUs=%d  bit-identical: cols deterministic=%s cols(HS)=%s rows(both images)=%s\n", n, C,
               cus, det ? "yes" : "NO", same_cols ? "yes" : "NO", same_rows ? "yes" : "NO");
 
+  const bool quick = argc > 3 && std::strcmp(argv[3], "quick") == 0;  // only the block below
+  {
+    // pass 1 on half-strip items (k_cols_half CPI = B / 2, 512 threads, two workgroups per CU,
+    // variant 20) against production (whole strips, 1024 threads, one per CU): fields must be
+    // bit-identical (same per-column arithmetic), then timing of the pass and the frame
+    CHECK(c1());
+    CHECK(hipDeviceSynchronize());
+    auto pab = snap(gab, ht * sizeof(float4)), pde = snap(gcd, ht * sizeof(float4)), pc = snap(ge, ht * sizeof(float2));
+    CHECK(hipMemset(gab, 0, ht * sizeof(float4)));
+    CHECK(hipMemset(gcd, 0, ht * sizeof(float4)));
+    CHECK(hipMemset(ge, 0, ht * sizeof(float2)));
+    auto c20 = [&] { return launch_half_columns(logn, fp, h0, gab, gcd, ge, spec, tw, 0, cus, hs, cus, nullptr, 20); };
+    CHECK(c20());
+    CHECK(hipDeviceSynchronize());
+    std::printf("cols half strips 2/CU vs production: gab, gde, gc\n");
+    const bool same20 = (int)diff(snap(gab, ht * sizeof(float4)), pab) & (int)diff(snap(gcd, ht * sizeof(float4)), pde) &
+                        (int)diff(snap(ge, ht * sizeof(float2)), pc);
+    std::vector<std::vector<float>> tq(4);
+    for (int r = 0; r < 7; r++)
+    {
+      tq[0].push_back(time_ms(c1, 10));
+      tq[1].push_back(time_ms(c20, 10));
+      tq[2].push_back(time_ms([&] { hipError_t e = c1(); return e == hipSuccess ? r1() : e; }, 10));
+      tq[3].push_back(time_ms([&] { hipError_t e = c20(); return e == hipSuccess ? r1() : e; }, 10));
+    }
+    const char* qn[] = {"cols HS whole strips (production)", "cols HS half strips, 2/CU", "frame production",
+                        "frame with half-strip cols"};
+    for (int k = 0; k < 4; k++)
+    {
+      std::sort(tq[k].begin(), tq[k].end());
+      std::printf("%-40s median %7.3f ms\n", qn[k], tq[k][3]);
+    }
+    std::printf("half-strip fields bit-identical: %s\n", same20 ? "yes" : "NO");
+    if (quick)
+      return 0;
+  }
   {
     // persistent grids (resident blocks x CUs, item loop) against one-shot grids (one block per
     // item: launchers called with a huge CU count), same kernels, same results. The H-scratch

@@ -348,6 +348,38 @@ def ifft_legs(n: int, cascades: int, calls: int = 6) -> dict:
     return out
 
 
+def large_ifft_legs(calls: int = 3) -> dict:
+    """Standalone EncodeIFFT at the sizes the frame path runs slabs at: 2 packed 8192^2 images (one
+    cascade: rows + columns in place, two-column items) and 2 packed 16384^2 images (rows, then the
+    four-step column transform through an N x 2048 work slab). 64 algorithmic B per texel as above;
+    the four-step order moves 96."""
+    import torch
+
+    import oceansimulation_amd as ocean
+
+    out = {}
+    for n in (8192, 16384):
+        imgs = 2
+        fft = ocean.FFTCalculator(n)
+        buf = torch.randn(imgs, n, n, 4, device="cuda", dtype=torch.float32) * 1e-30
+        fft.encode_ifft_batch(buf.data_ptr(), imgs)
+        sync()
+        t0 = time.perf_counter()
+        for _ in range(calls):
+            fft.encode_ifft_batch(buf.data_ptr(), imgs)
+        sync()
+        ms = (time.perf_counter() - t0) * 1e3 / calls
+        texels = imgs * n * n
+        out[str(n)] = {"workload": f"EncodeIFFT of {imgs} packed RGBA32F {n}x{n} images (1 cascade x 2), in place",
+                       "order": "rows + four-step columns (work slab)" if n == 16384 else "rows + columns in place",
+                       "ms_per_call": ms, "height_field_points_per_s": n * n / (ms * 1e-3),
+                       "GB_per_s_algorithmic": 64.0 * texels / (ms * 1e-3) / 1e9}
+        fft.close()
+        del buf
+        torch.cuda.empty_cache()
+    return out
+
+
 def surface_leg(calls: int = 20, cpu_seconds: float = 3.0) -> dict:
     """the renderer's consumer of the maps (waveShader.glsl vertex displacement,
     slope normal, Jacobian average) on WaveApp's scene: 3 cascades of 256^2 (L = 5/17/101 m) and
@@ -666,6 +698,11 @@ def main(argv=None):
             out["ifft_only"] = ifft_legs(n, C)
         except Exception as e:  # reported, never fatal to the headline measurement
             out["ifft_only"] = {"error": f"{type(e).__name__}: {e}"}
+        if rank == 0:
+            try:
+                out["ifft_only_large"] = large_ifft_legs()
+            except Exception as e:  # reported, never fatal to the headline measurement
+                out["ifft_only_large"] = {"error": f"{type(e).__name__}: {e}"}
     if rank == 0 and not args.no_surface:
         try:
             out["surface"] = surface_leg()

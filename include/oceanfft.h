@@ -81,7 +81,10 @@ int ocean_fft_destroy(ocean_fft* fft);
 size_t ocean_fft_texture_resolution(const ocean_fft* fft);
 /* FFTCalculator::EncodeIFFT(Vision::ID image) — src/FFTCalculator.cpp:73-114. In place on a
  * device RGBA32F N*N image: out = N^2 * ifft2(ifftshift(in)) on lanes xy and zw independently
- * (no normalisation, like the reference). No work image is needed. */
+ * (no normalisation, like the reference). The caller needs no work image; the plan allocates its
+ * own on first use where a faster order needs one (N = 4096: column-first through up to 8 images;
+ * N = 16384: rows, then a four-step column transform through an N x 2048 slab), and falls back to
+ * the in-place passes when that allocation fails. */
 int ocean_fft_encode_ifft(ocean_fft* fft, float* image);
 /* Batched EncodeIFFT over n_images contiguous images (image i at image + i*N*N*4 floats). */
 int ocean_fft_encode_ifft_batch(ocean_fft* fft, float* images, int n_images);

@@ -69,7 +69,12 @@ struct ocean_fft
   float2* twiddles = nullptr;  // two-level table, see FftShape in ocean_kernels.hip
   float4* work = nullptr;      // column-first EncodeIFFT work image (the reference's workImage)
   int work_images = 0;
+  size_t work_texels = 0;      // four-step EncodeIFFT (N = 16384): work slab of N x kFourStepSlab texels
 };
+
+// Four-step EncodeIFFT work slab width at N = 16384 (tools/microbench/ifft4bench,
+// profiles/r02_ifft4bench.log: 2048 columns 5.05 ms, whole image 5.39, in place 7.26)
+constexpr int kFourStepSlab = 2048;
 
 struct ocean_generator
 {
@@ -177,21 +182,27 @@ int ocean_fft_create(ocean_fft** out, size_t texture_size, void* hip_stream)
   }
 
   // Twiddle table exp(+2 pi i e / N), two levels (FFTCalculator's pass table analogue,
-  // src/FFTCalculator.cpp:14-32): [0, TB) = low part, [TB, TB+TA) = high part.
-  int lb = logn / 2;
-  int tb = 1 << lb, ta = 1 << (logn - lb);
-  std::vector<float2> tab(tb + ta);
+  // src/FFTCalculator.cpp:14-32): [0, TB) = low part, [TB, TB+TA) = high part. The four-step
+  // EncodeIFFT (N = 16384) appends the N/16-point table.
+  std::vector<float2> tab;
   const double two_pi = 6.283185307179586476925286766559;
-  for (int e2 = 0; e2 < tb; e2++)
-  {
-    double a = two_pi * e2 / (double)f->n;
-    tab[e2] = make_float2((float)std::cos(a), (float)std::sin(a));
-  }
-  for (int e2 = 0; e2 < ta; e2++)
-  {
-    double a = two_pi * ((double)e2 * tb) / (double)f->n;
-    tab[tb + e2] = make_float2((float)std::cos(a), (float)std::sin(a));
-  }
+  auto append_table = [&](int lg) {
+    const int lb = lg / 2, tb = 1 << lb, ta = 1 << (lg - lb);
+    const double len = (double)(1 << lg);
+    for (int e2 = 0; e2 < tb; e2++)
+    {
+      double a = two_pi * e2 / len;
+      tab.push_back(make_float2((float)std::cos(a), (float)std::sin(a)));
+    }
+    for (int e2 = 0; e2 < ta; e2++)
+    {
+      double a = two_pi * ((double)e2 * tb) / len;
+      tab.push_back(make_float2((float)std::cos(a), (float)std::sin(a)));
+    }
+  };
+  append_table(logn);
+  if (ifft_fourstep_supported(logn))
+    append_table(logn - 4);
   e = hipMalloc(&f->twiddles, tab.size() * sizeof(float2));
   if (e == hipSuccess)
     e = hipMemcpy(f->twiddles, tab.data(), tab.size() * sizeof(float2), hipMemcpyHostToDevice);
@@ -251,6 +262,7 @@ int ocean_fft_encode_ifft_batch(ocean_fft* fft, float* images, int n_images)
           (void)hipFree(fft->work);
         fft->work = w;
         fft->work_images = want;
+        fft->work_texels = (size_t)want * fft->n * fft->n;
       }
       else
         (void)hipGetLastError();  // no room for the work image: the in-place passes below
@@ -264,6 +276,33 @@ int ocean_fft_encode_ifft_batch(ocean_fft* fft, float* images, int n_images)
                                      fft->stream, fft->cus),
                 "column-first EncodeIFFT");
       }
+      return OCEAN_OK;
+    }
+  }
+  if (ifft_fourstep_supported(fft->logn) && fft->logn == 14)
+  {
+    // rows in place, then the column transform in four steps through a work slab of N x 2048
+    // texels (512 MiB): every access a >= 256-B row piece instead of one-column 16-B pieces
+    const size_t want = ifft_fourstep_work_texels(fft->logn, kFourStepSlab);
+    if (fft->work_texels < want)
+    {
+      float4* w = nullptr;
+      if (hipMalloc(&w, want * sizeof(float4)) == hipSuccess)
+      {
+        if (fft->work)
+          (void)hipFree(fft->work);
+        fft->work = w;
+        fft->work_texels = want;
+        fft->work_images = 0;
+      }
+      else
+        (void)hipGetLastError();  // no room for the slab: the in-place passes below
+    }
+    if (fft->work_texels >= want)
+    {
+      HIP_TRY(launch_ifft_fourstep(fft->logn, n_images, img, fft->work, kFourStepSlab, fft->twiddles,
+                                   fft->twiddles + twiddle_entries(fft->logn), fft->stream, fft->cus),
+              "four-step EncodeIFFT");
       return OCEAN_OK;
     }
   }

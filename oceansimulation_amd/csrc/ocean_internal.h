@@ -140,6 +140,13 @@ hipError_t launch_half_slab_rows(int logn, const FrameParams& fp, const HalfSlab
                                  float4* rm_de, float2* rm_c, float4* maps, float* jac, const FoamParams& foam,
                                  const float2* tw, hipStream_t stream, int cus);
 hipError_t launch_rows_ifft_rows(int logn, int rows, float4* data, const float2* tw, hipStream_t stream, int cus);
+// Standalone EncodeIFFT at N = 8192 / 16384: rows in place, then the column transform in four steps
+// through a work slab of N x wc texels (ifft_fourstep_work_texels), wc columns at a time. tw2: the
+// N/16-point twiddle table.
+bool ifft_fourstep_supported(int logn);
+size_t ifft_fourstep_work_texels(int logn, int wc);
+hipError_t launch_ifft_fourstep(int logn, int n_images, float4* images, float4* work, int wc, const float2* tw,
+                                const float2* tw2, hipStream_t stream, int cus);
 // Standalone EncodeIFFT, column-first through a work image of n_images * N^2 texels (N = 4096).
 bool ifft_colfirst_supported(int logn);
 hipError_t launch_ifft_colfirst(int logn, int n_images, float4* images, float4* work, const float2* tw,

@@ -422,6 +422,95 @@ __global__ __launch_bounds__(ColFirstCfg<LOGN>::WG1) void k_cols_to_blocks(int i
   }
 }
 
+// Standalone EncodeIFFT at N >= 8192: the column transform in four steps (N = 16 N2), so that no
+// access is a 16- or 32-byte column piece (one 16384-row column is 256 KiB: an in-place column
+// item holds one or two columns and reads 16-32-B pieces, 1.3-2.8 TB/s). For y index n = N2 n1 + n2
+// and k = k1 + 16 k2:  X[k1 + 16 k2] = sum_n2 W_N2^(n2 k2) [W_N^(n2 k1) sum_n1 x[N2 n1 + n2] W_16^(n1 k1)].
+// Step 1 (this kernel), per (column x, n2): the 16-point inverse DFT over rows N2 n1 + n2 (fftShift
+// on y folded into n1: row (n + N/2) mod N = N2 ((n1 + 8) mod 16) + n2), times W_N^(n2 k1), into the
+// work slab at row N2 k1 + n2, split planes. Lanes run along x: every load and store of a wave is one
+// 1-KiB row piece, and there is no LDS exchange. The work slab holds columns [x0, x0 + wc).
+template <int LOGN>
+__global__ __launch_bounds__(256) void k_cols4_step1(int images, int x0, int wc, const float4* __restrict__ img,
+                                                     float4* __restrict__ work, const float2* __restrict__ tw_glob)
+{
+  using S = FftShape<LOGN>;
+  constexpr int N = S::N, N2 = N / 16;
+  __shared__ float2 tw[S::TW_ENTRIES];
+  load_twiddles<LOGN>(tw, tw_glob);
+  const int xblocks = wc / 64;
+  const int total = images * xblocks * (N2 / 4);
+  for (int item = blockIdx.x; item < total; item += gridDim.x)
+  {
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    int t = item;
+    const int xbk = t % xblocks;
+    t /= xblocks;
+    const int n2 = (t % (N2 / 4)) * 4 + wv, im = t / (N2 / 4);
+    const int xl = xbk * 64 + lane;  // column within the slab
+    const float4* src = img + ((size_t)im << (2 * LOGN)) + x0 + xl;
+    CPair v[16];
+#pragma unroll
+    for (int n1 = 0; n1 < 16; n1++)
+    {
+      const f4v r = __builtin_nontemporal_load(reinterpret_cast<const f4v*>(src + (size_t)(N2 * ((n1 + 8) & 15) + n2) * N));
+      v[n1] = to_pair(make_float4(r.x, r.y, r.z, r.w));
+    }
+    idft16(v);
+    apply_stage_twiddles<LOGN>(v, n2, tw);  // v[k1] *= W_N^(n2 k1)
+    float4* dst = work + (size_t)im * N * wc + xl;
+#pragma unroll
+    for (int k1 = 0; k1 < 16; k1++)
+    {
+      const float4 o = pair_raw(v[k1]);
+      __builtin_nontemporal_store(f4v{o.x, o.y, o.z, o.w}, reinterpret_cast<f4v*>(dst + (size_t)(N2 * k1 + n2) * wc));
+    }
+  }
+}
+
+// Step 2, per (image, k1, strip of C slab columns): the N2-point inverse FFT along the work slab's
+// contiguous rows N2 k1 + n2 (n2 = i + m T), output X[k1 + 16 k2] to image row k1 + 16 k2 in the
+// reference layout. Loads and stores are C * 16 = 256-byte row pieces. tw_glob: the N2-point table.
+template <int LOGN2>
+__global__ __launch_bounds__(ColCfg<LOGN2>::WG) void k_cols4_step2(int images, int x0, int wc,
+                                                                 const float4* __restrict__ work, float4* __restrict__ img,
+                                                                 const float2* __restrict__ tw_glob)
+{
+  using S = FftShape<LOGN2>;
+  using K = ColCfg<LOGN2>;
+  constexpr int N2 = S::N, T = S::T, C = K::C, LOGN = LOGN2 + 4, N = N2 * 16;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  float2* tw = reinterpret_cast<float2*>(smem);
+  void* xch = smem + ((S::TW_ENTRIES * 8 + 15) / 16) * 16;
+  load_twiddles<LOGN2>(tw, tw_glob);
+  const int c0 = threadIdx.x % C, i0 = threadIdx.x / C;
+  const int strips = wc / C;
+  const int total = images * 16 * strips;
+  for (int item = blockIdx.x; item < total; item += gridDim.x)
+  {
+    const int c = opaque(c0), i = opaque(i0);
+    const int strip = item % strips, rest = item / strips, k1 = rest & 15, im = rest >> 4;
+    const int xl = strip * C + c;
+    const float4* src = work + (size_t)im * N * wc + (size_t)N2 * k1 * wc + xl;
+    CPair v[16];
+#pragma unroll
+    for (int m = 0; m < 16; m++)
+    {
+      const f4v r = __builtin_nontemporal_load(reinterpret_cast<const f4v*>(src + (size_t)(i + m * T) * wc));
+      v[m] = raw_pair(make_float4(r.x, r.y, r.z, r.w));
+    }
+    fft_run<LOGN2, C, true>(v, i, c, xch, tw);
+    float4* dst = img + ((size_t)im << (2 * LOGN)) + (size_t)k1 * N + x0 + xl;
+#pragma unroll
+    for (int m = 0; m < 16; m++)
+    {
+      const float4 o = from_pair(v[m]);
+      __builtin_nontemporal_store(f4v{o.x, o.y, o.z, o.w},
+                                  reinterpret_cast<f4v*>(dst + (size_t)16 * (i + m * T) * N));
+    }
+  }
+}
+
 // BLOCKED: input is pass 1's output after the exchange, inter[c][src][img][xb_local][y][B] for this
 // rank's w rows (xb = src * (w/B) + xb_local); otherwise row-major [c][img][y][x] (after
 // k_blocks_to_rows, used when B == 1).
@@ -1762,6 +1851,55 @@ hipError_t launch_half_slab_rows(int logn, const FrameParams& fp, const HalfSlab
       hipLaunchKernelGGL(kern, dim3(grid), dim3(S::T * RPW), lds, stream, fp, rm_ab, rm_de, rm_c, spec, maps, jac, foam,
                          tw, hsl.w, kp);
       return hipGetLastError();
+    }
+  });
+}
+
+bool ifft_fourstep_supported(int logn) { return logn == 13 || logn == 14; }
+
+size_t ifft_fourstep_work_texels(int logn, int wc) { return ((size_t)1 << logn) * (size_t)wc; }
+
+// Rows in place, then per slab of wc columns: step 1 (images -> work slab), step 2 (slab -> images).
+// Bytes: 3 x 32 per texel (the in-place order: 2 x 32, but its column pass reads and writes 16-B
+// pieces at N = 16384). Measured (tools/microbench/ifft4bench, profiles/r02_ifft4bench.log), one
+// 16384^2 image: in place 7.26 ms, four-step 5.05 ms (wc 2048); at 8192 the in-place order (two
+// columns per item, 32-B pieces) stays ahead, 4.78 vs 4.96 ms for 4 images.
+
+hipError_t launch_ifft_fourstep(int logn, int n_images, float4* images, float4* work, int wc, const float2* tw,
+                                const float2* tw2, hipStream_t stream, int cus)
+{
+  if (!ifft_fourstep_supported(logn))
+    return hipErrorInvalidValue;
+  const int n = 1 << logn;
+  if (wc < 64 || wc > n || n % wc != 0 || (wc & 63) != 0)
+    return hipErrorInvalidValue;
+  hipError_t e = launch_rows_ifft(logn, n_images, images, tw, stream, cus);
+  if (e != hipSuccess)
+    return e;
+  return with_logn(logn, [&](auto L) -> hipError_t {
+    constexpr int LOGN = decltype(L)::value;
+    if constexpr (LOGN < 13)
+      return hipErrorInvalidValue;
+    else
+    {
+      constexpr int LOGN2 = LOGN - 4;
+      using K2 = ColCfg<LOGN2>;
+      auto k1 = k_cols4_step1<LOGN>;
+      auto k2 = k_cols4_step2<LOGN2>;
+      const int lds2 = lds_bytes_cols<LOGN2>();
+      for (int im = 0; im < n_images; im++)
+        for (int x0 = 0; x0 < n; x0 += wc)
+        {
+          float4* img = images + ((size_t)im << (2 * LOGN));
+          const int g1 = persistent_grid(k1, 256, 0, (wc / 64) * ((n / 16) / 4), cus);
+          hipLaunchKernelGGL(k1, dim3(g1), dim3(256), 0, stream, 1, x0, wc, img, work, tw);
+          const int g2 = persistent_grid(k2, K2::WG, lds2, 16 * (wc / K2::C), cus);
+          hipLaunchKernelGGL(k2, dim3(g2), dim3(K2::WG), lds2, stream, 1, x0, wc, work, img, tw2);
+          const hipError_t le = hipGetLastError();
+          if (le != hipSuccess)
+            return le;
+        }
+      return hipSuccess;
     }
   });
 }

@@ -112,6 +112,41 @@ def test_encode_ifft_large_vs_float64(ocean, n):
     assert max(errs) <= FFT_TOL, errs
 
 
+@pytest.mark.parametrize("n", [8192, 16384])
+def test_encode_ifft_separable_vs_float64(ocean, n):
+    """EncodeIFFT at the slab sizes (16384: rows, then the four-step column transform through its
+    work slab) on an input that is a sum of two outer products per lane, whose float64 reference is
+    the sum of the outer products of the two 1D transforms: N^2 ifft2(ifftshift(a b^T)) =
+    (N ifft(ifftshift a)) (N ifft(ifftshift b))^T. Checked on 256 random rows."""
+    from oceansimulation_amd.hip import DeviceBuffer
+
+    rng = np.random.default_rng(n)
+    a = rng.standard_normal((2, 2, n)) + 1j * rng.standard_normal((2, 2, n))  # [term, lane, y]
+    b = rng.standard_normal((2, 2, n)) + 1j * rng.standard_normal((2, 2, n))  # [term, lane, x]
+    img = np.empty((n, n, 4), np.float32)
+    for lane in range(2):
+        m = np.einsum("ty,tx->yx", a[:, lane].astype(np.complex64), b[:, lane].astype(np.complex64))
+        img[..., 2 * lane] = m.real
+        img[..., 2 * lane + 1] = m.imag
+        del m
+    a64 = a[:, :, :].astype(np.complex64).astype(np.complex128)  # the values the GPU sees
+    b64 = b[:, :, :].astype(np.complex64).astype(np.complex128)
+    fa = n * np.fft.ifft(np.fft.ifftshift(a64, axes=-1), axis=-1)
+    fb = n * np.fft.ifft(np.fft.ifftshift(b64, axes=-1), axis=-1)
+    fft = ocean.FFTCalculator(n)
+    buf = DeviceBuffer.from_array(img)
+    del img
+    fft.EncodeIFFT(buf.ptr)
+    fft.synchronize()
+    got = buf.to_host((n, n, 4))
+    rows = np.sort(rng.choice(n, 256, replace=False))
+    for lane in range(2):
+        ref = np.einsum("ty,tx->yx", fa[:, lane, rows], fb[:, lane])
+        g = got[rows][..., 2 * lane] + 1j * got[rows][..., 2 * lane + 1]
+        err = np.abs(g - ref).max() / np.abs(ref).max()
+        assert err <= FFT_TOL, (n, lane, err)
+
+
 @pytest.mark.parametrize("n,b", [(512, 5), (4096, 10)])
 def test_encode_ifft_batch_matches_single(ocean, n, b):
     """Batched == one image at a time, bit for bit (at 4096: the column-first path through its

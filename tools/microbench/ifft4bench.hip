@@ -1,0 +1,139 @@
+// ifft4bench.hip — standalone EncodeIFFT at N = 8192 / 16384: the in-place passes (rows, then
+// columns held one or two per workgroup: 16/32-B pieces) against rows + the four-step column
+// transform through a work slab of wc columns (k_cols4_step1/2), timed interleaved; the two results
+// are compared (relative max error per image; the factorisations differ, so not bit-identical).
+// Usage: ifft4bench
+#include "../../oceansimulation_amd/csrc/ocean_kernels.hip"
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <functional>
+#include <string>
+#include <vector>
+
+using namespace oceanfft;
+
+#define CHECK(x)                                                                                   \
+  do                                                                                               \
+  {                                                                                                \
+    hipError_t e = (x);                                                                            \
+    if (e != hipSuccess)                                                                           \
+    {                                                                                              \
+      std::printf("HIP error %s at %s:%d\n", hipGetErrorString(e), __FILE__, __LINE__);            \
+      std::exit(1);                                                                                \
+    }                                                                                              \
+  } while (0)
+
+template <typename F>
+static float time_ms(F&& launch, int reps)
+{
+  hipEvent_t a, b;
+  CHECK(hipEventCreate(&a));
+  CHECK(hipEventCreate(&b));
+  CHECK(launch());
+  CHECK(hipDeviceSynchronize());
+  CHECK(hipEventRecord(a));
+  for (int r = 0; r < reps; r++)
+    CHECK(launch());
+  CHECK(hipEventRecord(b));
+  CHECK(hipEventSynchronize(b));
+  float ms;
+  CHECK(hipEventElapsedTime(&ms, a, b));
+  CHECK(hipEventDestroy(a));
+  CHECK(hipEventDestroy(b));
+  return ms / reps;
+}
+
+static std::vector<float2> table(int logn)
+{
+  const int n = 1 << logn, lb = logn / 2, tb = 1 << lb, ta = 1 << (logn - lb);
+  std::vector<float2> tab(tb + ta);
+  for (int e = 0; e < tb; e++)
+    tab[e] = make_float2((float)std::cos(2 * M_PI * e / n), (float)std::sin(2 * M_PI * e / n));
+  for (int e = 0; e < ta; e++)
+    tab[tb + e] = make_float2((float)std::cos(2 * M_PI * (double)e * tb / n), (float)std::sin(2 * M_PI * (double)e * tb / n));
+  return tab;
+}
+
+int main()
+{
+  int cus = 0;
+  CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0));
+  for (int logn : {13, 14})
+  {
+    const int n = 1 << logn, imgs = logn == 13 ? 4 : 1;
+    const size_t tex = (size_t)n * n * imgs;
+    std::vector<float4> h(tex);
+    uint32_t st = 12345;
+    for (size_t k = 0; k < tex; k++)
+    {
+      st = st * 1664525u + 1013904223u;
+      const float a = (st >> 8) * (1.0f / 16777216.0f) - 0.5f;
+      h[k] = make_float4(a, 0.5f * a, std::sin(0.001f * (float)(k % 9973)), -0.25f * a);
+    }
+    float4 *img, *ref, *work;
+    CHECK(hipMalloc(&img, tex * 16));
+    CHECK(hipMalloc(&ref, tex * 16));
+    CHECK(hipMalloc(&work, ifft_fourstep_work_texels(logn, n) * 16));
+    auto t1 = table(logn), t2 = table(logn - 4);
+    float2 *tw, *tw2;
+    CHECK(hipMalloc(&tw, t1.size() * 8));
+    CHECK(hipMalloc(&tw2, t2.size() * 8));
+    CHECK(hipMemcpy(tw, t1.data(), t1.size() * 8, hipMemcpyHostToDevice));
+    CHECK(hipMemcpy(tw2, t2.data(), t2.size() * 8, hipMemcpyHostToDevice));
+    // reference: in-place rows + columns
+    CHECK(hipMemcpy(ref, h.data(), tex * 16, hipMemcpyHostToDevice));
+    CHECK(launch_rows_ifft(logn, imgs, ref, tw, 0, cus));
+    CHECK(launch_cols(logn, imgs, ref, tw, 0, cus));
+    CHECK(hipDeviceSynchronize());
+    std::vector<float4> a(tex), b(tex);
+    CHECK(hipMemcpy(a.data(), ref, tex * 16, hipMemcpyDeviceToHost));
+    const int wcs[] = {512, 1024, 2048, n};
+    for (int wc : wcs)
+    {
+      CHECK(hipMemcpy(img, h.data(), tex * 16, hipMemcpyHostToDevice));
+      CHECK(launch_ifft_fourstep(logn, imgs, img, work, wc, tw, tw2, 0, cus));
+      CHECK(hipDeviceSynchronize());
+      CHECK(hipMemcpy(b.data(), img, tex * 16, hipMemcpyDeviceToHost));
+      double mx = 0, er = 0;
+      for (size_t k = 0; k < tex; k++)
+      {
+        const float* x = &a[k].x;
+        const float* y = &b[k].x;
+        for (int j = 0; j < 4; j++)
+        {
+          mx = std::max(mx, (double)std::fabs(x[j]));
+          er = std::max(er, (double)std::fabs(x[j] - y[j]));
+        }
+      }
+      std::printf("N=%d wc=%d: four-step vs in-place max |diff| / max |x| = %.3g\n", n, wc, er / mx);
+    }
+    std::vector<std::string> names = {"in place rows + cols"};
+    std::vector<std::function<hipError_t()>> runs = {[&] {
+      hipError_t e = launch_rows_ifft(logn, imgs, img, tw, 0, cus);
+      return e == hipSuccess ? launch_cols(logn, imgs, img, tw, 0, cus) : e;
+    }};
+    for (int wc : wcs)
+    {
+      names.push_back("rows + four-step cols, wc " + std::to_string(wc));
+      runs.push_back([&, wc] { return launch_ifft_fourstep(logn, imgs, img, work, wc, tw, tw2, 0, cus); });
+    }
+    std::vector<std::vector<float>> t(runs.size());
+    for (int r = 0; r < 5; r++)
+      for (size_t k = 0; k < runs.size(); k++)
+        t[k].push_back(time_ms(runs[k], 3));
+    for (size_t k = 0; k < runs.size(); k++)
+    {
+      std::sort(t[k].begin(), t[k].end());
+      std::printf("N=%d x%d %-36s median %7.3f ms\n", n, imgs, names[k].c_str(), t[k][2]);
+    }
+    CHECK(hipFree(img));
+    CHECK(hipFree(ref));
+    CHECK(hipFree(work));
+    CHECK(hipFree(tw));
+    CHECK(hipFree(tw2));
+  }
+  return 0;
+}

@@ -496,8 +496,10 @@ def slab_grid(args, rank: int, world: int, local: int) -> dict:
                      if exchange else "none (one rank)"),
         "column_pass_ms": ms[1] / max(cnt[1], 1),
         "row_pass_ms": ms[2] / max(cnt[2], 1),
-        "frame_path": "full spectrum" if args.full_spectrum else "half spectrum, strip-dealt (fields moved to "
-                      "row-major after the exchange)",
+        "frame_path": ("full spectrum" if args.full_spectrum else
+                       "half spectrum, strip-dealt (fields moved to row-major after the exchange)" if world > 1 else
+                       "half spectrum, four-step column pass (16-point step in registers, N/16-point step into "
+                       "the row-major fields; no transposes)"),
         "frame_hbm_bytes_per_point": sum(g.frame_bytes()),
         "exchange_bytes_per_rank": g.exchange_bytes * (world - 1) // world if world > 1 else 0,
         "serial_ms_per_frame": 1000.0 * el / per,

@@ -140,6 +140,15 @@ int ocean_generator_spectrum_block(const ocean_generator* gen);
  * (both give the reference's results within rounding). On a slab generator the switch changes
  * ocean_generator_exchange_bytes and re-seeds h0 at the next frame. */
 int ocean_generator_set_half_spectrum(ocean_generator* gen, int enable);
+/* Whole grids of N = 8192 / 16384 on one rank (ocean_generator_create, or a slab generator with
+ * ranks == 1), half spectrum: enable (default) = the column pass in four steps (N = 16 * N2: a
+ * 16-point step in registers, then N2-point transforms on 16-column strips straight into the row
+ * pass's row-major fields; no one-column work items and no transposes; h0 is then blocked
+ * ocean_generator_spectrum_block = 64 columns wide); 0 = the strip-dealt column pass + transposes
+ * that slabs of ranks > 1 run, bit-identical to them. Both give the reference's results within
+ * rounding. Switching re-lays h0 out at the next frame from the settings it was seeded with. No
+ * reference counterpart. */
+int ocean_generator_set_four_step(ocean_generator* gen, int enable);
 /* Algorithmic HBM bytes per height-field point of the column pass [0] and the row pass [1] of the
  * generator's current path (what bench.py prices the roofline with). */
 int ocean_generator_frame_bytes(const ocean_generator* gen, double per_point[2]);

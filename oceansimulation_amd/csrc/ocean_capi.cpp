@@ -111,6 +111,12 @@ struct ocean_generator
   std::vector<unsigned char> seedc_host; // what seedc holds
   bool h0_stale = false;                 // the h0 image is not written yet (materialise_h0)
   std::vector<ocean_settings> seed_settings;  // the settings the last fused re-seed evaluated
+  // whole grids of N = 8192 / 16384 on one rank (strip-dealt P = 1): column pass in four steps
+  // (launch_gen4_columns / _rows) instead of the dealt column pass + transposes; off: the dealt path
+  // that slabs of P > 1 run (bit-identical to them). ocean_generator_set_four_step.
+  bool four_step = true;
+  int h0_block = 0;                          // strip width the h0 image was last written with
+  std::vector<ocean_settings> h0_settings;   // the settings it was written from
   bool profiling = false;
   std::vector<EventPair> pending;
   std::vector<hipEvent_t> pool;
@@ -391,6 +397,17 @@ static HalfSlab half_slab_geom(int logn, int rank, int ranks)
   return h;
 }
 
+static bool uses_gen4(const ocean_generator* g)
+{
+  return g->four_step && g->hslab && g->ranks == 1 && gen4_supported(g->fft->logn);
+}
+
+// strip width of the h0 image the current frame path reads
+static int h0_block(const ocean_generator* g)
+{
+  return uses_gen4(g) ? gen4_h0_block() : spectrum_block(g->fft->logn);
+}
+
 static size_t h0_texels(const ocean_generator* g)
 {
   const size_t full = (size_t)g->fft->n * g->geom.w;  // the full path's column slab (whole grid: N^2)
@@ -400,10 +417,22 @@ static size_t h0_texels(const ocean_generator* g)
   return std::max(full, strips);
 }
 
+// ranks == 1 at 8192 / 16384 may run either column pass (ocean_generator_set_four_step): the
+// buffers take the larger of the two layouts
+static bool gen4_eligible(const ocean_generator* g) { return g->ranks == 1 && gen4_supported(g->fft->logn); }
+
+static size_t hslab_xbuf_bytes(const ocean_generator* g)
+{
+  const size_t dealt = (size_t)g->ranks * half_slab_block_bytes(g->fft->logn, g->cascades, g->hsl);
+  return gen4_eligible(g) ? std::max(dealt, gen4_buffer_bytes(g->fft->logn, g->cascades)) : dealt;
+}
+
 static hipError_t hslab_buffers(ocean_generator* g)
 {
   const int logn = g->fft->logn, C = g->cascades;
-  const size_t rt = half_slab_row_texels(logn, C, g->hsl.w);
+  size_t rt = half_slab_row_texels(logn, C, g->hsl.w);
+  if (gen4_eligible(g))
+    rt = std::max(rt, gen4_row_texels(logn, C));
   hipError_t e = hipSuccess;
   if (!g->rm_ab)
     e = hipMalloc(&g->rm_ab, rt * sizeof(float4));
@@ -412,7 +441,7 @@ static hipError_t hslab_buffers(ocean_generator* g)
   if (e == hipSuccess && !g->rm_c)
     e = hipMalloc(&g->rm_c, rt * sizeof(float2));
   if (e == hipSuccess && !g->xbuf)
-    e = hipMalloc(&g->xbuf, (size_t)g->ranks * half_slab_block_bytes(logn, C, g->hsl));
+    e = hipMalloc(&g->xbuf, hslab_xbuf_bytes(g));
   if (e == hipSuccess && !g->hs)
     e = hipMalloc(&g->hs, half_hs_bytes(logn, g->fft->device_cus));
   if (e == hipSuccess && g->ranks > 1 && !g->h0row)
@@ -553,6 +582,8 @@ ocean_settings* ocean_generator_settings(ocean_generator* g, int c)
 static int generate_spectrum_with(ocean_generator* g, const std::vector<ocean_settings>& settings)
 {
   g->h0_stale = false;
+  g->h0_block = h0_block(g);
+  g->h0_settings = settings;
   ocean_fft* f = g->fft;
   const size_t slab = h0_texels(g);
   for (int c = 0; c < g->cascades; c++)
@@ -581,7 +612,8 @@ static int generate_spectrum_with(ocean_generator* g, const std::vector<ocean_se
       continue;
     }
     HIP_TRY(timed(g, 0, [&] {
-              return launch_generate_spectrum(s, f->n, g->h0 + slab * c, f->stream, f->cus, g->geom.x0, g->geom.w);
+              return launch_generate_spectrum(s, f->n, g->h0 + slab * c, f->stream, f->cus, g->geom.x0, g->geom.w,
+                                              g->h0_block);
             }),
             "generateSpectrum");
   }
@@ -652,6 +684,12 @@ static int generator_columns(ocean_generator* g, float timestep, int update_spec
     int rc = materialise_h0(g);  // the next frames read the h0 image
     if (rc != OCEAN_OK)
       return rc;
+    if (g->h0_block != h0_block(g))  // the frame path changed (four-step on/off): same h0, new layout
+    {
+      rc = generate_spectrum_with(g, g->h0_settings);
+      if (rc != OCEAN_OK)
+        return rc;
+    }
   }
   FrameParams fp{};
   fp.cascades = g->cascades;
@@ -664,7 +702,13 @@ static int generator_columns(ocean_generator* g, float timestep, int update_spec
     fp.c[c].g = s.g;
     fp.c[c].h = s.h;
   }
-  if (g->hslab)
+  if (uses_gen4(g))
+    HIP_TRY(timed(g, 1, [&] {
+              return launch_gen4_columns(f->logn, fp, g->h0, out ? (void*)out : (void*)g->xbuf, f->twiddles, f->stream,
+                                         f->cus);
+            }),
+            "column pass (half spectrum, four-step)");
+  else if (g->hslab)
     HIP_TRY(timed(g, 1, [&] {
               return launch_half_slab_columns(f->logn, fp, g->hsl, g->ranks, g->h0, g->ranks == 1, g->h0row,
                                               out ? (void*)out : (void*)g->xbuf, f->twiddles, f->stream, f->cus,
@@ -694,7 +738,14 @@ static int generator_rows(ocean_generator* g, const float4* in)
   FoamParams foam{};
   for (int c = 0; c < g->cascades; c++)
     foam.displacement[c] = g->settings[c].displacement;
-  if (g->hslab)
+  if (uses_gen4(g))
+    HIP_TRY(timed(g, 2, [&] {
+              return launch_gen4_rows(f->logn, g->frame, in ? (const void*)in : (const void*)g->xbuf, g->rm_ab, g->rm_de,
+                                      g->rm_c, g->maps, g->jac, foam, f->twiddles, f->twiddles + twiddle_entries(f->logn),
+                                      f->stream, f->cus);
+            }),
+            "row pass (half spectrum, four-step)");
+  else if (g->hslab)
     HIP_TRY(timed(g, 2, [&] {
               return launch_half_slab_rows(f->logn, g->frame, g->hsl, in ? (const void*)in : (const void*)g->xbuf,
                                            g->rm_ab, g->rm_de, g->rm_c, g->maps, g->jac, foam, f->twiddles,
@@ -743,6 +794,14 @@ int ocean_generator_set_half_spectrum(ocean_generator* g, int enable)
   return OCEAN_OK;
 }
 
+int ocean_generator_set_four_step(ocean_generator* g, int enable)
+{
+  if (!g)
+    return fail(OCEAN_ERR_INVALID, "ocean_generator_set_four_step: null generator");
+  g->four_step = enable != 0;  // h0 is re-laid out by the next frame if its strip width changes
+  return OCEAN_OK;
+}
+
 int ocean_generator_frame_bytes(const ocean_generator* g, double per_point[2])
 {
   if (!g || !per_point)
@@ -780,7 +839,7 @@ size_t ocean_generator_exchange_bytes(const ocean_generator* g)
   if (!g)
     return 0;
   if (g->hslab)
-    return (size_t)g->ranks * half_slab_block_bytes(g->fft->logn, g->cascades, g->hsl);
+    return hslab_xbuf_bytes(g);
   return (size_t)g->cascades * 2 * g->fft->n * g->geom.w * sizeof(float4);
 }
 
@@ -938,7 +997,7 @@ float* ocean_generator_initial_spectrum(ocean_generator* g, int c)
 
 int ocean_generator_spectrum_block(const ocean_generator* g)
 {
-  return g ? spectrum_block(g->fft->logn) : 0;
+  return g ? (g->h0_block > 0 ? g->h0_block : h0_block(g)) : 0;  // the layout h0 holds now
 }
 
 int ocean_generator_set_profiling(ocean_generator* g, int enable)

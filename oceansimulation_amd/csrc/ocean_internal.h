@@ -103,7 +103,7 @@ struct HalfSlab
 // slab (width <= 0: the whole grid).
 int spectrum_block(int logn);
 hipError_t launch_generate_spectrum(const OceanSettings& s, int n, float4* h0, hipStream_t stream, int cus, int x0 = 0,
-                                    int width = 0);
+                                    int width = 0, int blk = 0);  // blk 0: spectrum_block(log2 N)
 // Half-spectrum generator path (whole grids, N = 1024 .. 4096): pass 1 (+ the Nyquist-row term
 // into spec, 2 * cascades rows of N float4) and pass 2. Field buffers: half_field_texels(logn) per
 // cascade each for gab, gcd (float4) and ge (float2).
@@ -140,6 +140,19 @@ hipError_t launch_half_slab_rows(int logn, const FrameParams& fp, const HalfSlab
                                  float4* rm_de, float2* rm_c, float4* maps, float* jac, const FoamParams& foam,
                                  const float2* tw, hipStream_t stream, int cus);
 hipError_t launch_rows_ifft_rows(int logn, int rows, float4* data, const float2* tw, hipStream_t stream, int cus);
+// Whole grids of N = 8192 / 16384 on one rank, column pass in four steps: h0 blocked gen4_h0_block()
+// columns wide; columns: the Nyquist-row term and step 1 into buf (a strip-dealt P = 1 block's
+// size and layout of parts); rows: step 2 into the row-major fields, then the row pass. tw2: the
+// N/16-point twiddle table.
+bool gen4_supported(int logn);
+int gen4_h0_block();
+size_t gen4_row_texels(int logn, int cascades);   // each row-major field (rm_*), padded row pitch
+size_t gen4_buffer_bytes(int logn, int cascades); // the column -> row buffer (parts + Nyquist term)
+hipError_t launch_gen4_columns(int logn, const FrameParams& fp, const float4* h0, void* buf, const float2* tw,
+                               hipStream_t stream, int cus);
+hipError_t launch_gen4_rows(int logn, const FrameParams& fp, const void* buf, float4* rm_ab, float4* rm_de, float2* rm_c,
+                            float4* maps, float* jac, const FoamParams& foam, const float2* tw, const float2* tw2,
+                            hipStream_t stream, int cus);
 // Standalone EncodeIFFT at N = 8192 / 16384: rows in place, then the column transform in four steps
 // through a work slab of N x wc texels (ifft_fourstep_work_texels), wc columns at a time. tw2: the
 // N/16-point twiddle table.

@@ -1202,6 +1202,173 @@ __global__ __launch_bounds__(FftShape<LOGN>::T * RPW_) void k_rows_half(
   }
 }
 
+// ------------------------------------------------------------------------------------------------
+// Whole grids of N = 16384 (one rank): the half-spectrum column pass in four steps, like the
+// standalone EncodeIFFT's (k_cols4_step1/2), so that no pass holds a 256-KiB column and nothing is
+// transposed afterwards. Kept column u' in [0, kp), kp = N/2 + B (u' < N/2: x = N/2 + u'; then the
+// Nyquist strip x = u' - N/2). With y index q = N2 n1 + n2 (q the fftShifted row), each field F
+// becomes sum_n2 W_N2^(n2 k2) [W_N^(n2 k1) sum_n1 F(N2 n1 + n2) W_16^(n1 k1)] at output row
+// k1 + 16 k2.
+//   step 1 (k_gen4_step1): per (u', n2): evolve H at the 16 rows N2 ((n1 + 8) mod 16) + n2 from h0
+//     (blocked 64 columns wide, kGen4Block: one 1-KiB row piece per wave load), then for the three
+//     field rounds (A, B), (D, E) and C: the 16-point DFT in registers, times W_N^(n2 k1), into the
+//     work parts at row N2 k1 + n2 (row-major [c][row][kp], 1-KiB pieces). No LDS exchange.
+//   step 2 (k_gen4_step2): per (c, k1, strip of 16 kept columns): the N2-point FFT along the work's
+//     contiguous rows N2 k1 + n2, out to the row-major fields rm[c][k1 + 16 k2][u'] the row pass
+//     (k_rows_half RM) reads; 256-B (gc: 128-B) pieces.
+// Bytes per grid point: h0 8 + parts 20, parts 20 + fields 20, then the row pass 56: 124, as the
+// strip-dealt column pass (28) + transposes (40) + rows (56), but without the one-column items.
+// ------------------------------------------------------------------------------------------------
+constexpr int kGen4Block = 64;  // h0 strip width on this path
+// Row pitch (texels) of the work parts and of the row-major fields: kp rounded up to 16 texels, so
+// every 16-column strip is whole 128-B lines (kp = N/2 + B is odd at 16384; an odd pitch put every
+// 256-B strip piece across three lines: step 2 took 2x as long).
+template <int LOGN>
+struct Gen4Cfg
+{
+  static constexpr int N = 1 << LOGN, N2 = N / 16, B = ColFirstCfg<LOGN>::B, KP = N / 2 + B;
+  static constexpr int PITCH = (KP + 15) / 16 * 16;
+};
+
+template <int LOGN, int MINW = 1>
+__global__ __launch_bounds__(256, MINW) void k_gen4_step1(FrameParams fp, const float4* __restrict__ h0,
+                                                    unsigned char* __restrict__ parts, const float2* __restrict__ tw_glob)
+{
+  using S = FftShape<LOGN>;
+  using G = Gen4Cfg<LOGN>;
+  constexpr int N = G::N, N2 = G::N2, KP = G::KP, PITCH = G::PITCH, XB = (KP + 63) / 64;
+  __shared__ float2 tw[S::TW_ENTRIES];
+  load_twiddles<LOGN>(tw, tw_glob);
+  const size_t part = (size_t)fp.cascades * N * PITCH;  // texels per part
+  float4* gab = reinterpret_cast<float4*>(parts);
+  float4* gde = gab + part;
+  float2* gc = reinterpret_cast<float2*>(gde + part);
+  const int total = fp.cascades * XB * (N2 / 4);
+  const float dim = (float)N;
+  for (int item = blockIdx.x; item < total; item += gridDim.x)
+  {
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    int t = item;
+    const int xbk = t % XB;
+    t /= XB;
+    const int n2 = (t % (N2 / 4)) * 4 + wv, c = t / (N2 / 4);
+    const int u = xbk * 64 + lane;
+    const bool live = u < KP;
+    const int uc = live ? u : KP - 1;  // columns past the last: loads clamped, nothing stored
+    const int x = uc < N / 2 ? N / 2 + uc : uc - N / 2;
+    const CascadeFrame f = fp.c[c];
+    // one descriptor for the item's h0 strip (uniform: 64 lanes = one 64-column block)
+    const float4* src = h0 + ((size_t)c * (N / kGen4Block) + x / kGen4Block) * N * kGen4Block;
+    const int loff = (n2 * kGen4Block + (x % kGen4Block)) * 16;
+    float2 H[16];
+    {
+      float4 a[16];
+#pragma unroll
+      for (int n1 = 0; n1 < 16; n1++)
+        a[n1] = ld4s<kStream>(src, loff, N2 * ((n1 + 8) & 15) * kGen4Block * 16);
+#pragma unroll
+      for (int n1 = 0; n1 < 16; n1++)
+        H[n1] = evolve(a[n1], make_kvec(x, N2 * ((n1 + 8) & 15) + n2, dim, f.dk).k, f);
+    }
+    // output row N2 k1 + n2 of the cascade: two descriptors per part (k1 < 8, k1 >= 8) keep the
+    // 32-bit offsets below 2 GiB
+    const size_t cb = (size_t)c * N * PITCH;
+    const int soff = (n2 * PITCH + u) * 16;
+#pragma unroll
+    for (int round = 0; round < 2; round++)
+    {
+      const int xr = opaque(x), n2r = opaque(n2);
+      CPair v[16];
+#pragma unroll
+      for (int n1 = 0; n1 < 16; n1++)
+      {
+        const KVec q = make_kvec(xr, N2 * ((n1 + 8) & 15) + n2r, dim, f.dk);
+        const float2 h = H[n1];
+        if (round == 0)  // (A, B) = (H, kz H)
+          v[n1] = CPair{f2v{h.x, q.kz * h.x}, f2v{h.y, q.kz * h.y}};
+        else  // (D, E) = (kz H / |k|, kz^2 H / |k|)
+        {
+          const float e = q.kz * q.dirz;
+          v[n1] = CPair{f2v{q.dirz * h.x, e * h.x}, f2v{q.dirz * h.y, e * h.y}};
+        }
+      }
+      idft16(v);
+      apply_stage_twiddles<LOGN>(v, n2r, tw);
+      float4* d0 = (round == 0 ? gab : gde) + cb;
+      float4* d1 = d0 + (size_t)8 * N2 * PITCH;
+      if (live)
+#pragma unroll
+        for (int k1 = 0; k1 < 16; k1++)
+          st4s<kStream>(k1 < 8 ? d0 : d1, soff, (k1 & 7) * N2 * PITCH * 16, pair_raw(v[k1]));
+    }
+    {
+      const int xr = opaque(x), n2r = opaque(n2);
+      float2 w[16];  // C = H / |k|, one complex lane
+#pragma unroll
+      for (int n1 = 0; n1 < 16; n1++)
+      {
+        const float inv = make_kvec(xr, N2 * ((n1 + 8) & 15) + n2r, dim, f.dk).inv;
+        w[n1] = make_float2(inv * H[n1].x, inv * H[n1].y);
+      }
+      idft16(w);
+      apply_stage_twiddles<LOGN>(w, n2r, tw);
+      float2* d0 = gc + cb;
+      if (live)
+#pragma unroll
+        for (int k1 = 0; k1 < 16; k1++)
+          st2s<kStream>(d0, soff / 2, k1 * N2 * PITCH * 8, w[k1]);
+    }
+  }
+}
+
+// Step 2 on one part: per (cascade, k1, strip of C columns) the N2-point FFT along rows N2 k1 + n2 of
+// `work`, out to rows k1 + 16 k2 of `rm`; both [c][N][pitch] in texels of 16 B. PAIRS: the texels
+// are split-plane CPairs (gab, gde: raw_pair / pair_raw); otherwise two adjacent float2 columns of gc
+// in the reference's (re0, im0, re1, im1) order, transformed as the two lanes of one CPair.
+// cols: columns to transform (< pitch). Descriptors: one for the strip's input rows, two for its
+// output (rows below and above 16 * 8 T) so the 32-bit offsets stay below 2 GiB.
+// CI: columns per workgroup (ColCfg's 16: 256-B pieces, one 1024-thread workgroup per CU at N2 =
+// 1024; 8: 128-B pieces, two 512-thread workgroups per CU).
+template <int LOGN2, bool PAIRS, int CI = ColCfg<LOGN2>::C>
+__global__ __launch_bounds__(FftShape<LOGN2>::T * CI, CI < ColCfg<LOGN2>::C ? 4 : 1) void k_gen4_step2(int cascades, int cols, int pitch,
+                                                                 const float4* __restrict__ work, float4* __restrict__ rm,
+                                                                 const float2* __restrict__ tw_glob)
+{
+  using S = FftShape<LOGN2>;
+  constexpr int N2 = S::N, T = S::T, C = CI, N = N2 * 16;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  float2* tw = reinterpret_cast<float2*>(smem);
+  void* xch = smem + ((S::TW_ENTRIES * 8 + 15) / 16) * 16;
+  load_twiddles<LOGN2>(tw, tw_glob);
+  const int c0 = threadIdx.x % C, i0 = threadIdx.x / C;
+  const int strips = (cols + C - 1) / C;
+  const int total = cascades * 16 * strips;
+  for (int item = blockIdx.x; item < total; item += gridDim.x)
+  {
+    const int cc = opaque(c0), i = opaque(i0);
+    const int strip = item % strips, rest = item / strips, k1 = rest & 15, c = rest >> 4;
+    const int u = strip * C + cc;
+    const bool live = u < cols;
+    const float4* src = work + ((size_t)c * N + (size_t)N2 * k1) * pitch;
+    const int loff = (i * pitch + (live ? u : cols - 1)) * 16;
+    CPair v[16];
+#pragma unroll
+    for (int m = 0; m < 16; m++)
+    {
+      const float4 r = ld4s<kStream>(src, loff, m * T * pitch * 16);
+      v[m] = PAIRS ? raw_pair(r) : to_pair(r);
+    }
+    fft_run<LOGN2, C, true>(v, i, cc, xch, tw);
+    float4* d0 = rm + ((size_t)c * N + k1) * pitch;
+    float4* d1 = d0 + (size_t)16 * 8 * T * pitch;
+    const int soff = (16 * i * pitch + u) * 16;
+    if (live)
+#pragma unroll
+      for (int m = 0; m < 16; m++)
+        st4s<kStream>(m < 8 ? d0 : d1, soff, (m & 7) * 16 * T * pitch * 16, PAIRS ? pair_raw(v[m]) : from_pair(v[m]));
+  }
+}
+
 // Strip-dealt half-spectrum fields -> row-major (HalfSlab blocks -> [c][yl][kp], kp = STRIPS * B):
 // the received blocks hold, per source rank r, its strips' w rows as [sl][yl][B] runs; the row pass
 // wants each row's kept columns u' = strip * B + b contiguous. 256 columns x 16 rows per tile
@@ -1543,13 +1710,15 @@ int spectrum_block(int logn)
 }
 
 hipError_t launch_generate_spectrum(const OceanSettings& s, int n, float4* h0, hipStream_t stream, int cus, int x0,
-                                    int width)
+                                    int width, int blk)
 {
   int logn = 0;
   while ((1 << logn) < n)
     logn++;
   if (width <= 0)
     width = n;
+  if (blk <= 0)
+    blk = spectrum_block(logn);
   const bool whole = x0 == 0 && width == n;  // a slab's partner columns belong to other ranks
   long total = whole ? (long)n * (n / 2) + n + n / 2 - 1 : (long)n * width;
   long blocks = (total + 255) / 256;
@@ -1559,14 +1728,14 @@ hipError_t launch_generate_spectrum(const OceanSettings& s, int n, float4* h0, h
   if (whole)
   {
     int lblk = 0;
-    while ((1 << lblk) < spectrum_block(logn))
+    while ((1 << lblk) < blk)
       lblk++;
     hipLaunchKernelGGL(k_generate_spectrum_pairs, dim3((unsigned)blocks), dim3(256), 0, stream,
                        spectrum_consts(s, n), logn, lblk, h0);
   }
   else
     hipLaunchKernelGGL(k_generate_spectrum, dim3((unsigned)blocks), dim3(256), 0, stream, spectrum_consts(s, n), n,
-                       spectrum_block(logn), x0, width, h0, n);
+                       blk, x0, width, h0, n);
   return hipGetLastError();
 }
 
@@ -1900,6 +2069,98 @@ hipError_t launch_ifft_fourstep(int logn, int n_images, float4* images, float4* 
             return le;
         }
       return hipSuccess;
+    }
+  });
+}
+
+// ---- whole grids of N = 8192 / 16384 on one rank: four-step column pass (k_gen4_step1/2) ----
+bool gen4_supported(int logn) { return logn == 13 || logn == 14; }
+
+int gen4_h0_block() { return kGen4Block; }
+
+size_t gen4_row_texels(int logn, int cascades)
+{
+  const int n = 1 << logn, kp = n / 2 + spectrum_block(logn);  // Gen4Cfg::KP
+  return (size_t)cascades * n * (size_t)((kp + 15) / 16 * 16);
+}
+
+size_t gen4_buffer_bytes(int logn, int cascades)
+{
+  return 40 * gen4_row_texels(logn, cascades) + (size_t)cascades * 2 * ((size_t)1 << logn) * sizeof(float4);
+}
+
+hipError_t launch_gen4_columns(int logn, const FrameParams& fp, const float4* h0, void* buf, const float2* tw,
+                               hipStream_t stream, int cus)
+{
+  return with_logn(logn, [&](auto L) -> hipError_t {
+    constexpr int LOGN = decltype(L)::value;
+    if constexpr (LOGN < 13)
+      return hipErrorInvalidValue;
+    else
+    {
+      using G = Gen4Cfg<LOGN>;
+      constexpr int N = G::N, KP = G::KP;
+      // the Nyquist-row term after the three parts
+      float4* spec = reinterpret_cast<float4*>((unsigned char*)buf + 40 * gen4_row_texels(LOGN, fp.cascades));
+      long blocks = ((long)fp.cascades * N + 255) / 256;
+      if (blocks > (long)cus * 4)
+        blocks = (long)cus * 4;
+      hipLaunchKernelGGL(k_half_nyquist, dim3((unsigned)blocks), dim3(256), 0, stream, fp, N, kGen4Block, h0, spec,
+                         (const float4*)nullptr, 1, (size_t)0, (const SpectrumConsts*)nullptr);
+      hipError_t e = hipGetLastError();
+      if (e != hipSuccess)
+        return e;
+      auto k1 = k_gen4_step1<LOGN>;
+      const int items = fp.cascades * ((KP + 63) / 64) * (N / 16 / 4);
+      hipLaunchKernelGGL(k1, dim3(persistent_grid(k1, 256, 0, items, cus)), dim3(256), 0, stream, fp, h0,
+                         (unsigned char*)buf, tw);
+      return hipGetLastError();
+    }
+  });
+}
+
+hipError_t launch_gen4_rows(int logn, const FrameParams& fp, const void* buf, float4* rm_ab, float4* rm_de, float2* rm_c,
+                            float4* maps, float* jac, const FoamParams& foam, const float2* tw, const float2* tw2,
+                            hipStream_t stream, int cus)
+{
+  return with_logn(logn, [&](auto L) -> hipError_t {
+    constexpr int LOGN = decltype(L)::value;
+    if constexpr (LOGN < 13)
+      return hipErrorInvalidValue;
+    else
+    {
+      using S = FftShape<LOGN>;
+      using G = Gen4Cfg<LOGN>;
+      constexpr int N = G::N, KP = G::KP, PITCH = G::PITCH, LOGN2 = LOGN - 4;
+      // 8 columns per workgroup at N2 = 1024 (512 threads, two per CU: 2.145 -> 2.015 ms for the three
+      // parts at 16384, tools/microbench/gen4bench); ColCfg's 16 at N2 = 512 (already 512 threads)
+      constexpr int CI = ColCfg<LOGN2>::C * FftShape<LOGN2>::T >= 1024 ? ColCfg<LOGN2>::C / 2 : ColCfg<LOGN2>::C;
+      constexpr int WG2 = FftShape<LOGN2>::T * CI;
+      const int C = fp.cascades;
+      const size_t part = gen4_row_texels(LOGN, C);
+      const float4* wab = reinterpret_cast<const float4*>(buf);
+      const float4* wde = wab + part;
+      const float4* wc = wde + part;  // gc (float2 texels) viewed as pairs of columns
+      const float4* spec = reinterpret_cast<const float4*>((const unsigned char*)buf + 40 * part);
+      const int lds2 = ((FftShape<LOGN2>::TW_ENTRIES * 8 + 15) / 16) * 16 + CI * FftShape<LOGN2>::PADDED * 8;
+      auto sp = k_gen4_step2<LOGN2, true, CI>;
+      auto sc = k_gen4_step2<LOGN2, false, CI>;
+      const int gp = persistent_grid(sp, WG2, lds2, C * 16 * ((KP + CI - 1) / CI), cus);
+      const int gcg = persistent_grid(sc, WG2, lds2, C * 16 * (((KP + 1) / 2 + CI - 1) / CI), cus);
+      hipLaunchKernelGGL(sp, dim3(gp), dim3(WG2), lds2, stream, C, KP, PITCH, wab, rm_ab, tw2);
+      hipLaunchKernelGGL(sp, dim3(gp), dim3(WG2), lds2, stream, C, KP, PITCH, wde, rm_de, tw2);
+      hipLaunchKernelGGL(sc, dim3(gcg), dim3(WG2), lds2, stream, C, (KP + 1) / 2, PITCH / 2, wc,
+                         reinterpret_cast<float4*>(rm_c), tw2);
+      hipError_t e = hipGetLastError();
+      if (e != hipSuccess)
+        return e;
+      constexpr int RPW = S::T >= 1024 ? 1 : 2;
+      auto kern = k_rows_half<LOGN, kStream, kStream, 0, RPW, true, true>;
+      const int lds = ((S::TW_ENTRIES * 8 + 15) / 16) * 16 + lds_row_slots<LOGN>(RPW) * 8;
+      const int grid = persistent_grid(kern, S::T * RPW, lds, C * (N / RPW), cus);
+      hipLaunchKernelGGL(kern, dim3(grid), dim3(S::T * RPW), lds, stream, fp, rm_ab, rm_de, rm_c, spec, maps, jac, foam, tw,
+                         N, PITCH);
+      return hipGetLastError();
     }
   });
 }

@@ -51,6 +51,11 @@ class SlabGenerator:
         exchange size changes with it and h0 is re-seeded at the next frame."""
         check(lib().ocean_generator_set_half_spectrum(self._h, 1 if enable else 0), "ocean_generator_set_half_spectrum")
 
+    def set_four_step(self, enable: bool) -> None:
+        """ranks == 1 at N = 8192 / 16384: the four-step column pass (default) or the strip-dealt
+        column pass + transposes (what ranks > 1 run, bit-identical to them)."""
+        check(lib().ocean_generator_set_four_step(self._h, 1 if enable else 0), "ocean_generator_set_four_step")
+
     def frame_bytes(self):
         """Algorithmic HBM bytes per point of the column pass and the row pass (transposes included)."""
         b = (ctypes.c_double * 2)()

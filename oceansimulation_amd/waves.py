@@ -102,6 +102,11 @@ class Generator:
         """Select the half-spectrum (default where supported) or the full-spectrum frame path."""
         check(lib().ocean_generator_set_half_spectrum(self._h, 1 if enable else 0), "ocean_generator_set_half_spectrum")
 
+    def set_four_step(self, enable: bool) -> None:
+        """Whole grids of 8192 / 16384 on one rank: the four-step column pass (default) or the
+        strip-dealt column pass + transposes that multi-rank slabs run (bit-identical to them)."""
+        check(lib().ocean_generator_set_four_step(self._h, 1 if enable else 0), "ocean_generator_set_four_step")
+
     def frame_bytes(self):
         """Algorithmic HBM bytes per point of the column and row pass of the current path."""
         out = (ctypes.c_double * 2)()

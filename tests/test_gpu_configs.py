@@ -154,6 +154,7 @@ def test_config5_geometry_16384_eight_ranks_bit_exact(ocean):
     steps = [0.25, 1.0 / 60.0, 2.0]
     fft = ocean.FFTCalculator(n)
     whole = ocean.Generator(fft, 1)
+    whole.set_four_step(False)  # the strip-dealt path the ranks run (four-step: test_four_step_*)
     slabs = [SlabGenerator(fft, r, P) for r in range(P)]
     sends = [DeviceBuffer(g.exchange_bytes) for g in slabs]
     recvs = [DeviceBuffer(g.exchange_bytes) for g in slabs]
@@ -174,6 +175,63 @@ def test_config5_geometry_16384_eight_ranks_bit_exact(ocean):
     for g in slabs:
         g.close()
     whole.close()
+    fft.close()
+
+
+@pytest.mark.parametrize("n", [8192, 16384])
+def test_four_step_whole_grid_matches_dealt_path(ocean, n):
+    """Whole grids of 8192 / 16384 on one rank: the four-step column pass (default; 16-point step
+    in registers, N/16-point step straight into the row-major fields) against the strip-dealt column
+    pass + transposes (ocean_generator_set_four_step(0), the multi-rank path), over frames with an
+    h0 re-layout in between (the switch re-seeds h0 from the settings it was seeded with, not the
+    edited ones), within the cross-path bound; a P = 1 slab generator takes the four-step path too."""
+    from oceansimulation_amd.slab import SlabGenerator, emulate_frame
+    from oceansimulation_amd.hip import DeviceBuffer
+
+    fft = ocean.FFTCalculator(n)
+    g4, gd = ocean.Generator(fft, 1), ocean.Generator(fft, 1)
+    gd.set_four_step(False)
+    for g in (g4, gd):
+        ocean.apply_settings(g.GetOceanSettings(0), planeSize=777.0)
+        g.CalculateOcean(0.5)
+    # an unflagged settings edit must not leak into h0 when the layout switches
+    g4.set_four_step(False)
+    ocean.apply_settings(g4.GetOceanSettings(0), U_10=3.0)
+    g4.CalculateOcean(1.0 / 60.0)
+    g4.set_four_step(True)
+    ocean.apply_settings(g4.GetOceanSettings(0), U_10=40.0)
+    g4.CalculateOcean(1.0 / 60.0)
+    gd.CalculateOcean(1.0 / 60.0)
+    gd.CalculateOcean(1.0 / 60.0)
+    for get in ("height_map_host", "displacement_map_host"):
+        a, b = getattr(g4, get)(0), getattr(gd, get)(0)
+        assert max(lane_err(a, b)) <= 1e-5, (n, get, lane_err(a, b))
+        del a, b
+    j4, jd = g4.jacobian_map_host(0), gd.jacobian_map_host(0)
+    assert np.abs(j4 - jd).max() <= 1e-5 * np.abs(jd).max()
+    del j4, jd
+    g4.close()
+    gd.close()
+    # a slab generator with one rank runs the same four-step path, through caller exchange buffers:
+    # bit-identical to a whole grid
+    w4, s1 = ocean.Generator(fft, 1), SlabGenerator(fft, 0, 1)
+    ocean.apply_settings(w4.GetOceanSettings(0), planeSize=777.0)
+    ocean.apply_settings(s1.GetOceanSettings(), planeSize=777.0)
+    snd, rcv = DeviceBuffer(s1.exchange_bytes), DeviceBuffer(s1.exchange_bytes)
+    from oceansimulation_amd import capi, hip
+
+    L = capi.lib()
+    for k, dt in enumerate((0.5, 1.0 / 60.0)):
+        w4.CalculateOcean(dt)
+        emulate_frame([s1], [snd], [rcv], dt, update_ocean=(k == 0))
+        hip.synchronize()
+        for get, tex in ((L.ocean_generator_height_map, 16), (L.ocean_generator_displacement_map, 16),
+                         (L.ocean_generator_jacobian_map, 4)):
+            assert _dev_equal(int(get(s1.handle, 0)), int(get(w4.handle, 0)), n * n * tex), (k, get.__name__)
+    snd.free()
+    rcv.free()
+    s1.close()
+    w4.close()
     fft.close()
 
 

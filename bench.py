@@ -190,24 +190,44 @@ def cascade_settings(rank: int, c: int) -> dict:
     return dict(planeSize=PLANES[c % len(PLANES)], seed=(12342 + 4097 * rank, 8934 + 4097 * (c // len(PLANES))))
 
 
-TRAFFIC_PROFILES = ["r01_v4_rocprof.json", "r01_v3_rocprof.json", "r01_hs_rocprof.json", "r01_rocprof.json"]
+def device_source_sha256(root: str = "") -> str:
+    """Hash of the device code (ocean_kernels.hip, ocean_internal.h, device/*.h): the same function as
+    tools/parse_rocprof.py's, which stamps it into every PMC summary (tests/test_host_logic.py checks
+    that the two agree)."""
+    import hashlib
+
+    root = root or ROOT
+    csrc = os.path.join(root, "oceansimulation_amd", "csrc")
+    files = [os.path.join(csrc, "ocean_kernels.hip"), os.path.join(csrc, "ocean_internal.h")]
+    files += sorted(os.path.join(csrc, "device", f) for f in os.listdir(os.path.join(csrc, "device")) if f.endswith(".h"))
+    h = hashlib.sha256()
+    for f in files:
+        with open(f, "rb") as fh:
+            h.update(os.path.relpath(f, root).encode() + b"\0" + fh.read())
+    return h.hexdigest()
 
 
 def measured_traffic(kernel: str, n: int, cascades: int):
-    """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC summary of this workload
-    (tools/profile_gpu.sh: separate --pmc FETCH_SIZE and --pmc WRITE_SIZE passes over bench.py,
-    read = 2 x FETCH_SIZE, write = WRITE_SIZE, KB = 1024 B; tools/parse_rocprof.py), or None."""
-    # newest collection first: the current kernels (r01_v4), then older ones (r01_v3, r01_hs; r01: full spectrum)
-    for path in [os.path.join(ROOT, "profiles", p) for p in TRAFFIC_PROFILES]:
+    """HBM bytes per launch of `kernel` from a committed rocprofv3 PMC summary of this workload AND of
+    this device code (profiles/*_rocprof.json whose device_source_sha256 equals the running tree's;
+    tools/profile_gpu.sh: separate --pmc FETCH_SIZE and --pmc WRITE_SIZE passes over bench.py, read =
+    2 x FETCH_SIZE, write = WRITE_SIZE, KB = 1024 B; tools/parse_rocprof.py), or None when no
+    summary of this build exists (the traffic of other builds is not attributed to this one)."""
+    sha = device_source_sha256()
+    prof_dir = os.path.join(ROOT, "profiles")
+    for name in sorted((f for f in os.listdir(prof_dir) if f.endswith("_rocprof.json")), reverse=True):
+        path = os.path.join(prof_dir, name)
         try:
             with open(path) as f:
                 prof = json.load(f)
         except (OSError, ValueError):
             continue
         rec = prof.get("kernels", {}).get(kernel)
-        if prof.get("n") == n and prof.get("cascades") == cascades and rec and rec.get("hbm_traffic_bytes"):
+        if (prof.get("device_source_sha256") == sha and prof.get("n") == n and prof.get("cascades") == cascades
+                and rec and rec.get("hbm_traffic_bytes")):
             return {"hbm_traffic_bytes": rec["hbm_traffic_bytes"],
-                    "source": f"{os.path.relpath(path, ROOT)} (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, same workload)"}
+                    "source": f"{os.path.relpath(path, ROOT)} (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, same "
+                              f"workload, same device code sha256 {sha[:12]})"}
     return None
 
 
@@ -683,6 +703,9 @@ def main(argv=None):
             out["roofline"]["traffic_bytes_per_launch"] = pmc["hbm_traffic_bytes"]
             out["roofline"]["algorithmic_bytes_per_launch"] = dom["bytes"]
             out["roofline"]["traffic_source"] = pmc["source"]
+        else:
+            out["roofline"]["traffic_note"] = ("no committed PMC summary of this device code "
+                                               f"(sha256 {device_source_sha256()[:12]}); tools/profile_gpu.sh")
         frame_gbs = (pass_bytes[0] + pass_bytes[1]) * per_launch_pts / ((p1_ms + p2_ms) * 1e-3) / 1e9
         out["kernels"] = {
             k: {"avg_ms": v["avg_ms"], "GB_per_s": v["bytes"] / (v["avg_ms"] * 1e-3) / 1e9,

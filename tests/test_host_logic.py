@@ -130,3 +130,31 @@ def test_bench_cpu_baseline_core_accounting(monkeypatch):
     monkeypatch.delenv("OMP_NUM_THREADS")
     threads, _, affinity = b.host_cores()
     assert threads == affinity
+
+
+def test_traffic_attribution_needs_same_device_code(tmp_path, monkeypatch):
+    """roofline.traffic comes only from a PMC summary stamped with the running tree's device-code
+    hash (bench.py and tools/parse_rocprof.py hash the same files the same way); a summary of other
+    device code is ignored."""
+    import json
+    import shutil
+
+    b = _bench()
+    src = open(os.path.join(ROOT, "tools", "parse_rocprof.py")).read().split("src, tag =")[0]
+    g = {"__file__": os.path.join(ROOT, "tools", "parse_rocprof.py"), "__name__": "parse_rocprof"}
+    exec(src, g)
+    assert g["device_source_sha256"]() == b.device_source_sha256()
+    assert g["base_name"]("void oceanfft::k_rows_half<12, 0, 2>(oceanfft::FrameParams, float*)") == "k_rows_half"
+    # a fake tree: same device code, one matching and one stale summary
+    root = tmp_path / "tree"
+    shutil.copytree(os.path.join(ROOT, "oceansimulation_amd", "csrc"), root / "oceansimulation_amd" / "csrc",
+                    ignore=shutil.ignore_patterns("build", "*.o"))
+    (root / "profiles").mkdir()
+    rec = {"kernels": {"k_rows_half": {"hbm_traffic_bytes": 123.0}}, "n": 4096, "cascades": 8}
+    (root / "profiles" / "r09_stale_rocprof.json").write_text(json.dumps(dict(rec, device_source_sha256="0" * 64)))
+    monkeypatch.setattr(b, "ROOT", str(root))
+    assert b.measured_traffic("k_rows_half", 4096, 8) is None
+    sha = b.device_source_sha256(str(root))
+    (root / "profiles" / "r01_same_rocprof.json").write_text(json.dumps(dict(rec, device_source_sha256=sha)))
+    got = b.measured_traffic("k_rows_half", 4096, 8)
+    assert got["hbm_traffic_bytes"] == 123.0 and "r01_same_rocprof.json" in got["source"]

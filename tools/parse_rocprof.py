@@ -8,10 +8,32 @@ Algorithmic bytes per launch come from the bench config (N, cascades) and DESIGN
 figures. Usage: tools/parse_rocprof.py <gpurun_out dir> <tag> [n] [cascades]
 """
 import csv
+import hashlib
 import json
 import os
 import statistics
 import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def device_source_sha256(root=ROOT):
+    """Hash of the device code the kernels are built from (ocean_kernels.hip + device/*.h, sorted):
+    bench.py takes roofline.traffic only from a summary whose hash equals the running tree's."""
+    csrc = os.path.join(root, "oceansimulation_amd", "csrc")
+    files = [os.path.join(csrc, "ocean_kernels.hip"), os.path.join(csrc, "ocean_internal.h")]
+    files += sorted(os.path.join(csrc, "device", f) for f in os.listdir(os.path.join(csrc, "device")) if f.endswith(".h"))
+    h = hashlib.sha256()
+    for f in files:
+        with open(f, "rb") as fh:
+            h.update(os.path.relpath(f, root).encode() + b"\0" + fh.read())
+    return h.hexdigest()
+
+
+def base_name(symbol):
+    """k_rows_half from 'void oceanfft::k_rows_half<12, 0, ...>(oceanfft::FrameParams, ...)'."""
+    s = symbol.split("(")[0].replace("void ", "").replace("oceanfft::", "").strip()
+    return s.split("<")[0]
 
 src, tag = sys.argv[1], sys.argv[2]
 n = int(sys.argv[3]) if len(sys.argv) > 3 else 4096
@@ -36,36 +58,50 @@ def find(sub, suffix):
     raise FileNotFoundError(f"{d}/*{suffix}")
 
 
-stats = {r["Name"]: r for r in read_csv(find("prof_trace", "kernel_stats.csv"))}
+stats = {}
+for r in read_csv(find("prof_trace", "kernel_stats.csv")):
+    stats[r["Name"]] = r
 counters = {}
 for sub, name in (("prof_fetch", "FETCH_SIZE"), ("prof_write", "WRITE_SIZE")):
     for r in read_csv(find(sub, "counter_collection.csv")):
         if r["Counter_Name"] == name:
             counters.setdefault(r["Kernel_Name"], {}).setdefault(name, []).append(float(r["Counter_Value"]))
+# full symbols (no -T): aggregate per base name, keeping the symbols each base name covered
+by_base = {}
+for sym in list(stats) + list(counters):
+    by_base.setdefault(base_name(sym), set()).add(sym)
 
-out = {"tag": tag, "n": n, "cascades": cascades, "kernels": {}}
+out = {"tag": tag, "n": n, "cascades": cascades, "device_source_sha256": device_source_sha256(), "kernels": {}}
 lines = [f"# rocprofv3 summary — {tag}", "",
          f"Workload: bench.py, {cascades} cascades of {n}x{n} per launch. Durations: `--kernel-trace --stats`. "
          "Traffic: separate `--pmc FETCH_SIZE` and `--pmc WRITE_SIZE` passes; read = 2 x FETCH_SIZE (gfx950 "
          "half-count correction), write = WRITE_SIZE; KB = 1024 B.", "",
          "| kernel | calls | avg ms | algorithmic GB/launch | measured HBM GB/launch (read + write) | traffic / algorithmic | achieved GB/s (algorithmic) |",
          "|---|---|---|---|---|---|---|"]
-for name, st in stats.items():
-    avg_ms = float(st["AverageNs"]) / 1e6
-    c = counters.get(name, {})
-    rd = statistics.median(c["FETCH_SIZE"]) * 1024 * 2 if "FETCH_SIZE" in c else None
-    wr = statistics.median(c["WRITE_SIZE"]) * 1024 if "WRITE_SIZE" in c else None
+for name in sorted(by_base):
+    syms = by_base[name]
+    st_list = [stats[sy] for sy in syms if sy in stats]
+    if not st_list:
+        continue
+    calls = sum(int(st["Calls"]) for st in st_list)
+    avg_ms = sum(float(st["AverageNs"]) * int(st["Calls"]) for st in st_list) / calls / 1e6
+    fe = [v for sy in syms for v in counters.get(sy, {}).get("FETCH_SIZE", [])]
+    wr_ = [v for sy in syms for v in counters.get(sy, {}).get("WRITE_SIZE", [])]
+    rd = statistics.median(fe) * 1024 * 2 if fe else None
+    wr = statistics.median(wr_) * 1024 if wr_ else None
     algo = ALGO.get(name)
     traffic = (rd + wr) if (rd is not None and wr is not None) else None
-    rec = {"calls": int(st["Calls"]), "avg_ms": avg_ms, "algorithmic_bytes": algo, "hbm_read_bytes": rd,
-           "hbm_write_bytes": wr, "hbm_traffic_bytes": traffic}
+    rec = {"calls": calls, "avg_ms": avg_ms, "algorithmic_bytes": algo, "hbm_read_bytes": rd,
+           "hbm_write_bytes": wr, "hbm_traffic_bytes": traffic, "symbols": sorted(syms)}
     if algo:
         rec["achieved_GBps_algorithmic"] = algo / (avg_ms * 1e-3) / 1e9
     out["kernels"][name] = rec
     f = lambda v: "-" if v is None else f"{v / 1e9:.3f}"
     ratio = f"{traffic / algo:.3f}" if (traffic and algo) else "-"
     ach = f"{rec['achieved_GBps_algorithmic']:.0f}" if algo else "-"
-    lines.append(f"| {name} | {st['Calls']} | {avg_ms:.3f} | {f(algo)} | {f(rd)} + {f(wr)} | {ratio} | {ach} |")
+    lines.append(f"| {name} | {calls} | {avg_ms:.3f} | {f(algo)} | {f(rd)} + {f(wr)} | {ratio} | {ach} |")
+lines += ["", f"Device source sha256: `{out['device_source_sha256']}` (bench.py uses this summary's traffic only for "
+          "the same device code)."]
 os.makedirs("profiles", exist_ok=True)
 with open(f"profiles/{tag}_rocprof.json", "w") as fh:
     json.dump(out, fh, indent=1)

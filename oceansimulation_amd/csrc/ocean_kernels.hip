@@ -1040,7 +1040,7 @@ __global__ __launch_bounds__(256) void k_half_nyquist(FrameParams fp, int n, int
 // FB: the field strips' width (half_group_offset); GRP: consecutive items run together on one XCD
 // (2: pairs, xcd_pair_slot; 4: FB = 2 with RGC = 8, where four items share each gc line).
 template <int LOGN, int LA = kStream, int SA = kStream, int ABL = 0, int RPW_ = 2, bool BOTH = false, bool RM = false,
-          int RG = 1, int RGC = 1, int FB = 4, int GRP = 2>
+          int RG = 1, int RGC = 1, int FB = 4, int GRP = 2, bool IL = true>
 __global__ __launch_bounds__(FftShape<LOGN>::T * RPW_) void k_rows_half(
     FrameParams fp, const float4* __restrict__ gab, const float4* __restrict__ gde, const float2* __restrict__ gc,
     const float4* __restrict__ spec, float4* __restrict__ maps, float* __restrict__ jac, FoamParams foam,
@@ -1059,7 +1059,14 @@ __global__ __launch_bounds__(FftShape<LOGN>::T * RPW_) void k_rows_half(
 
   const int blocks = (RM ? rows : N) / RPW;
   const int b0 = threadIdx.x % B, r0 = (threadIdx.x / B) % RPW, ihi0 = threadIdx.x / (B * RPW);
-  const int i20 = threadIdx.x % T, r20 = threadIdx.x / T;
+  // After the first exchange: RPW = 2 interleaves the two rows (lanes: row fastest) and their LDS
+  // regions (CI = 2, slot = 2 pa + row), so a wave's reads of 32 consecutive positions never straddle
+  // a pad slot: conflict-free exchanges at 4096 (the row layout cost one extra cycle per 32-lane read
+  // group, 262 K LDS cycles per CU per frame = SQ_LDS_BANK_CONFLICT; tools/lds_banks.py models both).
+  // (A/B, halfbench rows: 1.449 -> 1.417 ms at 8 x 4096^2, 0.341 -> 0.335 at 2048; at 1024 the row
+  // layout stays: 0.079 vs 0.083 ms). IL = false: the row layout.
+  constexpr int CI = (IL && RPW == 2 && T >= 128) ? 2 : 0;
+  const int i20 = CI ? (threadIdx.x / RPW) % T : threadIdx.x % T, r20 = CI ? threadIdx.x % RPW : threadIdx.x / T;
   const int total = fp.cascades * (BOTH ? 1 : 2) * blocks;
   const float dim = (float)N;
   // RPW = 2: C's row pairs are 64-B halves of 128-B lines; items 2p, 2p+1 (the same line) run
@@ -1180,7 +1187,7 @@ __global__ __launch_bounds__(FftShape<LOGN>::T * RPW_) void k_rows_half(
       __syncthreads();  // the transform's first exchange reuses the LDS
     const int i2 = opaque(i20), r2 = RPW == 1 ? 0 : opaque(r20);
     if constexpr (ABL != 2)
-      fft_run<LOGN, 0, true>(v, i, r, i2, r2, xch, tw);
+      fft_run<LOGN, CI, true>(v, i, r, i2, r2, xch, tw);
     float4* dst = maps + ((size_t)cimg * (RM ? rows : N) + y0) * N;
     const int woff = ((r2 << LOGN) + i2) * 16;
 #pragma unroll
@@ -1901,6 +1908,7 @@ hipError_t launch_half_rows(int logn, const FrameParams& fp, const float4* gab, 
                   : ablation == 12 ? k_rows_half<LOGN, 0, kStream, 0, 2, true, false, 4, 8, 2, 4>
                   : ablation == 13 ? k_rows_half<LOGN, 0, kStream, 0, 2, true, false, 2, 4, 2, 2>
                   : ablation == 14 ? k_rows_half<LOGN, 0, kStream, 0, 2, true, false, 4, 4, 2, 2>
+                  : ablation == 15 ? k_rows_half<LOGN, 0, kStream, 0, 2, true, false, RG, RGC, 4, 2, false>
                   : ablation == 7 ? k_rows_half<LOGN, kStream, kStream, 0, 2, true, false, RG, RGC>
                   : ablation == 6 ? k_rows_half<LOGN, kStream, kStream, 0, 2, false, false, RG, RGC>
                   : ablation == 1 ? k_rows_half<LOGN, kStream, kStream, 1>

@@ -1,6 +1,6 @@
 // halfbench.hip — interleaved A/B timing of half-spectrum frame-pass variants (8 cascades x 4096^2),
 // with a bit-identity check of every variant's output against the baseline variant.
-// Build: see Makefile target `microbench`. Usage: halfbench [logn] [cascades] [quick]
+// Build: see Makefile target `microbench`. Usage: halfbench [logn] [cascades] [quick|mall|rows]
 #include "../../oceansimulation_amd/csrc/ocean_kernels.hip"
 
 #include <algorithm>
@@ -162,7 +162,78 @@ int main(int argc, char** argv)
   std::printf("N=%d cascades=%d CUs=%d  bit-identical: cols deterministic=%s cols(HS)=%s rows(both images)=%s\n", n, C,
               cus, det ? "yes" : "NO", same_cols ? "yes" : "NO", same_rows ? "yes" : "NO");
 
-  const bool quick = argc > 3 && std::strcmp(argv[3], "quick") == 0;  // only the block below
+  const bool quick = argc > 3 && std::strcmp(argv[3], "quick") == 0;  // only the blocks below
+  const bool mall = argc > 3 && std::strcmp(argv[3], "mall") == 0;
+  if (argc > 3 && std::strcmp(argv[3], "rows") == 0)
+  {
+    // row pass: interleaved row regions after the first exchange (production) against the row
+    // layout (launch_half_rows ablation 15); same arithmetic, so bit-identical maps
+    CHECK(c1());
+    CHECK(r1());
+    CHECK(hipDeviceSynchronize());
+    auto pm = snap(maps, mb), pj = snap(jac, jb);
+    CHECK(hipMemset(maps, 0, mb));
+    auto r15 = [&] { return launch_half_rows(logn, fp, gab, gcd, ge, spec, maps, jac, foam, tw, 0, cus, 15); };
+    CHECK(r15());
+    CHECK(hipDeviceSynchronize());
+    std::printf("row layout vs interleaved rows:\n");
+    const bool same = (int)diff(snap(maps, mb), pm) & (int)diff(snap(jac, jb), pj);
+    std::vector<std::vector<float>> tr(2);
+    for (int r = 0; r < 9; r++)
+    {
+      tr[0].push_back(time_ms(r1, 10));
+      tr[1].push_back(time_ms(r15, 10));
+    }
+    for (int k = 0; k < 2; k++)
+      std::sort(tr[k].begin(), tr[k].end());
+    std::printf("rows, interleaved regions (production)  median %7.3f ms\n", tr[0][4]);
+    std::printf("rows, row layout (round 1)              median %7.3f ms  bit-identical %s\n", tr[1][4], same ? "yes" : "NO");
+    return 0;
+  }
+  if (mall)
+  {
+    // one cascade at a time (pass 1 then pass 2 per cascade: its 336 MB of fields may still sit in
+    // the 256 MB Infinity Cache when pass 2 reads them) against both passes over all cascades
+    const size_t ht1 = half_field_texels(logn);
+    auto per_cascade = [&] {
+      for (int c = 0; c < C; c++)
+      {
+        FrameParams f1{};
+        f1.cascades = 1;
+        f1.c[0] = fp.c[c];
+        FoamParams o1{};
+        o1.displacement[0] = foam.displacement[c];
+        hipError_t e = launch_half_columns(logn, f1, h0 + tex * c, gab + ht1 * c, gcd + ht1 * c, ge + ht1 * c,
+                                           spec + (size_t)2 * n * c, tw, 0, cus, hs, cus);
+        if (e == hipSuccess)
+          e = launch_half_rows(logn, f1, gab + ht1 * c, gcd + ht1 * c, ge + ht1 * c, spec + (size_t)2 * n * c,
+                               maps + tex * 2 * c, jac + tex * c, o1, tw, 0, cus);
+        if (e != hipSuccess)
+          return e;
+      }
+      return hipSuccess;
+    };
+    auto batched = [&] { hipError_t e = c1(); return e == hipSuccess ? r1() : e; };
+    CHECK(batched());
+    CHECK(hipDeviceSynchronize());
+    auto bm = snap(maps, mb), bj = snap(jac, jb);
+    CHECK(hipMemset(maps, 0, mb));
+    CHECK(per_cascade());
+    CHECK(hipDeviceSynchronize());
+    std::printf("per-cascade frame vs batched frame:\n");
+    const bool same = (int)diff(snap(maps, mb), bm) & (int)diff(snap(jac, jb), bj);
+    std::vector<std::vector<float>> tm(2);
+    for (int r = 0; r < 7; r++)
+    {
+      tm[0].push_back(time_ms(batched, 10));
+      tm[1].push_back(time_ms(per_cascade, 10));
+    }
+    for (int k = 0; k < 2; k++)
+      std::sort(tm[k].begin(), tm[k].end());
+    std::printf("frame batched (2 launches)          median %7.3f ms\n", tm[0][3]);
+    std::printf("frame per cascade (2 x %d launches) median %7.3f ms  bit-identical %s\n", C, tm[1][3], same ? "yes" : "NO");
+    return 0;
+  }
   {
     // pass 1 on half-strip items (k_cols_half CPI = B / 2, 512 threads, two workgroups per CU,
     // variant 20) against production (whole strips, 1024 threads, one per CU): fields must be

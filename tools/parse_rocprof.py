@@ -5,7 +5,7 @@ HBM traffic per launch, corrected as MI355X_MICROARCH.md §HBM prescribes for gf
   read  bytes = 2 * FETCH_SIZE * 1024   (FETCH_SIZE counts 128-B requests as 64 B; unit KB)
   write bytes =     WRITE_SIZE * 1024   (exact for 16-B-per-lane streaming stores)
 Algorithmic bytes per launch come from the bench config (N, cascades) and DESIGN.md's per-point
-figures. Usage: tools/parse_rocprof.py <gpurun_out dir> <tag> [n] [cascades]
+figures. Usage: tools/parse_rocprof.py <gpurun_out dir> <tag> [n] [cascades] [prefix] [frame|ifft]
 """
 import csv
 import hashlib
@@ -35,14 +35,29 @@ def base_name(symbol):
     s = symbol.split("(")[0].replace("void ", "").replace("oceanfft::", "").strip()
     return s.split("<")[0]
 
+
+def size_key(symbol, logn):
+    """The summary key: the base name for instantiations at the workload's log2 N (what bench.py
+    looks up), else base<first template argument> (other sizes: k_rows_half<14>, k_gen4_step2<10>)."""
+    s = symbol.split("(")[0].replace("void ", "").replace("oceanfft::", "").strip()
+    if "<" not in s:
+        return s
+    first = s.split("<", 1)[1].split(",")[0].split(">")[0].strip()
+    return s.split("<")[0] if first == str(logn) else f"{s.split('<')[0]}<{first}>"
+
 src, tag = sys.argv[1], sys.argv[2]
 n = int(sys.argv[3]) if len(sys.argv) > 3 else 4096
 cascades = int(sys.argv[4]) if len(sys.argv) > 4 else 8
+prefix = sys.argv[5] if len(sys.argv) > 5 else "prof"  # tools/profile_gpu.sh PREFIX
+mode = sys.argv[6] if len(sys.argv) > 6 else "frame"  # frame | ifft (EncodeIFFT chunks of 8 images)
 pts = n * n * cascades
 kept = (n // 2 + 4) / n  # half-spectrum path: columns u in [0, N/2) plus the 4-wide Nyquist strip
 ALGO = {"k_cols_evolve": 48 * pts, "k_rows_final": 68 * pts, "k_generate_spectrum": 16 * n * n,
         "k_generate_spectrum_pairs": 16 * n * n,
-        "k_cols_half": int((16 + 40) * kept * pts), "k_rows_half": int((40 * kept + 36) * pts)}
+        "k_cols_half": int((16 + 40) * kept * pts), "k_rows_half": int((40 * kept + 36) * pts),
+        "k_gen4_step1": int((16 + 40) * kept * pts)}
+if mode == "ifft":  # standalone EncodeIFFT at 4096: work-image chunks of 8 images, 32 B per texel per pass
+    ALGO["k_cols_to_blocks"] = ALGO["k_rows_final"] = 32 * 8 * n * n
 
 
 def read_csv(path):
@@ -59,17 +74,18 @@ def find(sub, suffix):
 
 
 stats = {}
-for r in read_csv(find("prof_trace", "kernel_stats.csv")):
+for r in read_csv(find(prefix + "_trace", "kernel_stats.csv")):
     stats[r["Name"]] = r
 counters = {}
-for sub, name in (("prof_fetch", "FETCH_SIZE"), ("prof_write", "WRITE_SIZE")):
+for sub, name in ((prefix + "_fetch", "FETCH_SIZE"), (prefix + "_write", "WRITE_SIZE")):
     for r in read_csv(find(sub, "counter_collection.csv")):
         if r["Counter_Name"] == name:
             counters.setdefault(r["Kernel_Name"], {}).setdefault(name, []).append(float(r["Counter_Value"]))
 # full symbols (no -T): aggregate per base name, keeping the symbols each base name covered
 by_base = {}
+logn = n.bit_length() - 1
 for sym in list(stats) + list(counters):
-    by_base.setdefault(base_name(sym), set()).add(sym)
+    by_base.setdefault(size_key(sym, logn), set()).add(sym)
 
 out = {"tag": tag, "n": n, "cascades": cascades, "device_source_sha256": device_source_sha256(), "kernels": {}}
 lines = [f"# rocprofv3 summary — {tag}", "",

@@ -400,6 +400,66 @@ __device__ __forceinline__ void fft_run(V* v, int i, int reg, void* lds, const f
   fft_run<LOGN, CI, SPLIT>(v, i, reg, i, reg, lds, tw);
 }
 
+// The same transform with each thread holding TWO positions of one transform (32 points: virtual
+// threads ia and ib = ia + T/2 of region reg), so half as many threads cover the workgroup's
+// transforms and each has twice the registers. Radix-16 stages only (N = 16^k); CI > 0 layouts,
+// split exchanges. Both groups are written before the barrier and read after it, so an exchange
+// costs the same barriers as fft_run's.
+template <int LOGN, int CI>
+__device__ __forceinline__ void exchange_x2(CPair* va, CPair* vb, int reg, void* lds_raw, int ia, int ib, int base_a,
+                                            int base_b, int st)
+{
+  using S = FftShape<LOGN>;
+  float2* lds = reinterpret_cast<float2*>(lds_raw);
+#pragma unroll
+  for (int half = 0; half < 2; half++)
+  {
+#pragma unroll
+    for (int t = 0; t < 16; t++)
+    {
+      lds[lds_slot<CI, S::PADDED>(reg, base_a + t * st)] = half_of(va[t], half);
+      lds[lds_slot<CI, S::PADDED>(reg, base_b + t * st)] = half_of(vb[t], half);
+    }
+    XSYNC();
+#pragma unroll
+    for (int m = 0; m < 16; m++)
+    {
+      set_half(va[m], half, lds[lds_slot<CI, S::PADDED>(reg, read_pidx<LOGN>(ia, m))]);
+      set_half(vb[m], half, lds[lds_slot<CI, S::PADDED>(reg, read_pidx<LOGN>(ib, m))]);
+    }
+    XSYNC();
+  }
+}
+
+template <int LOGN, int CI>
+__device__ __forceinline__ void fft_run_x2(CPair* va, CPair* vb, int ia, int reg, void* lds, const float2* __restrict__ tw)
+{
+  using S = FftShape<LOGN>;
+  constexpr int N = S::N, T = S::T;
+  static_assert(S::R0 == 16 && CI > 0, "radix-16 stages, column layout");
+  const int ib = ia + T / 2;
+  idft16(va);
+  idft16(vb);
+  // stage 0 outputs y[16 b + t] at pad16 = 17 b + t
+  exchange_x2<LOGN, CI>(va, vb, reg, lds, ia, ib, 17 * ia, 17 * ib, 1);
+  int p = 16;
+#pragma unroll
+  for (int s = 1; s < S::NSTAGE; s++)
+  {
+    const int stride = N / (16 * p);
+    apply_stage_twiddles<LOGN>(va, (ia & (p - 1)) * stride, tw);
+    apply_stage_twiddles<LOGN>(vb, (ib & (p - 1)) * stride, tw);
+    idft16(va);
+    idft16(vb);
+    if (s + 1 < S::NSTAGE)
+    {
+      const int ja = (ia / p) * 16 * p + (ia & (p - 1)), jb = (ib / p) * 16 * p + (ib & (p - 1));
+      exchange_x2<LOGN, CI>(va, vb, reg, lds, ia, ib, pad16(ja), pad16(jb), p + p / 16);
+    }
+    p *= 16;
+  }
+}
+
 template <int LOGN>
 __device__ __forceinline__ void load_twiddles(float2* tw_lds, const float2* __restrict__ tw_glob)
 {

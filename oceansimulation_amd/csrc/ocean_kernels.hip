@@ -962,6 +962,101 @@ __global__ __launch_bounds__(2 * FftShape<LOGN>::T) void k_cols_half2(FrameParam
   }
 }
 
+// Pass 1 with H in VGPRs (whole grids, N = 4096): one 4-column strip per item on T * B / 2 = 512
+// threads, each holding two positions (ia, ia + T/2) of one column, i.e. 32 points (fft_run_x2), so
+// the 32 evolved amplitudes H (64 VGPRs) stay in registers across the three rounds: no H scratch
+// (k_cols_half<HS> moves 24 B per kept texel through it) and h0 read once. Each store instruction of
+// a wave still covers 16 rows x 4 columns, i.e. whole 128-B lines of the row-group layout. 512
+// threads with 139 KiB of LDS: one workgroup per CU, 256 VGPRs per thread.
+// HB: the second position's H goes through a per-block scratch slice (hs) instead (fewer VGPRs).
+template <int LOGN, int LA = kStream, int SA = kStream, int RG = kHalfRG, int RGC = kHalfRGC, bool HB = false>
+__global__ __launch_bounds__(FftShape<LOGN>::T * 2) void k_cols_half4(FrameParams fp, const float4* __restrict__ h0,
+                                                                      float4* __restrict__ gab, float4* __restrict__ gde,
+                                                                      float2* __restrict__ gc,
+                                                                      const float2* __restrict__ tw_glob,
+                                                                      float2* __restrict__ hs)
+{
+  using S = FftShape<LOGN>;
+  using K = ColFirstCfg<LOGN>;
+  using HC = HalfCfg<LOGN>;
+  constexpr int N = S::N, T = S::T, B = K::B, STRIPS = HC::STRIPS;
+  static_assert(HC::SUPPORTED && B == 4 && S::R0 == 16, "4-column strips, radix-16 stages");
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  float2* tw = reinterpret_cast<float2*>(smem);
+  void* xch = smem + ((S::TW_ENTRIES * 8 + 15) / 16) * 16;
+  load_twiddles<LOGN>(tw, tw_glob);
+  const int total = fp.cascades * STRIPS;
+  const float dim = (float)N;
+  for (int item = blockIdx.x; item < total; item += gridDim.x)
+  {
+    const int c = item / STRIPS, s = item - c * STRIPS;
+    const int xb = s == STRIPS - 1 ? 0 : N / (2 * B) + s;
+    const CascadeFrame f = fp.c[c];
+    const float4* src = h0 + ((size_t)c * (N / B) + xb) * N * B;
+    const size_t gbase = (size_t)c * STRIPS * N * B + half_group_offset<LOGN, RG>(0, s);
+    const size_t cgbase = (size_t)c * STRIPS * N * B + half_group_offset<LOGN, RGC>(0, s);
+    float2 H[HB ? 1 : 2][16];
+    float2* hsb = hs + (size_t)blockIdx.x * 16 * (T * 2);
+    {
+      const int tid = opaque((int)threadIdx.x);
+      const int b = tid % B, ia = (tid / B) % (T / 2), x = xb * B + b;
+#pragma unroll
+      for (int g = 0; g < 2; g++)
+      {
+        const int p = ia + g * (T / 2);
+        float4 a[16];
+#pragma unroll
+        for (int m = 0; m < 16; m++)  // fftShift on y folded into the load
+          a[m] = ld4s<LA>(src, (p * B + b) * 16, ((m + 8) & 15) * T * B * 16);
+#pragma unroll
+        for (int m = 0; m < 16; m++)
+        {
+          const float2 h = evolve(a[m], make_kvec(x, p + ((m + 8) & 15) * T, dim, f.dk).k, f);
+          if (HB && g == 1)
+            st2s<0>(hsb, tid * 8, m * (T * 2) * 8, h);
+          else
+            H[g][m] = h;
+        }
+      }
+    }
+#pragma unroll
+    for (int round = 0; round < 3; round++)
+    {
+      // k-vectors recomputed per round (opaque: CSE would keep them live across the rounds)
+      const int tid = opaque((int)threadIdx.x);
+      const int b = tid % B, ia = (tid / B) % (T / 2), x = xb * B + b;
+      CPair v[2][16];
+#pragma unroll
+      for (int g = 0; g < 2; g++)
+#pragma unroll
+        for (int m = 0; m < 16; m++)
+        {
+          const float2 h = (HB && g == 1) ? ld2s<kStream>(hsb, tid * 8, m * (T * 2) * 8) : H[g == 1 && HB ? 0 : g][m];
+          v[g][m] = half_round_pack<LOGN>(round, h, make_kvec(x, ia + g * (T / 2) + ((m + 8) & 15) * T, dim, f.dk));
+        }
+      fft_run_x2<LOGN, B>(v[0], v[1], ia, b, xch, tw);
+#pragma unroll
+      for (int g = 0; g < 2; g++)
+      {
+        const int p = ia + g * (T / 2);
+#pragma unroll
+        for (int m = 0; m < 16; m++)
+        {
+          if (round == 0)
+            st4s<SA>(gab + gbase, half_group_offset<LOGN, RG>(p, 0, b) * 16, half_group_offset<LOGN, RG>(m * T, 0) * 16,
+                     pair_raw(v[g][m]));
+          else if (round == 1)
+            st4s<SA>(gde + gbase, half_group_offset<LOGN, RG>(p, 0, b) * 16, half_group_offset<LOGN, RG>(m * T, 0) * 16,
+                     pair_raw(v[g][m]));
+          else
+            st2s<SA>(gc + cgbase, half_group_offset<LOGN, RGC>(p, 0, b) * 8, half_group_offset<LOGN, RGC>(m * T, 0) * 8,
+                     make_float2(v[g][m].re.x, v[g][m].im.x));
+        }
+      }
+    }
+  }
+}
+
 // The Nyquist-row term: for u = -u' (0 < u' < N/2) the pass-2 rebuild s_F conj(G_F(q, u')) misses
 // (-1)^q Delta_F(u'), Delta_F(u') = F(-N/2, -u') - s_F conj(F(-N/2, u')). Its lanes (the kx
 // factors of pass 2 applied to Delta) form one row spectrum per image, spec[c][img][x] (zero
@@ -1845,6 +1940,17 @@ hipError_t launch_half_columns(int logn, const FrameParams& fp, const float4* h0
         const int hlds = ((S::TW_ENTRIES * 8 + 15) / 16) * 16 + 2 * S::PADDED * 16;
         const int hg = persistent_grid(hk, 2 * S::T, hlds, fp.cascades * 2 * HalfCfg<LOGN>::STRIPS, cus);
         hipLaunchKernelGGL(hk, dim3(hg), dim3(2 * S::T), hlds, stream, fp, h0, gab, gcd, ge, tw);
+        return hipGetLastError();
+      }
+      if constexpr (FftShape<LOGN>::R0 == 16)
+      if (variant == 22 && !seed)  // H in VGPRs: 32 points per thread, 512 threads (k_cols_half4)
+      {
+        auto hk = hs ? k_cols_half4<LOGN, kStream, kStream, kHalfRG, kHalfRGC, true> : k_cols_half4<LOGN>;
+        const int hlds = ((S::TW_ENTRIES * 8 + 15) / 16) * 16 + K::LDS1;
+        int hg = persistent_grid(hk, S::T * 2, hlds, fp.cascades * HalfCfg<LOGN>::STRIPS, cus);
+        if (hs && hg > hs_blocks)
+          hg = hs_blocks;
+        hipLaunchKernelGGL(hk, dim3(hg), dim3(S::T * 2), hlds, stream, fp, h0, gab, gcd, ge, tw, hs);
         return hipGetLastError();
       }
       if (variant == 20 && hs && !seed)  // half-strip items, two workgroups per CU (HS slices of half size)

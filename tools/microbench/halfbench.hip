@@ -250,17 +250,29 @@ int main(int argc, char** argv)
     std::printf("cols half strips 2/CU vs production: gab, gde, gc\n");
     const bool same20 = (int)diff(snap(gab, ht * sizeof(float4)), pab) & (int)diff(snap(gcd, ht * sizeof(float4)), pde) &
                         (int)diff(snap(ge, ht * sizeof(float2)), pc);
-    std::vector<std::vector<float>> tq(4);
+    auto c22 = [&] { return launch_half_columns(logn, fp, h0, gab, gcd, ge, spec, tw, 0, cus, hs, cus, nullptr, 22); };
+    CHECK(hipMemset(gab, 0, ht * sizeof(float4)));
+    CHECK(hipMemset(gcd, 0, ht * sizeof(float4)));
+    CHECK(hipMemset(ge, 0, ht * sizeof(float2)));
+    CHECK(c22());
+    CHECK(hipDeviceSynchronize());
+    std::printf("cols H in VGPRs (32 points per thread) vs production: gab, gde, gc\n");
+    const bool same22 = (int)diff(snap(gab, ht * sizeof(float4)), pab) & (int)diff(snap(gcd, ht * sizeof(float4)), pde) &
+                        (int)diff(snap(ge, ht * sizeof(float2)), pc);
+    std::printf("H-in-VGPR fields bit-identical: %s\n", same22 ? "yes" : "NO");
+    std::vector<std::vector<float>> tq(6);
     for (int r = 0; r < 7; r++)
     {
       tq[0].push_back(time_ms(c1, 10));
       tq[1].push_back(time_ms(c20, 10));
       tq[2].push_back(time_ms([&] { hipError_t e = c1(); return e == hipSuccess ? r1() : e; }, 10));
       tq[3].push_back(time_ms([&] { hipError_t e = c20(); return e == hipSuccess ? r1() : e; }, 10));
+      tq[4].push_back(time_ms(c22, 10));
+      tq[5].push_back(time_ms([&] { hipError_t e = c22(); return e == hipSuccess ? r1() : e; }, 10));
     }
     const char* qn[] = {"cols HS whole strips (production)", "cols HS half strips, 2/CU", "frame production",
-                        "frame with half-strip cols"};
-    for (int k = 0; k < 4; k++)
+                        "frame with half-strip cols", "cols H in VGPRs, 32 points/thread", "frame with H-in-VGPR cols"};
+    for (int k = 0; k < 6; k++)
     {
       std::sort(tq[k].begin(), tq[k].end());
       std::printf("%-40s median %7.3f ms\n", qn[k], tq[k][3]);

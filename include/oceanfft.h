@@ -149,6 +149,11 @@ int ocean_generator_set_half_spectrum(ocean_generator* gen, int enable);
  * rounding. Switching re-lays h0 out at the next frame from the settings it was seeded with. No
  * reference counterpart. */
 int ocean_generator_set_four_step(ocean_generator* gen, int enable);
+/* A re-seed requested by ocean_generator_calculate(.., update_spectrum = 1) — the reference app
+ * requests one on every frame (src/Waves.cpp:91-94) — is skipped when no h0 input (every settings
+ * field but `time`) changed since h0 was last seeded: it would reproduce the same image bit for bit.
+ * enable = 0 re-seeds on every request, as the reference does. Default 1. No reference counterpart. */
+int ocean_generator_set_h0_memo(ocean_generator* gen, int enable);
 /* Algorithmic HBM bytes per height-field point of the column pass [0] and the row pass [1] of the
  * generator's current path (what bench.py prices the roofline with). */
 int ocean_generator_frame_bytes(const ocean_generator* gen, double per_point[2]);

@@ -117,6 +117,10 @@ struct ocean_generator
   bool four_step = true;
   int h0_block = 0;                          // strip width the h0 image was last written with
   std::vector<ocean_settings> h0_settings;   // the settings it was written from
+  // the settings h0 was last seeded from (written or fused): a requested re-seed with the same
+  // h0 inputs (every field but `time`) would reproduce h0 bit for bit, so it is skipped
+  std::vector<ocean_settings> seeded;
+  bool memo_h0 = true;  // ocean_generator_set_h0_memo
   bool profiling = false;
   std::vector<EventPair> pending;
   std::vector<hipEvent_t> pool;
@@ -584,6 +588,7 @@ static int generate_spectrum_with(ocean_generator* g, const std::vector<ocean_se
   g->h0_stale = false;
   g->h0_block = h0_block(g);
   g->h0_settings = settings;
+  g->seeded = settings;
   ocean_fft* f = g->fft;
   const size_t slab = h0_texels(g);
   for (int c = 0; c < g->cascades; c++)
@@ -636,12 +641,32 @@ static int materialise_h0(ocean_generator* g)
 // First half of CalculateOcean: time += dt (src/Generator.cpp:50), h0 if requested (:55-59),
 // prepareFFT fused with the y direction of both EncodeIFFTs (:63-72). Output in destination-block
 // order into `out` (the internal buffer when null).
+// True when h0 seeded from `a` and from `b` is the same image: every field but the accumulated
+// time (generateSpectrum does not read it, spectrum.compute:157-172).
+static bool same_h0_inputs(const std::vector<ocean_settings>& a, const std::vector<ocean_settings>& b)
+{
+  if (a.size() != b.size())
+    return false;
+  for (size_t i = 0; i < a.size(); i++)
+  {
+    ocean_settings x = a[i], y = b[i];
+    x.time = y.time = 0.0f;
+    if (std::memcmp(&x, &y, sizeof(x)) != 0)
+      return false;
+  }
+  return true;
+}
+
 static int generator_columns(ocean_generator* g, float timestep, int update_spectrum, float4* out)
 {
   ocean_fft* f = g->fft;
   for (auto& s : g->settings)
     s.time += timestep;
   const void* seed = nullptr;
+  // The reference app asks for a re-seed on every frame (src/Waves.cpp:91-94); when the h0 inputs
+  // are unchanged since the last seeding the result would be bit-identical, so it is skipped.
+  if (update_spectrum && !g->update_spectrum && g->memo_h0 && same_h0_inputs(g->settings, g->seeded))
+    update_spectrum = 0;
   if (g->update_spectrum || update_spectrum)
   {
     // The generator's first seeding writes the h0 image. Explicit re-seeds (the reference app's
@@ -671,6 +696,7 @@ static int generator_columns(ocean_generator* g, float timestep, int update_spec
       seed = g->seedc;
       g->h0_stale = true;
       g->seed_settings = g->settings;
+      g->seeded = g->settings;
     }
     else
     {
@@ -791,6 +817,14 @@ int ocean_generator_set_half_spectrum(ocean_generator* g, int enable)
   g->hslab = enable && dealt;
   if (was_dealt_slab != (g->hslab && g->ranks > 1))
     g->update_spectrum = true;  // a slab's h0 layout changes (strips <-> column slab)
+  return OCEAN_OK;
+}
+
+int ocean_generator_set_h0_memo(ocean_generator* g, int enable)
+{
+  if (!g)
+    return fail(OCEAN_ERR_INVALID, "ocean_generator_set_h0_memo: null generator");
+  g->memo_h0 = enable != 0;
   return OCEAN_OK;
 }
 

@@ -107,6 +107,10 @@ class Generator:
         strip-dealt column pass + transposes that multi-rank slabs run (bit-identical to them)."""
         check(lib().ocean_generator_set_four_step(self._h, 1 if enable else 0), "ocean_generator_set_four_step")
 
+    def set_h0_memo(self, enable: bool) -> None:
+        """Skip requested re-seeds whose h0 inputs are unchanged (default) or re-seed every time."""
+        check(lib().ocean_generator_set_h0_memo(self._h, 1 if enable else 0), "ocean_generator_set_h0_memo")
+
     def frame_bytes(self):
         """Algorithmic HBM bytes per point of the column and row pass of the current path."""
         out = (ctypes.c_double * 2)()

@@ -393,6 +393,7 @@ def test_fused_reseed_frames(ocean, oracle):
     n, planes = 1024, [5.0, 23.0, 101.0]
     fft = ocean.FFTCalculator(n)
     fused, plain = ocean.Generator(fft, 3), ocean.Generator(fft, 3)
+    fused.set_h0_memo(False)  # re-seed on every request (unchanged settings would skip it)
     refs = []
     for c, L in enumerate(planes):
         for g in (fused, plain):
@@ -417,6 +418,35 @@ def test_fused_reseed_frames(ocean, oracle):
     fused.CalculateOcean(0.0, update_ocean=True)  # getter after a fused frame: the new settings
     ref = oracle.generate_spectrum(oracle.default_settings(U_10=20.0, planeSize=5.0), n)
     assert max(lane_err(fused.initial_spectrum_host(0), ref)) <= H0_TOL
+
+
+def test_h0_memo_skips_identical_reseeds(ocean, oracle):
+    """The reference app requests a re-seed every frame (src/Waves.cpp:91-94). With unchanged h0
+    inputs the re-seed is skipped (default): frames are bit-identical to frames without the request;
+    an edit of any h0 input (here U_10, then planeSize) with the request re-seeds (h0 equals the
+    oracle's for the new settings); `time` alone never re-seeds."""
+    n = 256
+    fft = ocean.FFTCalculator(n)
+    memo, plain = ocean.Generator(fft, 2), ocean.Generator(fft, 2)
+    for g in (memo, plain):
+        ocean.apply_settings(g.GetOceanSettings(1), planeSize=17.0)
+    for dt in (0.5, 1.0 / 60.0, 1.0 / 60.0):
+        memo.CalculateOcean(dt, update_ocean=True)
+        plain.CalculateOcean(dt)
+        for c in range(2):
+            assert np.array_equal(memo.height_map_host(c), plain.height_map_host(c))
+            assert np.array_equal(memo.displacement_map_host(c), plain.displacement_map_host(c))
+    ocean.apply_settings(memo.GetOceanSettings(0), U_10=20.0)
+    memo.CalculateOcean(1.0 / 60.0, update_ocean=True)
+    ref = oracle.generate_spectrum(oracle.default_settings(U_10=20.0), n)
+    assert max(lane_err(memo.initial_spectrum_host(0), ref)) <= H0_TOL
+    ocean.apply_settings(memo.GetOceanSettings(1), planeSize=23.0)
+    memo.CalculateOcean(1.0 / 60.0, update_ocean=True)
+    ref = oracle.generate_spectrum(oracle.default_settings(planeSize=23.0), n)
+    assert max(lane_err(memo.initial_spectrum_host(1), ref)) <= H0_TOL
+    memo.close()
+    plain.close()
+    fft.close()
 
 
 def test_errors_fail_loudly(ocean):

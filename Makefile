@@ -55,7 +55,7 @@ $(APP): examples/waveapp_headless.cpp $(WAVES)
 	    -L$(PKG) -lwaves -loceanfft -Wl,-rpath,'$$ORIGIN/../$(PKG)' -L/opt/rocm/lib -lamdhip64
 
 MB := tools/microbench
-microbench: $(MB)/gen4bench $(MB)/ifft4bench $(MB)/gridbench $(MB)/halfbench_nohs $(MB)/ifftbench $(MB)/transbench $(MB)/scatterbench $(MB)/halfbench $(MB)/genbench $(MB)/colbench $(MB)/copybench $(MB)/genbench_noxch $(MB)/genbench_nobar $(MB)/layoutbench
+microbench: $(MB)/rm16bench $(MB)/gen4bench $(MB)/ifft4bench $(MB)/gridbench $(MB)/halfbench_nohs $(MB)/ifftbench $(MB)/transbench $(MB)/scatterbench $(MB)/halfbench $(MB)/genbench $(MB)/colbench $(MB)/copybench $(MB)/genbench_noxch $(MB)/genbench_nobar $(MB)/layoutbench
 $(MB)/%: $(MB)/%.hip $(CSRC)/ocean_kernels.hip $(CSRC)/ocean_internal.h $(DEVICE_H)
 	$(HIPCC) $(HIPFLAGS) $< -o $@
 # timing ablations (wrong results by construction): no LDS exchanges / exchanges without barriers
@@ -67,7 +67,7 @@ $(MB)/genbench_nobar: $(MB)/genbench.hip $(CSRC)/ocean_kernels.hip $(CSRC)/ocean
 	$(HIPCC) $(HIPFLAGS) -DOCEAN_ABLATE_BARRIER $< -o $@
 
 clean:
-	rm -rf $(MB)/gen4bench $(MB)/ifft4bench $(MB)/gridbench $(MB)/halfbench_nohs $(MB)/ifftbench $(MB)/transbench $(MB)/scatterbench $(MB)/halfbench $(MB)/genbench $(MB)/colbench $(MB)/copybench $(MB)/genbench_noxch $(MB)/genbench_nobar $(MB)/layoutbench $(CSRC)/build $(LIB) $(WAVES) $(CPPTEST) $(APP)
+	rm -rf $(MB)/rm16bench $(MB)/gen4bench $(MB)/ifft4bench $(MB)/gridbench $(MB)/halfbench_nohs $(MB)/ifftbench $(MB)/transbench $(MB)/scatterbench $(MB)/halfbench $(MB)/genbench $(MB)/colbench $(MB)/copybench $(MB)/genbench_noxch $(MB)/genbench_nobar $(MB)/layoutbench $(CSRC)/build $(LIB) $(WAVES) $(CPPTEST) $(APP)
 	$(MAKE) -s -C oracle clean
 
 .PHONY: all clean microbench

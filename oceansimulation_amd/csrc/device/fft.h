@@ -276,10 +276,25 @@ __device__ __forceinline__ void touch(CPair& v) { asm volatile("" : "+v"(v.re), 
 #define XSYNC() __syncthreads()
 #endif
 
+// Exchange ordering. Workgroup transforms: a barrier. WAVE (the transform lives in one wavefront and
+// its LDS region is the wave's own): the LDS executes one wave's ds_* instructions in issue order, so
+// only the compiler has to keep the writes before the reads (and the reads before the next writes).
+template <bool WAVE>
+__device__ __forceinline__ void xsync()
+{
+  if constexpr (WAVE)
+  {
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_wave_barrier();
+  }
+  else
+    XSYNC();
+}
+
 // Write the 16 stage outputs (padded indices wp(t), region reg_w), barrier, read back the next
 // stage's inputs for the thread's (possibly different) position i_r in region reg_r, barrier.
 // SPLIT: float4 data exchanged as two float2 lanes through a float2 buffer (half the LDS).
-template <int LOGN, int CI, bool SPLIT, typename V, typename WP>
+template <int LOGN, int CI, bool SPLIT, bool WAVE = false, typename V, typename WP>
 __device__ __forceinline__ void exchange(V* v, int reg_w, int i_r, int reg_r, void* lds_raw, WP wp)
 {
   using S = FftShape<LOGN>;
@@ -294,11 +309,11 @@ __device__ __forceinline__ void exchange(V* v, int reg_w, int i_r, int reg_r, vo
 #pragma unroll
     for (int t = 0; t < 16; t++)
       lds[lds_slot<CI, S::PADDED>(reg_w, wp(t))] = v[t];
-    XSYNC();
+    xsync<WAVE>();
 #pragma unroll
     for (int m = 0; m < 16; m++)
       v[m] = lds[lds_slot<CI, S::PADDED>(reg_r, read_pidx<LOGN>(i_r, m))];
-    XSYNC();
+    xsync<WAVE>();
   }
   else
   {
@@ -310,11 +325,11 @@ __device__ __forceinline__ void exchange(V* v, int reg_w, int i_r, int reg_r, vo
 #pragma unroll
       for (int t = 0; t < 16; t++)
         lds[lds_slot<CI, S::PADDED>(reg_w, wp(t))] = half_of(v[t], half);
-      XSYNC();
+      xsync<WAVE>();
 #pragma unroll
       for (int m = 0; m < 16; m++)
         set_half(v[m], half, lds[lds_slot<CI, S::PADDED>(reg_r, read_pidx<LOGN>(i_r, m))]);
-      XSYNC();
+      xsync<WAVE>();
     }
   }
 }
@@ -325,7 +340,7 @@ __device__ __forceinline__ void exchange(V* v, int reg_w, int i_r, int reg_r, vo
 // reg2. Any bijection (i, reg) -> (i2, reg2) over the workgroup is valid: it lets the global loads
 // and the global stores use different lane mappings for free. Transforms with a single stage
 // (N = 16) have no exchange and require i2 == i, reg2 == reg.
-template <int LOGN, int CI, bool SPLIT, typename V>
+template <int LOGN, int CI, bool SPLIT, bool WAVE = false, typename V>
 __device__ __forceinline__ void fft_run(V* v, int i, int reg, int i2, int reg2, void* lds,
                                         const float2* __restrict__ tw)
 {
@@ -339,7 +354,7 @@ __device__ __forceinline__ void fft_run(V* v, int i, int reg, int i2, int reg2, 
     if constexpr (S::NSTAGE > 1)
     {
       const int base = 17 * i;  // pad16(16 i + t) = 17 i + t
-      exchange<LOGN, CI, SPLIT>(v, reg, i2, reg2, lds, [&](int t) { return base + t; });
+      exchange<LOGN, CI, SPLIT, WAVE>(v, reg, i2, reg2, lds, [&](int t) { return base + t; });
     }
   }
   else
@@ -363,7 +378,7 @@ __device__ __forceinline__ void fft_run(V* v, int i, int reg, int i2, int reg2, 
         v[u + t * U] = w[t];
     }
     // output of butterfly b = i + u*T, element t -> y[b*R0 + t]; v index q = u + t*U
-    exchange<LOGN, CI, SPLIT>(v, reg, i2, reg2, lds, [&](int q) {
+    exchange<LOGN, CI, SPLIT, WAVE>(v, reg, i2, reg2, lds, [&](int q) {
       int u = q % U, t = q / U;
       return pad16((i + u * T) * R0 + t);
     });
@@ -385,10 +400,10 @@ __device__ __forceinline__ void fft_run(V* v, int i, int reg, int i2, int reg2, 
       if (pp >= 16)
       {
         const int base = pad16(j), st = pp + pp / 16;
-        exchange<LOGN, CI, SPLIT>(v, reg2, i2, reg2, lds, [&](int t) { return base + t * st; });
+        exchange<LOGN, CI, SPLIT, WAVE>(v, reg2, i2, reg2, lds, [&](int t) { return base + t * st; });
       }
       else
-        exchange<LOGN, CI, SPLIT>(v, reg2, i2, reg2, lds, [&](int t) { return pad16(j + t * pp); });
+        exchange<LOGN, CI, SPLIT, WAVE>(v, reg2, i2, reg2, lds, [&](int t) { return pad16(j + t * pp); });
     }
     p *= 16;
   }

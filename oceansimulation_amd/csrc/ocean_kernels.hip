@@ -1134,22 +1134,51 @@ __global__ __launch_bounds__(256) void k_half_nyquist(FrameParams fp, int n, int
 // RG / RGC (whole grids): the field layout pass 1 wrote (half_group_offset).
 // FB: the field strips' width (half_group_offset); GRP: consecutive items run together on one XCD
 // (2: pairs, xcd_pair_slot; 4: FB = 2 with RGC = 8, where four items share each gc line).
+// XS (RPW = 1, N = 16 T, T = 1024: one row per 16-wave workgroup): the x transform in four steps
+// so that most of it runs between workgroup barriers instead of across them. With n = n1 + 16 n2
+// and k = k2 + T k1: a transposition through LDS (T_in, which also does the mirror exchange's job)
+// gives wave n1 the T inputs x(n1 + 16 n2); each wave runs its T-point sub-transform (fft_run<LOGN -
+// 4>, 64 lanes x 16 points) in its own LDS region, ordered by the LDS's in-order execution of one
+// wave's instructions instead of barriers; twiddles W_N^(n1 k2); a second transposition (T_out)
+// gives thread k2 the 16 values over n1, and a 16-point DFT in registers leaves X(k2 + T k1) in the
+// plain path's layout (coalesced stores). Barriers per image: 7 instead of 14 (mirror 2 + three
+// exchanges of two halves x 2 + 1). rm16bench priced the barriers of the 16384 pass at ~1 ms of
+// 3.8. tw2_glob: the T-point table (appended for 8192/16384 by ocean_fft_create).
+template <int LOGN>
+struct XsCfg
+{
+  static constexpr int L2 = LOGN - 4;
+  // region of one n1 (slots of 8 B): holds a sub-transform's padded exchange (PADDED + 4), and
+  // RS = 1 mod 16 spreads T_in's 16-lane writes (16 regions at once) over all 32 banks
+  static constexpr int RS = ((FftShape<L2>::PADDED + 4 + 14) / 16) * 16 + 1;
+  static constexpr int TW1 = ((FftShape<LOGN>::TW_ENTRIES * 8 + 15) / 16) * 16;
+  static constexpr int TW2 = ((FftShape<L2>::TW_ENTRIES * 8 + 15) / 16) * 16;
+  static constexpr int LDS = TW1 + TW2 + 16 * RS * 8;
+};
+
 template <int LOGN, int LA = kStream, int SA = kStream, int ABL = 0, int RPW_ = 2, bool BOTH = false, bool RM = false,
-          int RG = 1, int RGC = 1, int FB = 4, int GRP = 2, bool IL = true>
+          int RG = 1, int RGC = 1, int FB = 4, int GRP = 2, bool IL = true, bool XS = false>
 __global__ __launch_bounds__(FftShape<LOGN>::T * RPW_) void k_rows_half(
     FrameParams fp, const float4* __restrict__ gab, const float4* __restrict__ gde, const float2* __restrict__ gc,
     const float4* __restrict__ spec, float4* __restrict__ maps, float* __restrict__ jac, FoamParams foam,
-    const float2* __restrict__ tw_glob, int rows, int kp)
+    const float2* __restrict__ tw_glob, int rows, int kp, const float2* __restrict__ tw2_glob)
 {
   using S = FftShape<LOGN>;
   using K = ColFirstCfg<LOGN>;
   using HC = HalfCfg<LOGN>;
   constexpr int N = S::N, T = S::T, B = K::B, RPW = RPW_, STRIPS = HC::STRIPS, WG = T * RPW;
   static_assert(WG * 8 * 16 <= lds_row_slots<LOGN>(RPW) * 8, "mirror exchange fits the transform's LDS");
+  static_assert(!XS || (RPW == 1 && T == 1024), "XS: one 16-wave row per workgroup");
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   float2* tw = reinterpret_cast<float2*>(smem);
-  void* xch = smem + ((S::TW_ENTRIES * 8 + 15) / 16) * 16;
+  float2* tw2 = reinterpret_cast<float2*>(smem + XsCfg<LOGN>::TW1);
+  void* xch = smem + (XS ? XsCfg<LOGN>::TW1 + XsCfg<LOGN>::TW2 : ((S::TW_ENTRIES * 8 + 15) / 16) * 16);
   CPair* mir = reinterpret_cast<CPair*>(xch);  // [m < 8][thread]: lanes at -u for the partner
+  if constexpr (XS)
+  {
+    for (int e = threadIdx.x; e < FftShape<XsCfg<LOGN>::L2>::TW_ENTRIES; e += blockDim.x)
+      tw2[e] = tw2_glob[e];
+  }
   load_twiddles<LOGN>(tw, tw_glob);
 
   const int blocks = (RM ? rows : N) / RPW;
@@ -1187,7 +1216,7 @@ __global__ __launch_bounds__(FftShape<LOGN>::T * RPW_) void k_rows_half(
     const float sgy = (y & 1) ? -1.0f : 1.0f;  // (-1)^q of the Nyquist-row term
     const float4* sp = spec + (size_t)cimg * N;
     const int tid = opaque((int)threadIdx.x);
-    CPair v[16];
+    CPair v[16];  // XS: own lanes in v[m], the -u lanes in v[m + 8] until the transposition
 #pragma unroll
     for (int m = 0; m < 8; m++)
     {
@@ -1230,12 +1259,12 @@ __global__ __launch_bounds__(FftShape<LOGN>::T * RPW_) void k_rows_half(
                     f2v{-Dr - kx2 * Cr + sgy * s4.y, Ei - kx * Dr + sgy * s4.w}};
       }
       v[m] = own;
-      if constexpr (ABL == 3)
+      if constexpr (ABL == 3 || XS)
         v[m + 8] = neg;
       else
         mir[m * WG + tid] = neg;
     }
-    if constexpr (ABL != 3)
+    if constexpr (ABL != 3 && !XS)
       __syncthreads();
     // own elements m >= 8 (u < 0): from the partner's mirror slots; thread 0's m = 8 is the Nyquist
     // column (u = -N/2), read directly
@@ -1275,13 +1304,64 @@ __global__ __launch_bounds__(FftShape<LOGN>::T * RPW_) void k_rows_half(
                        f2v{q.re.x - kx2 * cc.x, -q.im.y - kx * q.re.x}};
         }
       }
-      else
+      else if constexpr (!XS)
         v[m] = mir[(i == 0 ? 16 - m : 15 - m) * WG + tp];
     }
-    if constexpr (ABL != 3)
+    if constexpr (ABL != 3 && !XS)
       __syncthreads();  // the transform's first exchange reuses the LDS
-    const int i2 = opaque(i20), r2 = RPW == 1 ? 0 : opaque(r20);
-    if constexpr (ABL != 2)
+    int i2 = opaque(i20), r2 = RPW == 1 ? 0 : opaque(r20);
+    if constexpr (XS)
+    {
+      // x index n = n1 + 16 n2, output k = k2 + 1024 k1 (T = 1024): transposition T_in gives wave
+      // n1 = w the inputs x(w + 16 n2) (own lanes at n, the -u lanes at N - n, thread 0's Nyquist
+      // column at N/2); the wave's 1024-point sub-transform; times W_N^(n1 k2); transposition T_out
+      // gives thread k2 = tid the 16 values Z_n1(k2); the 16-point DFT over n1 leaves
+      // v[k1] = X(tid + T k1): the plain path's store layout. LDS slot of n: (n mod 16) RS + n / 16.
+      constexpr int L2 = XsCfg<LOGN>::L2, RS = XsCfg<LOGN>::RS;
+      const int w = tid >> 6, l = tid & 63;
+      float2* xs = reinterpret_cast<float2*>(xch);
+      auto pslot = [&](int n) { return (n & 15) * RS + (n >> 4); };
+      __syncthreads();  // the previous image's T_out reads are done
+#pragma unroll
+      for (int h = 0; h < 2; h++)
+      {
+        if (h)
+          __syncthreads();
+#pragma unroll
+        for (int m = 0; m < 8; m++)
+        {
+          xs[pslot(i + m * T)] = half_of(v[m], h);
+          xs[pslot(m == 0 && i == 0 ? N / 2 : N - i - m * T)] = half_of(v[m + 8], h);
+        }
+        __syncthreads();
+#pragma unroll
+        for (int m = 0; m < 16; m++)
+          set_half(v[m], h, xs[w * RS + l + 64 * m]);
+      }
+      // region w is the wave's alone until T_out's first barrier: its exchanges need no barriers
+      fft_run<L2, 0, true, true>(v, l, 0, l, 0, xs + w * RS, tw2);  // v[m] = Y_w(l + 64 m)
+      const float2 base_w = twiddle<LOGN>(w * l, tw);
+#pragma unroll
+      for (int m = 0; m < 16; m++)
+        v[m] = cmul(v[m], base_w);
+      apply_stage_twiddles<LOGN>(v, 64 * w, tw);  // x W_N^(w (l + 64 m))
+#pragma unroll
+      for (int h = 0; h < 2; h++)
+      {
+        if (h)
+          __syncthreads();
+#pragma unroll
+        for (int m = 0; m < 16; m++)
+          xs[w * RS + l + 64 * m] = half_of(v[m], h);
+        __syncthreads();
+#pragma unroll
+        for (int n1 = 0; n1 < 16; n1++)
+          set_half(v[n1], h, xs[n1 * RS + tid]);
+      }
+      idft16(v);
+      i2 = tid;
+    }
+    else if constexpr (ABL != 2)
       fft_run<LOGN, CI, true>(v, i, r, i2, r2, xch, tw);
     float4* dst = maps + ((size_t)cimg * (RM ? rows : N) + y0) * N;
     const int woff = ((r2 << LOGN) + i2) * 16;
@@ -2025,7 +2105,7 @@ hipError_t launch_half_rows(int logn, const FrameParams& fp, const float4* gab, 
       const int lds = ((S::TW_ENTRIES * 8 + 15) / 16) * 16 + lds_row_slots<LOGN>(rpw) * 8;
       const int grid = persistent_grid(kern, S::T * rpw, lds, fp.cascades * per_item * (S::N / rpw), cus);
       hipLaunchKernelGGL(kern, dim3(grid), dim3(S::T * rpw), lds, stream, fp, gab, gcd, ge, rcorr, maps, jac, foam, tw,
-                         S::N, 0);
+                         S::N, 0, (const float2*)nullptr);
       return hipGetLastError();
     }
   });
@@ -2098,6 +2178,39 @@ hipError_t launch_half_slab_columns(int logn, const FrameParams& fp, const HalfS
   });
 }
 
+// The row pass over row-major fields (strip-dealt slabs after k_half_to_rows, and whole grids of
+// 8192/16384 after the four-step column pass). N = 16384 (T = 1024, one row per workgroup): the
+// XS x transform (barriers 14 -> 6 per image). tw: this size's table, followed by the N/16-point
+// table for the sizes the four-step paths serve (ocean_fft_create appends it for 8192 and 16384).
+int rm_rows_variant = 1;  // tools/microbench A/B: 0 = the plain transform
+
+template <int LOGN>
+hipError_t launch_rm_rows(const FrameParams& fp, const float4* rm_ab, const float4* rm_de, const float2* rm_c,
+                          const float4* spec, float4* maps, float* jac, const FoamParams& foam, const float2* tw,
+                          int rows, int kp, hipStream_t stream, int cus)
+{
+  using S = FftShape<LOGN>;
+  constexpr int RPW = S::T >= 1024 ? 1 : 2;
+  if constexpr (RPW == 1)
+  {
+    if (rm_rows_variant != 0)
+    {
+      auto kern = k_rows_half<LOGN, kStream, kStream, 0, 1, true, true, 1, 1, 4, 2, true, true>;
+      const int lds = XsCfg<LOGN>::LDS;
+      const int grid = persistent_grid(kern, S::T, lds, fp.cascades * rows, cus);
+      hipLaunchKernelGGL(kern, dim3(grid), dim3(S::T), lds, stream, fp, rm_ab, rm_de, rm_c, spec, maps, jac, foam, tw,
+                         rows, kp, tw + S::TW_ENTRIES);
+      return hipGetLastError();
+    }
+  }
+  auto kern = k_rows_half<LOGN, kStream, kStream, 0, RPW, true, true>;
+  const int lds = ((S::TW_ENTRIES * 8 + 15) / 16) * 16 + lds_row_slots<LOGN>(RPW) * 8;
+  const int grid = persistent_grid(kern, S::T * RPW, lds, fp.cascades * (rows / RPW), cus);
+  hipLaunchKernelGGL(kern, dim3(grid), dim3(S::T * RPW), lds, stream, fp, rm_ab, rm_de, rm_c, spec, maps, jac, foam, tw,
+                     rows, kp, (const float2*)nullptr);
+  return hipGetLastError();
+}
+
 hipError_t launch_half_slab_rows(int logn, const FrameParams& fp, const HalfSlab& hsl, const void* recv, float4* rm_ab,
                                  float4* rm_de, float2* rm_c, float4* maps, float* jac, const FoamParams& foam,
                                  const float2* tw, hipStream_t stream, int cus)
@@ -2127,12 +2240,7 @@ hipError_t launch_half_slab_rows(int logn, const FrameParams& fp, const HalfSlab
       hipError_t e = hipGetLastError();
       if (e != hipSuccess)
         return e;
-      constexpr int RPW = S::T >= 1024 ? 1 : 2;
-      auto kern = k_rows_half<LOGN, kStream, kStream, 0, RPW, true, true>;
-      const int lds = ((S::TW_ENTRIES * 8 + 15) / 16) * 16 + lds_row_slots<LOGN>(RPW) * 8;
-      const int grid = persistent_grid(kern, S::T * RPW, lds, C * (hsl.w / RPW), cus);
-      hipLaunchKernelGGL(kern, dim3(grid), dim3(S::T * RPW), lds, stream, fp, rm_ab, rm_de, rm_c, spec, maps, jac, foam,
-                         tw, hsl.w, kp);
+      return launch_rm_rows<LOGN>(fp, rm_ab, rm_de, rm_c, spec, maps, jac, foam, tw, hsl.w, kp, stream, cus);
       return hipGetLastError();
     }
   });
@@ -2243,7 +2351,6 @@ hipError_t launch_gen4_rows(int logn, const FrameParams& fp, const void* buf, fl
       return hipErrorInvalidValue;
     else
     {
-      using S = FftShape<LOGN>;
       using G = Gen4Cfg<LOGN>;
       constexpr int N = G::N, KP = G::KP, PITCH = G::PITCH, LOGN2 = LOGN - 4;
       // 8 columns per workgroup at N2 = 1024 (512 threads, two per CU: 2.145 -> 2.015 ms for the three
@@ -2268,13 +2375,7 @@ hipError_t launch_gen4_rows(int logn, const FrameParams& fp, const void* buf, fl
       hipError_t e = hipGetLastError();
       if (e != hipSuccess)
         return e;
-      constexpr int RPW = S::T >= 1024 ? 1 : 2;
-      auto kern = k_rows_half<LOGN, kStream, kStream, 0, RPW, true, true>;
-      const int lds = ((S::TW_ENTRIES * 8 + 15) / 16) * 16 + lds_row_slots<LOGN>(RPW) * 8;
-      const int grid = persistent_grid(kern, S::T * RPW, lds, C * (N / RPW), cus);
-      hipLaunchKernelGGL(kern, dim3(grid), dim3(S::T * RPW), lds, stream, fp, rm_ab, rm_de, rm_c, spec, maps, jac, foam, tw,
-                         N, PITCH);
-      return hipGetLastError();
+      return launch_rm_rows<LOGN>(fp, rm_ab, rm_de, rm_c, spec, maps, jac, foam, tw, N, PITCH, stream, cus);
     }
   });
 }

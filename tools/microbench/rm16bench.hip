@@ -1,0 +1,176 @@
+// rm16bench.hip — the row pass of whole 16384^2 grids (k_rows_half, RM layout, one row of both
+// images per 1024-thread item): the plain x transform (14 barriers per image) against XS (the
+// four-step x transform with per-wave sub-transforms, 6 barriers), with timing ablations: no HBM
+// loads (ABL 1), no x transform (ABL 2). Ablated outputs are wrong by construction. Builds with
+// -DOCEAN_ABLATE_EXCHANGE / -DOCEAN_ABLATE_BARRIER price the exchanges and barriers.
+// Usage: rm16bench
+#include "../../oceansimulation_amd/csrc/ocean_kernels.hip"
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <functional>
+#include <string>
+#include <vector>
+
+using namespace oceanfft;
+
+#define CHECK(x)                                                                                   \
+  do                                                                                               \
+  {                                                                                                \
+    hipError_t e = (x);                                                                            \
+    if (e != hipSuccess)                                                                           \
+    {                                                                                              \
+      std::printf("HIP error %s at %s:%d\n", hipGetErrorString(e), __FILE__, __LINE__);            \
+      std::exit(1);                                                                                \
+    }                                                                                              \
+  } while (0)
+
+template <typename F>
+static float time_ms(F&& launch, int reps)
+{
+  hipEvent_t a, b;
+  CHECK(hipEventCreate(&a));
+  CHECK(hipEventCreate(&b));
+  launch();
+  CHECK(hipDeviceSynchronize());
+  CHECK(hipEventRecord(a));
+  for (int r = 0; r < reps; r++)
+    launch();
+  CHECK(hipEventRecord(b));
+  CHECK(hipEventSynchronize(b));
+  float ms;
+  CHECK(hipEventElapsedTime(&ms, a, b));
+  CHECK(hipEventDestroy(a));
+  CHECK(hipEventDestroy(b));
+  return ms / reps;
+}
+
+__global__ void fill(float* p, size_t n, unsigned salt)
+{
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
+  {
+    unsigned h = (unsigned)i * 2654435761u ^ salt;
+    h ^= h >> 15;
+    h *= 2246822519u;
+    h ^= h >> 13;
+    p[i] = ((float)(h & 0xffff) - 32768.0f) * (1.0f / 32768.0f);
+  }
+}
+
+static float2* table(int logn)
+{
+  const int n = 1 << logn, lb = logn / 2, tb = 1 << lb, ta = 1 << (logn - lb);
+  std::vector<float2> tab(tb + ta);
+  for (int e = 0; e < tb; e++)
+    tab[e] = make_float2((float)std::cos(2 * M_PI * e / n), (float)std::sin(2 * M_PI * e / n));
+  for (int e = 0; e < ta; e++)
+    tab[tb + e] = make_float2((float)std::cos(2 * M_PI * (double)e * tb / n), (float)std::sin(2 * M_PI * (double)e * tb / n));
+  float2* d;
+  CHECK(hipMalloc(&d, tab.size() * 8));
+  CHECK(hipMemcpy(d, tab.data(), tab.size() * 8, hipMemcpyHostToDevice));
+  return d;
+}
+
+int main()
+{
+  constexpr int LOGN = 14;
+  using G = Gen4Cfg<LOGN>;
+  using S = FftShape<LOGN>;
+  constexpr int N = G::N, PITCH = G::PITCH;
+  const int C = 1;
+  const size_t rt = (size_t)N * PITCH;
+  float4 *rab, *rde, *spec, *maps;
+  float2* rc;
+  float* jac;
+  CHECK(hipMalloc(&rab, rt * 16));
+  CHECK(hipMalloc(&rde, rt * 16));
+  CHECK(hipMalloc(&rc, rt * 8));
+  CHECK(hipMalloc(&spec, (size_t)2 * N * 16));
+  CHECK(hipMalloc(&maps, (size_t)2 * N * N * 16));
+  CHECK(hipMalloc(&jac, (size_t)N * N * 4));
+  hipLaunchKernelGGL(fill, dim3(4096), dim3(256), 0, 0, (float*)rab, rt * 4, 1u);
+  hipLaunchKernelGGL(fill, dim3(4096), dim3(256), 0, 0, (float*)rde, rt * 4, 2u);
+  hipLaunchKernelGGL(fill, dim3(4096), dim3(256), 0, 0, (float*)rc, rt * 2, 3u);
+  hipLaunchKernelGGL(fill, dim3(256), dim3(256), 0, 0, (float*)spec, (size_t)2 * N * 4, 4u);
+  CHECK(hipDeviceSynchronize());
+  FrameParams fp{};
+  fp.cascades = C;
+  fp.c[0] = {2.0f * 3.14159265358f / 1000.0f, 37.5f, 9.8f, 100.0f};
+  FoamParams foam{};
+  foam.displacement[0] = 0.4f;
+  float2* tw = table(LOGN);
+  float2* tw2 = table(LOGN - 4);
+  const int lds = ((S::TW_ENTRIES * 8 + 15) / 16) * 16 + lds_row_slots<LOGN>(1) * 8;
+  auto mk = [&](auto kern, int per = 1) {
+    CHECK(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, lds));
+    return [=] {
+      hipLaunchKernelGGL(kern, dim3(C * N * per), dim3(S::T), lds, 0, fp, rab, rde, rc, spec, maps, jac, foam, tw, N,
+                         PITCH, (const float2*)nullptr);
+    };
+  };
+  struct V
+  {
+    std::string name;
+    std::function<void()> run;
+    std::vector<float> t;
+  };
+  auto mkx = [&](auto kern) {
+    CHECK(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, XsCfg<LOGN>::LDS));
+    return [=] {
+      hipLaunchKernelGGL(kern, dim3(C * N), dim3(S::T), XsCfg<LOGN>::LDS, 0, fp, rab, rde, rc, spec, maps, jac, foam, tw,
+                         N, PITCH, tw2);
+    };
+  };
+  std::vector<V> vs = {
+      {"row pass, plain transform (round 2)", mk(k_rows_half<LOGN, kStream, kStream, 0, 1, true, true>), {}},
+      {"XS (four-step x transform)", mkx(k_rows_half<LOGN, kStream, kStream, 0, 1, true, true, 1, 1, 4, 2, true, true>), {}},
+      {"XS, default-policy loads", mkx(k_rows_half<LOGN, 0, kStream, 0, 1, true, true, 1, 1, 4, 2, true, true>), {}},
+      {"XS ABL 1: no HBM loads", mkx(k_rows_half<LOGN, kStream, kStream, 1, 1, true, true, 1, 1, 4, 2, true, true>), {}},
+      {"ABL 1: no HBM loads", mk(k_rows_half<LOGN, kStream, kStream, 1, 1, true, true>), {}},
+      {"ABL 2: no x transform", mk(k_rows_half<LOGN, kStream, kStream, 2, 1, true, true>), {}},
+  };
+  // XS vs the plain transform: same lanes, different rounding order (max |diff| vs max |value|)
+  auto snapf = [&](const void* p, size_t n) {
+    std::vector<float> h(n / 4);
+    CHECK(hipMemcpy(h.data(), p, n, hipMemcpyDeviceToHost));
+    return h;
+  };
+  const size_t mb = (size_t)2 * N * N * 16, jb = (size_t)N * N * 4;
+  auto compare = [&](int a, int b, const char* what) {
+    vs[a].run();
+    CHECK(hipDeviceSynchronize());
+    const auto m0 = snapf(maps, mb), j0 = snapf(jac, jb);
+    CHECK(hipMemset(maps, 0, mb));
+    CHECK(hipMemset(jac, 0, jb));
+    vs[b].run();
+    CHECK(hipDeviceSynchronize());
+    const auto m1 = snapf(maps, mb), j1 = snapf(jac, jb);
+    double dm = 0, am = 0, dj = 0, aj = 0;
+    for (size_t k = 0; k < m0.size(); k++)
+    {
+      dm = std::max(dm, (double)std::fabs(m0[k] - m1[k]));
+      am = std::max(am, (double)std::fabs(m0[k]));
+    }
+    for (size_t k = 0; k < j0.size(); k++)
+    {
+      dj = std::max(dj, (double)std::fabs(j0[k] - j1[k]));
+      aj = std::max(aj, (double)std::fabs(j0[k]));
+    }
+    std::printf("%s: maps max|diff| %.3g of max|v| %.3g; jac %.3g of %.3g%s\n", what, dm, am, dj, aj,
+                m0 == m1 && j0 == j1 ? " (bit-identical)" : "");
+  };
+  compare(0, 1, "XS vs plain");
+  compare(1, 2, "XS streamed vs default-policy loads");
+  for (int r = 0; r < 5; r++)
+    for (auto& v : vs)
+      v.t.push_back(time_ms(v.run, 3));
+  const double bytes = 56.04 * (double)N * N;
+  for (auto& v : vs)
+  {
+    std::sort(v.t.begin(), v.t.end());
+    std::printf("%-32s median %7.3f ms  %7.1f GB/s at 56 B/pt\n", v.name.c_str(), v.t[2], bytes / v.t[2] / 1e6);
+  }
+  return 0;
+}

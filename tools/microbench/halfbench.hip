@@ -1,6 +1,6 @@
 // halfbench.hip — interleaved A/B timing of half-spectrum frame-pass variants (8 cascades x 4096^2),
 // with a bit-identity check of every variant's output against the baseline variant.
-// Build: see Makefile target `microbench`. Usage: halfbench [logn] [cascades] [quick|mall|rows]
+// Build: see Makefile target `microbench`. Usage: halfbench [logn] [cascades] [quick|mall|rows|overlap]
 #include "../../oceansimulation_amd/csrc/ocean_kernels.hip"
 
 #include <algorithm>
@@ -188,6 +188,81 @@ int main(int argc, char** argv)
       std::sort(tr[k].begin(), tr[k].end());
     std::printf("rows, interleaved regions (production)  median %7.3f ms\n", tr[0][4]);
     std::printf("rows, row layout (round 1)              median %7.3f ms  bit-identical %s\n", tr[1][4], same ? "yes" : "NO");
+    return 0;
+  }
+  if (argc > 3 && std::strcmp(argv[3], "overlap") == 0)
+  {
+    // cascade groups pipelined over two streams: pass 1 of group g+1 (VALU-bound) beside pass 2 of
+    // group g (HBM-bound), against both passes over all cascades on one stream
+    hipStream_t sa, sb;
+    CHECK(hipStreamCreateWithFlags(&sa, hipStreamNonBlocking));
+    CHECK(hipStreamCreateWithFlags(&sb, hipStreamNonBlocking));
+    std::vector<hipEvent_t> ev(C + 2);
+    for (auto& evt : ev)
+      CHECK(hipEventCreateWithFlags(&evt, hipEventDisableTiming));
+    const size_t ht1 = half_field_texels(logn);
+    auto grouped = [&](int G) {
+      const int per = C / G;
+      CHECK(hipEventRecord(ev[C], 0));
+      CHECK(hipStreamWaitEvent(sa, ev[C], 0));
+      CHECK(hipStreamWaitEvent(sb, ev[C], 0));
+      for (int g = 0; g < G; g++)
+      {
+        const int c0 = g * per;
+        FrameParams f1{};
+        f1.cascades = per;
+        FoamParams o1{};
+        for (int k = 0; k < per; k++)
+        {
+          f1.c[k] = fp.c[c0 + k];
+          o1.displacement[k] = foam.displacement[c0 + k];
+        }
+        hipError_t e = launch_half_columns(logn, f1, h0 + tex * c0, gab + ht1 * c0, gcd + ht1 * c0, ge + ht1 * c0,
+                                           spec + (size_t)2 * n * c0, tw, sa, cus, hs, cus);
+        if (e != hipSuccess)
+          return e;
+        CHECK(hipEventRecord(ev[g], sa));
+        CHECK(hipStreamWaitEvent(sb, ev[g], 0));
+        e = launch_half_rows(logn, f1, gab + ht1 * c0, gcd + ht1 * c0, ge + ht1 * c0, spec + (size_t)2 * n * c0,
+                             maps + tex * 2 * c0, jac + tex * c0, o1, tw, sb, cus);
+        if (e != hipSuccess)
+          return e;
+      }
+      CHECK(hipEventRecord(ev[C + 1], sb));
+      CHECK(hipStreamWaitEvent(0, ev[C + 1], 0));
+      CHECK(hipStreamWaitEvent(0, ev[G - 1], 0));
+      return hipSuccess;
+    };
+    auto batched = [&] { hipError_t e = c1(); return e == hipSuccess ? r1() : e; };
+    CHECK(batched());
+    CHECK(hipDeviceSynchronize());
+    auto bm = snap(maps, mb), bj = snap(jac, jb);
+    std::vector<int> gs;
+    for (int G = 2; G <= C; G *= 2)
+      if (C % G == 0)
+        gs.push_back(G);
+    std::vector<bool> same(gs.size());
+    for (size_t k = 0; k < gs.size(); k++)
+    {
+      CHECK(hipMemset(maps, 0, mb));
+      CHECK(grouped(gs[k]));
+      CHECK(hipDeviceSynchronize());
+      std::printf("%d groups vs batched frame:\n", gs[k]);
+      same[k] = (int)diff(snap(maps, mb), bm) & (int)diff(snap(jac, jb), bj);
+    }
+    std::vector<std::vector<float>> tm(1 + gs.size());
+    for (int r = 0; r < 7; r++)
+    {
+      tm[0].push_back(time_ms(batched, 10));
+      for (size_t k = 0; k < gs.size(); k++)
+        tm[1 + k].push_back(time_ms([&] { return grouped(gs[k]); }, 10));
+    }
+    for (auto& t : tm)
+      std::sort(t.begin(), t.end());
+    std::printf("frame batched, one stream            median %7.3f ms\n", tm[0][3]);
+    for (size_t k = 0; k < gs.size(); k++)
+      std::printf("frame %d groups, pass 2 on stream 2   median %7.3f ms  bit-identical %s\n", gs[k], tm[1 + k][3],
+                  same[k] ? "yes" : "NO");
     return 0;
   }
   if (mall)

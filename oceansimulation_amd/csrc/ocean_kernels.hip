@@ -2074,13 +2074,14 @@ hipError_t launch_half_rows(int logn, const FrameParams& fp, const float4* gab, 
     {
       using K = ColFirstCfg<LOGN>;
       using S = FftShape<LOGN>;
-      // ablation (tools/microbench): 1 no HBM loads, 2 no x transform, 3 no mirror exchange,
+      // ablation (tools/microbench; 1-3 on the production shape): 1 no HBM loads, 2 no x transform,
+      // 3 no mirror exchange,
       // 4 / 5 ColFirstCfg's rows per workgroup (one 1024-thread workgroup per CU) / one row
       // 0 (production): one item per row block for both images (C loaded once); 6: one image per
       // item (C loaded by both items of a row block)
       constexpr int R4 = K::RPW2;
       const int rpw = ablation == 4 ? R4 : ablation == 5 ? 1 : 2;
-      const int per_item = (ablation == 0 || ablation >= 7) ? 1 : 2;
+      const int per_item = (ablation <= 3 || ablation >= 7) ? 1 : 2;
       // production loads use the default policy: C's 128-B lines are shared by the paired items
       // (xcd_pair_slot) and streamed loads lost them before the partner's read (-5 %,
       // tools/microbench/halfbench); 7: streamed loads
@@ -2097,9 +2098,9 @@ hipError_t launch_half_rows(int logn, const FrameParams& fp, const float4* gab, 
                   : ablation == 15 ? k_rows_half<LOGN, 0, kStream, 0, 2, true, false, RG, RGC, 4, 2, false>
                   : ablation == 7 ? k_rows_half<LOGN, kStream, kStream, 0, 2, true, false, RG, RGC>
                   : ablation == 6 ? k_rows_half<LOGN, kStream, kStream, 0, 2, false, false, RG, RGC>
-                  : ablation == 1 ? k_rows_half<LOGN, kStream, kStream, 1>
-                  : ablation == 2 ? k_rows_half<LOGN, kStream, kStream, 2>
-                  : ablation == 3 ? k_rows_half<LOGN, kStream, kStream, 3>
+                  : ablation == 1 ? k_rows_half<LOGN, 0, kStream, 1, 2, true, false, RG, RGC>
+                  : ablation == 2 ? k_rows_half<LOGN, 0, kStream, 2, 2, true, false, RG, RGC>
+                  : ablation == 3 ? k_rows_half<LOGN, 0, kStream, 3, 2, true, false, RG, RGC>
                   : ablation == 4 ? k_rows_half<LOGN, kStream, kStream, 0, R4>
                                   : k_rows_half<LOGN, kStream, kStream, 0, 1>;
       const int lds = ((S::TW_ENTRIES * 8 + 15) / 16) * 16 + lds_row_slots<LOGN>(rpw) * 8;

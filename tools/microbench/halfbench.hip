@@ -1,6 +1,6 @@
 // halfbench.hip — interleaved A/B timing of half-spectrum frame-pass variants (8 cascades x 4096^2),
 // with a bit-identity check of every variant's output against the baseline variant.
-// Build: see Makefile target `microbench`. Usage: halfbench [logn] [cascades] [quick|mall|rows|overlap]
+// Build: see Makefile target `microbench`. Usage: halfbench [logn] [cascades] [quick|mall|rows|overlap|rowabl]
 #include "../../oceansimulation_amd/csrc/ocean_kernels.hip"
 
 #include <algorithm>
@@ -188,6 +188,25 @@ int main(int argc, char** argv)
       std::sort(tr[k].begin(), tr[k].end());
     std::printf("rows, interleaved regions (production)  median %7.3f ms\n", tr[0][4]);
     std::printf("rows, row layout (round 1)              median %7.3f ms  bit-identical %s\n", tr[1][4], same ? "yes" : "NO");
+    return 0;
+  }
+  if (argc > 3 && std::strcmp(argv[3], "rowabl") == 0)
+  {
+    // the production row pass and its timing ablations (wrong results by construction): 1 no HBM
+    // loads, 2 no x transform, 3 no mirror exchange; built with -DOCEAN_ABLATE_BARRIER /
+    // -DOCEAN_ABLATE_EXCHANGE (halfbench_nobar / _noxch) the exchanges lose their barriers / LDS
+    CHECK(c1());
+    CHECK(hipDeviceSynchronize());
+    const char* nm[] = {"rows (production)", "ABL 1: no HBM loads", "ABL 2: no x transform", "ABL 3: no mirror exchange"};
+    std::vector<std::vector<float>> tr(4);
+    for (int r = 0; r < 7; r++)
+      for (int a = 0; a < 4; a++)
+        tr[a].push_back(time_ms([&] { return launch_half_rows(logn, fp, gab, gcd, ge, spec, maps, jac, foam, tw, 0, cus, a); }, 10));
+    for (int a = 0; a < 4; a++)
+    {
+      std::sort(tr[a].begin(), tr[a].end());
+      std::printf("%-28s median %7.3f ms  %7.1f GB/s at 56 B/pt\n", nm[a], tr[a][3], 56.04 * pts / tr[a][3] / 1e6);
+    }
     return 0;
   }
   if (argc > 3 && std::strcmp(argv[3], "overlap") == 0)

@@ -681,8 +681,10 @@ __device__ __forceinline__ int half_group_offset(int y, int strip, int b = 0)
 // CPI: columns per item (B = the whole strip; B / 2: half strips, T * CPI threads, two workgroups
 // per CU so one's loads and stores overlap the other's transform; the strip's two halves are items
 // 2p, 2p + 1 on one XCD, whose loads share h0 lines and whose half-line stores meet in L2).
+// HP: the H scratch holds pairs (H(m), H(m + 1)) per thread in 16-B entries ([m / 2][thread]): 8
+// stores and 16 loads of 16 B per item instead of 16 and 32 of 8 B.
 template <int LOGN, int LA = 0, int SA = kStream, bool HS = false, bool SLAB = false, bool SEED = false, int RG = 1,
-          int RGC = 1, int CPI = ColFirstCfg<LOGN>::B>
+          int RGC = 1, int CPI = ColFirstCfg<LOGN>::B, bool HP = false>
 __global__ __launch_bounds__(FftShape<LOGN>::T * CPI, CPI < ColFirstCfg<LOGN>::B ? 4 : 1) void k_cols_half(FrameParams fp, const float4* __restrict__ h0,
                                                                      float4* __restrict__ gab, float4* __restrict__ gde,
                                                                      float2* __restrict__ gc,
@@ -752,14 +754,18 @@ __global__ __launch_bounds__(FftShape<LOGN>::T * CPI, CPI < ColFirstCfg<LOGN>::B
         {
           const int y = i + ((m + 8) & 15) * T;
           const float2 H = evolve(seed_texel(q, x, y, dim), make_kvec(x, y, dim, f.dk).k, f);
-          st2s<0>(hsb, hoff, m * WG * 8, H);
+          if constexpr (HP)
+            st2s<0>(hsb, hoff * 2 + (m & 1) * 8, (m >> 1) * WG * 16, H);
+          else
+            st2s<0>(hsb, hoff, m * WG * 8, H);
         }
         __threadfence_block();  // this thread's scratch stores are complete before it reads them back
 #pragma unroll
         for (int m = 0; m < 16; m++)
         {
           const int y = i + ((m + 8) & 15) * T;
-          pack(m, ld2s<kStream>(hsb, hoff, m * WG * 8), make_kvec(x, y, dim, f.dk));
+          pack(m, HP ? ld2s<kStream>(hsb, hoff * 2 + (m & 1) * 8, (m >> 1) * WG * 16) : ld2s<kStream>(hsb, hoff, m * WG * 8),
+               make_kvec(x, y, dim, f.dk));
         }
       }
       else if (!HS || round == 0)
@@ -767,6 +773,7 @@ __global__ __launch_bounds__(FftShape<LOGN>::T * CPI, CPI < ColFirstCfg<LOGN>::B
         float2* hsb = hs + (size_t)blockIdx.x * 16 * WG;
         const int hoff = opaque((int)threadIdx.x) * 8;
         float4 a[16];
+        float2 hprev = make_float2(0.0f, 0.0f);
 #pragma unroll
         for (int m = 0; m < 16; m++)  // fftShift on y folded into the load
           a[m] = ld4s<LA>(src, voff, ((m + 8) & 15) * T * B * 16);
@@ -777,7 +784,14 @@ __global__ __launch_bounds__(FftShape<LOGN>::T * CPI, CPI < ColFirstCfg<LOGN>::B
           const KVec q = make_kvec(x, y, dim, f.dk);
           const float2 H = evolve(a[m], q.k, f);
 #ifndef OCEAN_ABLATE_HS
-          if (HS)
+          if (HS && HP)
+          {
+            if (m & 1)
+              st4s<0>(hsb, hoff * 2, (m >> 1) * WG * 16, make_float4(hprev.x, hprev.y, H.x, H.y));
+            else
+              hprev = H;
+          }
+          else if (HS)
             st2s<0>(hsb, hoff, m * WG * 8, H);
 #else
           (void)hsb;
@@ -798,7 +812,17 @@ __global__ __launch_bounds__(FftShape<LOGN>::T * CPI, CPI < ColFirstCfg<LOGN>::B
           (void)hsb;
           pack(m, make_float2((float)hoff, (float)m), make_kvec(x, y, dim, f.dk));
 #else
-          pack(m, ld2s<kStream>(hsb, hoff, m * WG * 8), make_kvec(x, y, dim, f.dk));
+          if constexpr (HP)
+          {
+            if ((m & 1) == 0)
+            {
+              const float4 p = ld4s<kStream>(hsb, hoff * 2, (m >> 1) * WG * 16);
+              pack(m, make_float2(p.x, p.y), make_kvec(x, y, dim, f.dk));
+              pack(m + 1, make_float2(p.z, p.w), make_kvec(x, y + T, dim, f.dk));
+            }
+          }
+          else
+            pack(m, ld2s<kStream>(hsb, hoff, m * WG * 8), make_kvec(x, y, dim, f.dk));
 #endif
         }
       }
@@ -2002,7 +2026,8 @@ hipError_t launch_half_columns(int logn, const FrameParams& fp, const float4* h0
       // loads, 2 = sc1 field stores (dropped from L2: slower), 3 = sc1 + nt stores
       // 4..7: field layouts with row groups (RG, RGC) = (2, 2), (2, 4), (4, 4), (1, 1) (launch_half_rows 8..11)
       constexpr int RG = kHalfRG, RGC = kHalfRGC;
-      auto kern = seed ? k_cols_half<LOGN, 0, kStream, true, false, true, RG, RGC>
+      // HP (the H scratch in 16-B pairs): 0.921 -> 0.910 ms (halfbench hpair); variant 23: unpaired
+      auto kern = seed ? k_cols_half<LOGN, 0, kStream, true, false, true, RG, RGC, K::B, true>
                        : !hs ? k_cols_half<LOGN, 0, kStream, false, false, false, RG, RGC>
                        : variant == 1 ? k_cols_half<LOGN, 0, kStream, true, false, false, RG, RGC>
                        : variant == 2 ? k_cols_half<LOGN, kStream, 16, true, false, false, RG, RGC>
@@ -2011,7 +2036,8 @@ hipError_t launch_half_columns(int logn, const FrameParams& fp, const float4* h0
                        : variant == 5 ? k_cols_half<LOGN, kStream, kStream, true, false, false, 2, 4>
                        : variant == 6 ? k_cols_half<LOGN, kStream, kStream, true, false, false, 4, 4>
                        : variant == 7 ? k_cols_half<LOGN, kStream, kStream, true, false, false, 1, 1>
-                                      : k_cols_half<LOGN, kStream, kStream, true, false, false, RG, RGC>;
+                       : variant == 23 ? k_cols_half<LOGN, kStream, kStream, true, false, false, RG, RGC>
+                                      : k_cols_half<LOGN, kStream, kStream, true, false, false, RG, RGC, K::B, true>;
       if (variant >= 12 && variant <= 14 && !seed)  // half-strip items (k_cols_half2): H in VGPRs
       {
         auto hk = variant == 12   ? k_cols_half2<LOGN, 0, kStream, 4, 8>

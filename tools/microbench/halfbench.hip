@@ -1,6 +1,6 @@
 // halfbench.hip — interleaved A/B timing of half-spectrum frame-pass variants (8 cascades x 4096^2),
 // with a bit-identity check of every variant's output against the baseline variant.
-// Build: see Makefile target `microbench`. Usage: halfbench [logn] [cascades] [quick|mall|rows|overlap|rowabl]
+// Build: see Makefile target `microbench`. Usage: halfbench [logn] [cascades] [quick|mall|rows|overlap|rowabl|hpair]
 #include "../../oceansimulation_amd/csrc/ocean_kernels.hip"
 
 #include <algorithm>
@@ -188,6 +188,34 @@ int main(int argc, char** argv)
       std::sort(tr[k].begin(), tr[k].end());
     std::printf("rows, interleaved regions (production)  median %7.3f ms\n", tr[0][4]);
     std::printf("rows, row layout (round 1)              median %7.3f ms  bit-identical %s\n", tr[1][4], same ? "yes" : "NO");
+    return 0;
+  }
+  if (argc > 3 && std::strcmp(argv[3], "hpair") == 0)
+  {
+    // pass 1 with the H scratch in 8-B entries (variant 23, round 2) against production (16-B pairs):
+    // bit-identical fields
+    auto cp = [&] { return launch_half_columns(logn, fp, h0, gab, gcd, ge, spec, tw, 0, cus, hs, cus, nullptr, 23); };
+    CHECK(c1());
+    CHECK(hipDeviceSynchronize());
+    auto pab = snap(gab, ht * sizeof(float4)), pde = snap(gcd, ht * sizeof(float4)), pc = snap(ge, ht * sizeof(float2));
+    CHECK(hipMemset(gab, 0, ht * sizeof(float4)));
+    CHECK(hipMemset(gcd, 0, ht * sizeof(float4)));
+    CHECK(hipMemset(ge, 0, ht * sizeof(float2)));
+    CHECK(cp());
+    CHECK(hipDeviceSynchronize());
+    std::printf("cols with unpaired H scratch vs production: gab, gde, gc\n");
+    const bool same = (int)diff(snap(gab, ht * sizeof(float4)), pab) & (int)diff(snap(gcd, ht * sizeof(float4)), pde) &
+                      (int)diff(snap(ge, ht * sizeof(float2)), pc);
+    std::vector<std::vector<float>> t(2);
+    for (int r = 0; r < 9; r++)
+    {
+      t[0].push_back(time_ms(c1, 10));
+      t[1].push_back(time_ms(cp, 10));
+    }
+    for (auto& v : t)
+      std::sort(v.begin(), v.end());
+    std::printf("cols (production, pairs)   median %7.3f ms\n", t[0][4]);
+    std::printf("cols, unpaired H scratch   median %7.3f ms  bit-identical %s\n", t[1][4], same ? "yes" : "NO");
     return 0;
   }
   if (argc > 3 && std::strcmp(argv[3], "rowabl") == 0)

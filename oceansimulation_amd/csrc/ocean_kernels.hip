@@ -2209,7 +2209,7 @@ hipError_t launch_half_slab_columns(int logn, const FrameParams& fp, const HalfS
 // 8192/16384 after the four-step column pass). N = 16384 (T = 1024, one row per workgroup): the
 // XS x transform (barriers 14 -> 6 per image). tw: this size's table, followed by the N/16-point
 // table for the sizes the four-step paths serve (ocean_fft_create appends it for 8192 and 16384).
-int rm_rows_variant = 1;  // tools/microbench A/B: 0 = the plain transform
+static int rm_rows_variant = 1;  // tools/microbench A/B (same translation unit): 0 = the plain transform
 
 template <int LOGN>
 hipError_t launch_rm_rows(const FrameParams& fp, const float4* rm_ab, const float4* rm_de, const float2* rm_c,

@@ -683,8 +683,13 @@ __device__ __forceinline__ int half_group_offset(int y, int strip, int b = 0)
 // 2p, 2p + 1 on one XCD, whose loads share h0 lines and whose half-line stores meet in L2).
 // HP: the H scratch holds pairs (H(m), H(m + 1)) per thread in 16-B entries ([m / 2][thread]): 8
 // stores and 16 loads of 16 B per item instead of 16 and 32 of 8 B.
+// PC (packed C round, needs HS + HP and whole strips of B >= 2): round 2's CPair (C, 0) wastes its
+// second lane, so the first half of the workgroup transforms the strip's column pairs (2 p, 2 p + 1)
+// as (C_2p, C_2p+1) instead (CI = B / 2 interleaved transforms, H of both columns from the scratch
+// entries round 0 wrote) and stores 16-B gc pairs; the second half only matches the transform's
+// barriers. Per lane the arithmetic is the unpacked round's, so the fields are bit-identical.
 template <int LOGN, int LA = 0, int SA = kStream, bool HS = false, bool SLAB = false, bool SEED = false, int RG = 1,
-          int RGC = 1, int CPI = ColFirstCfg<LOGN>::B, bool HP = false>
+          int RGC = 1, int CPI = ColFirstCfg<LOGN>::B, bool HP = false, bool PC = false>
 __global__ __launch_bounds__(FftShape<LOGN>::T * CPI, CPI < ColFirstCfg<LOGN>::B ? 4 : 1) void k_cols_half(FrameParams fp, const float4* __restrict__ h0,
                                                                      float4* __restrict__ gab, float4* __restrict__ gde,
                                                                      float2* __restrict__ gc,
@@ -866,7 +871,60 @@ __global__ __launch_bounds__(FftShape<LOGN>::T * CPI, CPI < ColFirstCfg<LOGN>::B
                    make_float2(v[m].re.x, v[m].im.x));
       }
     };
-    if constexpr (HS)
+    // PC: round 2 as (C_2p, C_2p+1) pairs on the first half of the workgroup (see the template note)
+    auto run_round_c = [&]() __attribute__((always_inline)) {
+      constexpr int BP = B > 1 ? B / 2 : 1, NBAR = (S::NSTAGE - 1) * 4;  // split exchanges: 2 halves x 2 barriers
+      static_assert(!PC || (HS && HP && HALVES == 1 && B >= 2 && (WG / 2) % 64 == 0), "packed C round");
+      if (__builtin_amdgcn_readfirstlane((int)threadIdx.x) >= WG / 2)  // wave-uniform (scalar) branch
+      {
+#pragma unroll 1
+        for (int k = 0; k < NBAR; k++)
+          __syncthreads();
+        return;
+      }
+      const int t = opaque((int)threadIdx.x);
+      const int pr = t % BP, i = (t / BP) % T, ba = 2 * pr;
+      const int xa = xb * B + ba;
+      const float2* hsb = hs + (size_t)blockIdx.x * 16 * WG;
+      const int ha = (i * B + ba) * 16;  // round 0's thread (i, ba) wrote its pairs at byte 16 * (i B + ba)
+      CPair v[16];
+#pragma unroll
+      for (int m = 0; m < 16; m += 2)
+      {
+        const int y = i + ((m + 8) & 15) * T;  // m even: row y + T holds element m + 1
+        const float4 pa = ld4s<kStream>(hsb, ha, (m >> 1) * WG * 16);
+        const float4 pb = ld4s<kStream>(hsb, ha + 16, (m >> 1) * WG * 16);
+        const float ia0 = make_kvec(xa, y, dim, f.dk).inv, ib0 = make_kvec(xa + 1, y, dim, f.dk).inv;
+        const float ia1 = make_kvec(xa, y + T, dim, f.dk).inv, ib1 = make_kvec(xa + 1, y + T, dim, f.dk).inv;
+        v[m] = CPair{f2v{ia0 * pa.x, ib0 * pb.x}, f2v{ia0 * pa.y, ib0 * pb.y}};
+        v[m + 1] = CPair{f2v{ia1 * pa.z, ib1 * pb.z}, f2v{ia1 * pa.w, ib1 * pb.w}};
+      }
+      fft_run<LOGN, BP, true>(v, i, pr, xch, tw);
+#pragma unroll
+      for (int m = 0; m < 16; m++)
+      {
+        const float4 cc = make_float4(v[m].re.x, v[m].im.x, v[m].re.y, v[m].im.y);  // gc of columns ba, ba + 1
+        if constexpr (SLAB)
+        {
+          const size_t part = (size_t)fp.cascades * hsl.S * hsl.w * B;
+          const int q = (m * T) / hsl.w, yl0 = (m * T) % hsl.w;
+          const size_t el = (((size_t)c * hsl.S + s) * hsl.w + yl0) * B;
+          unsigned char* blk = send + sopaque((size_t)q * (part * 40 + (size_t)fp.cascades * 2 * N * 16));
+          st4<SA>(blk + part * 32 + el * 8, (i * B + ba) * 8, cc);
+        }
+        else if constexpr (RG == 1 && RGC == 1)
+          st4s<SA>(gc + gbase, (i * B + ba) * 8, m * T * B * 8, cc);
+        else
+          st4s<SA>(gc + cgbase, half_group_offset<LOGN, RGC>(i, 0, ba) * 8, half_group_offset<LOGN, RGC>(m * T, 0) * 8, cc);
+      }
+    };
+    if constexpr (HS && PC)
+    {
+      run_round(0);
+      run_round(1);
+      run_round_c();
+    }
+    else if constexpr (HS)
     {
 #pragma unroll
       for (int round = 0; round < 3; round++)  // specialised per round: 113 VGPRs, no spills
@@ -2037,6 +2095,7 @@ hipError_t launch_half_columns(int logn, const FrameParams& fp, const float4* h0
                        : variant == 6 ? k_cols_half<LOGN, kStream, kStream, true, false, false, 4, 4>
                        : variant == 7 ? k_cols_half<LOGN, kStream, kStream, true, false, false, 1, 1>
                        : variant == 23 ? k_cols_half<LOGN, kStream, kStream, true, false, false, RG, RGC>
+                       : variant == 24 ? k_cols_half<LOGN, kStream, kStream, true, false, false, RG, RGC, K::B, true, true>
                                       : k_cols_half<LOGN, kStream, kStream, true, false, false, RG, RGC, K::B, true>;
       if (variant >= 12 && variant <= 14 && !seed)  // half-strip items (k_cols_half2): H in VGPRs
       {

@@ -218,6 +218,37 @@ int main(int argc, char** argv)
     std::printf("cols, unpaired H scratch   median %7.3f ms  bit-identical %s\n", t[1][4], same ? "yes" : "NO");
     return 0;
   }
+  if (argc > 3 && std::strcmp(argv[3], "packc") == 0)
+  {
+    // pass 1 with round 2's (C, 0) CPairs packed as column pairs on half the workgroup (variant 24)
+    // against production: bit-identical fields (same per-lane arithmetic)
+    auto cp = [&] { return launch_half_columns(logn, fp, h0, gab, gcd, ge, spec, tw, 0, cus, hs, cus, nullptr, 24); };
+    CHECK(c1());
+    CHECK(hipDeviceSynchronize());
+    auto pab = snap(gab, ht * sizeof(float4)), pde = snap(gcd, ht * sizeof(float4)), pc = snap(ge, ht * sizeof(float2));
+    CHECK(hipMemset(gab, 0, ht * sizeof(float4)));
+    CHECK(hipMemset(gcd, 0, ht * sizeof(float4)));
+    CHECK(hipMemset(ge, 0, ht * sizeof(float2)));
+    CHECK(cp());
+    CHECK(hipDeviceSynchronize());
+    std::printf("cols with the packed C round vs production: gab, gde, gc\n");
+    const bool same = (int)diff(snap(gab, ht * sizeof(float4)), pab) & (int)diff(snap(gcd, ht * sizeof(float4)), pde) &
+                      (int)diff(snap(ge, ht * sizeof(float2)), pc);
+    std::vector<std::vector<float>> t(4);
+    for (int r = 0; r < 9; r++)
+    {
+      t[0].push_back(time_ms(c1, 10));
+      t[1].push_back(time_ms(cp, 10));
+      t[2].push_back(time_ms([&] { CHECK(c1()); return r1(); }, 10));
+      t[3].push_back(time_ms([&] { CHECK(cp()); return r1(); }, 10));
+    }
+    for (auto& v : t)
+      std::sort(v.begin(), v.end());
+    std::printf("cols (production)          median %7.3f ms   frame %7.3f ms\n", t[0][4], t[2][4]);
+    std::printf("cols, packed C round       median %7.3f ms   frame %7.3f ms  bit-identical %s\n", t[1][4], t[3][4],
+                same ? "yes" : "NO");
+    return 0;
+  }
   if (argc > 3 && std::strcmp(argv[3], "rowabl") == 0)
   {
     // the production row pass and its timing ablations (wrong results by construction): 1 no HBM

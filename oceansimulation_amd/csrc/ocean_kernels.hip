@@ -654,6 +654,10 @@ struct HalfCfg
 // (xcd_pair_slot); pass 1 stores 128-B pieces. Against strips (RG = 1): pass 2 1.637 -> 1.506 ms,
 // pass 1 0.934 -> 0.960 ms, frame 2.581 -> 2.477 ms at 8 x 4096^2 (tools/microbench/halfbench).
 constexpr int kHalfRG = 2, kHalfRGC = 4;
+// Pass 1's H pairs outside the scratch (k_cols_half HL / HK): one pair per thread in the LDS the
+// exchange leaves free, four in VGPRs (128 VGPRs at N = 4096, no spills); the scratch keeps 3 of 8.
+// 0.945 -> 0.817 ms per 8 x 4096^2, frame 2.332 -> 2.206 ms, fields bit-identical (halfbench hkeep).
+constexpr int kHalfHL = 1, kHalfHK = 4;
 // FB: columns per field strip (4 = the h0 strip; 2 = k_cols_half2's half strips, FS = 2 STRIPS).
 template <int LOGN, int RG, int FB = 4>
 __device__ __forceinline__ int half_group_offset(int y, int strip, int b = 0)
@@ -688,8 +692,12 @@ __device__ __forceinline__ int half_group_offset(int y, int strip, int b = 0)
 // as (C_2p, C_2p+1) instead (CI = B / 2 interleaved transforms, H of both columns from the scratch
 // entries round 0 wrote) and stores 16-B gc pairs; the second half only matches the transform's
 // barriers. Per lane the arithmetic is the unpacked round's, so the fields are bit-identical.
+// HL / HK (HP only): of the thread's 8 H pairs, pairs [0, HL) live in the LDS left over by the exchange
+// (16 B per thread each, after K::LDS1) and pairs [HL, HL + HK) in VGPRs from round 0 to round 2; only
+// the rest goes through the scratch. The scratch's HBM traffic (its lines are written back and, about
+// half of them, re-fetched: 1.30x algorithmic) costs 0.118 of 0.912 ms (halfbench_nohs).
 template <int LOGN, int LA = 0, int SA = kStream, bool HS = false, bool SLAB = false, bool SEED = false, int RG = 1,
-          int RGC = 1, int CPI = ColFirstCfg<LOGN>::B, bool HP = false, bool PC = false>
+          int RGC = 1, int CPI = ColFirstCfg<LOGN>::B, bool HP = false, bool PC = false, int HL = 0, int HK = 0>
 __global__ __launch_bounds__(FftShape<LOGN>::T * CPI, CPI < ColFirstCfg<LOGN>::B ? 4 : 1) void k_cols_half(FrameParams fp, const float4* __restrict__ h0,
                                                                      float4* __restrict__ gab, float4* __restrict__ gde,
                                                                      float2* __restrict__ gc,
@@ -704,9 +712,11 @@ __global__ __launch_bounds__(FftShape<LOGN>::T * CPI, CPI < ColFirstCfg<LOGN>::B
   constexpr int N = S::N, T = S::T, B = K::B, STRIPS = HC::STRIPS, WG = T * CPI, HALVES = B / CPI;
   static_assert(SLAB ? HC::SLAB_SUPPORTED : HC::SUPPORTED, "half-spectrum path: one strip per item (B = 4 unless SLAB)");
   static_assert(CPI * HALVES == B && HALVES <= 2 && (HALVES == 1 || (!SLAB && !SEED)), "whole or half strips");
+  static_assert((HL == 0 && HK == 0) || (HS && HP && !SEED && !PC && HL + HK <= 8), "H pairs outside the scratch");
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   float2* tw = reinterpret_cast<float2*>(smem);
   void* xch = smem + ((S::TW_ENTRIES * 8 + 15) / 16) * 16;
+  float4* hlds = reinterpret_cast<float4*>(static_cast<unsigned char*>(xch) + K::LDS1);  // HL pairs [p][thread]
   load_twiddles<LOGN>(tw, tw_glob);
 
   const int nstrips = SLAB ? hsl.nstrips : STRIPS;
@@ -730,6 +740,7 @@ __global__ __launch_bounds__(FftShape<LOGN>::T * CPI, CPI < ColFirstCfg<LOGN>::B
     const size_t cgbase = RGC == 1 ? ((size_t)c * STRIPS + s) * N * B
                                    : (size_t)c * STRIPS * N * B + half_group_offset<LOGN, RGC>(0, s);
     const int x = xb * B + b;
+    float4 hk[HK > 0 ? HK : 1];  // HK: H pairs kept in VGPRs across the rounds
     // one field round: (A, B), (D, E) or (C, 0) of the 16 texels, y-iFFT, store
     auto run_round = [&](int round) __attribute__((always_inline)) {
       const int i = (opaque((int)threadIdx.x) / CPI) % T;
@@ -791,8 +802,13 @@ __global__ __launch_bounds__(FftShape<LOGN>::T * CPI, CPI < ColFirstCfg<LOGN>::B
 #ifndef OCEAN_ABLATE_HS
           if (HS && HP)
           {
-            if (m & 1)
-              st4s<0>(hsb, hoff * 2, (m >> 1) * WG * 16, make_float4(hprev.x, hprev.y, H.x, H.y));
+            const int p = m >> 1;
+            if ((m & 1) && p < HL)
+              hlds[p * WG + threadIdx.x] = make_float4(hprev.x, hprev.y, H.x, H.y);
+            else if ((m & 1) && p < HL + HK)
+              hk[p - HL] = make_float4(hprev.x, hprev.y, H.x, H.y);
+            else if (m & 1)
+              st4s<0>(hsb, hoff * 2, p * WG * 16, make_float4(hprev.x, hprev.y, H.x, H.y));
             else
               hprev = H;
           }
@@ -821,7 +837,10 @@ __global__ __launch_bounds__(FftShape<LOGN>::T * CPI, CPI < ColFirstCfg<LOGN>::B
           {
             if ((m & 1) == 0)
             {
-              const float4 p = ld4s<kStream>(hsb, hoff * 2, (m >> 1) * WG * 16);
+              const int pi = m >> 1;
+              const float4 p = pi < HL        ? hlds[pi * WG + threadIdx.x]
+                               : pi < HL + HK ? hk[pi < HL + HK ? pi - HL : 0]
+                                              : ld4s<kStream>(hsb, hoff * 2, pi * WG * 16);
               pack(m, make_float2(p.x, p.y), make_kvec(x, y, dim, f.dk));
               pack(m + 1, make_float2(p.z, p.w), make_kvec(x, y + T, dim, f.dk));
             }
@@ -2096,7 +2115,15 @@ hipError_t launch_half_columns(int logn, const FrameParams& fp, const float4* h0
                        : variant == 7 ? k_cols_half<LOGN, kStream, kStream, true, false, false, 1, 1>
                        : variant == 23 ? k_cols_half<LOGN, kStream, kStream, true, false, false, RG, RGC>
                        : variant == 24 ? k_cols_half<LOGN, kStream, kStream, true, false, false, RG, RGC, K::B, true, true>
-                                      : k_cols_half<LOGN, kStream, kStream, true, false, false, RG, RGC, K::B, true>;
+                       : variant == 25 ? k_cols_half<LOGN, kStream, kStream, true, false, false, RG, RGC, K::B, true, false, 1, 0>
+                       : variant == 26 ? k_cols_half<LOGN, kStream, kStream, true, false, false, RG, RGC, K::B, true, false, 1, 1>
+                       : variant == 27 ? k_cols_half<LOGN, kStream, kStream, true, false, false, RG, RGC, K::B, true, false, 1, 2>
+                       : variant == 28 ? k_cols_half<LOGN, kStream, kStream, true, false, false, RG, RGC, K::B, true, false, 0, 2>
+                       : variant == 29 ? k_cols_half<LOGN, kStream, kStream, true, false, false, RG, RGC, K::B, true, false, 1, 3>
+                       : variant == 30 ? k_cols_half<LOGN, kStream, kStream, true, false, false, RG, RGC, K::B, true, false, 1, 4>
+                       : variant == 31 ? k_cols_half<LOGN, kStream, kStream, true, false, false, RG, RGC, K::B, true, false, 1, 5>
+                       : variant == 32 ? k_cols_half<LOGN, kStream, kStream, true, false, false, RG, RGC, K::B, true>
+                                      : k_cols_half<LOGN, kStream, kStream, true, false, false, RG, RGC, K::B, true, false, kHalfHL, kHalfHK>;
       if (variant >= 12 && variant <= 14 && !seed)  // half-strip items (k_cols_half2): H in VGPRs
       {
         auto hk = variant == 12   ? k_cols_half2<LOGN, 0, kStream, 4, 8>
@@ -2134,7 +2161,10 @@ hipError_t launch_half_columns(int logn, const FrameParams& fp, const float4* h0
                            (unsigned char*)nullptr, 1, seed);
         return hipGetLastError();
       }
-      const int lds = ((S::TW_ENTRIES * 8 + 15) / 16) * 16 + K::LDS1;
+      // H pairs in LDS (HL): production kHalfHL; variants 25..31 as named in halfbench hkeep, 32 none
+      const bool named = (variant >= 1 && variant <= 7) || (variant >= 23 && variant <= 32);  // the chain above
+      const int hl = seed || !hs ? 0 : !named ? kHalfHL : (variant >= 25 && variant <= 31 && variant != 28) ? 1 : 0;
+      const int lds = ((S::TW_ENTRIES * 8 + 15) / 16) * 16 + K::LDS1 + hl * K::WG1 * 16;
       int grid = persistent_grid(kern, K::WG1, lds, fp.cascades * HalfCfg<LOGN>::STRIPS, cus);
       if (hs && grid > hs_blocks)
         grid = hs_blocks;
@@ -2251,8 +2281,11 @@ hipError_t launch_half_slab_columns(int logn, const FrameParams& fp, const HalfS
       hipError_t e = hipGetLastError();
       if (e != hipSuccess || hsl.nstrips < 1)  // a rank past the last strip only builds the Nyquist-row term
         return e;
-      auto kern = k_cols_half<LOGN, kStream, kStream, true, true>;
-      const int lds = ((S::TW_ENTRIES * 8 + 15) / 16) * 16 + K::LDS1;
+      // slab items keep fewer pairs in VGPRs: with four, the SLAB store addressing spills 8-16 B (at
+      // N = 8192 already with two; one fits)
+      constexpr int HKS = LOGN == 13 ? 1 : kHalfHK - 1;
+      auto kern = k_cols_half<LOGN, kStream, kStream, true, true, false, 1, 1, K::B, true, false, kHalfHL, HKS>;
+      const int lds = ((S::TW_ENTRIES * 8 + 15) / 16) * 16 + K::LDS1 + kHalfHL * K::WG1 * 16;
       int grid = persistent_grid(kern, K::WG1, lds, fp.cascades * hsl.nstrips, cus);
       if (grid > hs_blocks)
         grid = hs_blocks;

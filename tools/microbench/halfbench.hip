@@ -249,6 +249,47 @@ int main(int argc, char** argv)
                 same ? "yes" : "NO");
     return 0;
   }
+  if (argc > 3 && std::strcmp(argv[3], "hkeep") == 0)
+  {
+    // pass 1 with some H pairs outside the scratch (variants 25..31: HL pairs in LDS, HK in VGPRs)
+    // against all pairs in the scratch; the frame with the production row pass
+    constexpr int NV = 8;
+    // variant 32 = round 2's earlier production (all 8 pairs in the scratch); production now = 30
+    const int vs[NV] = {32, 25, 26, 27, 28, 29, 30, 31};
+    const char* nm[NV] = {"8 pairs in scratch (variant 32)", "HL 1 HK 0", "HL 1 HK 1", "HL 1 HK 2", "HL 0 HK 2", "HL 1 HK 3",
+                          "HL 1 HK 4", "HL 1 HK 5"};
+    CHECK(c1());
+    CHECK(hipDeviceSynchronize());
+    auto pab = snap(gab, ht * sizeof(float4)), pde = snap(gcd, ht * sizeof(float4)), pc = snap(ge, ht * sizeof(float2));
+    bool same[NV] = {true};
+    for (int k = 1; k < NV; k++)
+    {
+      CHECK(hipMemset(gab, 0, ht * sizeof(float4)));
+      CHECK(hipMemset(gcd, 0, ht * sizeof(float4)));
+      CHECK(hipMemset(ge, 0, ht * sizeof(float2)));
+      CHECK(launch_half_columns(logn, fp, h0, gab, gcd, ge, spec, tw, 0, cus, hs, cus, nullptr, vs[k]));
+      CHECK(hipDeviceSynchronize());
+      std::printf("%s vs variant 32: gab, gde, gc\n", nm[k]);
+      same[k] = (int)diff(snap(gab, ht * sizeof(float4)), pab) & (int)diff(snap(gcd, ht * sizeof(float4)), pde) &
+                (int)diff(snap(ge, ht * sizeof(float2)), pc);
+    }
+    std::vector<std::vector<float>> t(NV), tf(NV);
+    for (int r = 0; r < 9; r++)
+      for (int k = 0; k < NV; k++)
+      {
+        auto ck = [&] { return launch_half_columns(logn, fp, h0, gab, gcd, ge, spec, tw, 0, cus, hs, cus, nullptr, vs[k]); };
+        t[k].push_back(time_ms(ck, 10));
+        tf[k].push_back(time_ms([&] { CHECK(ck()); return r1(); }, 10));
+      }
+    for (int k = 0; k < NV; k++)
+    {
+      std::sort(t[k].begin(), t[k].end());
+      std::sort(tf[k].begin(), tf[k].end());
+      std::printf("cols %-32s median %7.3f ms   frame %7.3f ms  bit-identical %s\n", nm[k], t[k][4], tf[k][4],
+                  same[k] ? "yes" : "NO");
+    }
+    return 0;
+  }
   if (argc > 3 && std::strcmp(argv[3], "rowabl") == 0)
   {
     // the production row pass and its timing ablations (wrong results by construction): 1 no HBM

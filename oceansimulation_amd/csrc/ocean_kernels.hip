@@ -657,7 +657,7 @@ constexpr int kHalfRG = 2, kHalfRGC = 4;
 // Pass 1's H pairs outside the scratch (k_cols_half HL / HK): one pair per thread in the LDS the
 // exchange leaves free, four in VGPRs (128 VGPRs at N = 4096, no spills); the scratch keeps 3 of 8.
 // 0.945 -> 0.817 ms per 8 x 4096^2, frame 2.332 -> 2.206 ms, fields bit-identical (halfbench hkeep).
-constexpr int kHalfHL = 1, kHalfHK = 4;
+constexpr int kHalfHL = 1, kHalfHK = 4, kHalfHKSeed = 2;  // the fused re-seed frame: variant 33 = all in scratch
 // FB: columns per field strip (4 = the h0 strip; 2 = k_cols_half2's half strips, FS = 2 STRIPS).
 template <int LOGN, int RG, int FB = 4>
 __device__ __forceinline__ int half_group_offset(int y, int strip, int b = 0)
@@ -712,7 +712,7 @@ __global__ __launch_bounds__(FftShape<LOGN>::T * CPI, CPI < ColFirstCfg<LOGN>::B
   constexpr int N = S::N, T = S::T, B = K::B, STRIPS = HC::STRIPS, WG = T * CPI, HALVES = B / CPI;
   static_assert(SLAB ? HC::SLAB_SUPPORTED : HC::SUPPORTED, "half-spectrum path: one strip per item (B = 4 unless SLAB)");
   static_assert(CPI * HALVES == B && HALVES <= 2 && (HALVES == 1 || (!SLAB && !SEED)), "whole or half strips");
-  static_assert((HL == 0 && HK == 0) || (HS && HP && !SEED && !PC && HL + HK <= 8), "H pairs outside the scratch");
+  static_assert((HL == 0 && HK == 0) || (HS && HP && !PC && HL + HK <= 8), "H pairs outside the scratch");
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   float2* tw = reinterpret_cast<float2*>(smem);
   void* xch = smem + ((S::TW_ENTRIES * 8 + 15) / 16) * 16;
@@ -770,18 +770,36 @@ __global__ __launch_bounds__(FftShape<LOGN>::T * CPI, CPI < ColFirstCfg<LOGN>::B
         {
           const int y = i + ((m + 8) & 15) * T;
           const float2 H = evolve(seed_texel(q, x, y, dim), make_kvec(x, y, dim, f.dk).k, f);
-          if constexpr (HP)
+          if (HP && (m >> 1) < HL)  // HL pairs: the LDS slot (a dynamic index is fine there)
+            reinterpret_cast<float2*>(hlds)[((m >> 1) * WG + threadIdx.x) * 2 + (m & 1)] = H;
+          else if constexpr (HP)
             st2s<0>(hsb, hoff * 2 + (m & 1) * 8, (m >> 1) * WG * 16, H);
           else
             st2s<0>(hsb, hoff, m * WG * 8, H);
         }
         __threadfence_block();  // this thread's scratch stores are complete before it reads them back
-#pragma unroll
-        for (int m = 0; m < 16; m++)
+        if constexpr (HP)
         {
-          const int y = i + ((m + 8) & 15) * T;
-          pack(m, HP ? ld2s<kStream>(hsb, hoff * 2 + (m & 1) * 8, (m >> 1) * WG * 16) : ld2s<kStream>(hsb, hoff, m * WG * 8),
-               make_kvec(x, y, dim, f.dk));
+          // read back by pairs; the HK pairs stay in VGPRs for rounds 1 and 2
+#pragma unroll
+          for (int m = 0; m < 16; m += 2)
+          {
+            const int y = i + ((m + 8) & 15) * T, p = m >> 1;
+            const float4 pp = p < HL ? hlds[p * WG + threadIdx.x] : ld4s<kStream>(hsb, hoff * 2, p * WG * 16);
+            if (p >= HL && p < HL + HK)
+              hk[p < HL + HK && p >= HL ? p - HL : 0] = pp;
+            pack(m, make_float2(pp.x, pp.y), make_kvec(x, y, dim, f.dk));
+            pack(m + 1, make_float2(pp.z, pp.w), make_kvec(x, y + T, dim, f.dk));
+          }
+        }
+        else
+        {
+#pragma unroll
+          for (int m = 0; m < 16; m++)
+          {
+            const int y = i + ((m + 8) & 15) * T;
+            pack(m, ld2s<kStream>(hsb, hoff, m * WG * 8), make_kvec(x, y, dim, f.dk));
+          }
         }
       }
       else if (!HS || round == 0)
@@ -2104,7 +2122,8 @@ hipError_t launch_half_columns(int logn, const FrameParams& fp, const float4* h0
       // 4..7: field layouts with row groups (RG, RGC) = (2, 2), (2, 4), (4, 4), (1, 1) (launch_half_rows 8..11)
       constexpr int RG = kHalfRG, RGC = kHalfRGC;
       // HP (the H scratch in 16-B pairs): 0.921 -> 0.910 ms (halfbench hpair); variant 23: unpaired
-      auto kern = seed ? k_cols_half<LOGN, 0, kStream, true, false, true, RG, RGC, K::B, true>
+      auto kern = seed && variant == 33 ? k_cols_half<LOGN, 0, kStream, true, false, true, RG, RGC, K::B, true>
+                  : seed ? k_cols_half<LOGN, 0, kStream, true, false, true, RG, RGC, K::B, true, false, kHalfHL, kHalfHKSeed>
                        : !hs ? k_cols_half<LOGN, 0, kStream, false, false, false, RG, RGC>
                        : variant == 1 ? k_cols_half<LOGN, 0, kStream, true, false, false, RG, RGC>
                        : variant == 2 ? k_cols_half<LOGN, kStream, 16, true, false, false, RG, RGC>
@@ -2163,7 +2182,8 @@ hipError_t launch_half_columns(int logn, const FrameParams& fp, const float4* h0
       }
       // H pairs in LDS (HL): production kHalfHL; variants 25..31 as named in halfbench hkeep, 32 none
       const bool named = (variant >= 1 && variant <= 7) || (variant >= 23 && variant <= 32);  // the chain above
-      const int hl = seed || !hs ? 0 : !named ? kHalfHL : (variant >= 25 && variant <= 31 && variant != 28) ? 1 : 0;
+      const int hl = seed ? (variant == 33 ? 0 : kHalfHL)
+                     : !hs ? 0 : !named ? kHalfHL : (variant >= 25 && variant <= 31 && variant != 28) ? 1 : 0;
       const int lds = ((S::TW_ENTRIES * 8 + 15) / 16) * 16 + K::LDS1 + hl * K::WG1 * 16;
       int grid = persistent_grid(kern, K::WG1, lds, fp.cascades * HalfCfg<LOGN>::STRIPS, cus);
       if (hs && grid > hs_blocks)

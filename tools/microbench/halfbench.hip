@@ -249,6 +249,55 @@ int main(int argc, char** argv)
                 same ? "yes" : "NO");
     return 0;
   }
+  if (argc > 3 && std::strcmp(argv[3], "seed") == 0)
+  {
+    // the fused re-seed pass 1 (h0 evaluated in round 0): production (H pairs in LDS / VGPRs /
+    // scratch) against variant 33 (all 8 pairs in the scratch); same evaluator, same fields
+    std::vector<SpectrumConsts> sc(C);
+    for (int c = 0; c < C; c++)
+    {
+      OceanSettings s{};
+      s.seed[0] = 12342;
+      s.seed[1] = 8934;
+      s.U_10 = 40;
+      s.theta_0 = 25;
+      s.F = 800000;
+      s.g = 9.8f;
+      s.swell = 0.5f;
+      s.h = 100;
+      s.displacement = 0.4f;
+      s.planeSize = planes[c % 8];
+      s.scale = 1;
+      s.spread = 0.2f;
+      seed_consts(s, n, &sc[c]);
+    }
+    SpectrumConsts* dsc;
+    CHECK(hipMalloc(&dsc, C * sizeof(SpectrumConsts)));
+    CHECK(hipMemcpy(dsc, sc.data(), C * sizeof(SpectrumConsts), hipMemcpyHostToDevice));
+    auto sv = [&](int v) { return launch_half_columns(logn, fp, h0, gab, gcd, ge, spec, tw, 0, cus, hs, cus, dsc, v); };
+    CHECK(sv(33));
+    CHECK(hipDeviceSynchronize());
+    auto pab = snap(gab, ht * sizeof(float4)), pde = snap(gcd, ht * sizeof(float4)), pc = snap(ge, ht * sizeof(float2));
+    CHECK(hipMemset(gab, 0, ht * sizeof(float4)));
+    CHECK(hipMemset(gcd, 0, ht * sizeof(float4)));
+    CHECK(hipMemset(ge, 0, ht * sizeof(float2)));
+    CHECK(sv(0));
+    CHECK(hipDeviceSynchronize());
+    std::printf("re-seed cols, production vs variant 33: gab, gde, gc\n");
+    const bool same = (int)diff(snap(gab, ht * sizeof(float4)), pab) & (int)diff(snap(gcd, ht * sizeof(float4)), pde) &
+                      (int)diff(snap(ge, ht * sizeof(float2)), pc);
+    std::vector<std::vector<float>> t(2);
+    for (int r = 0; r < 9; r++)
+    {
+      t[0].push_back(time_ms([&] { return sv(33); }, 10));
+      t[1].push_back(time_ms([&] { return sv(0); }, 10));
+    }
+    for (auto& v : t)
+      std::sort(v.begin(), v.end());
+    std::printf("re-seed cols, 8 pairs in scratch (33)  median %7.3f ms\n", t[0][4]);
+    std::printf("re-seed cols, production              median %7.3f ms  bit-identical %s\n", t[1][4], same ? "yes" : "NO");
+    return 0;
+  }
   if (argc > 3 && std::strcmp(argv[3], "hkeep") == 0)
   {
     // pass 1 with some H pairs outside the scratch (variants 25..31: HL pairs in LDS, HK in VGPRs)

@@ -1314,8 +1314,9 @@ __global__ __launch_bounds__(FftShape<LOGN>::T * RPW_) void k_rows_half(
   const float dim = (float)N;
   // RPW = 2: C's row pairs are 64-B halves of 128-B lines; items 2p, 2p+1 (the same line) run
   // together on one XCD so the line is fetched once
-  for (int item = RPW != 2 ? blockIdx.x : GRP == 4 ? xcd_group_slot<4>(blockIdx.x, gridDim.x)
-                                                    : xcd_pair_slot(blockIdx.x, gridDim.x);
+  // (RPW = 1 with GRP = 4, an A/B: the 4 rows of a gc line on one XCD)
+  for (int item = RPW != 2 && GRP != 4 ? blockIdx.x : GRP == 4 ? xcd_group_slot<4>(blockIdx.x, gridDim.x)
+                                                                : xcd_pair_slot(blockIdx.x, gridDim.x);
        item < total; item += gridDim.x)
   {
     const int cimg0 = item / blocks, y0 = (item - cimg0 * blocks) * RPW;
@@ -2142,6 +2143,9 @@ hipError_t launch_half_columns(int logn, const FrameParams& fp, const float4* h0
                        : variant == 30 ? k_cols_half<LOGN, kStream, kStream, true, false, false, RG, RGC, K::B, true, false, 1, 4>
                        : variant == 31 ? k_cols_half<LOGN, kStream, kStream, true, false, false, RG, RGC, K::B, true, false, 1, 5>
                        : variant == 32 ? k_cols_half<LOGN, kStream, kStream, true, false, false, RG, RGC, K::B, true>
+                       : variant == 34 ? k_cols_half<LOGN, kStream, kStream, true, false, false, 2, 2, K::B, true, false, kHalfHL, kHalfHK>
+                       : variant == 35 ? k_cols_half<LOGN, kStream, kStream, true, false, false, 4, 4, K::B, true, false, kHalfHL, kHalfHK>
+                       : variant == 36 ? k_cols_half<LOGN, kStream, kStream, true, false, false, 1, 1, K::B, true, false, kHalfHL, kHalfHK>
                                       : k_cols_half<LOGN, kStream, kStream, true, false, false, RG, RGC, K::B, true, false, kHalfHL, kHalfHK>;
       if (variant >= 12 && variant <= 14 && !seed)  // half-strip items (k_cols_half2): H in VGPRs
       {
@@ -2181,7 +2185,8 @@ hipError_t launch_half_columns(int logn, const FrameParams& fp, const float4* h0
         return hipGetLastError();
       }
       // H pairs in LDS (HL): production kHalfHL; variants 25..31 as named in halfbench hkeep, 32 none
-      const bool named = (variant >= 1 && variant <= 7) || (variant >= 23 && variant <= 32);  // the chain above
+      // the chain above with HL = 0 (34..36: production's H pairs with the field layouts of 4, 6, 7)
+      const bool named = (variant >= 1 && variant <= 7) || (variant >= 23 && variant <= 32);
       const int hl = seed ? (variant == 33 ? 0 : kHalfHL)
                      : !hs ? 0 : !named ? kHalfHL : (variant >= 25 && variant <= 31 && variant != 28) ? 1 : 0;
       const int lds = ((S::TW_ENTRIES * 8 + 15) / 16) * 16 + K::LDS1 + hl * K::WG1 * 16;
@@ -2215,14 +2220,21 @@ hipError_t launch_half_rows(int logn, const FrameParams& fp, const float4* gab, 
       // 0 (production): one item per row block for both images (C loaded once); 6: one image per
       // item (C loaded by both items of a row block)
       constexpr int R4 = K::RPW2;
-      const int rpw = ablation == 4 ? R4 : ablation == 5 ? 1 : 2;
+      // production at N = 4096: one row (both images) per 256-thread workgroup, four workgroups per
+      // CU, the 4 rows of a gc line on one XCD (GRP 4): 1.407 -> 1.377 ms per 8 x 4096^2, maps
+      // bit-identical (halfbench rowv 16); 17 = the two-row workgroups (production below 4096)
+      constexpr bool ONE_ROW = LOGN == 12;
+      const int rpw = ablation == 4 ? R4 : (ablation == 5 || ablation == 16 || (ablation == 0 && ONE_ROW)) ? 1 : 2;
       const int per_item = (ablation <= 3 || ablation >= 7) ? 1 : 2;
       // production loads use the default policy: C's 128-B lines are shared by the paired items
       // (xcd_pair_slot) and streamed loads lost them before the partner's read (-5 %,
       // tools/microbench/halfbench); 7: streamed loads
       // 8..11: the field layouts of launch_half_columns' variants 4..7
       constexpr int RG = kHalfRG, RGC = kHalfRGC;
-      auto kern = ablation == 0   ? k_rows_half<LOGN, 0, kStream, 0, 2, true, false, RG, RGC>
+      // 16: one row (both images) per 256-thread workgroup, four per CU, rows of a gc line on one XCD
+      auto kern = ablation == 0 && ONE_ROW ? k_rows_half<LOGN, 0, kStream, 0, 1, true, false, RG, RGC, 4, 4>
+                  : ablation == 0 || ablation == 17 ? k_rows_half<LOGN, 0, kStream, 0, 2, true, false, RG, RGC>
+                  : ablation == 16 ? k_rows_half<LOGN, 0, kStream, 0, 1, true, false, RG, RGC, 4, 4>
                   : ablation == 8 ? k_rows_half<LOGN, 0, kStream, 0, 2, true, false, 2, 2>
                   : ablation == 9 ? k_rows_half<LOGN, 0, kStream, 0, 2, true, false, 2, 4>
                   : ablation == 10 ? k_rows_half<LOGN, 0, kStream, 0, 2, true, false, 4, 4>

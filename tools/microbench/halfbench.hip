@@ -249,6 +249,80 @@ int main(int argc, char** argv)
                 same ? "yes" : "NO");
     return 0;
   }
+  if (argc > 4 && std::strcmp(argv[3], "rowv") == 0)
+  {
+    // row-pass variants (launch_half_rows ablation numbers from the command line) against production
+    // on the same fields: timing, and maps/Jacobian bit-identity
+    CHECK(c1());
+    CHECK(r1());
+    CHECK(hipDeviceSynchronize());
+    auto pm = snap(maps, mb), pj = snap(jac, jb);
+    std::vector<int> av{0};
+    for (int a = 4; a < argc; a++)
+      av.push_back(std::atoi(argv[a]));
+    std::vector<int> same(av.size(), 1);
+    for (size_t k = 1; k < av.size(); k++)
+    {
+      CHECK(hipMemset(maps, 0, mb));
+      CHECK(hipMemset(jac, 0, jb));
+      CHECK(launch_half_rows(logn, fp, gab, gcd, ge, spec, maps, jac, foam, tw, 0, cus, av[k]));
+      CHECK(hipDeviceSynchronize());
+      std::printf("rows variant %d vs production: maps, jacobian\n", av[k]);
+      same[k] = (int)diff(snap(maps, mb), pm) & (int)diff(snap(jac, jb), pj);
+    }
+    std::vector<std::vector<float>> t(av.size());
+    for (int r = 0; r < 9; r++)
+      for (size_t k = 0; k < av.size(); k++)
+        t[k].push_back(time_ms([&] { return launch_half_rows(logn, fp, gab, gcd, ge, spec, maps, jac, foam, tw, 0, cus, av[k]); }, 10));
+    for (size_t k = 0; k < av.size(); k++)
+    {
+      std::sort(t[k].begin(), t[k].end());
+      std::printf("rows variant %2d  median %7.3f ms  %7.1f GB/s at 56 B/pt  bit-identical %s\n", av[k], t[k][4],
+                  56.04 * pts / t[k][4] / 1e6, same[k] ? "yes" : "NO");
+    }
+    return 0;
+  }
+  if (argc > 3 && std::strcmp(argv[3], "layout2") == 0)
+  {
+    // field layouts (RG, RGC) re-measured with production's pass 1 (5 of 8 H pairs out of the
+    // scratch): pass 1 variants 34..36 with pass 2 variants 8, 10, 11; same arithmetic, so the maps
+    // must be bit-identical to production's
+    const int cv[4] = {0, 34, 35, 36}, rv[4] = {0, 8, 10, 11};
+    const char* ln[4] = {"(2, 4) production", "(2, 2)", "(4, 4)", "(1, 1) strips"};
+    CHECK(c1());
+    CHECK(r1());
+    CHECK(hipDeviceSynchronize());
+    auto pm = snap(maps, mb), pj = snap(jac, jb);
+    bool same[4] = {true, true, true, true};
+    for (int v = 1; v < 4; v++)
+    {
+      CHECK(hipMemset(maps, 0, mb));
+      CHECK(launch_half_columns(logn, fp, h0, gab, gcd, ge, spec, tw, 0, cus, hs, cus, nullptr, cv[v]));
+      CHECK(launch_half_rows(logn, fp, gab, gcd, ge, spec, maps, jac, foam, tw, 0, cus, rv[v]));
+      CHECK(hipDeviceSynchronize());
+      std::printf("layout %s vs production: maps, jacobian\n", ln[v]);
+      same[v] = (int)diff(snap(maps, mb), pm) & (int)diff(snap(jac, jb), pj);
+    }
+    std::vector<std::vector<float>> tc(4), tr(4), tf(4);
+    for (int r = 0; r < 9; r++)
+      for (int v = 0; v < 4; v++)
+      {
+        auto cl = [&] { return launch_half_columns(logn, fp, h0, gab, gcd, ge, spec, tw, 0, cus, hs, cus, nullptr, cv[v]); };
+        auto rl = [&] { return launch_half_rows(logn, fp, gab, gcd, ge, spec, maps, jac, foam, tw, 0, cus, rv[v]); };
+        tc[v].push_back(time_ms(cl, 10));
+        tr[v].push_back(time_ms(rl, 10));
+        tf[v].push_back(time_ms([&] { CHECK(cl()); return rl(); }, 10));
+      }
+    for (int v = 0; v < 4; v++)
+    {
+      std::sort(tc[v].begin(), tc[v].end());
+      std::sort(tr[v].begin(), tr[v].end());
+      std::sort(tf[v].begin(), tf[v].end());
+      std::printf("%-20s cols %7.3f  rows %7.3f  frame %7.3f ms (median)  bit-identical %s\n", ln[v], tc[v][4], tr[v][4],
+                  tf[v][4], same[v] ? "yes" : "NO");
+    }
+    return 0;
+  }
   if (argc > 3 && std::strcmp(argv[3], "seed") == 0)
   {
     // the fused re-seed pass 1 (h0 evaluated in round 0): production (H pairs in LDS / VGPRs /

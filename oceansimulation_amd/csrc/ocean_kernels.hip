@@ -2122,6 +2122,9 @@ hipError_t launch_half_columns(int logn, const FrameParams& fp, const float4* h0
       // loads, 2 = sc1 field stores (dropped from L2: slower), 3 = sc1 + nt stores
       // 4..7: field layouts with row groups (RG, RGC) = (2, 2), (2, 4), (4, 4), (1, 1) (launch_half_rows 8..11)
       constexpr int RG = kHalfRG, RGC = kHalfRGC;
+      // whole grids below 4096 keep 2 H pairs in VGPRs: 128 VGPRs, so two (2048) or four (1024)
+      // workgroups fit a CU (with 4: 134-136 VGPRs, one fewer)
+      constexpr int HKW = LOGN == 12 ? kHalfHK : 2;
       // HP (the H scratch in 16-B pairs): 0.921 -> 0.910 ms (halfbench hpair); variant 23: unpaired
       auto kern = seed && variant == 33 ? k_cols_half<LOGN, 0, kStream, true, false, true, RG, RGC, K::B, true>
                   : seed ? k_cols_half<LOGN, 0, kStream, true, false, true, RG, RGC, K::B, true, false, kHalfHL, kHalfHKSeed>
@@ -2146,7 +2149,7 @@ hipError_t launch_half_columns(int logn, const FrameParams& fp, const float4* h0
                        : variant == 34 ? k_cols_half<LOGN, kStream, kStream, true, false, false, 2, 2, K::B, true, false, kHalfHL, kHalfHK>
                        : variant == 35 ? k_cols_half<LOGN, kStream, kStream, true, false, false, 4, 4, K::B, true, false, kHalfHL, kHalfHK>
                        : variant == 36 ? k_cols_half<LOGN, kStream, kStream, true, false, false, 1, 1, K::B, true, false, kHalfHL, kHalfHK>
-                                      : k_cols_half<LOGN, kStream, kStream, true, false, false, RG, RGC, K::B, true, false, kHalfHL, kHalfHK>;
+                                      : k_cols_half<LOGN, kStream, kStream, true, false, false, RG, RGC, K::B, true, false, kHalfHL, HKW>;
       if (variant >= 12 && variant <= 14 && !seed)  // half-strip items (k_cols_half2): H in VGPRs
       {
         auto hk = variant == 12   ? k_cols_half2<LOGN, 0, kStream, 4, 8>
@@ -2191,8 +2194,11 @@ hipError_t launch_half_columns(int logn, const FrameParams& fp, const float4* h0
                      : !hs ? 0 : !named ? kHalfHL : (variant >= 25 && variant <= 31 && variant != 28) ? 1 : 0;
       const int lds = ((S::TW_ENTRIES * 8 + 15) / 16) * 16 + K::LDS1 + hl * K::WG1 * 16;
       int grid = persistent_grid(kern, K::WG1, lds, fp.cascades * HalfCfg<LOGN>::STRIPS, cus);
-      if (hs && grid > hs_blocks)
-        grid = hs_blocks;
+      // hs holds hs_blocks slices for 1024-thread workgroups (half_hs_bytes); a block uses 16 x WG1
+      // entries, so below 4096 each slice serves 1024 / WG1 blocks (variant 37: one, as before)
+      const int slices = variant == 37 ? hs_blocks : hs_blocks * (1024 / K::WG1);
+      if (hs && grid > slices)
+        grid = slices;
       if (grid < 1)
         return hipErrorInvalidValue;
       hipLaunchKernelGGL(kern, dim3(grid), dim3(K::WG1), lds, stream, fp, h0, gab, gcd, ge, tw, hs, HalfSlab{},

@@ -249,6 +249,38 @@ int main(int argc, char** argv)
                 same ? "yes" : "NO");
     return 0;
   }
+  if (argc > 3 && std::strcmp(argv[3], "cap") == 0)
+  {
+    // pass 1 below 4096: grid capped at one H-scratch slice per 1024 threads (production: 1024 / WG1
+    // blocks per slice, so 2048 runs two workgroups per CU and 1024 four) against one block per slice
+    // (variant 37, round 2's earlier cap); same kernel, same fields
+    auto cp = [&] { return launch_half_columns(logn, fp, h0, gab, gcd, ge, spec, tw, 0, cus, hs, cus, nullptr, 37); };
+    CHECK(c1());
+    CHECK(hipDeviceSynchronize());
+    auto pab = snap(gab, ht * sizeof(float4)), pde = snap(gcd, ht * sizeof(float4)), pc = snap(ge, ht * sizeof(float2));
+    CHECK(hipMemset(gab, 0, ht * sizeof(float4)));
+    CHECK(hipMemset(gcd, 0, ht * sizeof(float4)));
+    CHECK(hipMemset(ge, 0, ht * sizeof(float2)));
+    CHECK(cp());
+    CHECK(hipDeviceSynchronize());
+    std::printf("cols, one block per scratch slice vs production: gab, gde, gc\n");
+    const bool same = (int)diff(snap(gab, ht * sizeof(float4)), pab) & (int)diff(snap(gcd, ht * sizeof(float4)), pde) &
+                      (int)diff(snap(ge, ht * sizeof(float2)), pc);
+    std::vector<std::vector<float>> t(4);
+    for (int r = 0; r < 9; r++)
+    {
+      t[0].push_back(time_ms(c1, 10));
+      t[1].push_back(time_ms(cp, 10));
+      t[2].push_back(time_ms([&] { CHECK(c1()); return r1(); }, 10));
+      t[3].push_back(time_ms([&] { CHECK(cp()); return r1(); }, 10));
+    }
+    for (auto& v : t)
+      std::sort(v.begin(), v.end());
+    std::printf("N=%d x %d  cols (production)            median %7.3f ms   frame %7.3f ms\n", n, C, t[0][4], t[2][4]);
+    std::printf("N=%d x %d  cols, one block per slice    median %7.3f ms   frame %7.3f ms  bit-identical %s\n", n, C,
+                t[1][4], t[3][4], same ? "yes" : "NO");
+    return 0;
+  }
   if (argc > 4 && std::strcmp(argv[3], "rowv") == 0)
   {
     // row-pass variants (launch_half_rows ablation numbers from the command line) against production

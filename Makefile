@@ -21,8 +21,11 @@ APP := examples/waveapp_headless
 
 all: $(LIB) $(WAVES) $(ORACLE) $(CPPTEST) $(APP)
 
-DEVICE_H := $(wildcard $(CSRC)/device/*.h)
-$(CSRC)/build/ocean_kernels.o: $(CSRC)/ocean_kernels.hip $(CSRC)/ocean_internal.h $(DEVICE_H)
+DEVICE_H := $(wildcard $(CSRC)/device/*.h) $(CSRC)/ocean_internal.h $(CSRC)/launch_common.h
+# one translation unit per frame path, compiled in parallel
+KERNEL_TUS := ocean_kernels launch_half launch_slab launch_fft
+KERNEL_OBJS := $(KERNEL_TUS:%=$(CSRC)/build/%.o)
+$(CSRC)/build/%.o: $(CSRC)/%.hip $(DEVICE_H)
 	@mkdir -p $(CSRC)/build
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
@@ -30,7 +33,7 @@ $(CSRC)/build/ocean_capi.o: $(CSRC)/ocean_capi.cpp $(CSRC)/ocean_internal.h incl
 	@mkdir -p $(CSRC)/build
 	$(HIPCC) $(HIPFLAGS) -x hip -c $< -o $@
 
-$(LIB): $(CSRC)/build/ocean_kernels.o $(CSRC)/build/ocean_capi.o
+$(LIB): $(KERNEL_OBJS) $(CSRC)/build/ocean_capi.o
 	$(HIPCC) --offload-arch=$(ARCH) -shared -o $@ $^ -Wl,-soname,liboceanfft.so
 
 # C++ drop-in layer (Waves::FFTCalculator / Waves::Generator / Vision::RenderDevice shim) over the C ABI.
@@ -56,14 +59,15 @@ $(APP): examples/waveapp_headless.cpp $(WAVES)
 
 MB := tools/microbench
 microbench: $(MB)/rm16bench $(MB)/gen4bench $(MB)/ifft4bench $(MB)/gridbench $(MB)/halfbench_nohs $(MB)/ifftbench $(MB)/transbench $(MB)/scatterbench $(MB)/halfbench $(MB)/genbench $(MB)/colbench $(MB)/copybench $(MB)/genbench_noxch $(MB)/genbench_nobar $(MB)/layoutbench
-$(MB)/%: $(MB)/%.hip $(CSRC)/ocean_kernels.hip $(CSRC)/ocean_internal.h $(DEVICE_H)
+MB_DEPS := $(KERNEL_TUS:%=$(CSRC)/%.hip) $(DEVICE_H) $(MB)/ab_kernels.h $(MB)/all_kernels.h
+$(MB)/%: $(MB)/%.hip $(MB_DEPS)
 	$(HIPCC) $(HIPFLAGS) $< -o $@
 # timing ablations (wrong results by construction): no LDS exchanges / exchanges without barriers
-$(MB)/genbench_noxch: $(MB)/genbench.hip $(CSRC)/ocean_kernels.hip $(CSRC)/ocean_internal.h $(DEVICE_H)
+$(MB)/genbench_noxch: $(MB)/genbench.hip $(MB_DEPS)
 	$(HIPCC) $(HIPFLAGS) -DOCEAN_ABLATE_EXCHANGE $< -o $@
-$(MB)/halfbench_nohs: $(MB)/halfbench.hip $(CSRC)/ocean_kernels.hip $(CSRC)/ocean_internal.h $(DEVICE_H)
+$(MB)/halfbench_nohs: $(MB)/halfbench.hip $(MB_DEPS)
 	$(HIPCC) $(HIPFLAGS) -DOCEAN_ABLATE_HS $< -o $@
-$(MB)/genbench_nobar: $(MB)/genbench.hip $(CSRC)/ocean_kernels.hip $(CSRC)/ocean_internal.h $(DEVICE_H)
+$(MB)/genbench_nobar: $(MB)/genbench.hip $(MB_DEPS)
 	$(HIPCC) $(HIPFLAGS) -DOCEAN_ABLATE_BARRIER $< -o $@
 
 clean:

@@ -191,14 +191,14 @@ def cascade_settings(rank: int, c: int) -> dict:
 
 
 def device_source_sha256(root: str = "") -> str:
-    """Hash of the device code (ocean_kernels.hip, ocean_internal.h, device/*.h): the same function as
+    """Hash of the device code (csrc/*.hip, csrc/*.h, device/*.h): the same function as
     tools/parse_rocprof.py's, which stamps it into every PMC summary (tests/test_host_logic.py checks
     that the two agree)."""
     import hashlib
 
     root = root or ROOT
     csrc = os.path.join(root, "oceansimulation_amd", "csrc")
-    files = [os.path.join(csrc, "ocean_kernels.hip"), os.path.join(csrc, "ocean_internal.h")]
+    files = sorted(os.path.join(csrc, f) for f in os.listdir(csrc) if f.endswith(".hip") or f.endswith(".h"))
     files += sorted(os.path.join(csrc, "device", f) for f in os.listdir(os.path.join(csrc, "device")) if f.endswith(".h"))
     h = hashlib.sha256()
     for f in files:
@@ -517,9 +517,8 @@ def slab_grid(args, rank: int, world: int, local: int) -> dict:
         "column_pass_ms": ms[1] / max(cnt[1], 1),
         "row_pass_ms": ms[2] / max(cnt[2], 1),
         "frame_path": ("full spectrum" if args.full_spectrum else
-                       "half spectrum, strip-dealt (fields moved to row-major after the exchange)" if world > 1 else
-                       "half spectrum, four-step column pass (16-point step in registers, N/16-point step into "
-                       "the row-major fields; no transposes)"),
+                       "half spectrum, four-step column pass (16-point step in registers, N/16-point step written "
+                       "in destination-block order; the row pass reads the received blocks, no transposes)"),
         "frame_hbm_bytes_per_point": sum(g.frame_bytes()),
         "exchange_bytes_per_rank": g.exchange_bytes * (world - 1) // world if world > 1 else 0,
         "serial_ms_per_frame": 1000.0 * el / per,

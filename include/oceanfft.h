@@ -125,8 +125,10 @@ float* ocean_generator_jacobian_map(ocean_generator* gen, int cascade);
 /* The initialSpectrum image (private in the reference, src/Generator.h:86): (h0(k), conj(h0(-k)))
  * per texel, stored strip-blocked: texel (x, y) at index ((x / B) * N + y) * B + (x % B) with
  * B = ocean_generator_spectrum_block(gen), so the column pass streams it contiguously. Slab
- * generators hold only their own columns: the column slab (full spectrum), or their kept strips in
- * order, each N * B texels (half spectrum; the Nyquist strip x = 0 .. B-1 last). */
+ * generators hold only their own columns: the column slab (full spectrum), their kept strips in
+ * order, each N * B texels (strip-dealt half spectrum; the Nyquist strip x = 0 .. B-1 last), or their
+ * kept columns x = N/2 + u0 .. blocked 64 wide from u0, the last rank then the block of x = 0 .. 63
+ * (four-step, ocean_slab_layout half == 2). The pointer is writable: see ocean_generator_set_h0_memo. */
 float* ocean_generator_initial_spectrum(ocean_generator* gen, int cascade);
 int ocean_generator_spectrum_block(const ocean_generator* gen);
 
@@ -134,25 +136,27 @@ int ocean_generator_spectrum_block(const ocean_generator* gen);
  * u >= 0 half of the columns, as 5 complex fields (H, kz H, H/|k|, kz H/|k|, kz^2 H/|k|), and the
  * row pass rebuilds the reference's 4 packed lanes from Hermitian symmetry plus the reference's
  * Nyquist-row term. Whole grids of 1024 .. 4096 use the blocked layout (84 HBM bytes
- * per point instead of 116); slab generators, and whole grids of 8192 / 16384, deal the kept
- * strips over the ranks and move the received fields to row-major before the row pass (124 bytes
- * per point; exchange 20 bytes per point instead of 32). enable = 0 selects the full-spectrum path
- * (both give the reference's results within rounding). On a slab generator the switch changes
- * ocean_generator_exchange_bytes and re-seeds h0 at the next frame. */
+ * per point instead of 116). N = 8192 / 16384 (whole grids and slabs) run the four-step column pass,
+ * whose second step writes destination-block order, so the row pass reads the exchanged blocks
+ * directly (124 bytes per point; exchange 20 bytes per point instead of 32); slabs of 1024 .. 4096
+ * deal the kept strips over the ranks and move the received fields to row-major before the row pass.
+ * enable = 0 selects the full-spectrum path (both give the reference's results within rounding). On a
+ * slab generator the switch changes ocean_generator_exchange_bytes and re-seeds h0 at the next frame. */
 int ocean_generator_set_half_spectrum(ocean_generator* gen, int enable);
-/* Whole grids of N = 8192 / 16384 on one rank (ocean_generator_create, or a slab generator with
- * ranks == 1), half spectrum: enable (default) = the column pass in four steps (N = 16 * N2: a
- * 16-point step in registers, then N2-point transforms on 16-column strips straight into the row
- * pass's row-major fields; no one-column work items and no transposes; h0 is then blocked
- * ocean_generator_spectrum_block = 64 columns wide); 0 = the strip-dealt column pass + transposes
- * that slabs of ranks > 1 run, bit-identical to them. Both give the reference's results within
- * rounding. Switching re-lays h0 out at the next frame from the settings it was seeded with. No
- * reference counterpart. */
+/* N = 8192 / 16384, half spectrum (whole grids and slabs): enable (default) = the column pass in four
+ * steps (N = 16 * N2: a 16-point step in registers, then N2-point transforms on 8-column strips
+ * written straight into destination-block order; no one-column work items and no transposes; h0 is
+ * then blocked ocean_generator_spectrum_block = 64 columns wide, a slab holding only its own kept
+ * columns); 0 = the strip-dealt column pass + transposes into row-major fields. Both give the
+ * reference's results within rounding. Switching changes ocean_generator_exchange_bytes and re-lays h0
+ * out at the next frame from the settings it was seeded with. No reference counterpart. */
 int ocean_generator_set_four_step(ocean_generator* gen, int enable);
 /* A re-seed requested by ocean_generator_calculate(.., update_spectrum = 1) — the reference app
  * requests one on every frame (src/Waves.cpp:91-94) — is skipped when no h0 input (every settings
  * field but `time`) changed since h0 was last seeded: it would reproduce the same image bit for bit.
- * enable = 0 re-seeds on every request, as the reference does. Default 1. No reference counterpart. */
+ * Handing out the h0 pointer (ocean_generator_initial_spectrum) makes the next requested re-seed run,
+ * since the caller may have written h0 through it. enable = 0 re-seeds on every request, as the
+ * reference does. Default 1. No reference counterpart. */
 int ocean_generator_set_h0_memo(ocean_generator* gen, int enable);
 /* Algorithmic HBM bytes per height-field point of the column pass [0] and the row pass [1] of the
  * generator's current path (what bench.py prices the roofline with). */
@@ -177,9 +181,11 @@ int ocean_generator_slab_rows(ocean_generator* gen, const float* recv);
 int ocean_generator_slab_info(const ocean_generator* gen, int* rank, int* ranks, int* row0, int* rows);
 /* Host-only geometry of a one-cascade slab generator (no device needed): out = {first kept strip,
  * strips this rank transforms, strip slots per block, rows per block (N / ranks), exchange block
- * bytes, exchange bytes} for the half-spectrum path (half != 0: the STRIPS = N / (2B) + 1 kept
- * strips dealt ceil(STRIPS / ranks) per rank), or {first column, columns, 0, rows, block bytes,
- * exchange bytes} for the full-spectrum path. */
+ * bytes, exchange bytes} for the strip-dealt half-spectrum path (half == 1: the STRIPS = N / (2B) + 1
+ * kept strips dealt ceil(STRIPS / ranks) per rank); {first kept column u0, kept columns N / (2 ranks),
+ * 1 if the rank also holds the Nyquist column, rows, block bytes, exchange bytes} for the four-step
+ * path (half == 2, N = 8192 / 16384: the default there); or {first column, columns, 0, rows, block
+ * bytes, exchange bytes} for the full-spectrum path (half == 0). */
 int ocean_slab_layout(size_t texture_size, int rank, int ranks, int half, int64_t out[6]);
 
 /* ---- instrumentation (bench) ------------------------------------------------------------- */

@@ -1,0 +1,244 @@
+// device/k_fft.h — kernels of the standalone EncodeIFFT (src/FFTCalculator.cpp:73-114,
+// resources/fft.compute:21-88) on caller-owned row-major RGBA32F images: the in-place row and column
+// passes, the column-first strided pass of N = 4096, and the four-step column transform of N = 16384.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "ocean_internal.h"
+#include "device/fft.h"
+#include "device/grid.h"
+#include "device/memory.h"
+
+namespace oceanfft
+{
+
+// ------------------------------------------------------------------------------------------------
+// FFTCalculator::EncodeIFFT path on caller-owned row-major images: row pass then column pass,
+// both in place (no work image).
+// ------------------------------------------------------------------------------------------------
+template <int LOGN>
+struct RowCfg
+{
+  using S = FftShape<LOGN>;
+  static constexpr int RPW = S::T >= 256 ? 1 : 256 / S::T;  // rows per workgroup iteration
+  static constexpr int WG = S::T * RPW;
+  static constexpr bool SPLIT = (S::N * 16 > 96 * 1024);   // float4 exchange would not fit
+  static constexpr int LDS_BYTES = lds_row_slots<LOGN>(RPW) * (SPLIT ? 8 : 16);
+  // waves per SIMD the LDS budget admits (>= 1): caps VGPRs so registers never limit residency
+  static constexpr int WGS_PER_CU = (150 * 1024) / (LDS_BYTES + 2048) < 1 ? 1 : (150 * 1024) / (LDS_BYTES + 2048);
+  static constexpr int MIN_WAVES_RAW = WGS_PER_CU * (WG / 64) / 4;
+  static constexpr int MIN_WAVES = MIN_WAVES_RAW < 1 ? 1 : (MIN_WAVES_RAW > 8 ? 8 : MIN_WAVES_RAW);
+};
+
+// Row pass of a plain EncodeIFFT on packed images [n_images][N][N] float4, in place.
+template <int LOGN>
+__global__ __launch_bounds__(RowCfg<LOGN>::WG, RowCfg<LOGN>::MIN_WAVES) void k_rows_ifft(
+    int rows, float4* __restrict__ images, const float2* __restrict__ tw_glob)
+{
+  using S = FftShape<LOGN>;
+  using R = RowCfg<LOGN>;
+  constexpr int N = S::N, T = S::T;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  float2* tw = reinterpret_cast<float2*>(smem);
+  void* xch = smem + ((S::TW_ENTRIES * 8 + 15) / 16) * 16;
+  load_twiddles<LOGN>(tw, tw_glob);
+
+  const int rho0 = threadIdx.x / T, i0 = threadIdx.x % T;
+  const int total = rows;  // rows of N packed texels, contiguous (n_images * N for whole images)
+  for (int row0 = blockIdx.x * R::RPW; row0 < total; row0 += gridDim.x * R::RPW)
+  {
+    const int i = opaque(i0), rho = R::RPW == 1 ? 0 : opaque(rho0);
+    // rows row0 .. row0+RPW-1 are contiguous: uniform base, lane offset (rho*N + i)*16; the
+    // range limit zeroes/drops rows past the last image (ragged tail for small N)
+    float4* lines = images + ((size_t)row0 << LOGN);
+    const int lim = clamp_bytes((int64_t)(total - row0) * N * 16);
+    const int voff = ((rho << LOGN) + i) * 16;
+    CPair v[16];
+#pragma unroll
+    for (int m = 0; m < 16; m++)
+      v[m] = to_pair(ld4(lines + ((m + 8) & 15) * T, voff, lim));  // fftShift on x folded into the load
+    fft_run<LOGN, 0, R::SPLIT>(v, i, rho, xch, tw);
+#pragma unroll
+    for (int m = 0; m < 16; m++)
+      st4(lines + m * T, voff, from_pair(v[m]), lim);
+  }
+}
+
+// Column pass in place: strips of C texel columns, transformed along y.
+template <int LOGN>
+__global__ __launch_bounds__(ColCfg<LOGN>::WG) void k_cols(int n_images, float4* __restrict__ images,
+                                                           const float2* __restrict__ tw_glob)
+{
+  using S = FftShape<LOGN>;
+  using K = ColCfg<LOGN>;
+  constexpr int T = S::T, C = K::C;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  float2* tw = reinterpret_cast<float2*>(smem);
+  void* xch = smem + ((S::TW_ENTRIES * 8 + 15) / 16) * 16;
+  load_twiddles<LOGN>(tw, tw_glob);
+
+  const int c0 = threadIdx.x % C, i0 = threadIdx.x / C;
+  const int total = n_images * K::STRIPS;
+  for (int item = xcd_pair_slot(blockIdx.x, gridDim.x); item < total; item += gridDim.x)
+  {
+    const int c = opaque(c0), i = opaque(i0);
+    const int img = item / K::STRIPS, strip = item - img * K::STRIPS;
+    const int x = strip * C + c;
+    // image rows i + mm*T: uniform base per mm (SGPR), lane offset (i*N + x)*16 shared by all mm
+    float4* ibase = images + ((size_t)img << (2 * LOGN));
+    const int voff = ((i << LOGN) + x) * 16;
+    CPair v[16];
+#pragma unroll
+    for (int m = 0; m < 16; m++)
+    {
+      // input q = i + m*T sits in row (q + N/2) mod N = i + ((m + 8) mod 16)*T: fftShift on y
+      const int mm = (m + 8) & 15;
+      v[m] = to_pair(ld4(ibase + ((size_t)(mm * T) << LOGN), voff));
+    }
+    fft_run<LOGN, C, true>(v, i, c, xch, tw);
+#pragma unroll
+    for (int m = 0; m < 16; m++)
+      st4(ibase + ((size_t)(m * T) << LOGN), voff, from_pair(v[m]));
+  }
+}
+
+// Standalone EncodeIFFT, column-first with a work image (src/FFTCalculator.cpp keeps a workImage
+// too): pass A reads the caller's row-major image in strips of B columns (64-B pieces per row,
+// the only strided access), iFFTs along y with the fftShift folded into the row index, and writes
+// the blocked split-plane work image work[img][x/B][y][B] contiguously; pass B is k_rows_final on
+// it (256-B runs in, row-major rows out, no Jacobian). Measured patterns (profiles/
+// r01_colbench_patterns.log): strided read + contiguous write 3.4 TB/s, against 2.1-2.4 TB/s for
+// the in-place column pass that reads and writes 64-B pieces.
+// LA: default-policy loads. Each 128-B line is read half by this block and half by the block of
+// the adjacent strip (same XCD, same time); streamed (nt) loads lost the line before the partner's
+// read: 1.38 -> 1.12 ms per 8 images (tools/microbench/ifftbench; grouping 4 or 8 strips: no gain).
+template <int LOGN, int LA = 0, int GROUP = 2>
+__global__ __launch_bounds__(ColFirstCfg<LOGN>::WG1) void k_cols_to_blocks(int images, const float4* __restrict__ src_images,
+                                                                          float4* __restrict__ work,
+                                                                          const float2* __restrict__ tw_glob)
+{
+  using S = FftShape<LOGN>;
+  using K = ColFirstCfg<LOGN>;
+  constexpr int N = S::N, T = S::T, B = K::B, SPW = K::SPW;
+  static_assert(SPW == 1, "one strip per item");
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  float2* tw = reinterpret_cast<float2*>(smem);
+  void* xch = smem + ((S::TW_ENTRIES * 8 + 15) / 16) * 16;
+  load_twiddles<LOGN>(tw, tw_glob);
+  const int strips = N / B;
+  const int total = images * strips;
+  // adjacent strips (the two 64-B halves of each 128-B line) on blocks b, b+8: one XCD, one L2
+  for (int item = xcd_group_slot<GROUP>(blockIdx.x, gridDim.x); item < total; item += gridDim.x)
+  {
+    const int tid = opaque((int)threadIdx.x);
+    const int b = tid % B, i = (tid / B) % T;
+    const int img = item / strips, xb = item - img * strips;
+    // row y = i + mm*T of the input, column xb*B + b: uniform base per m, lane offset (i*N + b)*16
+    const float4* src = src_images + ((size_t)img << (2 * LOGN)) + (size_t)xb * B;
+    const int voff = ((i << LOGN) + b) * 16;
+    CPair v[16];
+#pragma unroll
+    for (int m = 0; m < 16; m++)
+      v[m] = to_pair(ld4<LA>(src + ((size_t)(((m + 8) & 15) * T) << LOGN), voff));  // fftShift on y
+    fft_run<LOGN, K::C1, true>(v, i, b, xch, tw);
+    float4* dst = work + ((size_t)img << (2 * LOGN)) + (size_t)xb * N * B;
+    const int soff = (i * B + b) * 16;
+#pragma unroll
+    for (int m = 0; m < 16; m++)
+      st4<kStream>(dst + m * T * B, soff, pair_raw(v[m]));
+  }
+}
+
+// Standalone EncodeIFFT at N >= 8192: the column transform in four steps (N = 16 N2), so that no
+// access is a 16- or 32-byte column piece (one 16384-row column is 256 KiB: an in-place column
+// item holds one or two columns and reads 16-32-B pieces, 1.3-2.8 TB/s). For y index n = N2 n1 + n2
+// and k = k1 + 16 k2:  X[k1 + 16 k2] = sum_n2 W_N2^(n2 k2) [W_N^(n2 k1) sum_n1 x[N2 n1 + n2] W_16^(n1 k1)].
+// Step 1 (this kernel), per (column x, n2): the 16-point inverse DFT over rows N2 n1 + n2 (fftShift
+// on y folded into n1: row (n + N/2) mod N = N2 ((n1 + 8) mod 16) + n2), times W_N^(n2 k1), into the
+// work slab at row N2 k1 + n2, split planes. Lanes run along x: every load and store of a wave is one
+// 1-KiB row piece, and there is no LDS exchange. The work slab holds columns [x0, x0 + wc).
+template <int LOGN>
+__global__ __launch_bounds__(256) void k_cols4_step1(int images, int x0, int wc, const float4* __restrict__ img,
+                                                     float4* __restrict__ work, const float2* __restrict__ tw_glob)
+{
+  using S = FftShape<LOGN>;
+  constexpr int N = S::N, N2 = N / 16;
+  __shared__ float2 tw[S::TW_ENTRIES];
+  load_twiddles<LOGN>(tw, tw_glob);
+  const int xblocks = wc / 64;
+  const int total = images * xblocks * (N2 / 4);
+  for (int item = blockIdx.x; item < total; item += gridDim.x)
+  {
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    int t = item;
+    const int xbk = t % xblocks;
+    t /= xblocks;
+    const int n2 = (t % (N2 / 4)) * 4 + wv, im = t / (N2 / 4);
+    const int xl = xbk * 64 + lane;  // column within the slab
+    const float4* src = img + ((size_t)im << (2 * LOGN)) + x0 + xl;
+    CPair v[16];
+#pragma unroll
+    for (int n1 = 0; n1 < 16; n1++)
+    {
+      const f4v r = __builtin_nontemporal_load(reinterpret_cast<const f4v*>(src + (size_t)(N2 * ((n1 + 8) & 15) + n2) * N));
+      v[n1] = to_pair(make_float4(r.x, r.y, r.z, r.w));
+    }
+    idft16(v);
+    apply_stage_twiddles<LOGN>(v, n2, tw);  // v[k1] *= W_N^(n2 k1)
+    float4* dst = work + (size_t)im * N * wc + xl;
+#pragma unroll
+    for (int k1 = 0; k1 < 16; k1++)
+    {
+      const float4 o = pair_raw(v[k1]);
+      __builtin_nontemporal_store(f4v{o.x, o.y, o.z, o.w}, reinterpret_cast<f4v*>(dst + (size_t)(N2 * k1 + n2) * wc));
+    }
+  }
+}
+
+// Step 2, per (image, k1, strip of C slab columns): the N2-point inverse FFT along the work slab's
+// contiguous rows N2 k1 + n2 (n2 = i + m T), output X[k1 + 16 k2] to image row k1 + 16 k2 in the
+// reference layout. Loads and stores are C * 16 = 256-byte row pieces. tw_glob: the N2-point table.
+template <int LOGN2>
+__global__ __launch_bounds__(ColCfg<LOGN2>::WG) void k_cols4_step2(int images, int x0, int wc,
+                                                                 const float4* __restrict__ work, float4* __restrict__ img,
+                                                                 const float2* __restrict__ tw_glob)
+{
+  using S = FftShape<LOGN2>;
+  using K = ColCfg<LOGN2>;
+  constexpr int N2 = S::N, T = S::T, C = K::C, LOGN = LOGN2 + 4, N = N2 * 16;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  float2* tw = reinterpret_cast<float2*>(smem);
+  void* xch = smem + ((S::TW_ENTRIES * 8 + 15) / 16) * 16;
+  load_twiddles<LOGN2>(tw, tw_glob);
+  const int c0 = threadIdx.x % C, i0 = threadIdx.x / C;
+  const int strips = wc / C;
+  const int total = images * 16 * strips;
+  for (int item = blockIdx.x; item < total; item += gridDim.x)
+  {
+    const int c = opaque(c0), i = opaque(i0);
+    const int strip = item % strips, rest = item / strips, k1 = rest & 15, im = rest >> 4;
+    const int xl = strip * C + c;
+    const float4* src = work + (size_t)im * N * wc + (size_t)N2 * k1 * wc + xl;
+    CPair v[16];
+#pragma unroll
+    for (int m = 0; m < 16; m++)
+    {
+      const f4v r = __builtin_nontemporal_load(reinterpret_cast<const f4v*>(src + (size_t)(i + m * T) * wc));
+      v[m] = raw_pair(make_float4(r.x, r.y, r.z, r.w));
+    }
+    fft_run<LOGN2, C, true>(v, i, c, xch, tw);
+    float4* dst = img + ((size_t)im << (2 * LOGN)) + (size_t)k1 * N + x0 + xl;
+#pragma unroll
+    for (int m = 0; m < 16; m++)
+    {
+      const float4 o = from_pair(v[m]);
+      __builtin_nontemporal_store(f4v{o.x, o.y, o.z, o.w},
+                                  reinterpret_cast<f4v*>(dst + (size_t)16 * (i + m * T) * N));
+    }
+  }
+}
+
+}  // namespace oceanfft

@@ -162,4 +162,13 @@ __device__ __forceinline__ float2 spectrum_amplitude(const SpectrumConsts& q, fl
   return make_float2(q.c * (rad * cs) * amp, q.c * (rad * sn) * amp);
 }
 
+// One h0 texel evaluated in place: (h0(k), conj(h0(-k))), -k at index N - i
+// (spectrum.compute:160-168), with the evaluator and arguments of k_generate_spectrum(_pairs) (ocean_kernels.hip).
+__device__ __forceinline__ float4 seed_texel(const SpectrumConsts& q, int x, int y, float dim)
+{
+  const float2 a = spectrum_amplitude(q, (float)x, (float)y);
+  const float2 c = spectrum_amplitude(q, dim - (float)x, dim - (float)y);
+  return make_float4(a.x, a.y, c.x, -c.y);
+}
+
 }  // namespace oceanfft

@@ -1,0 +1,103 @@
+// launch_common.h — host-side launch helpers shared by the kernel translation units: dispatch on
+// log2 N, and grid sizing (one-shot grids on the whole device, persistent grids under a CU budget).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <mutex>
+#include <type_traits>
+#include <vector>
+
+namespace oceanfft
+{
+
+// LDS bytes of the twiddle table of an N = 2^LOGN transform, rounded to 16 B (the exchange follows it)
+template <int TW_ENTRIES>
+constexpr int tw_bytes() { return ((TW_ENTRIES * 8 + 15) / 16) * 16; }
+
+template <typename F>
+inline hipError_t with_logn(int logn, F&& f)
+{
+  switch (logn)
+  {
+  case 4: return f(std::integral_constant<int, 4>{});
+  case 5: return f(std::integral_constant<int, 5>{});
+  case 6: return f(std::integral_constant<int, 6>{});
+  case 7: return f(std::integral_constant<int, 7>{});
+  case 8: return f(std::integral_constant<int, 8>{});
+  case 9: return f(std::integral_constant<int, 9>{});
+  case 10: return f(std::integral_constant<int, 10>{});
+  case 11: return f(std::integral_constant<int, 11>{});
+  case 12: return f(std::integral_constant<int, 12>{});
+  case 13: return f(std::integral_constant<int, 13>{});
+  case 14: return f(std::integral_constant<int, 14>{});
+  default: return hipErrorInvalidValue;
+  }
+}
+
+// Grid sizing. With the whole device available (cus >= the device's CUs) every kernel with an item
+// loop gets a one-shot grid, one block per work item: the hardware dispatcher then hands items out
+// in order, so the blocks in flight at any time work on neighbouring items (adjacent strips share
+// 128-B lines in L2, rows stream through neighbouring DRAM pages). Measured against persistent grids
+// (resident blocks x CUs, same kernels; tools/microbench/gridbench, profiles/r02_gridbench.log):
+// row pass 1.513 -> 1.453 ms, EncodeIFFT strided pass 1.115 -> 0.927 ms, 16384 column pass 6.69 ->
+// 5.56 ms. Under a CU budget (ocean_fft_set_cu_budget: CUs left free for RCCL's copy kernels in
+// the slab pipeline) grids stay persistent, so at most `cus` CUs' worth of blocks exist. Kernels
+// with per-block scratch (the H scratch of the half-spectrum column pass) cap the grid themselves.
+// The occupancy query and the dynamic-LDS attribute are set once per kernel instantiation (host API
+// calls cost microseconds; a frame is two launches).
+inline int device_cu_count()
+{
+  static const int n = [] {
+    int dev = 0, c = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+      return 0;
+    return c;
+  }();
+  return n;
+}
+
+inline bool g_force_persistent = false;  // tools/microbench A/B only
+
+inline bool one_shot_grids(int cus)
+{
+  const int d = device_cu_count();
+  return !g_force_persistent && d > 0 && cus >= d;
+}
+
+struct LaunchCacheEntry
+{
+  const void* kernel;
+  int lds;
+  int per_cu;
+};
+
+template <typename K>
+int persistent_grid(K kernel, int wg, int lds, int items, int cus)
+{
+  static std::mutex mu;
+  static std::vector<LaunchCacheEntry> cache;
+  int per_cu = -1;
+  {
+    std::lock_guard<std::mutex> lock(mu);
+    for (const auto& e : cache)
+      if (e.kernel == (const void*)kernel && e.lds == lds)
+        per_cu = e.per_cu;
+    if (per_cu < 0)
+    {
+      per_cu = 0;
+      (void)hipFuncSetAttribute((const void*)kernel, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+      if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, wg, lds) != hipSuccess || per_cu < 1)
+        per_cu = 1;
+      cache.push_back({(const void*)kernel, lds, per_cu});
+    }
+  }
+  if (one_shot_grids(cus))
+    return items < 1 ? 1 : items;
+  long g = (long)per_cu * cus;
+  if (g > items)
+    g = items;
+  return g < 1 ? 1 : (int)g;
+}
+
+}  // namespace oceanfft

@@ -1,0 +1,230 @@
+// launch_fft.hip — the standalone EncodeIFFT (src/FFTCalculator.cpp:73-114) on caller-owned
+// row-major images, and the full-spectrum generator frame (116 B per point). Kernels:
+// device/k_fft.h, device/k_full.h.
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "ocean_internal.h"
+#include "launch_common.h"
+#include "device/fft.h"
+#include "device/grid.h"
+#include "device/k_fft.h"
+#include "device/k_full.h"
+#include "device/memory.h"
+
+namespace oceanfft
+{
+
+template <int LOGN>
+int lds_bytes_rows()
+{
+  using S = FftShape<LOGN>;
+  return ((S::TW_ENTRIES * 8 + 15) / 16) * 16 + RowCfg<LOGN>::LDS_BYTES;
+}
+template <int LOGN>
+int lds_bytes_cols()
+{
+  using S = FftShape<LOGN>;
+  return ((S::TW_ENTRIES * 8 + 15) / 16) * 16 + ColCfg<LOGN>::LDS_BYTES;
+}
+
+
+// B == 1 (N = 16384: one 256-KiB column per CU) makes the blocked layout column-major, whose rows
+// the row pass could only read 16 bytes at a time. This tiled transpose (64 x 64 texels through
+// LDS, 1-KiB runs on both sides) turns inter[c][src][img][x_local][y] into row-major
+// out[c][img][y][x] for the rank's w rows.
+__global__ __launch_bounds__(256) void k_blocks_to_rows(int cascades, int n, int w, const float4* __restrict__ in,
+                                                        float4* __restrict__ out)
+{
+  __shared__ float4 tile[64][65];
+  const int tiles_x = n / 64, tiles_y = w / 64;
+  const int total = cascades * 2 * tiles_x * tiles_y;
+  for (int item = blockIdx.x; item < total; item += gridDim.x)
+  {
+    const int cimg = item / (tiles_x * tiles_y), t = item % (tiles_x * tiles_y);
+    const int c = cimg >> 1, img = cimg & 1;
+    const int tx = t % tiles_x, ty = t / tiles_x;
+    // read: 64 columns x 64 rows; column x is contiguous in y
+    for (int k = 0; k < 16; k++)
+    {
+      const int L = k * 256 + threadIdx.x, col = L >> 6, row = L & 63;
+      const int x = tx * 64 + col, srcr = x / w, xl = x % w;
+      tile[col][row] = in[(size_t)c * 2 * n * w + ((size_t)(srcr * 2 + img) * w + xl) * w + ty * 64 + row];
+    }
+    __syncthreads();
+    for (int k = 0; k < 16; k++)
+    {
+      const int L = k * 256 + threadIdx.x, row = L >> 6, col = L & 63;
+      out[((size_t)cimg * w + ty * 64 + row) * n + tx * 64 + col] = tile[col][row];
+    }
+    __syncthreads();
+  }
+}
+
+hipError_t launch_cols_evolve(int logn, const FrameParams& fp, const SlabGeom& g, const float4* h0, float4* inter,
+                              const float2* tw, hipStream_t stream, int cus, int keep)
+{
+  return with_logn(logn, [&](auto L) -> hipError_t {
+    constexpr int LOGN = decltype(L)::value;
+    using K = ColFirstCfg<LOGN>;
+    using S = FftShape<LOGN>;
+    auto kern = keep >= 16 ? k_cols_evolve<LOGN, 16>
+                           : (keep >= 8 ? k_cols_evolve<LOGN, 8> : (keep >= 4 ? k_cols_evolve<LOGN, 4> : k_cols_evolve<LOGN, 0>));
+    const int lds = ((S::TW_ENTRIES * 8 + 15) / 16) * 16 + K::LDS1;
+    const int items = fp.cascades * ((g.w / K::B) / K::SPW);
+    const int grid = persistent_grid(kern, K::WG1, lds, items, cus);
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(K::WG1), lds, stream, fp, g, h0, inter, tw);
+    return hipGetLastError();
+  });
+}
+
+bool ifft_fourstep_supported(int logn) { return fourstep_table(logn); }
+
+size_t ifft_fourstep_work_texels(int logn, int wc) { return ((size_t)1 << logn) * (size_t)wc; }
+
+// Rows in place, then per slab of wc columns: step 1 (images -> work slab), step 2 (slab -> images).
+// Bytes: 3 x 32 per texel (the in-place order: 2 x 32, but its column pass reads and writes 16-B
+// pieces at N = 16384). Measured (tools/microbench/ifft4bench, profiles/r02_ifft4bench.log), one
+// 16384^2 image: in place 7.26 ms, four-step 5.05 ms (wc 2048); at 8192 the in-place order (two
+// columns per item, 32-B pieces) stays ahead, 4.78 vs 4.96 ms for 4 images.
+
+hipError_t launch_ifft_fourstep(int logn, int n_images, float4* images, float4* work, int wc, const float2* tw,
+                                const float2* tw2, hipStream_t stream, int cus)
+{
+  if (!ifft_fourstep_supported(logn) || !tw2)
+    return hipErrorInvalidValue;
+  const int n = 1 << logn;
+  if (wc < 64 || wc > n || n % wc != 0 || (wc & 63) != 0)
+    return hipErrorInvalidValue;
+  hipError_t e = launch_rows_ifft(logn, n_images, images, tw, stream, cus);
+  if (e != hipSuccess)
+    return e;
+  return with_logn(logn, [&](auto L) -> hipError_t {
+    constexpr int LOGN = decltype(L)::value;
+    if constexpr (LOGN < 13)
+      return hipErrorInvalidValue;
+    else
+    {
+      constexpr int LOGN2 = LOGN - 4;
+      using K2 = ColCfg<LOGN2>;
+      auto k1 = k_cols4_step1<LOGN>;
+      auto k2 = k_cols4_step2<LOGN2>;
+      const int lds2 = lds_bytes_cols<LOGN2>();
+      for (int im = 0; im < n_images; im++)
+        for (int x0 = 0; x0 < n; x0 += wc)
+        {
+          float4* img = images + ((size_t)im << (2 * LOGN));
+          const int g1 = persistent_grid(k1, 256, 0, (wc / 64) * ((n / 16) / 4), cus);
+          hipLaunchKernelGGL(k1, dim3(g1), dim3(256), 0, stream, 1, x0, wc, img, work, tw);
+          const int g2 = persistent_grid(k2, K2::WG, lds2, 16 * (wc / K2::C), cus);
+          hipLaunchKernelGGL(k2, dim3(g2), dim3(K2::WG), lds2, stream, 1, x0, wc, work, img, tw2);
+          const hipError_t le = hipGetLastError();
+          if (le != hipSuccess)
+            return le;
+        }
+      return hipSuccess;
+    }
+  });
+}
+
+bool ifft_colfirst_supported(int logn) { return logn == 12; }
+
+hipError_t launch_ifft_colfirst(int logn, int n_images, float4* images, float4* work, const float2* tw,
+                                hipStream_t stream, int cus)
+{
+  if (!ifft_colfirst_supported(logn))
+    return hipErrorInvalidValue;
+  constexpr int LOGN = 12;
+  using K = ColFirstCfg<LOGN>;
+  using S = FftShape<LOGN>;
+  const int tw_bytes = ((S::TW_ENTRIES * 8 + 15) / 16) * 16;
+  {
+    auto kern = k_cols_to_blocks<LOGN>;
+    const int lds = tw_bytes + K::LDS1;
+    const int grid = persistent_grid(kern, K::WG1, lds, n_images * (S::N / K::B), cus);
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(K::WG1), lds, stream, n_images, images, work, tw);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess)
+      return e;
+  }
+  auto kern = k_rows_final<LOGN, true>;
+  const int lds = tw_bytes + K::LDS2;
+  const SlabGeom g{0, S::N};
+  const int grid = persistent_grid(kern, K::WG2, lds, n_images * (S::N / K::RPW2), cus);
+  hipLaunchKernelGGL(kern, dim3(grid), dim3(K::WG2), lds, stream, n_images, g, work, images, (float*)nullptr,
+                     FoamParams{}, tw);
+  return hipGetLastError();
+}
+
+hipError_t launch_rows_final(int logn, int cascades, const SlabGeom& g, const float4* inter, float4* scratch,
+                             float4* maps, float* jac, const FoamParams& foam, const float2* tw, hipStream_t stream,
+                             int cus)
+{
+  const bool transpose = rows_need_transpose(logn) && scratch != nullptr;
+  if (transpose)
+  {
+    const int n = 1 << logn;
+    const int items = cascades * 2 * (n / 64) * (g.w / 64);
+    const int grid = persistent_grid(k_blocks_to_rows, 256, 0, items, cus);
+    hipLaunchKernelGGL(k_blocks_to_rows, dim3(grid), dim3(256), 0, stream, cascades, n, g.w, inter, scratch);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess)
+      return e;
+  }
+  return with_logn(logn, [&](auto L) -> hipError_t {
+    constexpr int LOGN = decltype(L)::value;
+    using K = ColFirstCfg<LOGN>;
+    using S = FftShape<LOGN>;
+    const int lds = ((S::TW_ENTRIES * 8 + 15) / 16) * 16 + K::LDS2;
+    const int items = cascades * 2 * (g.w / K::RPW2);
+    if (transpose)
+    {
+      auto kern = k_rows_final<LOGN, false>;
+      const int grid = persistent_grid(kern, K::WG2, lds, items, cus);
+      hipLaunchKernelGGL(kern, dim3(grid), dim3(K::WG2), lds, stream, 2 * cascades, g, scratch, maps, jac, foam, tw);
+    }
+    else
+    {
+      auto kern = k_rows_final<LOGN, true>;
+      const int grid = persistent_grid(kern, K::WG2, lds, items, cus);
+      hipLaunchKernelGGL(kern, dim3(grid), dim3(K::WG2), lds, stream, 2 * cascades, g, inter, maps, jac, foam, tw);
+    }
+    return hipGetLastError();
+  });
+}
+
+hipError_t launch_rows_ifft_rows(int logn, int rows, float4* data, const float2* tw, hipStream_t stream, int cus)
+{
+  return with_logn(logn, [&](auto L) -> hipError_t {
+    constexpr int LOGN = decltype(L)::value;
+    using R = RowCfg<LOGN>;
+    auto kern = k_rows_ifft<LOGN>;
+    int lds = lds_bytes_rows<LOGN>();
+    int items = (rows + R::RPW - 1) / R::RPW;
+    int grid = persistent_grid(kern, R::WG, lds, items, cus);
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(R::WG), lds, stream, rows, data, tw);
+    return hipGetLastError();
+  });
+}
+
+hipError_t launch_rows_ifft(int logn, int n_images, float4* images, const float2* tw, hipStream_t stream, int cus)
+{
+  return launch_rows_ifft_rows(logn, n_images << logn, images, tw, stream, cus);
+}
+
+hipError_t launch_cols(int logn, int n_images, float4* images, const float2* tw, hipStream_t stream, int cus)
+{
+  return with_logn(logn, [&](auto L) -> hipError_t {
+    constexpr int LOGN = decltype(L)::value;
+    using K = ColCfg<LOGN>;
+    int lds = lds_bytes_cols<LOGN>();
+    int items = n_images * K::STRIPS;
+    auto kern = k_cols<LOGN>;
+    int grid = persistent_grid(kern, K::WG, lds, items, cus);
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(K::WG), lds, stream, n_images, images, tw);
+    return hipGetLastError();
+  });
+}
+
+}  // namespace oceanfft

@@ -1,0 +1,105 @@
+// launch_half.hip — the half-spectrum generator frame of whole grids, N = 1024 .. 4096 (84 B per
+// point): k_cols_half (evolve + y iFFT of the five field multiples of H over the kept
+// columns) and k_rows_half (Hermitian rebuild + x iFFT + maps + Jacobian). Kernels:
+// device/k_half_cols.h, device/k_half_rows.h. The A/B variants measured against these live in
+// tools/microbench/ab_kernels.h, outside the library.
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "ocean_internal.h"
+#include "launch_common.h"
+#include "device/grid.h"
+#include "device/k_half_cols.h"
+#include "device/k_half_rows.h"
+#include "device/spectrum.h"
+
+namespace oceanfft
+{
+
+bool half_spectrum_supported(int logn) { return logn >= 10 && logn <= 12; }
+
+size_t half_field_texels(int logn)
+{
+  const size_t n = (size_t)1 << logn;
+  return (n / 8 + 1) * n * 4;  // HalfCfg: STRIPS * N * B per cascade (B = 4)
+}
+
+size_t half_hs_bytes(int logn, int blocks)
+{
+  return half_slab_supported(logn) ? (size_t)blocks * 16 * 1024 * sizeof(float2) : 0;  // WG1 <= 1024
+}
+
+hipError_t launch_half_columns(int logn, const FrameParams& fp, const float4* h0, float4* gab, float4* gcd, float2* ge,
+                               float4* spec, const float2* tw, hipStream_t stream, int cus, float2* hs, int hs_blocks,
+                               const void* seed_consts)
+{
+  if (!hs)  // the H scratch (half_hs_bytes): H evolved once per item instead of once per field round
+    return hipErrorInvalidValue;
+  const SpectrumConsts* seed = static_cast<const SpectrumConsts*>(seed_consts);
+  return with_logn(logn, [&](auto L) -> hipError_t {
+    constexpr int LOGN = decltype(L)::value;
+    if constexpr (!HalfCfg<LOGN>::SUPPORTED)
+      return hipErrorInvalidValue;
+    else
+    {
+      using K = ColFirstCfg<LOGN>;
+      using S = FftShape<LOGN>;
+      // the Nyquist-row term: one row spectrum per image
+      hipError_t e = launch_half_nyquist(fp, S::N, K::B, h0, spec, nullptr, 1, 0, seed, stream, cus);
+      if (e != hipSuccess)
+        return e;
+      // Field layout: row groups (kHalfRG, kHalfRGC). The H scratch in 16-B pairs (HP), one pair per
+      // thread in the LDS the exchange leaves free (kHalfHL) and kHalfHK pairs in VGPRs at 4096 (2
+      // below: 128 VGPRs, so two (2048) or four (1024) workgroups share a CU). h0 is read once per
+      // item, streamed (nt), which leaves the XCD's L2 to the scratch. The fused re-seed frame (seed)
+      // evaluates h0 in round 0 and keeps kHalfHKSeed pairs in VGPRs.
+      constexpr int RG = kHalfRG, RGC = kHalfRGC;
+      constexpr int HKW = LOGN == 12 ? kHalfHK : 2;
+      auto kern = seed ? k_cols_half<LOGN, 0, kStream, true, false, true, RG, RGC, K::B, true, false, kHalfHL, kHalfHKSeed>
+                       : k_cols_half<LOGN, kStream, kStream, true, false, false, RG, RGC, K::B, true, false, kHalfHL, HKW>;
+      const int lds = ((S::TW_ENTRIES * 8 + 15) / 16) * 16 + K::LDS1 + kHalfHL * K::WG1 * 16;
+      int grid = persistent_grid(kern, K::WG1, lds, fp.cascades * HalfCfg<LOGN>::STRIPS, cus);
+      // hs holds hs_blocks slices for 1024-thread workgroups (half_hs_bytes); a block uses 16 x WG1
+      // entries, so below 4096 each slice serves 1024 / WG1 blocks
+      const int slices = hs_blocks * (1024 / K::WG1);
+      if (grid > slices)
+        grid = slices;
+      if (grid < 1)
+        return hipErrorInvalidValue;
+      hipLaunchKernelGGL(kern, dim3(grid), dim3(K::WG1), lds, stream, fp, h0, gab, gcd, ge, tw, hs, HalfSlab{},
+                         (unsigned char*)nullptr, 1, seed);  // gcd/ge: (D, E) / C
+      return hipGetLastError();
+    }
+  });
+}
+
+hipError_t launch_half_rows(int logn, const FrameParams& fp, const float4* gab, const float4* gcd, const float2* ge,
+                            const float4* rcorr, float4* maps, float* jac, const FoamParams& foam, const float2* tw,
+                            hipStream_t stream, int cus)
+{
+  return with_logn(logn, [&](auto L) -> hipError_t {
+    constexpr int LOGN = decltype(L)::value;
+    if constexpr (!HalfCfg<LOGN>::SUPPORTED)
+      return hipErrorInvalidValue;
+    else
+    {
+      using S = FftShape<LOGN>;
+      // One item = both images of its rows (C loaded once, kept in VGPRs for image 1); loads use the
+      // default policy so the gc lines shared by neighbouring items survive until the partner's read
+      // (streamed loads: -5 %, tools/microbench/halfbench). At N = 4096 one row per 256-thread
+      // workgroup, four per CU, the 4 rows of a gc line grouped on one XCD: 1.407 -> 1.377 ms per
+      // 8 x 4096^2 against two-row workgroups (halfbench rowv 16), which stay below 4096.
+      constexpr int RG = kHalfRG, RGC = kHalfRGC;
+      constexpr int RPW = LOGN == 12 ? 1 : 2, GRP = LOGN == 12 ? 4 : 2;
+      auto kern = k_rows_half<LOGN, 0, kStream, 0, RPW, true, false, RG, RGC, 4, GRP>;
+      const int lds = ((S::TW_ENTRIES * 8 + 15) / 16) * 16 + lds_row_slots<LOGN>(RPW) * 8;
+      const int grid = persistent_grid(kern, S::T * RPW, lds, fp.cascades * (S::N / RPW), cus);
+      hipLaunchKernelGGL(kern, dim3(grid), dim3(S::T * RPW), lds, stream, fp, gab, gcd, ge, rcorr, maps, jac, foam, tw,
+                         S::N, RowSrc{}, (const float2*)nullptr);
+      return hipGetLastError();
+    }
+  });
+}
+
+}  // namespace oceanfft

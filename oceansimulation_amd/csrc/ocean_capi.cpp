@@ -66,7 +66,8 @@ struct ocean_fft
   int device_cus = 0;  // CUs of the device
   int cus = 0;         // CU budget persistent grids are sized for (ocean_fft_set_cu_budget)
   hipStream_t stream = nullptr;
-  float2* twiddles = nullptr;  // two-level table, see FftShape in ocean_kernels.hip
+  float2* twiddles = nullptr;  // two-level table, see FftShape in device/fft.h
+  float2* tw2 = nullptr;       // the N/16-point table after it (fourstep_table sizes), else null
   float4* work = nullptr;      // column-first EncodeIFFT work image (the reference's workImage)
   int work_images = 0;
   size_t work_texels = 0;      // four-step EncodeIFFT (N = 16384): work slab of N x kFourStepSlab texels
@@ -97,23 +98,26 @@ struct ocean_generator
   float4* gcd = nullptr;  // (kz H/|k|, kz^2 H/|k|)
   float2* ge = nullptr;   // H/|k|
   float4* spec = nullptr; // [cascade][2][N]: the Nyquist-row term R
-  // strip-dealt half-spectrum path (slabs of N >= 1024, whole grids of N = 8192 / 16384)
+  // half-spectrum paths of slabs (N >= 1024) and of whole grids of N = 8192 / 16384: the four-step
+  // column pass (gen4, N = 8192 / 16384, default) or the strip-dealt one (hsl)
   bool hslab = false;
   bool slab = false;  // created by ocean_generator_create_slab (also with ranks == 1)
   HalfSlab hsl{};
+  Gen4Geom g4{};
   float4* h0row = nullptr;                            // slabs: [cascade][N], row y = 0 of every column
-  float4* rm_ab = nullptr;                            // row-major fields [cascade][w][kp] after the exchange
+  float4* rm_ab = nullptr;                            // strip-dealt: row-major fields [cascade][w][kp] after the exchange
   float4* rm_de = nullptr;
   float2* rm_c = nullptr;
+  unsigned char* parts = nullptr;                     // four-step: step 1's output [field][cascade][N][lp]
   unsigned char* xbuf = nullptr;                      // internal exchange buffer (ranks == 1, or null send/recv)
+  size_t xbuf_bytes = 0;
   // fused re-seed frames (blocked half path): h0 evaluated inside pass 1, the h0 image left stale
   void* seedc = nullptr;                 // device: one seed_consts record per cascade
   std::vector<unsigned char> seedc_host; // what seedc holds
   bool h0_stale = false;                 // the h0 image is not written yet (materialise_h0)
   std::vector<ocean_settings> seed_settings;  // the settings the last fused re-seed evaluated
-  // whole grids of N = 8192 / 16384 on one rank (strip-dealt P = 1): column pass in four steps
-  // (launch_gen4_columns / _rows) instead of the dealt column pass + transposes; off: the dealt path
-  // that slabs of P > 1 run (bit-identical to them). ocean_generator_set_four_step.
+  // N = 8192 / 16384: the four-step column pass writing destination-block order (launch_gen4_columns
+  // / _rows); off: the strip-dealt column pass + transposes. ocean_generator_set_four_step.
   bool four_step = true;
   int h0_block = 0;                          // strip width the h0 image was last written with
   std::vector<ocean_settings> h0_settings;   // the settings it was written from
@@ -211,7 +215,8 @@ int ocean_fft_create(ocean_fft** out, size_t texture_size, void* hip_stream)
     }
   };
   append_table(logn);
-  if (ifft_fourstep_supported(logn))
+  const size_t tw2_at = tab.size();
+  if (fourstep_table(logn))
     append_table(logn - 4);
   e = hipMalloc(&f->twiddles, tab.size() * sizeof(float2));
   if (e == hipSuccess)
@@ -223,6 +228,8 @@ int ocean_fft_create(ocean_fft** out, size_t texture_size, void* hip_stream)
     delete f;
     return hip_fail(e, "ocean_fft_create: twiddle table");
   }
+  if (fourstep_table(logn))
+    f->tw2 = f->twiddles + tw2_at;
   *out = f;
   return OCEAN_OK;
 }
@@ -310,8 +317,8 @@ int ocean_fft_encode_ifft_batch(ocean_fft* fft, float* images, int n_images)
     }
     if (fft->work_texels >= want)
     {
-      HIP_TRY(launch_ifft_fourstep(fft->logn, n_images, img, fft->work, kFourStepSlab, fft->twiddles,
-                                   fft->twiddles + twiddle_entries(fft->logn), fft->stream, fft->cus),
+      HIP_TRY(launch_ifft_fourstep(fft->logn, n_images, img, fft->work, kFourStepSlab, fft->twiddles, fft->tw2,
+                                   fft->stream, fft->cus),
               "four-step EncodeIFFT");
       return OCEAN_OK;
     }
@@ -403,7 +410,7 @@ static HalfSlab half_slab_geom(int logn, int rank, int ranks)
 
 static bool uses_gen4(const ocean_generator* g)
 {
-  return g->four_step && g->hslab && g->ranks == 1 && gen4_supported(g->fft->logn);
+  return g->four_step && g->hslab && gen4_supported(g->fft->logn);
 }
 
 // strip width of the h0 image the current frame path reads
@@ -412,42 +419,62 @@ static int h0_block(const ocean_generator* g)
   return uses_gen4(g) ? gen4_h0_block() : spectrum_block(g->fft->logn);
 }
 
+// h0 texels per cascade: the whole grid (ranks == 1), or the largest of a slab's layouts (its column
+// slab, its dealt strips, its four-step columns blocked 64 wide), so switching paths needs no reallocation
 static size_t h0_texels(const ocean_generator* g)
 {
   const size_t full = (size_t)g->fft->n * g->geom.w;  // the full path's column slab (whole grid: N^2)
   if (g->ranks == 1)
     return full;
   const size_t strips = (size_t)g->hsl.nstrips * spectrum_block(g->fft->logn) * g->fft->n;
-  return std::max(full, strips);
+  size_t t = std::max(full, strips);
+  if (gen4_supported(g->fft->logn))
+    t = std::max(t, g->g4.h0_cstride);
+  return t;
 }
-
-// ranks == 1 at 8192 / 16384 may run either column pass (ocean_generator_set_four_step): the
-// buffers take the larger of the two layouts
-static bool gen4_eligible(const ocean_generator* g) { return g->ranks == 1 && gen4_supported(g->fft->logn); }
 
 static size_t hslab_xbuf_bytes(const ocean_generator* g)
 {
-  const size_t dealt = (size_t)g->ranks * half_slab_block_bytes(g->fft->logn, g->cascades, g->hsl);
-  return gen4_eligible(g) ? std::max(dealt, gen4_buffer_bytes(g->fft->logn, g->cascades)) : dealt;
+  if (uses_gen4(g))
+    return (size_t)g->ranks * g->g4.blk_bytes;
+  return (size_t)g->ranks * half_slab_block_bytes(g->fft->logn, g->cascades, g->hsl);
 }
 
+// The buffers of the current half-spectrum slab path (allocated when the path is first used; a path
+// switch keeps the other path's buffers). Four-step: step 1's parts and the exchange blocks (ranks ==
+// 1: one block, read back by the row pass). Strip-dealt: the row-major fields and the H scratch.
 static hipError_t hslab_buffers(ocean_generator* g)
 {
   const int logn = g->fft->logn, C = g->cascades;
-  size_t rt = half_slab_row_texels(logn, C, g->hsl.w);
-  if (gen4_eligible(g))
-    rt = std::max(rt, gen4_row_texels(logn, C));
   hipError_t e = hipSuccess;
-  if (!g->rm_ab)
-    e = hipMalloc(&g->rm_ab, rt * sizeof(float4));
-  if (e == hipSuccess && !g->rm_de)
-    e = hipMalloc(&g->rm_de, rt * sizeof(float4));
-  if (e == hipSuccess && !g->rm_c)
-    e = hipMalloc(&g->rm_c, rt * sizeof(float2));
-  if (e == hipSuccess && !g->xbuf)
-    e = hipMalloc(&g->xbuf, hslab_xbuf_bytes(g));
-  if (e == hipSuccess && !g->hs)
-    e = hipMalloc(&g->hs, half_hs_bytes(logn, g->fft->device_cus));
+  if (uses_gen4(g))
+  {
+    if (!g->parts)
+      e = hipMalloc(&g->parts, gen4_parts_bytes(logn, C, g->g4));
+  }
+  else
+  {
+    const size_t rt = half_slab_row_texels(logn, C, g->hsl.w);
+    if (!g->rm_ab)
+      e = hipMalloc(&g->rm_ab, rt * sizeof(float4));
+    if (e == hipSuccess && !g->rm_de)
+      e = hipMalloc(&g->rm_de, rt * sizeof(float4));
+    if (e == hipSuccess && !g->rm_c)
+      e = hipMalloc(&g->rm_c, rt * sizeof(float2));
+    if (e == hipSuccess && !g->hs)
+      e = hipMalloc(&g->hs, half_hs_bytes(logn, g->fft->device_cus));
+  }
+  const size_t xb = hslab_xbuf_bytes(g);
+  if (e == hipSuccess && g->xbuf_bytes < xb)
+  {
+    if (g->xbuf)
+      (void)hipFree(g->xbuf);
+    g->xbuf = nullptr;
+    g->xbuf_bytes = 0;
+    e = hipMalloc(&g->xbuf, xb);
+    if (e == hipSuccess)
+      g->xbuf_bytes = xb;
+  }
   if (e == hipSuccess && g->ranks > 1 && !g->h0row)
     e = hipMalloc(&g->h0row, (size_t)C * g->fft->n * sizeof(float4));
   return e;
@@ -483,6 +510,8 @@ static int generator_alloc(ocean_generator** out, ocean_fft* fft, int cascades, 
   g->half = g->half && !is_slab;
   g->hslab = !g->half && half_slab_supported(fft->logn) && (is_slab || fft->logn > 12);
   g->hsl = half_slab_geom(fft->logn, rank, ranks);
+  if (gen4_supported(fft->logn))
+    g->g4 = gen4_geom(fft->logn, cascades, rank, ranks, ranks == 1);
   hipError_t e = hipMalloc(&g->h0, h0_texels(g) * cascades * sizeof(float4));
   if (e == hipSuccess && !g->half && !g->hslab)
     e = full_buffers(g);
@@ -561,7 +590,7 @@ int ocean_generator_destroy(ocean_generator* g)
   if (g->jac)
     (void)hipFree(g->jac);
   for (void* p : {(void*)g->gab, (void*)g->gcd, (void*)g->ge, (void*)g->spec, (void*)g->hs, (void*)g->h0row, g->seedc,
-                  (void*)g->rm_ab, (void*)g->rm_de, (void*)g->rm_c, (void*)g->xbuf})
+                  (void*)g->rm_ab, (void*)g->rm_de, (void*)g->rm_c, (void*)g->parts, (void*)g->xbuf})
     if (p)
       (void)hipFree(p);
   delete g;
@@ -595,6 +624,25 @@ static int generate_spectrum_with(ocean_generator* g, const std::vector<ocean_se
   {
     OceanSettings s;
     std::memcpy(&s, &settings[c], sizeof(s));
+    if (uses_gen4(g) && g->ranks > 1)
+    {
+      // this rank's kept columns x = N/2 + u0 .. (blocked 64 wide), rank P - 1 also the block of
+      // x = 0 .. 63 (the Nyquist column x = 0 is its first); plus row 0 of every column
+      const Gen4Geom& q = g->g4;
+      float4* base = g->h0 + q.h0_cstride * c;
+      HIP_TRY(timed(g, 0, [&] {
+                hipError_t e = launch_generate_spectrum(s, f->n, base + q.h0_reg, f->stream, f->cus,
+                                                        f->n / 2 + q.u0, q.cols, gen4_h0_block());
+                if (e == hipSuccess && q.nyq)
+                  e = launch_generate_spectrum(s, f->n, base + q.h0_nyq, f->stream, f->cus, 0, gen4_h0_block(),
+                                               gen4_h0_block());
+                if (e == hipSuccess)
+                  e = launch_generate_spectrum_row(s, f->n, g->h0row + (size_t)c * f->n, f->stream);
+                return e;
+              }),
+              "generateSpectrum");
+      continue;
+    }
     if (g->hslab && g->ranks > 1)
     {
       // this rank's strips: the regular ones are columns N/2 + strip*B .. (contiguous), the last
@@ -602,7 +650,7 @@ static int generate_spectrum_with(ocean_generator* g, const std::vector<ocean_se
       const int B = spectrum_block(f->logn), strips = half_strips(f->logn);
       const HalfSlab& h = g->hsl;
       const int nreg = std::max(0, std::min(h.nstrips, strips - 1 - h.strip0));
-      float4* base = g->h0 + (size_t)c * h.nstrips * f->n * B;
+      float4* base = g->h0 + h0_texels(g) * c;
       HIP_TRY(timed(g, 0, [&] {
                 hipError_t e = hipSuccess;
                 if (nreg > 0)
@@ -728,10 +776,17 @@ static int generator_columns(ocean_generator* g, float timestep, int update_spec
     fp.c[c].g = s.g;
     fp.c[c].h = s.h;
   }
+  if (g->hslab)
+  {
+    hipError_t e = hslab_buffers(g);  // the current path's buffers (a path switch allocates here)
+    if (e != hipSuccess)
+      return fail(e == hipErrorOutOfMemory ? OCEAN_ERR_OOM : OCEAN_ERR_HIP,
+                  std::string("column pass buffers: ") + hipGetErrorString(e));
+  }
   if (uses_gen4(g))
     HIP_TRY(timed(g, 1, [&] {
-              return launch_gen4_columns(f->logn, fp, g->h0, out ? (void*)out : (void*)g->xbuf, f->twiddles, f->stream,
-                                         f->cus);
+              return launch_gen4_columns(f->logn, fp, g->g4, g->h0, g->ranks > 1 ? g->h0row : nullptr, g->parts,
+                                         out ? (void*)out : (void*)g->xbuf, f->twiddles, f->tw2, f->stream, f->cus);
             }),
             "column pass (half spectrum, four-step)");
   else if (g->hslab)
@@ -766,16 +821,15 @@ static int generator_rows(ocean_generator* g, const float4* in)
     foam.displacement[c] = g->settings[c].displacement;
   if (uses_gen4(g))
     HIP_TRY(timed(g, 2, [&] {
-              return launch_gen4_rows(f->logn, g->frame, in ? (const void*)in : (const void*)g->xbuf, g->rm_ab, g->rm_de,
-                                      g->rm_c, g->maps, g->jac, foam, f->twiddles, f->twiddles + twiddle_entries(f->logn),
-                                      f->stream, f->cus);
+              return launch_gen4_rows(f->logn, g->frame, g->g4, in ? (const void*)in : (const void*)g->xbuf, g->maps,
+                                      g->jac, foam, f->twiddles, f->tw2, f->stream, f->cus);
             }),
             "row pass (half spectrum, four-step)");
   else if (g->hslab)
     HIP_TRY(timed(g, 2, [&] {
               return launch_half_slab_rows(f->logn, g->frame, g->hsl, in ? (const void*)in : (const void*)g->xbuf,
                                            g->rm_ab, g->rm_de, g->rm_c, g->maps, g->jac, foam, f->twiddles,
-                                           f->stream, f->cus);
+                                           f->tw2, f->stream, f->cus);
             }),
             "row pass (half spectrum, strip-dealt)");
   else if (g->half)
@@ -802,6 +856,9 @@ int ocean_generator_set_half_spectrum(ocean_generator* g, int enable)
   const bool dealt = !blocked && half_slab_supported(logn) && (g->slab || logn > 12);
   if (enable && !blocked && !dealt)
     return fail(OCEAN_ERR_INVALID, "ocean_generator_set_half_spectrum: N = 1024 .. 16384 only");
+  const bool was_half = g->half, was_hslab = g->hslab;
+  g->half = enable && blocked;
+  g->hslab = enable && dealt;
   hipError_t e = hipSuccess;
   if (!enable)
     e = full_buffers(g);
@@ -810,13 +867,14 @@ int ocean_generator_set_half_spectrum(ocean_generator* g, int enable)
   else
     e = hslab_buffers(g);
   if (e != hipSuccess)
+  {
+    g->half = was_half;
+    g->hslab = was_hslab;
     return fail(e == hipErrorOutOfMemory ? OCEAN_ERR_OOM : OCEAN_ERR_HIP,
                 std::string("ocean_generator_set_half_spectrum: ") + hipGetErrorString(e));
-  const bool was_dealt_slab = g->hslab && g->ranks > 1;
-  g->half = enable && blocked;
-  g->hslab = enable && dealt;
-  if (was_dealt_slab != (g->hslab && g->ranks > 1))
-    g->update_spectrum = true;  // a slab's h0 layout changes (strips <-> column slab)
+  }
+  if ((was_hslab && g->ranks > 1) != (g->hslab && g->ranks > 1))
+    g->update_spectrum = true;  // a slab's h0 layout changes (its strips or columns <-> its column slab)
   return OCEAN_OK;
 }
 
@@ -833,6 +891,13 @@ int ocean_generator_set_four_step(ocean_generator* g, int enable)
   if (!g)
     return fail(OCEAN_ERR_INVALID, "ocean_generator_set_four_step: null generator");
   g->four_step = enable != 0;  // h0 is re-laid out by the next frame if its strip width changes
+  if (g->hslab)
+  {
+    const hipError_t e = hslab_buffers(g);  // exchange_bytes reports the new path's size from here on
+    if (e != hipSuccess)
+      return fail(e == hipErrorOutOfMemory ? OCEAN_ERR_OOM : OCEAN_ERR_HIP,
+                  std::string("ocean_generator_set_four_step: ") + hipGetErrorString(e));
+  }
   return OCEAN_OK;
 }
 
@@ -840,7 +905,16 @@ int ocean_generator_frame_bytes(const ocean_generator* g, double per_point[2])
 {
   if (!g || !per_point)
     return fail(OCEAN_ERR_INVALID, "ocean_generator_frame_bytes: null argument");
-  if (g->half || g->hslab)
+  if (uses_gen4(g))
+  {
+    // the kept columns u' in [0, N/2) and the Nyquist column: step 1 reads h0 (16) and writes 5
+    // complex fields (40), step 2 reads and writes them (40 + 40, into the exchange blocks) | the row
+    // pass reads them (40) and writes the maps + Jacobian (36)
+    const double n = g->fft->n, kept = (n / 2 + 1) / n;
+    per_point[0] = (16.0 + 40.0 + 80.0) * kept;
+    per_point[1] = 40.0 * kept + 36.0;
+  }
+  else if (g->half || g->hslab)
   {
     // h0 of the kept columns (half + the Nyquist strip) + 5 complex fields out; 5 fields in, maps +
     // Jacobian; the strip-dealt path also moves the received fields to row-major (40 in + 40 out)
@@ -902,8 +976,16 @@ int ocean_slab_layout(size_t texture_size, int rank, int ranks, int half, int64_
     return fail(OCEAN_ERR_INVALID, "ocean_slab_layout: N a power of two in [16, 16384], ranks a power of two <= 16");
   if (half && !half_slab_supported(logn))
     return fail(OCEAN_ERR_INVALID, "ocean_slab_layout: the half-spectrum path needs N >= 1024");
+  if (half == 2 && !gen4_supported(logn))
+    return fail(OCEAN_ERR_INVALID, "ocean_slab_layout: the four-step path needs N = 8192 or 16384");
   const int n = 1 << logn, w = n / ranks;
-  if (half)
+  if (half == 2)
+  {
+    const Gen4Geom q = gen4_geom(logn, 1, rank, ranks, ranks == 1);
+    const int64_t v[6] = {q.u0, q.cols, q.nyq, q.w, (int64_t)q.blk_bytes, (int64_t)q.blk_bytes * ranks};
+    std::memcpy(out, v, sizeof(v));
+  }
+  else if (half)
   {
     const HalfSlab h = half_slab_geom(logn, rank, ranks);
     const int64_t blk = (int64_t)half_slab_block_bytes(logn, 1, h);
@@ -1026,6 +1108,9 @@ float* ocean_generator_initial_spectrum(ocean_generator* g, int c)
     return nullptr;
   if (materialise_h0(g) != OCEAN_OK)  // after fused re-seed frames
     return nullptr;
+  // the caller may write h0 through this pointer: the next requested re-seed must regenerate it, as
+  // the reference does on every request (src/Generator.cpp:55-59), so the h0 memo forgets its inputs
+  g->seeded.clear();
   return reinterpret_cast<float*>(g->h0 + h0_texels(g) * c);
 }
 

@@ -99,6 +99,41 @@ struct HalfSlab
   int w;        // rows per block = rows of this rank's row pass
 };
 
+// Four-step column pass of one rank (N = 8192 / 16384; whole grids: P = 1), SURVEY §8e. The
+// N/2 regular kept columns u' (x = N/2 + u') are dealt cols = N / (2P) per rank; rank P - 1 also
+// transforms the Nyquist column u = -N/2 (x = 0) as its local column `cols`. Step 1 writes the rank's
+// parts [c][N][lp]; step 2 writes its output rows straight into destination-block order: block q
+// (rows [q w, q w + w), bound for rank q) = gab | gde | gc parts [c][w][lp] (16, 16, 8 B elements),
+// then the frame's Nyquist-row term [c][2][N] float4. After the equal-split all-to-all the row pass
+// reads row y's columns from the P source blocks directly (RowSrc): no transpose.
+struct Gen4Geom
+{
+  int u0;            // first regular kept column of this rank
+  int cols;          // regular kept columns of this rank, N / (2P) (a multiple of 64)
+  int nyq;           // 1: this rank also transforms the Nyquist column (local column `cols`)
+  int lp;            // row pitch (texels) of the parts and of the block fields: cols + 16
+  int w;             // rows per block, N / P
+  int ranks;         // P
+  size_t h0_cstride; // h0 texels per cascade
+  size_t h0_reg;     // texel offset in a cascade's h0 of the 64-column block holding local column 0
+  size_t h0_nyq;     // texel offset of the 64-column block whose first column is x = 0
+  size_t blk_bytes;  // exchange block bytes
+};
+
+// Row-pass source of row-major fields (k_rows_half RM): element u in [0, N/2) of local row y of
+// cascade c sits at ab + (u / cpr) * src_stride + ((c * rows + y) * lp + u % cpr) * 16 (de likewise,
+// c with 8-B elements); the Nyquist column u = -N/2 in source block nyq_src at column cpr.
+struct RowSrc
+{
+  const unsigned char* ab;
+  const unsigned char* de;
+  const unsigned char* c;
+  size_t src_stride;  // bytes between source blocks
+  int cpr;            // columns per source block (a multiple of 64)
+  int lp;             // row pitch in elements
+  int nyq_src;        // source block of the Nyquist column
+};
+
 // h0 is stored strip-blocked [xb][y][blk]; blk = spectrum_block(log2 N). x0/width select a column
 // slab (width <= 0: the whole grid).
 int spectrum_block(int logn);
@@ -115,14 +150,19 @@ size_t half_hs_bytes(int logn, int blocks);  // also the strip-dealt path's
 // seed_consts (optional, device array of one seed_consts_bytes() record per cascade, needs hs): the
 // fused re-seed frame — pass 1 evaluates h0 itself and neither reads nor writes the h0 image.
 hipError_t launch_half_columns(int logn, const FrameParams& fp, const float4* h0, float4* gab, float4* gcd, float2* ge,
-                               float4* spec, const float2* tw, hipStream_t stream, int cus, float2* hs = nullptr,
-                               int hs_blocks = 0, const void* seed_consts = nullptr, int variant = 0);
+                               float4* spec, const float2* tw, hipStream_t stream, int cus, float2* hs, int hs_blocks,
+                               const void* seed_consts = nullptr);
 // generateSpectrum's settings-only constants (host, the oracle's fp32 expressions), as a device record
 size_t seed_consts_bytes();
 void seed_consts(const OceanSettings& s, int n, void* out);
 hipError_t launch_half_rows(int logn, const FrameParams& fp, const float4* gab, const float4* gcd, const float2* ge,
                             const float4* rcorr, float4* maps, float* jac, const FoamParams& foam, const float2* tw,
-                            hipStream_t stream, int cus, int ablation = 0);
+                            hipStream_t stream, int cus);
+// The Nyquist-row term of the half-spectrum paths (k_half_nyquist): spec[c][2][N] from row y = 0 of
+// h0 (h0row [c][N] when given, else the whole grid's h0 blocked blk columns wide; seed: evaluated in
+// place), written `copies` times copy_stride bytes apart (one copy per exchange block).
+hipError_t launch_half_nyquist(const FrameParams& fp, int n, int blk, const float4* h0, float4* spec, const float4* h0row,
+                               int copies, size_t copy_stride, const void* seed, hipStream_t stream, int cus);
 // Strip-dealt half-spectrum path (HalfSlab): N = 1024 .. 16384. Columns: the Nyquist-row term (from
 // h0 when h0_full, i.e. the whole grid's blocked h0, else from h0row = row 0 of every column) into
 // every destination block of `send`, and pass 1 of the rank's strips into the blocks (ranks *
@@ -138,21 +178,25 @@ hipError_t launch_half_slab_columns(int logn, const FrameParams& fp, const HalfS
                                     hipStream_t stream, int cus, float2* hs, int hs_blocks);
 hipError_t launch_half_slab_rows(int logn, const FrameParams& fp, const HalfSlab& hsl, const void* recv, float4* rm_ab,
                                  float4* rm_de, float2* rm_c, float4* maps, float* jac, const FoamParams& foam,
-                                 const float2* tw, hipStream_t stream, int cus);
+                                 const float2* tw, const float2* tw2, hipStream_t stream, int cus);
 hipError_t launch_rows_ifft_rows(int logn, int rows, float4* data, const float2* tw, hipStream_t stream, int cus);
-// Whole grids of N = 8192 / 16384 on one rank, column pass in four steps: h0 blocked gen4_h0_block()
-// columns wide; columns: the Nyquist-row term and step 1 into buf (a strip-dealt P = 1 block's
-// size and layout of parts); rows: step 2 into the row-major fields, then the row pass. tw2: the
-// N/16-point twiddle table.
+// The four-step column pass (Gen4Geom; N = 8192 / 16384, whole grids and slabs of P <= 16). h0: the
+// whole grid's image blocked gen4_h0_block() columns wide (whole_h0), or the rank's columns
+// (gen4_geom's h0_* offsets). Columns: the Nyquist-row term into every block of `send`, step 1 into
+// `parts` (gen4_parts_bytes), step 2 into the destination blocks of `send` (ranks * blk_bytes).
+// Rows: the row pass over the w rows of the received blocks. tw2: the N/16-point twiddle table.
 bool gen4_supported(int logn);
 int gen4_h0_block();
-size_t gen4_row_texels(int logn, int cascades);   // each row-major field (rm_*), padded row pitch
-size_t gen4_buffer_bytes(int logn, int cascades); // the column -> row buffer (parts + Nyquist term)
-hipError_t launch_gen4_columns(int logn, const FrameParams& fp, const float4* h0, void* buf, const float2* tw,
-                               hipStream_t stream, int cus);
-hipError_t launch_gen4_rows(int logn, const FrameParams& fp, const void* buf, float4* rm_ab, float4* rm_de, float2* rm_c,
-                            float4* maps, float* jac, const FoamParams& foam, const float2* tw, const float2* tw2,
-                            hipStream_t stream, int cus);
+Gen4Geom gen4_geom(int logn, int cascades, int rank, int ranks, bool whole_h0);
+size_t gen4_parts_bytes(int logn, int cascades, const Gen4Geom& g);
+hipError_t launch_gen4_columns(int logn, const FrameParams& fp, const Gen4Geom& g, const float4* h0, const float4* h0row,
+                               void* parts, void* send, const float2* tw, const float2* tw2, hipStream_t stream, int cus);
+hipError_t launch_gen4_rows(int logn, const FrameParams& fp, const Gen4Geom& g, const void* recv, float4* maps, float* jac,
+                            const FoamParams& foam, const float2* tw, const float2* tw2, hipStream_t stream, int cus);
+// The N/16-point twiddle table that the four-step paths (gen4, the standalone EncodeIFFT at 8192 /
+// 16384) and the XS row pass of 16384 read: ocean_fft_create appends it exactly for these sizes, and
+// the launchers that need it fail on a null tw2 instead of reading past the table.
+bool fourstep_table(int logn);
 // Standalone EncodeIFFT at N = 8192 / 16384: rows in place, then the column transform in four steps
 // through a work slab of N x wc texels (ifft_fourstep_work_texels), wc columns at a time. tw2: the
 // N/16-point twiddle table.

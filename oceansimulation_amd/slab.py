@@ -52,8 +52,9 @@ class SlabGenerator:
         check(lib().ocean_generator_set_half_spectrum(self._h, 1 if enable else 0), "ocean_generator_set_half_spectrum")
 
     def set_four_step(self, enable: bool) -> None:
-        """ranks == 1 at N = 8192 / 16384: the four-step column pass (default) or the strip-dealt
-        column pass + transposes (what ranks > 1 run, bit-identical to them)."""
+        """N = 8192 / 16384: the four-step column pass writing destination-block order (default; the
+        row pass reads the received blocks directly) or the strip-dealt column pass + transposes.
+        Changes exchange_bytes."""
         check(lib().ocean_generator_set_four_step(self._h, 1 if enable else 0), "ocean_generator_set_four_step")
 
     def frame_bytes(self):

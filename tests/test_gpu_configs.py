@@ -139,23 +139,23 @@ def test_h0_16384_sampled_vs_oracle(ocean, oracle):
     fft.close()
 
 
-@pytest.mark.slow
-def test_config5_geometry_16384_eight_ranks_bit_exact(ocean):
-    """BASELINE configs[4] geometry on one GPU: 8 SlabGenerators over the single 16384^2 grid
-    (default settings), each seeding its dealt strips, column pass into destination-block order,
-    the equal-split all-to-all as device copies, transposes + row pass on its 2048 rows; the
-    stitched maps and Jacobian must equal the whole-grid generator's bit for bit, frame after
-    frame (the first seeds h0)."""
+def _slabs_vs_whole(ocean, n, P, steps, four_step=True, settings=None):
+    """P SlabGenerators over one n x n grid, frames emulated in one process (equal-split all-to-all
+    as device copies), against the whole-grid generator on the same path, compared bit for bit on
+    the device after every frame (the first seeds h0)."""
     from oceansimulation_amd import capi, hip
     from oceansimulation_amd.hip import DeviceBuffer
     from oceansimulation_amd.slab import SlabGenerator, emulate_frame
 
-    n, P = 16384, 8
-    steps = [0.25, 1.0 / 60.0, 2.0]
+    settings = settings or {}
     fft = ocean.FFTCalculator(n)
     whole = ocean.Generator(fft, 1)
-    whole.set_four_step(False)  # the strip-dealt path the ranks run (four-step: test_four_step_*)
+    whole.set_four_step(four_step)
+    ocean.apply_settings(whole.GetOceanSettings(0), **settings)
     slabs = [SlabGenerator(fft, r, P) for r in range(P)]
+    for g in slabs:
+        g.set_four_step(four_step)
+        ocean.apply_settings(g.GetOceanSettings(), **settings)
     sends = [DeviceBuffer(g.exchange_bytes) for g in slabs]
     recvs = [DeviceBuffer(g.exchange_bytes) for g in slabs]
     L = capi.lib()
@@ -169,13 +169,38 @@ def test_config5_geometry_16384_eight_ranks_bit_exact(ocean):
                              (L.ocean_generator_jacobian_map, 4)):
                 slab_ptr = int(get(g.handle, 0))
                 whole_ptr = int(get(whole.handle, 0)) + r * w * n * tex
-                assert _dev_equal(slab_ptr, whole_ptr, w * n * tex), (k, r, get.__name__)
+                assert _dev_equal(slab_ptr, whole_ptr, w * n * tex), (n, P, four_step, k, r, get.__name__)
     for buf in sends + recvs:
         buf.free()
     for g in slabs:
         g.close()
     whole.close()
     fft.close()
+
+
+@pytest.mark.slow
+def test_config5_geometry_16384_eight_ranks_bit_exact(ocean):
+    """BASELINE configs[4] geometry on one GPU: 8 SlabGenerators over the single 16384^2 grid
+    (default settings). Each seeds its 1024 kept columns (rank 7 also the Nyquist column), runs the
+    four-step column pass whose second step writes the 8 destination blocks, the equal-split
+    all-to-all runs as device copies, and the row pass reads its 2048 rows from the 8 received
+    blocks (no transpose). The stitched maps and Jacobian equal the whole-grid generator's bit for
+    bit, frame after frame (src/Generator.cpp:45-83 split over ranks)."""
+    _slabs_vs_whole(ocean, 16384, 8, [0.25, 1.0 / 60.0, 2.0])
+
+
+@pytest.mark.parametrize("n,P", [(8192, 2), (8192, 8), (8192, 16), (16384, 16)])
+def test_four_step_slabs_bit_exact(ocean, n, P):
+    """The four-step slab path at the other rank counts the launcher accepts: 16 ranks put 256
+    (8192) or 512 (16384) kept columns on each rank and make every destination block's rows a
+    single 16-row group of step 2's output."""
+    _slabs_vs_whole(ocean, n, P, [0.5, 1.0 / 60.0], settings=dict(planeSize=777.0))
+
+
+def test_dealt_slabs_8192_bit_exact(ocean):
+    """The strip-dealt slab path (ocean_generator_set_four_step(0): one-column items, transposes after
+    the exchange) against the whole grid on the same path."""
+    _slabs_vs_whole(ocean, 8192, 4, [0.5, 1.0 / 60.0], four_step=False, settings=dict(planeSize=777.0))
 
 
 @pytest.mark.parametrize("n", [8192, 16384])

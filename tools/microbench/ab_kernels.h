@@ -1,0 +1,419 @@
+// ab_kernels.h — microbenchmark-only kernel variants and launchers (tools/microbench): the A/B
+// alternatives measured against the production frame passes (DESIGN.md §4 "Tried and not kept",
+// profiles/r0*_halfbench_*.log), kept out of liboceanfft.so. Production launchers: launch_half.hip,
+// launch_slab.hip, launch_fft.hip. Included after them by all_kernels.h.
+#pragma once
+
+namespace oceanfft
+{
+
+// Pass 1 on half strips (whole grids): a 2T-thread workgroup (512 at N = 4096, 256 VGPRs, one per
+// CU) transforms 2 columns per item, so the thread's 16 evolved amplitudes H stay in VGPRs (32)
+// across the three rounds: no H scratch (k_cols_half<HS> moves 24 B per kept texel through it).
+// Field strips are FB = 2 columns wide (half_group_offset<.., 2>): with RG rows per group, one store
+// instruction of a wave (32 rows x 2 columns) writes whole 128-B lines when RG * 2 * 16 B = 128 B
+// (gab, gde: RG = 4; gc: RGC = 8). The two halves of an h0 strip (items 2p, 2p + 1) run together
+// on one XCD (xcd_pair_slot), so each 64-B h0 row is fetched once for both (default-policy loads).
+// The Nyquist strip's second half (columns 2, 3: u < 0) is not needed and is skipped. The exchange
+// moves whole CPairs (2 x PADDED x 16 B = 139 KiB of LDS at N = 4096).
+// A/B only (launch_half_columns variants 12..14 with launch_half_rows 12..14; halfbench,
+// profiles/r01_halfbench_halfstrips.log): pass 1 takes 0.81 ms against 0.96, but pass 2 then reads
+// half lines (a 2-row item holds half of each 4-row x 2-column line): 1.64 ms against 1.52, frame
+// 2.447 against 2.486 ms. Half-line stores (RG = 2, paired workgroups, default policy) lose the pass-1
+// gain instead (0.96 ms). Production keeps 4-column items with the H scratch.
+// The field CPair of a round: (A, B), (D, E) or (C, 0) from H (k_cols_half's pack).
+template <int LOGN>
+__device__ __forceinline__ CPair half_round_pack(int round, float2 H, const KVec& q)
+{
+  if (round == 0)  // (A, B) = (H, kz H)
+    return CPair{f2v{H.x, q.kz * H.x}, f2v{H.y, q.kz * H.y}};
+  if (round == 1)  // (D, E) = (kz H / |k|, kz^2 H / |k|)
+  {
+    const float e = q.kz * q.dirz;
+    return CPair{f2v{q.dirz * H.x, e * H.x}, f2v{q.dirz * H.y, e * H.y}};
+  }
+  return CPair{f2v{q.inv * H.x, 0.0f}, f2v{q.inv * H.y, 0.0f}};  // (C, 0) = (H / |k|, 0)
+}
+
+// SAC: gc's store policy (default: SA).
+template <int LOGN, int LA = 0, int SA = kStream, int RG = 4, int RGC = 8, int SAC = SA>
+__global__ __launch_bounds__(2 * FftShape<LOGN>::T) void k_cols_half2(FrameParams fp, const float4* __restrict__ h0,
+                                                                      float4* __restrict__ gab, float4* __restrict__ gde,
+                                                                      float2* __restrict__ gc,
+                                                                      const float2* __restrict__ tw_glob)
+{
+  using S = FftShape<LOGN>;
+  using K = ColFirstCfg<LOGN>;
+  using HC = HalfCfg<LOGN>;
+  constexpr int N = S::N, T = S::T, B = K::B, STRIPS = HC::STRIPS, FS = 2 * STRIPS;
+  static_assert(HC::SUPPORTED && B == 4, "half strips of 4-column h0 strips");
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  float2* tw = reinterpret_cast<float2*>(smem);
+  void* xch = smem + ((S::TW_ENTRIES * 8 + 15) / 16) * 16;
+  load_twiddles<LOGN>(tw, tw_glob);
+
+  const int total = fp.cascades * FS;
+  const float dim = (float)N;
+  for (int item = xcd_pair_slot(blockIdx.x, gridDim.x); item < total; item += gridDim.x)
+  {
+    const int c = item / FS, fs = item - c * FS, s = fs >> 1, h = fs & 1;
+    if (s == STRIPS - 1 && h == 1)
+      continue;  // Nyquist strip, columns 2 and 3 (u < 0): unused (uniform per workgroup)
+    const int xb = s == STRIPS - 1 ? 0 : N / (2 * B) + s;
+    const CascadeFrame f = fp.c[c];
+    const float4* src = h0 + ((size_t)c * (N / B) + xb) * N * B;
+    const size_t cbase = (size_t)c * STRIPS * N * B;
+    const size_t gbase = cbase + half_group_offset<LOGN, RG, 2>(0, fs);
+    const size_t cgbase = cbase + half_group_offset<LOGN, RGC, 2>(0, fs);
+    float2 H[16];
+    {
+      const int tid = opaque((int)threadIdx.x);
+      const int b2 = tid % 2, i = (tid / 2) % T, x = xb * B + 2 * h + b2;
+      const int voff = (i * B + 2 * h + b2) * 16;
+      float4 a[16];
+#pragma unroll
+      for (int m = 0; m < 16; m++)  // fftShift on y folded into the load
+        a[m] = ld4<LA>(src + ((m + 8) & 15) * T * B, voff);
+#pragma unroll
+      for (int m = 0; m < 16; m++)
+      {
+        const int y = i + ((m + 8) & 15) * T;
+        H[m] = evolve(a[m], make_kvec(x, y, dim, f.dk).k, f);
+      }
+    }
+#pragma unroll
+    for (int round = 0; round < 3; round++)
+    {
+      // k-vectors recomputed per round (opaque: CSE would keep 48 of them live)
+      const int tr = opaque((int)threadIdx.x);
+      const int br = tr % 2, ir = (tr / 2) % T, xr = xb * B + 2 * h + br;
+      CPair v[16];
+#pragma unroll
+      for (int m = 0; m < 16; m++)
+      {
+        const int y = ir + ((m + 8) & 15) * T;
+        v[m] = half_round_pack<LOGN>(round, H[m], make_kvec(xr, y, dim, f.dk));
+      }
+      fft_run<LOGN, 2, false>(v, ir, br, xch, tw);
+#pragma unroll
+      for (int m = 0; m < 16; m++)
+      {
+        if (round == 0)
+          st4<SA>(gab + gbase + half_group_offset<LOGN, RG, 2>(m * T, 0), half_group_offset<LOGN, RG, 2>(ir, 0, br) * 16,
+                  pair_raw(v[m]));
+        else if (round == 1)
+          st4<SA>(gde + gbase + half_group_offset<LOGN, RG, 2>(m * T, 0), half_group_offset<LOGN, RG, 2>(ir, 0, br) * 16,
+                  pair_raw(v[m]));
+        else
+          st2<SAC>(gc + cgbase + half_group_offset<LOGN, RGC, 2>(m * T, 0), half_group_offset<LOGN, RGC, 2>(ir, 0, br) * 8,
+                  make_float2(v[m].re.x, v[m].im.x));
+      }
+    }
+  }
+}
+
+// Pass 1 with H in VGPRs (whole grids, N = 4096): one 4-column strip per item on T * B / 2 = 512
+// threads, each holding two positions (ia, ia + T/2) of one column, i.e. 32 points (fft_run_x2), so
+// the 32 evolved amplitudes H (64 VGPRs) stay in registers across the three rounds: no H scratch
+// (k_cols_half<HS> moves 24 B per kept texel through it) and h0 read once. Each store instruction of
+// a wave still covers 16 rows x 4 columns, i.e. whole 128-B lines of the row-group layout. 512
+// threads with 139 KiB of LDS: one workgroup per CU, 256 VGPRs per thread.
+// HB: the second position's H goes through a per-block scratch slice (hs) instead (fewer VGPRs).
+template <int LOGN, int LA = kStream, int SA = kStream, int RG = kHalfRG, int RGC = kHalfRGC, bool HB = false>
+__global__ __launch_bounds__(FftShape<LOGN>::T * 2) void k_cols_half4(FrameParams fp, const float4* __restrict__ h0,
+                                                                      float4* __restrict__ gab, float4* __restrict__ gde,
+                                                                      float2* __restrict__ gc,
+                                                                      const float2* __restrict__ tw_glob,
+                                                                      float2* __restrict__ hs)
+{
+  using S = FftShape<LOGN>;
+  using K = ColFirstCfg<LOGN>;
+  using HC = HalfCfg<LOGN>;
+  constexpr int N = S::N, T = S::T, B = K::B, STRIPS = HC::STRIPS;
+  static_assert(HC::SUPPORTED && B == 4 && S::R0 == 16, "4-column strips, radix-16 stages");
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  float2* tw = reinterpret_cast<float2*>(smem);
+  void* xch = smem + ((S::TW_ENTRIES * 8 + 15) / 16) * 16;
+  load_twiddles<LOGN>(tw, tw_glob);
+  const int total = fp.cascades * STRIPS;
+  const float dim = (float)N;
+  for (int item = blockIdx.x; item < total; item += gridDim.x)
+  {
+    const int c = item / STRIPS, s = item - c * STRIPS;
+    const int xb = s == STRIPS - 1 ? 0 : N / (2 * B) + s;
+    const CascadeFrame f = fp.c[c];
+    const float4* src = h0 + ((size_t)c * (N / B) + xb) * N * B;
+    const size_t gbase = (size_t)c * STRIPS * N * B + half_group_offset<LOGN, RG>(0, s);
+    const size_t cgbase = (size_t)c * STRIPS * N * B + half_group_offset<LOGN, RGC>(0, s);
+    float2 H[HB ? 1 : 2][16];
+    float2* hsb = hs + (size_t)blockIdx.x * 16 * (T * 2);
+    {
+      const int tid = opaque((int)threadIdx.x);
+      const int b = tid % B, ia = (tid / B) % (T / 2), x = xb * B + b;
+#pragma unroll
+      for (int g = 0; g < 2; g++)
+      {
+        const int p = ia + g * (T / 2);
+        float4 a[16];
+#pragma unroll
+        for (int m = 0; m < 16; m++)  // fftShift on y folded into the load
+          a[m] = ld4s<LA>(src, (p * B + b) * 16, ((m + 8) & 15) * T * B * 16);
+#pragma unroll
+        for (int m = 0; m < 16; m++)
+        {
+          const float2 h = evolve(a[m], make_kvec(x, p + ((m + 8) & 15) * T, dim, f.dk).k, f);
+          if (HB && g == 1)
+            st2s<0>(hsb, tid * 8, m * (T * 2) * 8, h);
+          else
+            H[g][m] = h;
+        }
+      }
+    }
+#pragma unroll
+    for (int round = 0; round < 3; round++)
+    {
+      // k-vectors recomputed per round (opaque: CSE would keep them live across the rounds)
+      const int tid = opaque((int)threadIdx.x);
+      const int b = tid % B, ia = (tid / B) % (T / 2), x = xb * B + b;
+      CPair v[2][16];
+#pragma unroll
+      for (int g = 0; g < 2; g++)
+#pragma unroll
+        for (int m = 0; m < 16; m++)
+        {
+          const float2 h = (HB && g == 1) ? ld2s<kStream>(hsb, tid * 8, m * (T * 2) * 8) : H[g == 1 && HB ? 0 : g][m];
+          v[g][m] = half_round_pack<LOGN>(round, h, make_kvec(x, ia + g * (T / 2) + ((m + 8) & 15) * T, dim, f.dk));
+        }
+      fft_run_x2<LOGN, B>(v[0], v[1], ia, b, xch, tw);
+#pragma unroll
+      for (int g = 0; g < 2; g++)
+      {
+        const int p = ia + g * (T / 2);
+#pragma unroll
+        for (int m = 0; m < 16; m++)
+        {
+          if (round == 0)
+            st4s<SA>(gab + gbase, half_group_offset<LOGN, RG>(p, 0, b) * 16, half_group_offset<LOGN, RG>(m * T, 0) * 16,
+                     pair_raw(v[g][m]));
+          else if (round == 1)
+            st4s<SA>(gde + gbase, half_group_offset<LOGN, RG>(p, 0, b) * 16, half_group_offset<LOGN, RG>(m * T, 0) * 16,
+                     pair_raw(v[g][m]));
+          else
+            st2s<SA>(gc + cgbase, half_group_offset<LOGN, RGC>(p, 0, b) * 8, half_group_offset<LOGN, RGC>(m * T, 0) * 8,
+                     make_float2(v[g][m].re.x, v[g][m].im.x));
+        }
+      }
+    }
+  }
+}
+
+// launch_half_columns with the A/B variants of halfbench (0 = production, numbered as in the logs)
+hipError_t launch_half_columns_ab(int logn, const FrameParams& fp, const float4* h0, float4* gab, float4* gcd, float2* ge,
+                               float4* spec, const float2* tw, hipStream_t stream, int cus, float2* hs = nullptr,
+                               int hs_blocks = 0, const void* seed_consts = nullptr, int variant = 0)
+{
+  const SpectrumConsts* seed = static_cast<const SpectrumConsts*>(seed_consts);
+  return with_logn(logn, [&](auto L) -> hipError_t {
+    constexpr int LOGN = decltype(L)::value;
+    if constexpr (!HalfCfg<LOGN>::SUPPORTED)
+      return hipErrorInvalidValue;
+    else
+    {
+      using K = ColFirstCfg<LOGN>;
+      using S = FftShape<LOGN>;
+      const int n = S::N;
+      hipError_t e = launch_half_nyquist(fp, n, K::B, h0, spec, nullptr, 1, 0, seed, stream, cus);
+      if (e != hipSuccess)
+        return e;
+      // hs: per-block H scratch (half_hs_bytes): H evolved once instead of once per round
+      if (seed && !hs)
+        return hipErrorInvalidValue;
+      // HS: h0 is read once per item, streamed (nt), which leaves the XCD's L2 to the H scratch
+      // (0.972 -> 0.935 ms, tools/microbench/halfbench). variant (halfbench): 1 = default-policy h0
+      // loads, 2 = sc1 field stores (dropped from L2: slower), 3 = sc1 + nt stores
+      // 4..7: field layouts with row groups (RG, RGC) = (2, 2), (2, 4), (4, 4), (1, 1) (launch_half_rows 8..11)
+      constexpr int RG = kHalfRG, RGC = kHalfRGC;
+      // whole grids below 4096 keep 2 H pairs in VGPRs: 128 VGPRs, so two (2048) or four (1024)
+      // workgroups fit a CU (with 4: 134-136 VGPRs, one fewer)
+      constexpr int HKW = LOGN == 12 ? kHalfHK : 2;
+      // HP (the H scratch in 16-B pairs): 0.921 -> 0.910 ms (halfbench hpair); variant 23: unpaired
+      auto kern = seed && variant == 33 ? k_cols_half<LOGN, 0, kStream, true, false, true, RG, RGC, K::B, true>
+                  : seed ? k_cols_half<LOGN, 0, kStream, true, false, true, RG, RGC, K::B, true, false, kHalfHL, kHalfHKSeed>
+                       : !hs ? k_cols_half<LOGN, 0, kStream, false, false, false, RG, RGC>
+                       : variant == 1 ? k_cols_half<LOGN, 0, kStream, true, false, false, RG, RGC>
+                       : variant == 2 ? k_cols_half<LOGN, kStream, 16, true, false, false, RG, RGC>
+                       : variant == 3 ? k_cols_half<LOGN, kStream, 18, true, false, false, RG, RGC>
+                       : variant == 4 ? k_cols_half<LOGN, kStream, kStream, true, false, false, 2, 2>
+                       : variant == 5 ? k_cols_half<LOGN, kStream, kStream, true, false, false, 2, 4>
+                       : variant == 6 ? k_cols_half<LOGN, kStream, kStream, true, false, false, 4, 4>
+                       : variant == 7 ? k_cols_half<LOGN, kStream, kStream, true, false, false, 1, 1>
+                       : variant == 23 ? k_cols_half<LOGN, kStream, kStream, true, false, false, RG, RGC>
+                       : variant == 24 ? k_cols_half<LOGN, kStream, kStream, true, false, false, RG, RGC, K::B, true, true>
+                       : variant == 25 ? k_cols_half<LOGN, kStream, kStream, true, false, false, RG, RGC, K::B, true, false, 1, 0>
+                       : variant == 26 ? k_cols_half<LOGN, kStream, kStream, true, false, false, RG, RGC, K::B, true, false, 1, 1>
+                       : variant == 27 ? k_cols_half<LOGN, kStream, kStream, true, false, false, RG, RGC, K::B, true, false, 1, 2>
+                       : variant == 28 ? k_cols_half<LOGN, kStream, kStream, true, false, false, RG, RGC, K::B, true, false, 0, 2>
+                       : variant == 29 ? k_cols_half<LOGN, kStream, kStream, true, false, false, RG, RGC, K::B, true, false, 1, 3>
+                       : variant == 30 ? k_cols_half<LOGN, kStream, kStream, true, false, false, RG, RGC, K::B, true, false, 1, 4>
+                       : variant == 31 ? k_cols_half<LOGN, kStream, kStream, true, false, false, RG, RGC, K::B, true, false, 1, 5>
+                       : variant == 32 ? k_cols_half<LOGN, kStream, kStream, true, false, false, RG, RGC, K::B, true>
+                       : variant == 34 ? k_cols_half<LOGN, kStream, kStream, true, false, false, 2, 2, K::B, true, false, kHalfHL, kHalfHK>
+                       : variant == 35 ? k_cols_half<LOGN, kStream, kStream, true, false, false, 4, 4, K::B, true, false, kHalfHL, kHalfHK>
+                       : variant == 36 ? k_cols_half<LOGN, kStream, kStream, true, false, false, 1, 1, K::B, true, false, kHalfHL, kHalfHK>
+                                      : k_cols_half<LOGN, kStream, kStream, true, false, false, RG, RGC, K::B, true, false, kHalfHL, HKW>;
+      if (variant >= 12 && variant <= 14 && !seed)  // half-strip items (k_cols_half2): H in VGPRs
+      {
+        auto hk = variant == 12   ? k_cols_half2<LOGN, 0, kStream, 4, 8>
+                  : variant == 13 ? k_cols_half2<LOGN, 0, 0, 2, 4>
+                                  : k_cols_half2<LOGN, 0, kStream, 4, 4, 0>;
+        const int hlds = ((S::TW_ENTRIES * 8 + 15) / 16) * 16 + 2 * S::PADDED * 16;
+        const int hg = persistent_grid(hk, 2 * S::T, hlds, fp.cascades * 2 * HalfCfg<LOGN>::STRIPS, cus);
+        hipLaunchKernelGGL(hk, dim3(hg), dim3(2 * S::T), hlds, stream, fp, h0, gab, gcd, ge, tw);
+        return hipGetLastError();
+      }
+      if constexpr (FftShape<LOGN>::R0 == 16)
+      if (variant == 22 && !seed)  // H in VGPRs: 32 points per thread, 512 threads (k_cols_half4)
+      {
+        auto hk = hs ? k_cols_half4<LOGN, kStream, kStream, kHalfRG, kHalfRGC, true> : k_cols_half4<LOGN>;
+        const int hlds = ((S::TW_ENTRIES * 8 + 15) / 16) * 16 + K::LDS1;
+        int hg = persistent_grid(hk, S::T * 2, hlds, fp.cascades * HalfCfg<LOGN>::STRIPS, cus);
+        if (hs && hg > hs_blocks)
+          hg = hs_blocks;
+        hipLaunchKernelGGL(hk, dim3(hg), dim3(S::T * 2), hlds, stream, fp, h0, gab, gcd, ge, tw, hs);
+        return hipGetLastError();
+      }
+      if (variant == 20 && hs && !seed)  // half-strip items, two workgroups per CU (HS slices of half size)
+      {
+        auto hk = k_cols_half<LOGN, 0, 0, true, false, false, RG, RGC, K::B / 2>;
+        const int wg = S::T * (K::B / 2);
+        const int hlds = ((S::TW_ENTRIES * 8 + 15) / 16) * 16 + (K::B / 2) * S::PADDED * 8;
+        int hg = persistent_grid(hk, wg, hlds, fp.cascades * HalfCfg<LOGN>::STRIPS * 2, cus);
+        const int slices = hs_blocks * (K::WG1 / wg);
+        if (hg > slices)
+          hg = slices;
+        hg &= ~15;  // xcd_pair_slot needs a multiple of 16 blocks
+        if (hg < 16)
+          return hipErrorInvalidValue;
+        hipLaunchKernelGGL(hk, dim3(hg), dim3(wg), hlds, stream, fp, h0, gab, gcd, ge, tw, hs, HalfSlab{},
+                           (unsigned char*)nullptr, 1, seed);
+        return hipGetLastError();
+      }
+      // H pairs in LDS (HL): production kHalfHL; variants 25..31 as named in halfbench hkeep, 32 none
+      // the chain above with HL = 0 (34..36: production's H pairs with the field layouts of 4, 6, 7)
+      const bool named = (variant >= 1 && variant <= 7) || (variant >= 23 && variant <= 32);
+      const int hl = seed ? (variant == 33 ? 0 : kHalfHL)
+                     : !hs ? 0 : !named ? kHalfHL : (variant >= 25 && variant <= 31 && variant != 28) ? 1 : 0;
+      const int lds = ((S::TW_ENTRIES * 8 + 15) / 16) * 16 + K::LDS1 + hl * K::WG1 * 16;
+      int grid = persistent_grid(kern, K::WG1, lds, fp.cascades * HalfCfg<LOGN>::STRIPS, cus);
+      // hs holds hs_blocks slices for 1024-thread workgroups (half_hs_bytes); a block uses 16 x WG1
+      // entries, so below 4096 each slice serves 1024 / WG1 blocks (variant 37: one, as before)
+      const int slices = variant == 37 ? hs_blocks : hs_blocks * (1024 / K::WG1);
+      if (hs && grid > slices)
+        grid = slices;
+      if (grid < 1)
+        return hipErrorInvalidValue;
+      hipLaunchKernelGGL(kern, dim3(grid), dim3(K::WG1), lds, stream, fp, h0, gab, gcd, ge, tw, hs, HalfSlab{},
+                         (unsigned char*)nullptr, 1, seed);  // gcd/ge: (D, E) / C
+      return hipGetLastError();
+    }
+  });
+}
+
+hipError_t launch_half_rows_ab(int logn, const FrameParams& fp, const float4* gab, const float4* gcd, const float2* ge,
+                            const float4* rcorr, float4* maps, float* jac, const FoamParams& foam, const float2* tw,
+                            hipStream_t stream, int cus, int ablation = 0)
+{
+  return with_logn(logn, [&](auto L) -> hipError_t {
+    constexpr int LOGN = decltype(L)::value;
+    if constexpr (!HalfCfg<LOGN>::SUPPORTED)
+      return hipErrorInvalidValue;
+    else
+    {
+      using K = ColFirstCfg<LOGN>;
+      using S = FftShape<LOGN>;
+      // ablation (tools/microbench; 1-3 on the production shape): 1 no HBM loads, 2 no x transform,
+      // 3 no mirror exchange,
+      // 4 / 5 ColFirstCfg's rows per workgroup (one 1024-thread workgroup per CU) / one row
+      // 0 (production): one item per row block for both images (C loaded once); 6: one image per
+      // item (C loaded by both items of a row block)
+      constexpr int R4 = K::RPW2;
+      // production at N = 4096: one row (both images) per 256-thread workgroup, four workgroups per
+      // CU, the 4 rows of a gc line on one XCD (GRP 4): 1.407 -> 1.377 ms per 8 x 4096^2, maps
+      // bit-identical (halfbench rowv 16); 17 = the two-row workgroups (production below 4096)
+      constexpr bool ONE_ROW = LOGN == 12;
+      const int rpw = ablation == 4 ? R4 : (ablation == 5 || ablation == 16 || (ablation == 0 && ONE_ROW)) ? 1 : 2;
+      const int per_item = (ablation <= 3 || ablation >= 7) ? 1 : 2;
+      // production loads use the default policy: C's 128-B lines are shared by the paired items
+      // (xcd_pair_slot) and streamed loads lost them before the partner's read (-5 %,
+      // tools/microbench/halfbench); 7: streamed loads
+      // 8..11: the field layouts of launch_half_columns' variants 4..7
+      constexpr int RG = kHalfRG, RGC = kHalfRGC;
+      // 16: one row (both images) per 256-thread workgroup, four per CU, rows of a gc line on one XCD
+      auto kern = ablation == 0 && ONE_ROW ? k_rows_half<LOGN, 0, kStream, 0, 1, true, false, RG, RGC, 4, 4>
+                  : ablation == 0 || ablation == 17 ? k_rows_half<LOGN, 0, kStream, 0, 2, true, false, RG, RGC>
+                  : ablation == 16 ? k_rows_half<LOGN, 0, kStream, 0, 1, true, false, RG, RGC, 4, 4>
+                  : ablation == 8 ? k_rows_half<LOGN, 0, kStream, 0, 2, true, false, 2, 2>
+                  : ablation == 9 ? k_rows_half<LOGN, 0, kStream, 0, 2, true, false, 2, 4>
+                  : ablation == 10 ? k_rows_half<LOGN, 0, kStream, 0, 2, true, false, 4, 4>
+                  : ablation == 11 ? k_rows_half<LOGN, 0, kStream, 0, 2, true, false, 1, 1>
+                  : ablation == 12 ? k_rows_half<LOGN, 0, kStream, 0, 2, true, false, 4, 8, 2, 4>
+                  : ablation == 13 ? k_rows_half<LOGN, 0, kStream, 0, 2, true, false, 2, 4, 2, 2>
+                  : ablation == 14 ? k_rows_half<LOGN, 0, kStream, 0, 2, true, false, 4, 4, 2, 2>
+                  : ablation == 15 ? k_rows_half<LOGN, 0, kStream, 0, 2, true, false, RG, RGC, 4, 2, false>
+                  : ablation == 7 ? k_rows_half<LOGN, kStream, kStream, 0, 2, true, false, RG, RGC>
+                  : ablation == 6 ? k_rows_half<LOGN, kStream, kStream, 0, 2, false, false, RG, RGC>
+                  : ablation == 1 ? k_rows_half<LOGN, 0, kStream, 1, 2, true, false, RG, RGC>
+                  : ablation == 2 ? k_rows_half<LOGN, 0, kStream, 2, 2, true, false, RG, RGC>
+                  : ablation == 3 ? k_rows_half<LOGN, 0, kStream, 3, 2, true, false, RG, RGC>
+                  : ablation == 4 ? k_rows_half<LOGN, kStream, kStream, 0, R4>
+                                  : k_rows_half<LOGN, kStream, kStream, 0, 1>;
+      const int lds = ((S::TW_ENTRIES * 8 + 15) / 16) * 16 + lds_row_slots<LOGN>(rpw) * 8;
+      const int grid = persistent_grid(kern, S::T * rpw, lds, fp.cascades * per_item * (S::N / rpw), cus);
+      hipLaunchKernelGGL(kern, dim3(grid), dim3(S::T * rpw), lds, stream, fp, gab, gcd, ge, rcorr, maps, jac, foam, tw,
+                         S::N, RowSrc{}, (const float2*)nullptr);
+      return hipGetLastError();
+    }
+  });
+}
+
+// A/B hook for tools/microbench/genbench at N = 4096. Pass 1: variant 0/1 = KEEP 0/4 with default
+// policy on the twice-read h0, 2 = KEEP 4 all loads default, 3 = KEEP 4 compute only (no HBM). Pass 2: cache policy 0 default, 1 nt stores, 2 nt loads + stores.
+hipError_t launch_policy_variant(int pass, int policy, const FrameParams& fp, const SlabGeom& g, const float4* in,
+                                 float4* out, float* jac, const FoamParams& foam, const float2* tw, hipStream_t stream,
+                                 int cus)
+{
+  constexpr int LOGN = 12;
+  using K = ColFirstCfg<LOGN>;
+  using S = FftShape<LOGN>;
+  if (pass == 1)
+  {
+    auto kern = policy == 0 ? k_cols_evolve<LOGN, 0, kStream, kStream, false, 0>
+                            : (policy == 1 ? k_cols_evolve<LOGN, 4, kStream, kStream, false, 0>
+                                           : (policy == 2 ? k_cols_evolve<LOGN, 4, 0, kStream, false, 0>
+                                                          : (policy == 3 ? k_cols_evolve<LOGN, 4, kStream, kStream, true>
+                                                                         : k_cols_evolve<LOGN, 4, kStream, kStream, false, 0, true>)));
+    const int lds = ((S::TW_ENTRIES * 8 + 15) / 16) * 16 + K::LDS1;
+    const int items = fp.cascades * ((g.w / K::B) / K::SPW);
+    const int grid = persistent_grid(kern, K::WG1, lds, items, cus);
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(K::WG1), lds, stream, fp, g, in, out, tw);
+  }
+  else
+  {
+    // policy 3: 2 rows per workgroup (512 threads, half the LDS: two workgroups per CU);
+    // 4 / 5: ablations compute only / memory only
+    const int rpw = policy == 3 ? 2 : K::RPW2;
+    auto kern = policy == 0 ? k_rows_final<LOGN, true, 0, 0>
+                : policy == 1 ? k_rows_final<LOGN, true, 0, 2>
+                : policy == 2 ? k_rows_final<LOGN, true, 2, 2>
+                : policy == 3 ? k_rows_final<LOGN, true, 2, 2, 2>
+                : policy == 4 ? k_rows_final<LOGN, true, 2, 2, K::RPW2, 1>
+                              : k_rows_final<LOGN, true, 2, 2, K::RPW2, 2>;
+    const int lds = ((S::TW_ENTRIES * 8 + 15) / 16) * 16 + lds_row_slots<LOGN>(rpw) * 8;
+    const int items = fp.cascades * 2 * (g.w / rpw);
+    const int grid = persistent_grid(kern, S::T * rpw, lds, items, cus);
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(S::T * rpw), lds, stream, 2 * fp.cascades, g, in, out, jac, foam, tw);
+  }
+  return hipGetLastError();
+}
+
+}  // namespace oceanfft

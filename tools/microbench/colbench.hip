@@ -2,7 +2,7 @@
 // Build: hipcc --offload-arch=gfx950 -O3 -fno-slp-vectorize -std=c++17 -I include -I oceansimulation_amd/csrc \
 //        tools/microbench/colbench.hip -o tools/microbench/colbench
 // Runs on 8 images of 4096^2 float4 (2 GiB), in place, and prints GB/s for each variant.
-#include "../../oceansimulation_amd/csrc/ocean_kernels.hip"
+#include "all_kernels.h"
 
 #include <cstdio>
 #include <cstdlib>

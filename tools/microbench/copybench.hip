@@ -1,7 +1,7 @@
 // copybench.hip — which streaming forms reach the HBM ceiling on gfx950 (out-of-place copies of
 // 2 GiB float4, read + write counted). Variants: plain pointer vs buffer (SRD) access, unroll depth,
 // cache-policy aux bits on the buffer loads/stores, workgroup size.
-#include "../../oceansimulation_amd/csrc/ocean_kernels.hip"
+#include "all_kernels.h"
 
 #include <cstdio>
 #include <cstdlib>

@@ -2,7 +2,7 @@
 // step 1 at several occupancy bounds and step 2 at 16 / 8 columns per workgroup, interleaved, with
 // the production launchers' frame for reference. Outputs are compared with the production variant
 // (bit-identical: same arithmetic, different launch shapes). Usage: gen4bench
-#include "../../oceansimulation_amd/csrc/ocean_kernels.hip"
+#include "all_kernels.h"
 
 #include <algorithm>
 #include <cmath>
@@ -63,8 +63,7 @@ static float2* table(int logn)
 int main()
 {
   constexpr int LOGN = 14, LOGN2 = 10;
-  using G = Gen4Cfg<LOGN>;
-  constexpr int N = G::N, KP = G::KP, PITCH = G::PITCH;
+  constexpr int N = 1 << LOGN;
   int cus = 0;
   CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0));
   const int C = 1;
@@ -87,19 +86,19 @@ int main()
   FrameParams fp{};
   fp.cascades = C;
   fp.c[0] = {2.0f * 3.14159265358f / s.planeSize, 37.5f, s.g, s.h};
-  unsigned char* buf;
-  const size_t bb = gen4_buffer_bytes(LOGN, C), rt = gen4_row_texels(LOGN, C);
-  CHECK(hipMalloc(&buf, bb));
-  float4 *rab, *rde, *rc;
-  CHECK(hipMalloc(&rab, rt * 16));
-  CHECK(hipMalloc(&rde, rt * 16));
-  CHECK(hipMalloc(&rc, rt * 8));
+  // whole grid (P = 1): step 1 into the parts, step 2 into the one exchange block
+  const Gen4Geom g = gen4_geom(LOGN, C, 0, 1, true);
+  const int KP = g.cols + g.nyq, PITCH = g.lp;
+  unsigned char *buf, *blk;
+  const size_t part = (size_t)C * N * PITCH;  // texels per part
+  CHECK(hipMalloc(&buf, gen4_parts_bytes(LOGN, C, g)));
+  CHECK(hipMalloc(&blk, g.blk_bytes));
+  const size_t rt = (size_t)C * g.w * PITCH;  // texels per block field
   float2 *tw = table(LOGN), *tw2 = table(LOGN2);
   const int items1 = C * ((KP + 63) / 64) * (N / 64);
   auto s1 = [&](auto kern) {
-    return [=] { hipLaunchKernelGGL(kern, dim3(items1), dim3(256), 0, 0, fp, h0, buf, tw); };
+    return [=] { hipLaunchKernelGGL(kern, dim3(items1), dim3(256), 0, 0, fp, g, h0, buf, tw); };
   };
-  const size_t part = rt;
   const float4* wab = reinterpret_cast<const float4*>(buf);
   auto s2 = [&](auto kp, auto kc, int ci) {
     const int lds = ((FftShape<LOGN2>::TW_ENTRIES * 8 + 15) / 16) * 16 + ci * FftShape<LOGN2>::PADDED * 8;
@@ -108,11 +107,12 @@ int main()
     const int gpn = C * 16 * ((KP + ci - 1) / ci), gcn = C * 16 * (((KP + 1) / 2 + ci - 1) / ci);
     const int wg = FftShape<LOGN2>::T * ci;
     return [=] {
-      hipLaunchKernelGGL(kp, dim3(gpn), dim3(wg), lds, 0, C, KP, PITCH, wab, rab, tw2);
-      hipLaunchKernelGGL(kp, dim3(gpn), dim3(wg), lds, 0, C, KP, PITCH, wab + part, rde, tw2);
-      hipLaunchKernelGGL(kc, dim3(gcn), dim3(wg), lds, 0, C, (KP + 1) / 2, PITCH / 2, wab + 2 * part, rc, tw2);
+      hipLaunchKernelGGL(kp, dim3(gpn), dim3(wg), lds, 0, C, KP, PITCH, wab, blk, (size_t)0, g, tw2);
+      hipLaunchKernelGGL(kp, dim3(gpn), dim3(wg), lds, 0, C, KP, PITCH, wab + part, blk, 16 * rt, g, tw2);
+      hipLaunchKernelGGL(kc, dim3(gcn), dim3(wg), lds, 0, C, (KP + 1) / 2, PITCH / 2, wab + 2 * part, blk, 32 * rt, g, tw2);
     };
   };
+  float4* rab = reinterpret_cast<float4*>(blk);
   struct V
   {
     std::string name;
@@ -126,8 +126,8 @@ int main()
       {"step 1, min 2 waves/SIMD", s1(k_gen4_step1<LOGN, 2>), 28 * pts, {}},
       {"step 1, min 3 waves/SIMD", s1(k_gen4_step1<LOGN, 3>), 28 * pts, {}},
       {"step 1, min 4 waves/SIMD", s1(k_gen4_step1<LOGN, 4>), 28 * pts, {}},
-      {"step 2, 16 columns/WG (production)", s2(k_gen4_step2<LOGN2, true>, k_gen4_step2<LOGN2, false>, 16), 40 * pts, {}},
-      {"step 2, 8 columns/WG, 2 WG/CU", s2(k_gen4_step2<LOGN2, true, 8>, k_gen4_step2<LOGN2, false, 8>, 8), 40 * pts, {}},
+      {"step 2, 8 columns/WG, 2 WG/CU (production)", s2(k_gen4_step2<LOGN2, true, 8>, k_gen4_step2<LOGN2, false, 8>, 8), 40 * pts, {}},
+      {"step 2, 16 columns/WG", s2(k_gen4_step2<LOGN2, true>, k_gen4_step2<LOGN2, false>, 16), 40 * pts, {}},
       {"step 2, 4 columns/WG", s2(k_gen4_step2<LOGN2, true, 4>, k_gen4_step2<LOGN2, false, 4>, 4), 40 * pts, {}},
   };
   // identity: each variant's output vs the first of its step
@@ -154,7 +154,7 @@ int main()
     CHECK(hipMemset(rab, 0, rt * 16));
     vs[k].run();
     CHECK(hipDeviceSynchronize());
-    std::printf("%s: rm_ab %s\n", vs[k].name.c_str(), snap(rab, rt * 16) == ref2 ? "bit-identical" : "DIFFER");
+    std::printf("%s: block gab %s\n", vs[k].name.c_str(), snap(rab, rt * 16) == ref2 ? "bit-identical" : "DIFFER");
   }
   for (int r = 0; r < 5; r++)
     for (auto& v : vs)

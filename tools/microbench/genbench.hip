@@ -1,6 +1,6 @@
 // genbench.hip — interleaved A/B timing of the generator frame passes (8 cascades x 4096^2).
 // Build: see Makefile target `microbench`.
-#include "../../oceansimulation_amd/csrc/ocean_kernels.hip"
+#include "all_kernels.h"
 
 #include <algorithm>
 #include <cmath>
@@ -104,8 +104,8 @@ int main(int argc, char** argv)
     CHECK(hipMalloc(&ge, ht * sizeof(float2)));
     CHECK(hipMalloc(&spec, (size_t)C * 2 * n * sizeof(float4)));
   }
-  auto h1 = [&] { return launch_half_columns(logn, fp, h0, gab, gcd, ge, spec, tw, 0, cus); };
-  auto h2 = [&] { return launch_half_rows(logn, fp, gab, gcd, ge, spec, maps, jac, foam, tw, 0, cus); };
+  auto h1 = [&] { return launch_half_columns_ab(logn, fp, h0, gab, gcd, ge, spec, tw, 0, cus); };
+  auto h2 = [&] { return launch_half_rows_ab(logn, fp, gab, gcd, ge, spec, maps, jac, foam, tw, 0, cus); };
   auto p1r = [&] { return launch_cols_evolve(logn, fp, geom, h0, inter, tw, 0, cus, 0); };
   auto p1k = [&] { return launch_cols_evolve(logn, fp, geom, h0, inter, tw, 0, cus, 16); };
   auto p1h = [&] { return launch_cols_evolve(logn, fp, geom, h0, inter, tw, 0, cus, default_keep(logn)); };
@@ -180,7 +180,7 @@ int main(int argc, char** argv)
     {
       static const char* names[] = {"", "half pass2 no HBM loads", "half pass2 no FFT", "half pass2 no mirror exchange",
                                     "half pass2 4 rows per WG (1 WG/CU)", "half pass2 1 row per WG (4 WG/CU)"};
-      auto ha = [&] { return launch_half_rows(logn, fp, gab, gcd, ge, spec, maps, jac, foam, tw, 0, cus, a); };
+      auto ha = [&] { return launch_half_rows_ab(logn, fp, gab, gcd, ge, spec, maps, jac, foam, tw, 0, cus, a); };
       std::vector<float> ta;
       for (int r = 0; r < rounds; r++)
         ta.push_back(time_ms(ha, reps));

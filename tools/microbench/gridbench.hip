@@ -4,7 +4,7 @@
 // (all CUs available); g_force_persistent gives the persistent grid of the same kernel.
 // Also times the in-place EncodeIFFT passes at 8192 and 16384 (rows then columns).
 // Usage: gridbench
-#include "../../oceansimulation_amd/csrc/ocean_kernels.hip"
+#include "all_kernels.h"
 
 #include <algorithm>
 #include <cmath>
@@ -258,6 +258,7 @@ int main()
     CHECK(hipMalloc(&maps, (size_t)n * n * 2 * 16));
     CHECK(hipMalloc(&jac, (size_t)n * n * 4));
     float2* tw = make_twiddles(logn);
+    float2* tw2 = make_twiddles(logn - 4);  // the XS row pass's N/16-point table
     FrameParams fp{};
     fp.cascades = 1;
     fp.c[0] = {2.0f * 3.14159265358f / 1000.0f, 37.5f, 9.8f, 100.0f};
@@ -266,9 +267,9 @@ int main()
     const double pts = (double)n * n;
     std::vector<Case> cs = {
         {"16384 transposes + rows persistent (round-1 default)", 96.0 * pts,
-         [&] { return persist([&] { return launch_half_slab_rows(logn, fp, hsl, recv, rab, rde, rc, maps, jac, foam, tw, 0, cus); }); }},
+         [&] { return persist([&] { return launch_half_slab_rows(logn, fp, hsl, recv, rab, rde, rc, maps, jac, foam, tw, tw2, 0, cus); }); }},
         {"16384 transposes + rows one-shot", 96.0 * pts,
-         [&] { return launch_half_slab_rows(logn, fp, hsl, recv, rab, rde, rc, maps, jac, foam, tw, 0, BIG); }},
+         [&] { return launch_half_slab_rows(logn, fp, hsl, recv, rab, rde, rc, maps, jac, foam, tw, tw2, 0, BIG); }},
     };
     run_cases(cs, 5, 3);
   }

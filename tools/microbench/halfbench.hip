@@ -1,7 +1,7 @@
 // halfbench.hip — interleaved A/B timing of half-spectrum frame-pass variants (8 cascades x 4096^2),
 // with a bit-identity check of every variant's output against the baseline variant.
 // Build: see Makefile target `microbench`. Usage: halfbench [logn] [cascades] [quick|mall|rows|overlap|rowabl|hpair]
-#include "../../oceansimulation_amd/csrc/ocean_kernels.hip"
+#include "all_kernels.h"
 
 #include <algorithm>
 #include <cmath>
@@ -108,11 +108,11 @@ int main(int argc, char** argv)
   CHECK(hipDeviceSynchronize());
   const double pts = (double)tex * C;
 
-  auto c0 = [&] { return launch_half_columns(logn, fp, h0, gab, gcd, ge, spec, tw, 0, cus); };
-  auto c1 = [&] { return launch_half_columns(logn, fp, h0, gab, gcd, ge, spec, tw, 0, cus, hs, cus); };
-  auto r0 = [&] { return launch_half_rows(logn, fp, gab, gcd, ge, spec, maps, jac, foam, tw, 0, cus, 6); };
-  auto r1 = [&] { return launch_half_rows(logn, fp, gab, gcd, ge, spec, maps, jac, foam, tw, 0, cus); };
-  auto r2 = [&] { return launch_half_rows(logn, fp, gab, gcd, ge, spec, maps, jac, foam, tw, 0, cus, 7); };
+  auto c0 = [&] { return launch_half_columns_ab(logn, fp, h0, gab, gcd, ge, spec, tw, 0, cus); };
+  auto c1 = [&] { return launch_half_columns_ab(logn, fp, h0, gab, gcd, ge, spec, tw, 0, cus, hs, cus); };
+  auto r0 = [&] { return launch_half_rows_ab(logn, fp, gab, gcd, ge, spec, maps, jac, foam, tw, 0, cus, 6); };
+  auto r1 = [&] { return launch_half_rows_ab(logn, fp, gab, gcd, ge, spec, maps, jac, foam, tw, 0, cus); };
+  auto r2 = [&] { return launch_half_rows_ab(logn, fp, gab, gcd, ge, spec, maps, jac, foam, tw, 0, cus, 7); };
 
   // bit identity: baseline frame, then each variant on the same inputs (float compare, NaN-aware)
   const size_t mb = tex * C * 2 * sizeof(float4), jb = tex * C * sizeof(float);
@@ -173,7 +173,7 @@ int main(int argc, char** argv)
     CHECK(hipDeviceSynchronize());
     auto pm = snap(maps, mb), pj = snap(jac, jb);
     CHECK(hipMemset(maps, 0, mb));
-    auto r15 = [&] { return launch_half_rows(logn, fp, gab, gcd, ge, spec, maps, jac, foam, tw, 0, cus, 15); };
+    auto r15 = [&] { return launch_half_rows_ab(logn, fp, gab, gcd, ge, spec, maps, jac, foam, tw, 0, cus, 15); };
     CHECK(r15());
     CHECK(hipDeviceSynchronize());
     std::printf("row layout vs interleaved rows:\n");
@@ -194,7 +194,7 @@ int main(int argc, char** argv)
   {
     // pass 1 with the H scratch in 8-B entries (variant 23, round 2) against production (16-B pairs):
     // bit-identical fields
-    auto cp = [&] { return launch_half_columns(logn, fp, h0, gab, gcd, ge, spec, tw, 0, cus, hs, cus, nullptr, 23); };
+    auto cp = [&] { return launch_half_columns_ab(logn, fp, h0, gab, gcd, ge, spec, tw, 0, cus, hs, cus, nullptr, 23); };
     CHECK(c1());
     CHECK(hipDeviceSynchronize());
     auto pab = snap(gab, ht * sizeof(float4)), pde = snap(gcd, ht * sizeof(float4)), pc = snap(ge, ht * sizeof(float2));
@@ -222,7 +222,7 @@ int main(int argc, char** argv)
   {
     // pass 1 with round 2's (C, 0) CPairs packed as column pairs on half the workgroup (variant 24)
     // against production: bit-identical fields (same per-lane arithmetic)
-    auto cp = [&] { return launch_half_columns(logn, fp, h0, gab, gcd, ge, spec, tw, 0, cus, hs, cus, nullptr, 24); };
+    auto cp = [&] { return launch_half_columns_ab(logn, fp, h0, gab, gcd, ge, spec, tw, 0, cus, hs, cus, nullptr, 24); };
     CHECK(c1());
     CHECK(hipDeviceSynchronize());
     auto pab = snap(gab, ht * sizeof(float4)), pde = snap(gcd, ht * sizeof(float4)), pc = snap(ge, ht * sizeof(float2));
@@ -254,7 +254,7 @@ int main(int argc, char** argv)
     // pass 1 below 4096: grid capped at one H-scratch slice per 1024 threads (production: 1024 / WG1
     // blocks per slice, so 2048 runs two workgroups per CU and 1024 four) against one block per slice
     // (variant 37, round 2's earlier cap); same kernel, same fields
-    auto cp = [&] { return launch_half_columns(logn, fp, h0, gab, gcd, ge, spec, tw, 0, cus, hs, cus, nullptr, 37); };
+    auto cp = [&] { return launch_half_columns_ab(logn, fp, h0, gab, gcd, ge, spec, tw, 0, cus, hs, cus, nullptr, 37); };
     CHECK(c1());
     CHECK(hipDeviceSynchronize());
     auto pab = snap(gab, ht * sizeof(float4)), pde = snap(gcd, ht * sizeof(float4)), pc = snap(ge, ht * sizeof(float2));
@@ -297,7 +297,7 @@ int main(int argc, char** argv)
     {
       CHECK(hipMemset(maps, 0, mb));
       CHECK(hipMemset(jac, 0, jb));
-      CHECK(launch_half_rows(logn, fp, gab, gcd, ge, spec, maps, jac, foam, tw, 0, cus, av[k]));
+      CHECK(launch_half_rows_ab(logn, fp, gab, gcd, ge, spec, maps, jac, foam, tw, 0, cus, av[k]));
       CHECK(hipDeviceSynchronize());
       std::printf("rows variant %d vs production: maps, jacobian\n", av[k]);
       same[k] = (int)diff(snap(maps, mb), pm) & (int)diff(snap(jac, jb), pj);
@@ -305,7 +305,7 @@ int main(int argc, char** argv)
     std::vector<std::vector<float>> t(av.size());
     for (int r = 0; r < 9; r++)
       for (size_t k = 0; k < av.size(); k++)
-        t[k].push_back(time_ms([&] { return launch_half_rows(logn, fp, gab, gcd, ge, spec, maps, jac, foam, tw, 0, cus, av[k]); }, 10));
+        t[k].push_back(time_ms([&] { return launch_half_rows_ab(logn, fp, gab, gcd, ge, spec, maps, jac, foam, tw, 0, cus, av[k]); }, 10));
     for (size_t k = 0; k < av.size(); k++)
     {
       std::sort(t[k].begin(), t[k].end());
@@ -329,8 +329,8 @@ int main(int argc, char** argv)
     for (int v = 1; v < 4; v++)
     {
       CHECK(hipMemset(maps, 0, mb));
-      CHECK(launch_half_columns(logn, fp, h0, gab, gcd, ge, spec, tw, 0, cus, hs, cus, nullptr, cv[v]));
-      CHECK(launch_half_rows(logn, fp, gab, gcd, ge, spec, maps, jac, foam, tw, 0, cus, rv[v]));
+      CHECK(launch_half_columns_ab(logn, fp, h0, gab, gcd, ge, spec, tw, 0, cus, hs, cus, nullptr, cv[v]));
+      CHECK(launch_half_rows_ab(logn, fp, gab, gcd, ge, spec, maps, jac, foam, tw, 0, cus, rv[v]));
       CHECK(hipDeviceSynchronize());
       std::printf("layout %s vs production: maps, jacobian\n", ln[v]);
       same[v] = (int)diff(snap(maps, mb), pm) & (int)diff(snap(jac, jb), pj);
@@ -339,8 +339,8 @@ int main(int argc, char** argv)
     for (int r = 0; r < 9; r++)
       for (int v = 0; v < 4; v++)
       {
-        auto cl = [&] { return launch_half_columns(logn, fp, h0, gab, gcd, ge, spec, tw, 0, cus, hs, cus, nullptr, cv[v]); };
-        auto rl = [&] { return launch_half_rows(logn, fp, gab, gcd, ge, spec, maps, jac, foam, tw, 0, cus, rv[v]); };
+        auto cl = [&] { return launch_half_columns_ab(logn, fp, h0, gab, gcd, ge, spec, tw, 0, cus, hs, cus, nullptr, cv[v]); };
+        auto rl = [&] { return launch_half_rows_ab(logn, fp, gab, gcd, ge, spec, maps, jac, foam, tw, 0, cus, rv[v]); };
         tc[v].push_back(time_ms(cl, 10));
         tr[v].push_back(time_ms(rl, 10));
         tf[v].push_back(time_ms([&] { CHECK(cl()); return rl(); }, 10));
@@ -380,7 +380,7 @@ int main(int argc, char** argv)
     SpectrumConsts* dsc;
     CHECK(hipMalloc(&dsc, C * sizeof(SpectrumConsts)));
     CHECK(hipMemcpy(dsc, sc.data(), C * sizeof(SpectrumConsts), hipMemcpyHostToDevice));
-    auto sv = [&](int v) { return launch_half_columns(logn, fp, h0, gab, gcd, ge, spec, tw, 0, cus, hs, cus, dsc, v); };
+    auto sv = [&](int v) { return launch_half_columns_ab(logn, fp, h0, gab, gcd, ge, spec, tw, 0, cus, hs, cus, dsc, v); };
     CHECK(sv(33));
     CHECK(hipDeviceSynchronize());
     auto pab = snap(gab, ht * sizeof(float4)), pde = snap(gcd, ht * sizeof(float4)), pc = snap(ge, ht * sizeof(float2));
@@ -422,7 +422,7 @@ int main(int argc, char** argv)
       CHECK(hipMemset(gab, 0, ht * sizeof(float4)));
       CHECK(hipMemset(gcd, 0, ht * sizeof(float4)));
       CHECK(hipMemset(ge, 0, ht * sizeof(float2)));
-      CHECK(launch_half_columns(logn, fp, h0, gab, gcd, ge, spec, tw, 0, cus, hs, cus, nullptr, vs[k]));
+      CHECK(launch_half_columns_ab(logn, fp, h0, gab, gcd, ge, spec, tw, 0, cus, hs, cus, nullptr, vs[k]));
       CHECK(hipDeviceSynchronize());
       std::printf("%s vs variant 32: gab, gde, gc\n", nm[k]);
       same[k] = (int)diff(snap(gab, ht * sizeof(float4)), pab) & (int)diff(snap(gcd, ht * sizeof(float4)), pde) &
@@ -432,7 +432,7 @@ int main(int argc, char** argv)
     for (int r = 0; r < 9; r++)
       for (int k = 0; k < NV; k++)
       {
-        auto ck = [&] { return launch_half_columns(logn, fp, h0, gab, gcd, ge, spec, tw, 0, cus, hs, cus, nullptr, vs[k]); };
+        auto ck = [&] { return launch_half_columns_ab(logn, fp, h0, gab, gcd, ge, spec, tw, 0, cus, hs, cus, nullptr, vs[k]); };
         t[k].push_back(time_ms(ck, 10));
         tf[k].push_back(time_ms([&] { CHECK(ck()); return r1(); }, 10));
       }
@@ -456,7 +456,7 @@ int main(int argc, char** argv)
     std::vector<std::vector<float>> tr(4);
     for (int r = 0; r < 7; r++)
       for (int a = 0; a < 4; a++)
-        tr[a].push_back(time_ms([&] { return launch_half_rows(logn, fp, gab, gcd, ge, spec, maps, jac, foam, tw, 0, cus, a); }, 10));
+        tr[a].push_back(time_ms([&] { return launch_half_rows_ab(logn, fp, gab, gcd, ge, spec, maps, jac, foam, tw, 0, cus, a); }, 10));
     for (int a = 0; a < 4; a++)
     {
       std::sort(tr[a].begin(), tr[a].end());
@@ -491,13 +491,13 @@ int main(int argc, char** argv)
           f1.c[k] = fp.c[c0 + k];
           o1.displacement[k] = foam.displacement[c0 + k];
         }
-        hipError_t e = launch_half_columns(logn, f1, h0 + tex * c0, gab + ht1 * c0, gcd + ht1 * c0, ge + ht1 * c0,
+        hipError_t e = launch_half_columns_ab(logn, f1, h0 + tex * c0, gab + ht1 * c0, gcd + ht1 * c0, ge + ht1 * c0,
                                            spec + (size_t)2 * n * c0, tw, sa, cus, hs, cus);
         if (e != hipSuccess)
           return e;
         CHECK(hipEventRecord(ev[g], sa));
         CHECK(hipStreamWaitEvent(sb, ev[g], 0));
-        e = launch_half_rows(logn, f1, gab + ht1 * c0, gcd + ht1 * c0, ge + ht1 * c0, spec + (size_t)2 * n * c0,
+        e = launch_half_rows_ab(logn, f1, gab + ht1 * c0, gcd + ht1 * c0, ge + ht1 * c0, spec + (size_t)2 * n * c0,
                              maps + tex * 2 * c0, jac + tex * c0, o1, tw, sb, cus);
         if (e != hipSuccess)
           return e;
@@ -552,10 +552,10 @@ int main(int argc, char** argv)
         f1.c[0] = fp.c[c];
         FoamParams o1{};
         o1.displacement[0] = foam.displacement[c];
-        hipError_t e = launch_half_columns(logn, f1, h0 + tex * c, gab + ht1 * c, gcd + ht1 * c, ge + ht1 * c,
+        hipError_t e = launch_half_columns_ab(logn, f1, h0 + tex * c, gab + ht1 * c, gcd + ht1 * c, ge + ht1 * c,
                                            spec + (size_t)2 * n * c, tw, 0, cus, hs, cus);
         if (e == hipSuccess)
-          e = launch_half_rows(logn, f1, gab + ht1 * c, gcd + ht1 * c, ge + ht1 * c, spec + (size_t)2 * n * c,
+          e = launch_half_rows_ab(logn, f1, gab + ht1 * c, gcd + ht1 * c, ge + ht1 * c, spec + (size_t)2 * n * c,
                                maps + tex * 2 * c, jac + tex * c, o1, tw, 0, cus);
         if (e != hipSuccess)
           return e;
@@ -593,13 +593,13 @@ int main(int argc, char** argv)
     CHECK(hipMemset(gab, 0, ht * sizeof(float4)));
     CHECK(hipMemset(gcd, 0, ht * sizeof(float4)));
     CHECK(hipMemset(ge, 0, ht * sizeof(float2)));
-    auto c20 = [&] { return launch_half_columns(logn, fp, h0, gab, gcd, ge, spec, tw, 0, cus, hs, cus, nullptr, 20); };
+    auto c20 = [&] { return launch_half_columns_ab(logn, fp, h0, gab, gcd, ge, spec, tw, 0, cus, hs, cus, nullptr, 20); };
     CHECK(c20());
     CHECK(hipDeviceSynchronize());
     std::printf("cols half strips 2/CU vs production: gab, gde, gc\n");
     const bool same20 = (int)diff(snap(gab, ht * sizeof(float4)), pab) & (int)diff(snap(gcd, ht * sizeof(float4)), pde) &
                         (int)diff(snap(ge, ht * sizeof(float2)), pc);
-    auto c22 = [&] { return launch_half_columns(logn, fp, h0, gab, gcd, ge, spec, tw, 0, cus, hs, cus, nullptr, 22); };
+    auto c22 = [&] { return launch_half_columns_ab(logn, fp, h0, gab, gcd, ge, spec, tw, 0, cus, hs, cus, nullptr, 22); };
     CHECK(hipMemset(gab, 0, ht * sizeof(float4)));
     CHECK(hipMemset(gcd, 0, ht * sizeof(float4)));
     CHECK(hipMemset(ge, 0, ht * sizeof(float2)));
@@ -635,12 +635,12 @@ int main(int argc, char** argv)
     // item: launchers called with a huge CU count), same kernels, same results. The H-scratch
     // column pass needs one scratch slice per resident block, so its no-scratch forms stand in.
     const int BIG = 1 << 20;
-    auto rp = [&] { return launch_half_rows(logn, fp, gab, gcd, ge, spec, maps, jac, foam, tw, 0, cus); };
-    auto ro = [&] { return launch_half_rows(logn, fp, gab, gcd, ge, spec, maps, jac, foam, tw, 0, BIG); };
-    auto wp = [&] { return launch_half_columns(logn, fp, h0, gab, gcd, ge, spec, tw, 0, cus, nullptr, 0, nullptr, 0); };
-    auto wo = [&] { return launch_half_columns(logn, fp, h0, gab, gcd, ge, spec, tw, 0, BIG, nullptr, 0, nullptr, 0); };
-    auto hp = [&] { return launch_half_columns(logn, fp, h0, gab, gcd, ge, spec, tw, 0, cus, nullptr, 0, nullptr, 12); };
-    auto ho = [&] { return launch_half_columns(logn, fp, h0, gab, gcd, ge, spec, tw, 0, BIG, nullptr, 0, nullptr, 12); };
+    auto rp = [&] { return launch_half_rows_ab(logn, fp, gab, gcd, ge, spec, maps, jac, foam, tw, 0, cus); };
+    auto ro = [&] { return launch_half_rows_ab(logn, fp, gab, gcd, ge, spec, maps, jac, foam, tw, 0, BIG); };
+    auto wp = [&] { return launch_half_columns_ab(logn, fp, h0, gab, gcd, ge, spec, tw, 0, cus, nullptr, 0, nullptr, 0); };
+    auto wo = [&] { return launch_half_columns_ab(logn, fp, h0, gab, gcd, ge, spec, tw, 0, BIG, nullptr, 0, nullptr, 0); };
+    auto hp = [&] { return launch_half_columns_ab(logn, fp, h0, gab, gcd, ge, spec, tw, 0, cus, nullptr, 0, nullptr, 12); };
+    auto ho = [&] { return launch_half_columns_ab(logn, fp, h0, gab, gcd, ge, spec, tw, 0, BIG, nullptr, 0, nullptr, 12); };
     const char* nm[] = {"rows persistent", "rows one-shot", "cols re-evolve persistent", "cols re-evolve one-shot",
                         "cols half2 persistent", "cols half2 one-shot"};
     std::vector<std::vector<float>> tt(6);
@@ -668,7 +668,7 @@ int main(int argc, char** argv)
     std::vector<std::vector<float>> tv(4);
     for (int r = 0; r < 7; r++)
       for (int v = 0; v < 4; v++)
-        tv[v].push_back(time_ms([&] { return launch_half_columns(logn, fp, h0, gab, gcd, ge, spec, tw, 0, cus, hs, cus,
+        tv[v].push_back(time_ms([&] { return launch_half_columns_ab(logn, fp, h0, gab, gcd, ge, spec, tw, 0, cus, hs, cus,
                                                                  nullptr, v); }, 10));
     for (int v = 0; v < 4; v++)
     {
@@ -692,8 +692,8 @@ int main(int argc, char** argv)
     {
       CHECK(hipMemset(maps, 0, mb));
       CHECK(hipMemset(jac, 0, jb));
-      CHECK(launch_half_columns(logn, fp, h0, gab, gcd, ge, spec, tw, 0, cus, hs, cus, nullptr, cv[v]));
-      CHECK(launch_half_rows(logn, fp, gab, gcd, ge, spec, maps, jac, foam, tw, 0, cus, rv[v]));
+      CHECK(launch_half_columns_ab(logn, fp, h0, gab, gcd, ge, spec, tw, 0, cus, hs, cus, nullptr, cv[v]));
+      CHECK(launch_half_rows_ab(logn, fp, gab, gcd, ge, spec, maps, jac, foam, tw, 0, cus, rv[v]));
       CHECK(hipDeviceSynchronize());
       std::printf("%s vs production frame:\n", ln[v]);
       same[v] = (int)diff(snap(maps, mb), pm) & (int)diff(snap(jac, jb), pj);
@@ -702,8 +702,8 @@ int main(int argc, char** argv)
     for (int r = 0; r < 7; r++)
       for (int v = 0; v < NV; v++)
       {
-        auto cl = [&] { return launch_half_columns(logn, fp, h0, gab, gcd, ge, spec, tw, 0, cus, hs, cus, nullptr, cv[v]); };
-        auto rl = [&] { return launch_half_rows(logn, fp, gab, gcd, ge, spec, maps, jac, foam, tw, 0, cus, rv[v]); };
+        auto cl = [&] { return launch_half_columns_ab(logn, fp, h0, gab, gcd, ge, spec, tw, 0, cus, hs, cus, nullptr, cv[v]); };
+        auto rl = [&] { return launch_half_rows_ab(logn, fp, gab, gcd, ge, spec, maps, jac, foam, tw, 0, cus, rv[v]); };
         tc[v].push_back(time_ms(cl, 10));
         tr[v].push_back(time_ms(rl, 10));
         tf[v].push_back(time_ms([&] { hipError_t e = cl(); return e == hipSuccess ? rl() : e; }, 10));

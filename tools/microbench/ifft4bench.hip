@@ -3,7 +3,7 @@
 // transform through a work slab of wc columns (k_cols4_step1/2), timed interleaved; the two results
 // are compared (relative max error per image; the factorisations differ, so not bit-identical).
 // Usage: ifft4bench
-#include "../../oceansimulation_amd/csrc/ocean_kernels.hip"
+#include "all_kernels.h"
 
 #include <algorithm>
 #include <cmath>

@@ -1,7 +1,7 @@
 // ifftbench.hip — the standalone EncodeIFFT's strided column pass (k_cols_to_blocks, 8 packed 4096^2
 // images read in 64-B row pieces) under load cache policy x XCD grouping of adjacent strips, and the
 // row pass that follows, timed interleaved in one process. Output checked identical across variants.
-#include "../../oceansimulation_amd/csrc/ocean_kernels.hip"
+#include "all_kernels.h"
 
 #include <algorithm>
 #include <cstring>

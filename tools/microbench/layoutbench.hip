@@ -3,7 +3,7 @@
 // (pass 1 writes 64-B halves of 128-B block rows, two workgroups per block paired on one XCD;
 // pass 2 reads 512-B runs). No arithmetic: loads, stores and the same lane maps as the kernels.
 // 8 cascades x 4096^2, h0 16 B/pt, intermediate 32 B/pt, maps 32 B/pt + Jacobian 4 B/pt.
-#include "../../oceansimulation_amd/csrc/ocean_kernels.hip"
+#include "all_kernels.h"
 
 #include <algorithm>
 #include <cstdio>

@@ -4,7 +4,7 @@
 // loads (ABL 1), no x transform (ABL 2). Ablated outputs are wrong by construction. Builds with
 // -DOCEAN_ABLATE_EXCHANGE / -DOCEAN_ABLATE_BARRIER price the exchanges and barriers.
 // Usage: rm16bench
-#include "../../oceansimulation_amd/csrc/ocean_kernels.hip"
+#include "all_kernels.h"
 
 #include <algorithm>
 #include <cmath>
@@ -76,9 +76,8 @@ static float2* table(int logn)
 int main()
 {
   constexpr int LOGN = 14;
-  using G = Gen4Cfg<LOGN>;
   using S = FftShape<LOGN>;
-  constexpr int N = G::N, PITCH = G::PITCH;
+  constexpr int N = 1 << LOGN, PITCH = N / 2 + 16;  // the four-step path's row pitch at P = 1
   const int C = 1;
   const size_t rt = (size_t)N * PITCH;
   float4 *rab, *rde, *spec, *maps;
@@ -103,11 +102,13 @@ int main()
   float2* tw = table(LOGN);
   float2* tw2 = table(LOGN - 4);
   const int lds = ((S::TW_ENTRIES * 8 + 15) / 16) * 16 + lds_row_slots<LOGN>(1) * 8;
+  const RowSrc rs{reinterpret_cast<const unsigned char*>(rab), reinterpret_cast<const unsigned char*>(rde),
+                  reinterpret_cast<const unsigned char*>(rc), 0, N / 2, PITCH, 0};
   auto mk = [&](auto kern, int per = 1) {
     CHECK(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, lds));
     return [=] {
       hipLaunchKernelGGL(kern, dim3(C * N * per), dim3(S::T), lds, 0, fp, rab, rde, rc, spec, maps, jac, foam, tw, N,
-                         PITCH, (const float2*)nullptr);
+                         rs, (const float2*)nullptr);
     };
   };
   struct V
@@ -120,7 +121,7 @@ int main()
     CHECK(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, XsCfg<LOGN>::LDS));
     return [=] {
       hipLaunchKernelGGL(kern, dim3(C * N), dim3(S::T), XsCfg<LOGN>::LDS, 0, fp, rab, rde, rc, spec, maps, jac, foam, tw,
-                         N, PITCH, tw2);
+                         N, rs, tw2);
     };
   };
   std::vector<V> vs = {

@@ -3,7 +3,7 @@
 // row-major [R][K] float4 image (R = 16384 rows, 16 B per row); `group` consecutive columns are given
 // to workgroups of one XCD that run concurrently (blocks b, b+8, ... under round-robin placement), so
 // a 128-B line is covered by 8 workgroups' pieces. Compared with contiguous streams of the same bytes.
-#include "../../oceansimulation_amd/csrc/ocean_kernels.hip"
+#include "all_kernels.h"
 
 #include <cstdio>
 #include <cstdlib>

@@ -2,7 +2,7 @@
 // in [strip][row] (8193 strips x 16384 rows of float4, strip-major) -> out [row][strip] (row-major).
 // Each tile is TU strips x TY rows through LDS; reads are TY-texel runs per strip, writes TU-texel
 // runs per row. BATCH: all loads issued before the LDS writes.
-#include "../../oceansimulation_amd/csrc/ocean_kernels.hip"
+#include "all_kernels.h"
 
 #include <cstdio>
 #include <cstdlib>

@@ -18,10 +18,10 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def device_source_sha256(root=ROOT):
-    """Hash of the device code the kernels are built from (ocean_kernels.hip + device/*.h, sorted):
+    """Hash of the device code the kernels are built from (csrc/*.hip, csrc/*.h, device/*.h, sorted):
     bench.py takes roofline.traffic only from a summary whose hash equals the running tree's."""
     csrc = os.path.join(root, "oceansimulation_amd", "csrc")
-    files = [os.path.join(csrc, "ocean_kernels.hip"), os.path.join(csrc, "ocean_internal.h")]
+    files = sorted(os.path.join(csrc, f) for f in os.listdir(csrc) if f.endswith(".hip") or f.endswith(".h"))
     files += sorted(os.path.join(csrc, "device", f) for f in os.listdir(os.path.join(csrc, "device")) if f.endswith(".h"))
     h = hashlib.sha256()
     for f in files:

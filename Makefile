@@ -34,7 +34,7 @@ $(CSRC)/build/ocean_capi.o: $(CSRC)/ocean_capi.cpp $(CSRC)/ocean_internal.h incl
 	$(HIPCC) $(HIPFLAGS) -x hip -c $< -o $@
 
 $(LIB): $(KERNEL_OBJS) $(CSRC)/build/ocean_capi.o
-	$(HIPCC) --offload-arch=$(ARCH) -shared -o $@ $^ -Wl,-soname,liboceanfft.so
+	$(HIPCC) --offload-arch=$(ARCH) -shared -o $@ $^ -Wl,-soname,liboceanfft.so -L/opt/rocm/lib -lrccl
 
 # C++ drop-in layer (Waves::FFTCalculator / Waves::Generator / Vision::RenderDevice shim) over the C ABI.
 WAVES_SRC := $(CSRC)/waves/RenderDevice.cpp $(CSRC)/waves/FFTCalculator.cpp $(CSRC)/waves/Generator.cpp \

@@ -6,9 +6,11 @@ cascade a rank owns: h(k,t) evolution + packing, two packed 2D inverse FFTs (4 c
 Jacobian, i.e. the full reference payload. h0 is seeded in warm-up and, as in the reference API
 (src/Generator.h:39-45), only regenerated on a settings change; its cost is reported separately.
 
-Workload (BASELINE.json configs[3], per GPU): 8 independent 4096^2 cascades, default settings, plane
-sizes 5/17/101/251/509/1021/2039/4093 m (extending src/Waves.cpp:27). Ranks own disjoint cascade
-sets (seed offset 4097*rank: non-overlapping noise tiles) — weak scaling, no data-path collective.
+Workload (BASELINE.json configs[3]): 8 independent 4096^2 cascades, default
+settings, plane sizes 5/17/101/251/509/1021/2039/4093 m (extending src/Waves.cpp:27), all 8 batched on
+1 GPU and 8/N per GPU on N GPUs (strong scaling: the same 8 cascades whatever N; no data-path
+collective). The weak-scaling leg (8 cascades per GPU, seeds offset 4097*rank: disjoint noise tiles)
+is reported beside it under "weak_scaling".
 
 Launch: python bench.py [--gpus N --steps K --warmup W], one rank per GPU. Under torch.distributed.run
 (WORLD_SIZE set) the process is one rank. Started directly with --gpus N > 1, it first checks that N
@@ -56,7 +58,8 @@ def parse(argv=None):
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--n", type=int, default=4096, help="grid side N")
-    ap.add_argument("--cascades", type=int, default=8, help="cascades per GPU")
+    ap.add_argument("--cascades", type=int, default=8,
+                    help="cascades of the whole job (strong scaling: split over the GPUs; weak leg: per GPU)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="target CPU-baseline sample length")
     ap.add_argument("--no-profile", action="store_true", help="skip per-kernel HIP event timing")
@@ -187,7 +190,19 @@ def sync():
 
 
 def cascade_settings(rank: int, c: int) -> dict:
+    """Settings of cascade c of the weak-scaling leg's rank `rank`; rank 0's are the job's global
+    cascades (the strong-scaling headline: global cascade c = cascade_settings(0, c))."""
     return dict(planeSize=PLANES[c % len(PLANES)], seed=(12342 + 4097 * rank, 8934 + 4097 * (c // len(PLANES))))
+
+
+def rank_cascades(total: int, rank: int, world: int) -> list:
+    """Global cascades rank `rank` owns when `total` cascades are split over `world` GPUs (strong
+    scaling, SURVEY §8d config 4: all 8 on 1 GPU, 8/P per GPU at P = 2, 4, 8): contiguous, disjoint,
+    together all of them."""
+    if total % world != 0:
+        raise ValueError(f"{total} cascades do not split evenly over {world} GPUs")
+    per = total // world
+    return list(range(rank * per, rank * per + per))
 
 
 def device_source_sha256(root: str = "") -> str:
@@ -295,14 +310,8 @@ def host_cores():
     return max(1, threads), machine, affinity
 
 
-def cpu_baseline(n: int, target_s: float):
-    """The oracle (CPU restatement of the reference FFTCalculator/Generator) on the host cores this
-    process has (host_cores())."""
-    from oracle import oracle as O
-
-    O.build()
-    threads, machine, affinity = host_cores()
-    O.set_threads(threads)
+def _oracle_frames(O, n: int, target_s: float, max_frames: int = 50):
+    """Frames of the oracle's CalculateOcean (1 cascade, L = 5 m) for about target_s seconds, at least one."""
     g = O.OracleGenerator(n, O.default_settings(planeSize=PLANES[0]))
     g.calculate_ocean(1.0 / 60.0)  # seeds h0 (excluded, like the GPU warm-up)
     frames, t0 = 0, time.perf_counter()
@@ -310,20 +319,93 @@ def cpu_baseline(n: int, target_s: float):
         g.calculate_ocean(1.0 / 60.0)
         frames += 1
         el = time.perf_counter() - t0
-        if el >= target_s or frames >= 50:
-            break
+        if el >= target_s or frames >= max_frames:
+            return frames, el
+
+
+def cpu_baseline(n: int, target_s: float):
+    """The oracle (CPU restatement of the reference FFTCalculator/Generator) on the host cores this
+    process has (host_cores()), and on one thread (single-threaded and all-cores)."""
+    from oracle import oracle as O
+
+    O.build()
+    threads, machine, affinity = host_cores()
+    O.set_threads(threads)
+    frames, el = _oracle_frames(O, n, target_s)
+    cores = O.get_threads()
+    O.set_threads(1)
+    frames1, el1 = _oracle_frames(O, n, target_s)
+    O.set_threads(threads)
     return {
         "value": n * n * frames / el,
         "unit": "height-field points/s",
-        "cores": O.get_threads(),
+        "cores": cores,
         "host_cpus": machine,
         "affinity_cpus": affinity,
         "cores_note": "cores = OpenMP threads used = this process's CPU share (OMP_NUM_THREADS, else the "
                       "affinity mask); host_cpus = os.cpu_count() of the whole machine",
         "kind": "port",
         "sample": f"1 cascade {n}x{n}, {frames} frames of CalculateOcean (fp32 radix-2 restatement of "
-                  f"src/FFTCalculator.cpp + spectrum.compute, OpenMP {O.get_threads()} threads), {el:.1f} s",
+                  f"src/FFTCalculator.cpp + spectrum.compute, OpenMP {cores} threads), {el:.1f} s",
+        "single_thread": {"value": n * n * frames1 / el1, "cores": 1,
+                          "sample": f"1 cascade {n}x{n}, {frames1} frame(s) of CalculateOcean on 1 thread, {el1:.1f} s"},
     }
+
+
+def timed_frames(gen, steps: int, dt: float, world: int):
+    """Wall time of `steps` CalculateOcean calls, barrier + synchronize on both sides, max over ranks."""
+    sync()
+    barrier(world)
+    sync()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        gen.CalculateOcean(dt)
+    sync()
+    barrier(world)
+    sync()
+    return max_over_ranks(time.perf_counter() - t0, world)
+
+
+def weak_leg(ocean, fft, args, rank: int, world: int, dt: float) -> dict:
+    """Weak scaling (secondary): every rank runs its own args.cascades cascades (seeds offset 4097 *
+    rank, disjoint noise tiles), so the job grows with N; value = all ranks' points / max time."""
+    n, C = args.n, args.cascades
+    gen = ocean.Generator(fft, C)
+    for c in range(C):
+        ocean.apply_settings(gen.GetOceanSettings(c), **cascade_settings(rank, c))
+    for _ in range(max(args.warmup, 2)):
+        gen.CalculateOcean(dt)
+    el = timed_frames(gen, args.steps, dt, world)
+    gen.close()
+    return {"what": f"{C} cascades of {n}^2 per GPU (the job grows with the GPU count)", "cascades_per_gpu": C,
+            "ms_per_step": 1000.0 * el / args.steps, "points_per_s": float(n) * n * C * world * args.steps / el}
+
+
+def one_cascade_leg(ocean, fft, args, dt: float) -> dict:
+    """The P = 8 point of the strong-scaling headline on one GPU: ONE 4096^2 cascade per frame (what
+    each of 8 GPUs runs when the 8 cascades are split 1 per GPU; src/Waves.cpp:20-39 runs one generator
+    per cascade). Launch tails weigh more than in the 8-cascade batch."""
+    n = args.n
+    gen = ocean.Generator(fft, 1)
+    ocean.apply_settings(gen.GetOceanSettings(0), **cascade_settings(0, 0))
+    for _ in range(max(args.warmup, 2)):
+        gen.CalculateOcean(dt)
+    steps = max(args.steps, 20)
+    el = timed_frames(gen, steps, dt, 1)
+    gen.set_profiling(True)
+    gen.kernel_times()
+    for _ in range(steps):
+        gen.CalculateOcean(dt)
+    ms, cnt = gen.kernel_times()
+    b = sum(gen.frame_bytes())
+    gen.close()
+    frame_ms = 1000.0 * el / steps
+    passes_ms = ms[1] / max(cnt[1], 1) + ms[2] / max(cnt[2], 1)
+    return {"what": f"1 cascade of {n}^2 per frame (the per-GPU share at 8 GPUs)",
+            "one_cascade_ms": frame_ms, "one_cascade_passes_ms": passes_ms,
+            "points_per_s": float(n) * n / (frame_ms * 1e-3),
+            "frac_hbm_peak": b * n * n / (frame_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
+            "frame_hbm_bytes_per_point": b}
 
 
 def ifft_legs(n: int, cascades: int, calls: int = 6) -> dict:
@@ -452,25 +534,31 @@ def surface_leg(calls: int = 20, cpu_seconds: float = 3.0) -> dict:
 
 def slab_grid(args, rank: int, world: int, local: int) -> dict:
     """BASELINE configs[4]: one N x N grid (default 16384^2, full payload) split over the ranks.
-    Column pass on a column slab, one equal-split RCCL all-to-all (torch all_to_all_single on the
-    "nccl" backend), row pass on a row slab. At world == 1 the whole grid runs on one GPU with no
-    exchange: the scaling denominator.
-    With an exchange, two legs are timed: serial frames (columns, all-to-all, rows) and the
-    SlabPipeline (frame f's all-to-all beside frame f+1's column pass and frame f-1's row pass,
-    passes sized for all CUs but --slab-reserve-cus). The headline is the pipelined rate."""
+    Column pass on the rank's kept columns (four-step, destination-block order), one equal-split
+    all-to-all, row pass on the rank's row slab straight from the received blocks. With RCCL
+    (backend "nccl") the exchange is the library's own (ocean_generator_slab_frame: grouped ncclSend /
+    ncclRecv inside the C ABI); the --shared-gpu rehearsal uses torch's gloo all_to_all_single, host
+    staged. At world == 1 the whole grid runs on one GPU with no exchange: the scaling denominator.
+    With an exchange, serial frames (columns, all-to-all, rows) and pipelined frames (frame f's
+    all-to-all beside frame f+1's column pass and frame f-1's row pass, passes sized for all CUs but
+    --slab-reserve-cus) are timed; the headline is the better of the two. The all-to-all alone is timed
+    with torch's all_to_all_single of the same size (the achieved per-rank exchange rate)."""
     import torch
     import torch.distributed as dist
 
     import oceansimulation_amd as ocean
-    from oceansimulation_amd.slab import SlabGenerator, SlabPipeline, TorchExchange, TorchExchangeSlots
+    from oceansimulation_amd.slab import (RcclComm, SlabGenerator, SlabPipeline, TorchExchange, TorchExchangeSlots,
+                                          torch_share_id)
 
     n = args.slab_n
     exchange = world > 1 or (args.slab_force_exchange and dist.is_available() and dist.is_initialized())
+    native = exchange and dist.get_backend() == "nccl"
     device = torch.device("cuda", local)
     fft = ocean.FFTCalculator(n)
     g = SlabGenerator(fft, rank, world)
     if args.full_spectrum:
         g.set_half_spectrum(False)
+    comm = RcclComm(rank, world, torch_share_id) if native else None
 
     def timed(run_steps):
         sync()
@@ -484,10 +572,12 @@ def slab_grid(args, rank: int, world: int, local: int) -> dict:
         return max_over_ranks(time.perf_counter() - t0, world)
 
     # ---- serial frames ----
-    ex = TorchExchange(g.exchange_bytes, device) if exchange else None
+    ex = TorchExchange(g.exchange_bytes, device) if exchange and not native else None
 
     def frame(dt, update=False):
-        if ex is None:
+        if comm is not None:
+            g.frame(comm, dt, update)
+        elif ex is None:
             g.columns(dt, update)
             g.rows_pass()
         else:
@@ -495,7 +585,7 @@ def slab_grid(args, rank: int, world: int, local: int) -> dict:
             ex()
             g.rows_pass(ex.recv.data_ptr())
 
-    frame(1.0 / 60.0, update=True)  # seeds this rank's h0 column slab
+    frame(1.0 / 60.0, update=True)  # seeds this rank's h0 columns
     frame(1.0 / 60.0)
     g.set_profiling(True)
     g.kernel_times()
@@ -511,9 +601,9 @@ def slab_grid(args, rank: int, world: int, local: int) -> dict:
     out = {
         "config": f"single {n}x{n} grid, full payload, slab-decomposed over {world} GPU(s)",
         "ranks": world,
-        "exchange": (("rccl all_to_all_single" if dist.get_backend() == "nccl" else
-                      f"{dist.get_backend()} all_to_all_single, host-staged (rehearsal, not a measurement)")
-                     if exchange else "none (one rank)"),
+        "exchange": ("rccl: ocean_generator_slab_frame (grouped ncclSend / ncclRecv in the C ABI)" if native else
+                     f"{dist.get_backend()} all_to_all_single, host-staged (rehearsal, not a measurement)" if exchange
+                     else "none (one rank)"),
         "column_pass_ms": ms[1] / max(cnt[1], 1),
         "row_pass_ms": ms[2] / max(cnt[2], 1),
         "frame_path": ("full spectrum" if args.full_spectrum else
@@ -524,16 +614,19 @@ def slab_grid(args, rank: int, world: int, local: int) -> dict:
         "serial_ms_per_frame": 1000.0 * el / per,
     }
     out["serial_exchange_and_gaps_ms"] = out["serial_ms_per_frame"] - out["column_pass_ms"] - out["row_pass_ms"]
-    if ex is not None:
+    if exchange:
         # the all-to-all alone (no passes): the achieved per-rank exchange rate over xGMI
+        xo = ex if ex is not None else TorchExchange(g.exchange_bytes, device)
+
         def exchange_steps():
             for _ in range(per):
-                ex()
+                xo()
 
         el = timed(exchange_steps)
         out["exchange_only_ms"] = 1000.0 * el / per
         moved = g.exchange_bytes * (world - 1) // world if world > 1 else g.exchange_bytes
         out["exchange_GBps_per_rank"] = moved / (el / per) / 1e9
+        del xo
     del ex
     torch.cuda.empty_cache()
 
@@ -541,30 +634,95 @@ def slab_grid(args, rank: int, world: int, local: int) -> dict:
     if exchange:
         reserve = max(0, min(args.slab_reserve_cus, fft.cus - 1))
         fft.set_cu_budget(fft.cus - reserve)
-        slots = TorchExchangeSlots(g.exchange_bytes, device)
-        sends, recvs = slots.ptrs()
-        pipe = SlabPipeline([g], sends, recvs, slots)
+        if comm is not None:
+            step = lambda: g.frame_pipelined(comm, 1.0 / 60.0)  # noqa: E731
+            flush = g.flush
+        else:
+            slots = TorchExchangeSlots(g.exchange_bytes, device)
+            sends, recvs = slots.ptrs()
+            pipe = SlabPipeline([g], sends, recvs, slots)
+            step = lambda: pipe.step(1.0 / 60.0)  # noqa: E731
+            flush = pipe.flush
         for _ in range(2):
-            pipe.step(1.0 / 60.0)
-        pipe.flush()
+            step()
+        flush()
 
         def pipelined_steps():
             for _ in range(per):
-                pipe.step(1.0 / 60.0)
-            pipe.flush()
+                step()
+            flush()
 
         el = timed(pipelined_steps)
         fft.set_cu_budget(0)
         out["pipelined_ms_per_frame"] = 1000.0 * el / per
         out["reserved_cus"] = reserve
-        del pipe, slots
         torch.cuda.empty_cache()
         out["ms_per_frame"] = min(out["pipelined_ms_per_frame"], out["serial_ms_per_frame"])
     else:
         out["ms_per_frame"] = out["serial_ms_per_frame"]
     out["points_per_s"] = float(n) * n / (out["ms_per_frame"] * 1e-3)
     g.close()
+    if comm is not None:
+        comm.close()
     fft.close()
+    return out
+
+
+def p8_rank_projection(args, one_gpu_frame_ms: float, ranks: int = 8) -> dict:
+    """The per-rank cost of BASELINE configs[4] (the 16384^2 grid over 8 GPUs) measured on ONE GPU:
+    all 8 ranks' SlabGenerators in this process, frames emulated with the equal-split all-to-all as
+    device copies (oceansimulation_amd.slab.emulate_frame), each rank's column and row passes timed with
+    HIP events on their stream. On 8 GPUs every rank runs the same kernels on its own device, so
+    max(passes) bounds the pipelined 8-GPU frame from below when the exchange hides behind it; the
+    exchange itself is not measurable here (one device), so its bytes and the xGMI rate that would
+    hide it are reported instead."""
+    import oceansimulation_amd as ocean
+    from oceansimulation_amd.hip import DeviceBuffer
+    from oceansimulation_amd.slab import SlabGenerator, emulate_frame
+
+    n, dt = args.slab_n, 1.0 / 60.0
+    fft = ocean.FFTCalculator(n)
+    slabs = [SlabGenerator(fft, r, ranks) for r in range(ranks)]
+    sends = [DeviceBuffer(g.exchange_bytes) for g in slabs]
+    recvs = [DeviceBuffer(g.exchange_bytes) for g in slabs]
+    try:
+        emulate_frame(slabs, sends, recvs, dt, update_ocean=True)
+        emulate_frame(slabs, sends, recvs, dt)
+        for g in slabs:
+            g.set_profiling(True)
+            g.kernel_times()
+        for _ in range(args.slab_steps):
+            emulate_frame(slabs, sends, recvs, dt)
+        cols, rows = [], []
+        for g in slabs:
+            ms, cnt = g.kernel_times()
+            cols.append(ms[1] / max(cnt[1], 1))
+            rows.append(ms[2] / max(cnt[2], 1))
+        passes = [c + r for c, r in zip(cols, rows)]
+        worst = max(passes)
+        moved = slabs[0].exchange_bytes * (ranks - 1) // ranks
+        per_point = sum(slabs[0].frame_bytes())
+        out = {
+            "what": f"{ranks} slab ranks of the single {n}x{n} grid emulated on one GPU (exchange as device copies, "
+                    "not timed); per-rank column pass (four-step, destination-block order) + row pass",
+            "ranks": ranks,
+            "column_pass_ms": cols,
+            "row_pass_ms": rows,
+            "passes_ms": worst,
+            "passes_ms_mean": sum(passes) / ranks,
+            "frac_hbm_peak": per_point * n * n / ranks / (worst * 1e-3) / 1e9 / HBM_PEAK_GBS,
+            "frame_hbm_bytes_per_point": per_point,
+            "one_gpu_frame_ms": one_gpu_frame_ms,
+            "projected_speedup_vs_1gpu": one_gpu_frame_ms / worst,
+            "exchange_bytes_per_rank": moved,
+            "xgmi_GBps_per_rank_to_hide_exchange": moved / (worst * 1e-3) / 1e9,
+        }
+    finally:
+        for b in sends + recvs:
+            b.free()
+        for g in slabs:
+            g.close()
+        fft.close()
     return out
 
 
@@ -587,11 +745,13 @@ def main(argv=None):
     rank, world, local = dist_setup(force=args.slab_force_exchange, shared_gpu=args.shared_gpu)
     import oceansimulation_amd as ocean
 
-    n, C = args.n, args.cascades
+    n, total = args.n, args.cascades
+    mine = rank_cascades(total, rank, world)  # strong scaling: this rank's share of the job's cascades
+    C = len(mine)
     fft = ocean.FFTCalculator(n)  # default (null) stream == torch's default stream
     gen = ocean.Generator(fft, C)
-    for c in range(C):
-        ocean.apply_settings(gen.GetOceanSettings(c), **cascade_settings(rank, c))
+    for k, c in enumerate(mine):
+        ocean.apply_settings(gen.GetOceanSettings(k), **cascade_settings(0, c))
     if args.full_spectrum:
         gen.set_half_spectrum(False)
     pass_bytes = gen.frame_bytes()
@@ -647,7 +807,7 @@ def main(argv=None):
         el_forced = reseed_loop()  # the re-seed the reference performs on every frame
         gen.set_h0_memo(True)
 
-    points = float(n) * n * C * args.steps * world
+    points = float(n) * n * total * args.steps
     value = points / el_max
     out = {
         "metric": METRIC,
@@ -658,17 +818,19 @@ def main(argv=None):
         "warmup": args.warmup,
         "ms_per_step": 1000.0 * el_max / args.steps,
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong",
         "vs_baseline": None,
         "dtype": "f32",
         "data": "synthetic (procedural JONSWAP h0 from the reference hash; default settings)",
         "config": {
-            "workload": f"{C} independent {n}x{n} cascades per GPU, full payload (height+slopes, choppy Dx/Dz, "
-                        f"Jacobian); step = CalculateOcean for all (evolve + 2 packed 2D iFFTs + foam)",
+            "workload": f"{total} independent {n}x{n} cascades (BASELINE configs[3]), {C} per GPU, full payload "
+                        f"(height+slopes, choppy Dx/Dz, Jacobian); step = CalculateOcean for all (evolve + 2 packed "
+                        f"2D iFFTs + foam)",
             "n": n,
+            "cascades": total,
             "cascades_per_gpu": C,
-            "plane_sizes_m": [PLANES[c % len(PLANES)] for c in range(C)],
-            "parallelism": f"cascades sharded over {world} GPU(s), no collective",
+            "plane_sizes_m": [PLANES[c % len(PLANES)] for c in range(total)],
+            "parallelism": f"the {total} cascades split {C} per GPU over {world} GPU(s) (strong scaling), no collective",
             "frame_path": "half spectrum" if half else "full spectrum",
             "frame_hbm_bytes_per_point": pass_bytes[0] + pass_bytes[1],
         },
@@ -678,12 +840,12 @@ def main(argv=None):
             "what": "the reference app's loop: CalculateOcean(dt, updateOcean=true) each frame (src/Waves.cpp:91-94); "
                     "h0 inputs unchanged, so the re-seed is skipped (it would be bit-identical)",
             "ms_per_step": 1000.0 * el_reseed / args.steps,
-            "points_per_s": float(n) * n * C * args.steps * world / el_reseed,
+            "points_per_s": float(n) * n * total * args.steps / el_reseed,
             "forced_reseed": {
                 "what": "the same loop re-seeding h0 on every request (ocean_generator_set_h0_memo(0)), as the "
                         "reference does: h0 evaluated inside the column pass",
                 "ms_per_step": 1000.0 * el_forced / args.steps,
-                "points_per_s": float(n) * n * C * args.steps * world / el_forced,
+                "points_per_s": float(n) * n * total * args.steps / el_forced,
             },
         }
     if not args.no_profile and cnt[1] > 0 and cnt[2] > 0:
@@ -727,8 +889,16 @@ def main(argv=None):
                                                "frac_hbm_peak": frame_gbs / HBM_PEAK_GBS}
         out["kernels"]["h0_seed_ms"] = h0_ms
     gen.close()
-    fft.close()
     watchdog = start_legs_watchdog(out, rank, args.legs_timeout)
+    try:
+        if world > 1:
+            out["weak_scaling"] = weak_leg(ocean, fft, args, rank, world, dt)
+        else:
+            out["strong_scaling"] = one_cascade_leg(ocean, fft, args, dt)
+            out["strong_scaling"]["batched_ms_per_cascade"] = out["ms_per_step"] / C
+    except Exception as e:  # reported, never fatal to the headline measurement
+        out["weak_scaling" if world > 1 else "strong_scaling"] = {"error": f"{type(e).__name__}: {e}"}
+    fft.close()
     if not args.no_ifft:
         try:
             out["ifft_only"] = ifft_legs(n, C)
@@ -747,8 +917,10 @@ def main(argv=None):
     if not args.no_slab:
         try:
             out["slab"] = slab_grid(args, rank, world, local)
+            if world == 1 and "ms_per_frame" in out["slab"]:
+                out["slab"]["p8_rank_projection"] = p8_rank_projection(args, out["slab"]["ms_per_frame"])
         except Exception as e:  # reported, never fatal to the headline measurement
-            out["slab"] = {"error": f"{type(e).__name__}: {e}"}
+            out["slab"] = dict(out.get("slab", {}), error=f"{type(e).__name__}: {e}")
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(n, args.cpu_seconds)
     if not watchdog.finish():

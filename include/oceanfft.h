@@ -188,6 +188,31 @@ int ocean_generator_slab_info(const ocean_generator* gen, int* rank, int* ranks,
  * bytes, exchange bytes} for the full-spectrum path (half == 0). */
 int ocean_slab_layout(size_t texture_size, int rank, int ranks, int half, int64_t out[6]);
 
+/* ---- the slab exchange over RCCL (xGMI) ---------------------------------------------------
+ * The frame of a slab generator with the all-to-all inside the library: P grouped ncclSend /
+ * ncclRecv pairs of exchange_bytes / P between the column and the row pass, on the
+ * generator's stream (serial) or on a second stream (pipelined). The communicator spans the P ranks
+ * of the grid, rank r = the slab rank (one process per GPU, the current HIP device). */
+#define OCEAN_COMM_ID_BYTES 128
+typedef struct ocean_comm ocean_comm;
+/* ncclGetUniqueId: created by one rank and handed to every rank's ocean_comm_create by the caller
+ * (MPI, a file, torch.distributed ...). */
+int ocean_comm_unique_id(unsigned char id[OCEAN_COMM_ID_BYTES]);
+/* ncclCommInitRank(nranks, id, rank) on the current device; collective over the nranks processes. */
+int ocean_comm_create(ocean_comm** out, const unsigned char id[OCEAN_COMM_ID_BYTES], int nranks, int rank);
+/* Use a communicator the caller already has (an ncclComm_t; not destroyed by ocean_comm_destroy). */
+int ocean_comm_wrap(ocean_comm** out, void* nccl_comm, int nranks, int rank);
+int ocean_comm_destroy(ocean_comm* comm);
+/* One frame: time += dt, h0 if needed, column pass into the library's send buffer, the all-to-all,
+ * row pass — all enqueued on the generator's stream (src/Generator.cpp:45-83 over P ranks). */
+int ocean_generator_slab_frame(ocean_generator* gen, ocean_comm* comm, float timestep, int update_spectrum);
+/* Pipelined frames over two buffer slots: frame f's all-to-all runs on a second stream beside frame
+ * f + 1's column pass and frame f - 1's row pass, so the steady state is max(exchange, passes); the
+ * maps lag the last issued frame by one until ocean_generator_slab_flush. Size the passes with
+ * ocean_fft_set_cu_budget to leave CUs to RCCL's kernels. */
+int ocean_generator_slab_frame_pipelined(ocean_generator* gen, ocean_comm* comm, float timestep, int update_spectrum);
+int ocean_generator_slab_flush(ocean_generator* gen);
+
 /* ---- instrumentation (bench) ------------------------------------------------------------- */
 /* When enabled, each kernel launch of the generator is bracketed by HIP events on its stream. */
 int ocean_generator_set_profiling(ocean_generator* gen, int enable);

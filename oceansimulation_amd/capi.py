@@ -17,6 +17,7 @@ OCEAN_ERR_HIP = 2
 OCEAN_ERR_NO_DEVICE = 3
 OCEAN_ERR_OOM = 4
 OCEAN_MAX_CASCADES = 64
+OCEAN_COMM_ID_BYTES = 128
 
 
 class OceanSettings(ctypes.Structure):
@@ -90,6 +91,13 @@ SIGNATURES = {
     "ocean_generator_set_h0_memo": (_i, [_vp, _i]),
     "ocean_generator_frame_bytes": (_i, [_vp, _vp]),
     "ocean_slab_layout": (_i, [_sz, _i, _i, _i, ctypes.POINTER(ctypes.c_int64)]),
+    "ocean_comm_unique_id": (_i, [_vp]),
+    "ocean_comm_create": (_i, [ctypes.POINTER(_vp), _vp, _i, _i]),
+    "ocean_comm_wrap": (_i, [ctypes.POINTER(_vp), _vp, _i, _i]),
+    "ocean_comm_destroy": (_i, [_vp]),
+    "ocean_generator_slab_frame": (_i, [_vp, _vp, _f, _i]),
+    "ocean_generator_slab_frame_pipelined": (_i, [_vp, _vp, _f, _i]),
+    "ocean_generator_slab_flush": (_i, [_vp]),
 }
 
 _lib = None

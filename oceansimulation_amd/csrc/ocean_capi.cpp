@@ -6,6 +6,7 @@
 #include "oceanfft.h"
 
 #include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
 
 #include <algorithm>
 #include <cmath>
@@ -125,6 +126,17 @@ struct ocean_generator
   // h0 inputs (every field but `time`) would reproduce h0 bit for bit, so it is skipped
   std::vector<ocean_settings> seeded;
   bool memo_h0 = true;  // ocean_generator_set_h0_memo
+  // ocean_generator_slab_frame[_pipelined]: the library's own exchange buffers over RCCL, two slots
+  // (frame f in slot f % 2), the exchange on its own stream
+  unsigned char* xsend[2] = {nullptr, nullptr};
+  unsigned char* xrecv[2] = {nullptr, nullptr};
+  size_t xslot_bytes = 0;
+  hipStream_t comm_stream = nullptr;
+  hipEvent_t cols_done[2] = {nullptr, nullptr}, xchg_done[2] = {nullptr, nullptr}, rows_done[2] = {nullptr, nullptr};
+  bool rows_recorded[2] = {false, false};
+  int pending_slot = -1;           // slot whose row pass is still to be issued
+  FrameParams slot_frame[2]{};     // the column pass's per-cascade values of the frame in each slot
+  int64_t frames_issued = 0;
   bool profiling = false;
   std::vector<EventPair> pending;
   std::vector<hipEvent_t> pool;
@@ -589,6 +601,17 @@ int ocean_generator_destroy(ocean_generator* g)
     (void)hipFree(g->maps);
   if (g->jac)
     (void)hipFree(g->jac);
+  for (int k = 0; k < 2; k++)
+  {
+    for (hipEvent_t ev : {g->cols_done[k], g->xchg_done[k], g->rows_done[k]})
+      if (ev)
+        (void)hipEventDestroy(ev);
+    for (void* p : {(void*)g->xsend[k], (void*)g->xrecv[k]})
+      if (p)
+        (void)hipFree(p);
+  }
+  if (g->comm_stream)
+    (void)hipStreamDestroy(g->comm_stream);
   for (void* p : {(void*)g->gab, (void*)g->gcd, (void*)g->ge, (void*)g->spec, (void*)g->hs, (void*)g->h0row, g->seedc,
                   (void*)g->rm_ab, (void*)g->rm_de, (void*)g->rm_c, (void*)g->parts, (void*)g->xbuf})
     if (p)
@@ -964,6 +987,237 @@ int ocean_generator_slab_rows(ocean_generator* g, const float* recv)
   if (!g)
     return fail(OCEAN_ERR_INVALID, "ocean_generator_slab_rows: null generator");
   return generator_rows(g, recv ? reinterpret_cast<const float4*>(recv) : (g->hslab ? nullptr : g->inter));
+}
+
+// ---------------------------------------------------------------------------------------------
+// Slab exchange over RCCL: the equal-split all-to-all between the column and the row pass (SURVEY
+// §8e), as P grouped ncclSend / ncclRecv pairs of exchange_bytes / P on the generator's streams.
+// ---------------------------------------------------------------------------------------------
+}  // extern "C"
+
+struct ocean_comm
+{
+  ncclComm_t comm = nullptr;
+  int nranks = 0, rank = 0;
+  bool owned = false;
+};
+
+namespace
+{
+int nccl_fail(ncclResult_t r, const char* what)
+{
+  return fail(OCEAN_ERR_HIP, std::string(what) + ": " + ncclGetErrorString(r));
+}
+
+// Enqueue this frame's all-to-all (send slot -> recv slot) on `stream`.
+int exchange_blocks(ocean_generator* g, ocean_comm* c, const unsigned char* send, unsigned char* recv,
+                    hipStream_t stream)
+{
+  const size_t blk = ocean_generator_exchange_bytes(g) / g->ranks;
+  ncclResult_t r = ncclGroupStart();
+  for (int q = 0; q < g->ranks && r == ncclSuccess; q++)
+  {
+    r = ncclSend(send + q * blk, blk, ncclUint8, q, c->comm, stream);
+    if (r == ncclSuccess)
+      r = ncclRecv(recv + q * blk, blk, ncclUint8, q, c->comm, stream);
+  }
+  const ncclResult_t e = ncclGroupEnd();
+  if (r != ncclSuccess)
+    return nccl_fail(r, "slab exchange (ncclSend / ncclRecv)");
+  if (e != ncclSuccess)
+    return nccl_fail(e, "slab exchange (ncclGroupEnd)");
+  return OCEAN_OK;
+}
+
+// The two exchange slots, the comm stream and its events (first use, or after a path switch that
+// changed exchange_bytes).
+int frame_slots(ocean_generator* g)
+{
+  const size_t bytes = ocean_generator_exchange_bytes(g);
+  if (g->xslot_bytes < bytes)
+  {
+    if (g->pending_slot >= 0)
+      return fail(OCEAN_ERR_INVALID, "slab frame: the exchange size changed with a frame in flight (flush first)");
+    for (int k = 0; k < 2; k++)
+      for (unsigned char** p : {&g->xsend[k], &g->xrecv[k]})
+      {
+        if (*p)
+          (void)hipFree(*p);
+        *p = nullptr;
+      }
+    g->xslot_bytes = 0;
+    for (int k = 0; k < 2; k++)
+    {
+      HIP_TRY(hipMalloc(&g->xsend[k], bytes), "slab frame: exchange buffers");
+      HIP_TRY(hipMalloc(&g->xrecv[k], bytes), "slab frame: exchange buffers");
+    }
+    g->xslot_bytes = bytes;
+  }
+  if (!g->comm_stream)
+  {
+    HIP_TRY(hipStreamCreateWithFlags(&g->comm_stream, hipStreamNonBlocking), "slab frame: comm stream");
+    for (int k = 0; k < 2; k++)
+      for (hipEvent_t* ev : {&g->cols_done[k], &g->xchg_done[k], &g->rows_done[k]})
+        HIP_TRY(hipEventCreateWithFlags(ev, hipEventDisableTiming), "slab frame: events");
+  }
+  return OCEAN_OK;
+}
+
+int check_comm(const ocean_generator* g, const ocean_comm* c, const char* who)
+{
+  if (!g || !c || !c->comm)
+    return fail(OCEAN_ERR_INVALID, std::string(who) + ": null generator or communicator");
+  if (c->nranks != g->ranks || c->rank != g->rank)
+    return fail(OCEAN_ERR_INVALID, std::string(who) + ": communicator rank " + std::to_string(c->rank) + " of " +
+                                       std::to_string(c->nranks) + " does not match slab rank " +
+                                       std::to_string(g->rank) + " of " + std::to_string(g->ranks));
+  return OCEAN_OK;
+}
+
+// Row pass of the frame in slot s (its own column-pass values: pipelined rows run after the next
+// frame's column pass).
+int slot_rows(ocean_generator* g, int s)
+{
+  ocean_fft* f = g->fft;
+  HIP_TRY(hipStreamWaitEvent(f->stream, g->xchg_done[s], 0), "slab frame: wait for the exchange");
+  const FrameParams newest = g->frame;
+  g->frame = g->slot_frame[s];
+  const int rc = generator_rows(g, reinterpret_cast<const float4*>(g->xrecv[s]));
+  g->frame = newest;
+  if (rc != OCEAN_OK)
+    return rc;
+  HIP_TRY(hipEventRecord(g->rows_done[s], f->stream), "slab frame: events");
+  g->rows_recorded[s] = true;
+  return OCEAN_OK;
+}
+
+// Column pass of frame f into slot f % 2 and its exchange on the comm stream.
+int slot_columns_and_exchange(ocean_generator* g, ocean_comm* c, float timestep, int update_spectrum, int& slot)
+{
+  ocean_fft* f = g->fft;
+  const int s = (int)(g->frames_issued % 2);
+  int rc = generator_columns(g, timestep, update_spectrum, reinterpret_cast<float4*>(g->xsend[s]));
+  if (rc != OCEAN_OK)
+    return rc;
+  g->slot_frame[s] = g->frame;
+  HIP_TRY(hipEventRecord(g->cols_done[s], f->stream), "slab frame: events");
+  HIP_TRY(hipStreamWaitEvent(g->comm_stream, g->cols_done[s], 0), "slab frame: stream order");
+  if (g->rows_recorded[s])  // frame f - 2's row pass has finished reading recv[s]
+    HIP_TRY(hipStreamWaitEvent(g->comm_stream, g->rows_done[s], 0), "slab frame: stream order");
+  rc = exchange_blocks(g, c, g->xsend[s], g->xrecv[s], g->comm_stream);
+  if (rc != OCEAN_OK)
+    return rc;
+  HIP_TRY(hipEventRecord(g->xchg_done[s], g->comm_stream), "slab frame: events");
+  g->frames_issued++;
+  slot = s;
+  return OCEAN_OK;
+}
+}  // namespace
+
+extern "C" {
+
+int ocean_comm_unique_id(unsigned char id[OCEAN_COMM_ID_BYTES])
+{
+  static_assert(OCEAN_COMM_ID_BYTES == NCCL_UNIQUE_ID_BYTES, "RCCL unique id size");
+  if (!id)
+    return fail(OCEAN_ERR_INVALID, "ocean_comm_unique_id: null id");
+  ncclUniqueId u;
+  const ncclResult_t r = ncclGetUniqueId(&u);
+  if (r != ncclSuccess)
+    return nccl_fail(r, "ncclGetUniqueId");
+  std::memcpy(id, u.internal, NCCL_UNIQUE_ID_BYTES);
+  return OCEAN_OK;
+}
+
+int ocean_comm_create(ocean_comm** out, const unsigned char id[OCEAN_COMM_ID_BYTES], int nranks, int rank)
+{
+  if (!out || !id || nranks < 1 || rank < 0 || rank >= nranks)
+    return fail(OCEAN_ERR_INVALID, "ocean_comm_create: null argument or rank outside [0, nranks)");
+  *out = nullptr;
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0)
+    return fail(OCEAN_ERR_NO_DEVICE, "ocean_comm_create: no HIP device visible");
+  ncclUniqueId u;
+  std::memcpy(u.internal, id, NCCL_UNIQUE_ID_BYTES);
+  auto* c = new ocean_comm();
+  const ncclResult_t r = ncclCommInitRank(&c->comm, nranks, u, rank);
+  if (r != ncclSuccess)
+  {
+    delete c;
+    return nccl_fail(r, "ncclCommInitRank");
+  }
+  c->nranks = nranks;
+  c->rank = rank;
+  c->owned = true;
+  *out = c;
+  return OCEAN_OK;
+}
+
+int ocean_comm_wrap(ocean_comm** out, void* nccl_comm, int nranks, int rank)
+{
+  if (!out || !nccl_comm || nranks < 1 || rank < 0 || rank >= nranks)
+    return fail(OCEAN_ERR_INVALID, "ocean_comm_wrap: null argument or rank outside [0, nranks)");
+  auto* c = new ocean_comm();
+  c->comm = static_cast<ncclComm_t>(nccl_comm);
+  c->nranks = nranks;
+  c->rank = rank;
+  *out = c;
+  return OCEAN_OK;
+}
+
+int ocean_comm_destroy(ocean_comm* comm)
+{
+  if (!comm)
+    return OCEAN_OK;
+  ncclResult_t r = ncclSuccess;
+  if (comm->owned && comm->comm)
+    r = ncclCommDestroy(comm->comm);
+  delete comm;
+  return r == ncclSuccess ? OCEAN_OK : nccl_fail(r, "ncclCommDestroy");
+}
+
+int ocean_generator_slab_frame(ocean_generator* g, ocean_comm* comm, float timestep, int update_spectrum)
+{
+  int rc = check_comm(g, comm, "ocean_generator_slab_frame");
+  if (rc == OCEAN_OK && g->pending_slot >= 0)
+    rc = ocean_generator_slab_flush(g);  // a pipelined frame in flight lands first
+  if (rc == OCEAN_OK)
+    rc = frame_slots(g);
+  int s = 0;
+  if (rc == OCEAN_OK)
+    rc = slot_columns_and_exchange(g, comm, timestep, update_spectrum, s);
+  return rc != OCEAN_OK ? rc : slot_rows(g, s);
+}
+
+int ocean_generator_slab_frame_pipelined(ocean_generator* g, ocean_comm* comm, float timestep, int update_spectrum)
+{
+  int rc = check_comm(g, comm, "ocean_generator_slab_frame_pipelined");
+  if (rc == OCEAN_OK)
+    rc = frame_slots(g);
+  int s = 0;
+  if (rc == OCEAN_OK)
+    rc = slot_columns_and_exchange(g, comm, timestep, update_spectrum, s);
+  if (rc != OCEAN_OK)
+    return rc;
+  if (g->pending_slot >= 0)
+  {
+    rc = slot_rows(g, g->pending_slot);
+    if (rc != OCEAN_OK)
+      return rc;
+  }
+  g->pending_slot = s;
+  return OCEAN_OK;
+}
+
+int ocean_generator_slab_flush(ocean_generator* g)
+{
+  if (!g)
+    return fail(OCEAN_ERR_INVALID, "ocean_generator_slab_flush: null generator");
+  if (g->pending_slot < 0)
+    return OCEAN_OK;
+  const int s = g->pending_slot;
+  g->pending_slot = -1;
+  return slot_rows(g, s);
 }
 
 int ocean_slab_layout(size_t texture_size, int rank, int ranks, int half, int64_t out[6])

@@ -10,9 +10,12 @@ Frames are independent until their exchange (the column pass depends only on h0 
 pass (two buffer slots, the exchange on its own stream); steady state is max(exchange, passes)
 instead of their sum. Maps then lag the last issued frame by one until `flush()`.
 
-Two exchanges are provided:
-  * `TorchExchange`: torch.distributed.all_to_all_single over the "nccl" backend (RCCL on ROCm),
-    one process per GPU — used by bench.py;
+Three exchanges are provided:
+  * `RcclComm` + `SlabGenerator.frame` / `frame_pipelined`: the library's own all-to-all, grouped
+    ncclSend / ncclRecv over RCCL inside the C ABI (ocean_generator_slab_frame[_pipelined]), one
+    process per GPU — used by bench.py;
+  * `TorchExchange`: torch.distributed.all_to_all_single over the "nccl" backend (RCCL on ROCm), the
+    comparator leg and the one-GPU gloo rehearsal;
   * `emulate_frame`: P slab generators in one process/GPU, blocks moved by device copies — used by
     the parity tests to check the decomposition against the whole-grid generator.
 """
@@ -80,6 +83,20 @@ class SlabGenerator:
     def rows_pass(self, recv_ptr: int | None = None) -> None:
         check(lib().ocean_generator_slab_rows(self._h, ctypes.c_void_p(recv_ptr or 0)), "ocean_generator_slab_rows")
 
+    def frame(self, comm: "RcclComm", timestep: float, update_ocean: bool = False) -> None:
+        """Columns, the RCCL all-to-all and rows, all inside the library (ocean_generator_slab_frame)."""
+        check(lib().ocean_generator_slab_frame(self._h, comm.handle, ctypes.c_float(timestep), 1 if update_ocean else 0),
+              "ocean_generator_slab_frame")
+
+    def frame_pipelined(self, comm: "RcclComm", timestep: float, update_ocean: bool = False) -> None:
+        """Frame f's all-to-all on the library's comm stream beside frame f + 1's column pass and frame
+        f - 1's row pass; the maps lag by one frame until flush()."""
+        check(lib().ocean_generator_slab_frame_pipelined(self._h, comm.handle, ctypes.c_float(timestep),
+                                                         1 if update_ocean else 0), "ocean_generator_slab_frame_pipelined")
+
+    def flush(self) -> None:
+        check(lib().ocean_generator_slab_flush(self._h), "ocean_generator_slab_flush")
+
     def height_map_host(self) -> np.ndarray:
         self.fft.synchronize()
         return hip.to_host(int(lib().ocean_generator_height_map(self._h, 0)), (self.rows, self.n, 4))
@@ -113,11 +130,56 @@ class SlabGenerator:
             pass
 
 
-def slab_layout(n: int, rank: int, ranks: int, half: bool = True):
-    """ocean_slab_layout: (first strip, strips, strip slots per block, rows, block bytes, exchange
-    bytes) of a one-cascade slab generator; host-only, no device needed."""
+class RcclComm:
+    """The C ABI's RCCL communicator over the P ranks of one grid (ocean_comm_create). Rank 0's unique
+    id reaches the other ranks through `share_id(bytes) -> bytes` (e.g. a torch.distributed broadcast)."""
+
+    def __init__(self, rank: int, ranks: int, share_id):
+        from .capi import OCEAN_COMM_ID_BYTES
+
+        uid = (ctypes.c_ubyte * OCEAN_COMM_ID_BYTES)()
+        if rank == 0:
+            check(lib().ocean_comm_unique_id(uid), "ocean_comm_unique_id")
+        got = share_id(bytes(uid))
+        uid = (ctypes.c_ubyte * OCEAN_COMM_ID_BYTES).from_buffer_copy(got)
+        h = ctypes.c_void_p()
+        check(lib().ocean_comm_create(ctypes.byref(h), uid, ranks, rank), "ocean_comm_create")
+        self._h = h
+
+    @property
+    def handle(self):
+        return self._h
+
+    def close(self) -> None:
+        if self._h:
+            lib().ocean_comm_destroy(self._h)
+            self._h = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def torch_share_id(uid: bytes) -> bytes:
+    """Broadcast rank 0's communicator id over the default torch.distributed group (any backend)."""
+    import torch.distributed as dist
+
+    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+        return uid
+    box = [uid]
+    dist.broadcast_object_list(box, src=0)
+    return box[0]
+
+
+def slab_layout(n: int, rank: int, ranks: int, half=True):
+    """ocean_slab_layout: half = True / 1: the strip-dealt path (first strip, strips, strip slots per
+    block, rows, block bytes, exchange bytes); 2: the four-step path (first kept column, kept columns,
+    holds the Nyquist column, rows, block bytes, exchange bytes); False / 0: the full spectrum. Host
+    only, no device needed."""
     out = (ctypes.c_int64 * 6)()
-    check(lib().ocean_slab_layout(n, rank, ranks, 1 if half else 0, out), "ocean_slab_layout")
+    check(lib().ocean_slab_layout(n, rank, ranks, int(half), out), "ocean_slab_layout")
     return tuple(int(v) for v in out)
 
 

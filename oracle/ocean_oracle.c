@@ -241,13 +241,16 @@ void oracle_spectrum_texels(const oracle_settings* s, int n, int64_t count, cons
   }
 }
 
-/* resources/spectrum.compute:183-240 */
-void oracle_prepare_fft(const oracle_settings* s, int n, const float* h0, float* height, float* disp)
+/* resources/spectrum.compute:183-240 on the spectrum rows [y0, y0 + rows); h0, height, disp hold
+ * those rows only (rows * N float4 each). */
+void oracle_prepare_fft_rows(const oracle_settings* s, int n, int y0, int rows, const float* h0, float* height,
+                             float* disp)
 {
   const float dim = (float)n;
 #pragma omp parallel for num_threads(g_threads) schedule(static)
-  for (int y = 0; y < n; y++)
+  for (int r = 0; r < rows; r++)
   {
+    const int y = y0 + r;
     for (int x = 0; x < n; x++)
     {
       float dk = 2.0f * PI_SPECTRUM / s->planeSize;
@@ -262,7 +265,7 @@ void oracle_prepare_fft(const oracle_settings* s, int n, const float* h0, float*
       }
       float k = len + 1e-6f;
 
-      const float* a = h0 + 4 * ((size_t)y * n + x);
+      const float* a = h0 + 4 * ((size_t)r * n + x);
       float phase = dispersion(s, k) * s->time;
       float wc = cosf(phase), ws = sinf(phase);
 
@@ -285,8 +288,8 @@ void oracle_prepare_fft(const oracle_settings* s, int n, const float* h0, float*
       float dDZdz_x = -kz * dirz * hx, dDZdz_y = -kz * dirz * hy;
       float dDXdz_x = -kz * dirx * hx, dDXdz_y = -kz * dirx * hy;
 
-      float* o0 = height + 4 * ((size_t)y * n + x);
-      float* o1 = disp + 4 * ((size_t)y * n + x);
+      float* o0 = height + 4 * ((size_t)r * n + x);
+      float* o1 = disp + 4 * ((size_t)r * n + x);
       o0[0] = hx - dhdx_y;
       o0[1] = hy + dhdx_x;
       o0[2] = dhdz_x - disX_y;
@@ -297,6 +300,12 @@ void oracle_prepare_fft(const oracle_settings* s, int n, const float* h0, float*
       o1[3] = dDZdz_y + dDXdz_x;
     }
   }
+}
+
+/* resources/spectrum.compute:183-240 */
+void oracle_prepare_fft(const oracle_settings* s, int n, const float* h0, float* height, float* disp)
+{
+  oracle_prepare_fft_rows(s, n, 0, n, h0, height, disp);
 }
 
 /* resources/fft.compute:21-28 — out[(p + SIZE/2) % SIZE] = in[p] on both axes. */

@@ -60,6 +60,9 @@ void oracle_spectrum_texels(const oracle_settings* s, int n, int64_t count, cons
 
 /* resources/spectrum.compute:183-240. height, disp: N*N float4 each. */
 void oracle_prepare_fft(const oracle_settings* s, int n, const float* h0, float* height, float* disp);
+/* The same on spectrum rows [y0, y0 + rows) only: h0, height, disp hold rows * N float4 each. */
+void oracle_prepare_fft_rows(const oracle_settings* s, int n, int y0, int rows, const float* h0, float* height,
+                             float* disp);
 
 /* src/FFTCalculator.cpp:73-114 with resources/fft.compute:21-88 (SIZE generalised to n).
  * In-place on image (N*N float4); work: scratch N*N float4 (the reference's workImage). */

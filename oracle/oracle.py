@@ -73,6 +73,7 @@ def lib():
         L.oracle_generate_spectrum.argtypes = [sp, ctypes.c_int, fp]
         L.oracle_spectrum_texels.argtypes = [sp, ctypes.c_int, ctypes.c_int64, ctypes.POINTER(ctypes.c_int32), fp]
         L.oracle_prepare_fft.argtypes = [sp, ctypes.c_int, fp, fp, fp]
+        L.oracle_prepare_fft_rows.argtypes = [sp, ctypes.c_int, ctypes.c_int, ctypes.c_int, fp, fp, fp]
         L.oracle_encode_ifft.argtypes = [ctypes.c_int, fp, fp]
         L.oracle_compute_foam.argtypes = [sp, ctypes.c_int, fp, fp]
         L.oracle_calculate_ocean.argtypes = [sp, ctypes.c_int, ctypes.c_float, ctypes.c_int, fp, fp, fp, fp, fp]
@@ -136,6 +137,47 @@ def prepare_fft(s: OracleSettings, n: int, h0: np.ndarray):
     disp = np.zeros((n, n, 4), np.float32)
     lib().oracle_prepare_fft(ctypes.byref(s), n, _fp(np.ascontiguousarray(h0, np.float32)), _fp(height), _fp(disp))
     return height, disp
+
+
+def spectrum_rows(s: OracleSettings, n: int, y0: int, rows: int) -> np.ndarray:
+    """generateSpectrum's texels on rows [y0, y0 + rows) of an N x N image -> (rows, N, 4)."""
+    y, x = np.meshgrid(np.arange(y0, y0 + rows, dtype=np.int32), np.arange(n, dtype=np.int32), indexing="ij")
+    return spectrum_texels(s, n, np.stack([x.ravel(), y.ravel()], 1)).reshape(rows, n, 4)
+
+
+def prepare_fft_rows(s: OracleSettings, n: int, y0: int, h0_rows: np.ndarray):
+    """prepareFFT on the spectrum rows [y0, y0 + len(h0_rows)) -> (height, disp) rows."""
+    rows = h0_rows.shape[0]
+    height = np.zeros((rows, n, 4), np.float32)
+    disp = np.zeros((rows, n, 4), np.float32)
+    lib().oracle_prepare_fft_rows(ctypes.byref(s), n, y0, rows, _fp(np.ascontiguousarray(h0_rows, np.float32)),
+                                  _fp(height), _fp(disp))
+    return height, disp
+
+
+def sampled_frame(s: OracleSettings, n: int, xs, ys, chunk: int = 256):
+    """The frame's maps at the sample points (xs x ys) without a full-size transform: the oracle's h0
+    and prepareFFT (fp32, the reference's arithmetic) on spectrum rows in chunks, then the 2D inverse
+    DFT of EncodeIFFT (N^2 ifft2(ifftshift), src/FFTCalculator.cpp:73-114) evaluated in float64 at
+    those points only: out(x, y) = sum_{i, j} X[j][i] exp(2 pi i ((i - N/2) x + (j - N/2) y) / N).
+    Returns (height, disp, jacobian) of shape (len(ys), len(xs), 4 | 4 | -)."""
+    xs, ys = np.asarray(xs), np.asarray(ys)
+    idx = np.arange(n, dtype=np.float64) - n / 2
+    ex = np.exp(2j * np.pi * np.outer(idx, xs) / n)  # [N, X]
+    ey = np.exp(2j * np.pi * np.outer(idx, ys) / n)  # [N, Y]
+    acc = np.zeros((4, len(ys), n), np.complex128)   # lanes: height xy, zw; disp xy, zw
+    for y0 in range(0, n, chunk):
+        rows = min(chunk, n - y0)
+        h, d = prepare_fft_rows(s, n, y0, spectrum_rows(s, n, y0, rows))
+        for k, (img, lane) in enumerate(((h, 0), (h, 1), (d, 0), (d, 1))):
+            z = img[..., 2 * lane].astype(np.float64) + 1j * img[..., 2 * lane + 1].astype(np.float64)
+            acc[k] += ey[y0:y0 + rows].T @ z
+    out = acc @ ex  # [4, Y, X]
+    height = np.stack([out[0].real, out[0].imag, out[1].real, out[1].imag], -1)
+    disp = np.stack([out[2].real, out[2].imag, out[3].real, out[3].imag], -1)
+    lam = float(s.displacement)
+    jac = (1 + lam * disp[..., 1]) * (1 + lam * disp[..., 2]) - lam * lam * disp[..., 3] ** 2
+    return height, disp, jac
 
 
 def encode_ifft(img: np.ndarray) -> np.ndarray:

@@ -1,7 +1,13 @@
 """Parity metrics and tolerances used by the tests (stated once, here).
 
-lane_err: for a packed RGBA32F image, the two complex lanes (xy, zw) are compared separately:
-          max |got - ref| over the lane / max |ref| over the lane (complex modulus).
+lane_err:    for a packed RGBA32F image, the two complex lanes (xy, zw) are compared separately:
+             max |got - ref| over the lane / max |ref| over the lane (complex modulus). Used for
+             EncodeIFFT on arbitrary inputs, where a lane is one transform.
+channel_err: each of the 4 real channels of a map on its own: max |got - ref| / max |ref| per
+             channel. The generator's maps are 8 real fields (src/Generator.h:76-80: heightMap =
+             (h, dh/dx, dh/dz, Dx), displacementMap = (Dz, dDx/dx, dDz/dz, dDx/dz)); a lane pairs a
+             height with a slope up to |k|max ~ 1e3 times larger, so the lane metric would judge h
+             against the slope's scale. Frames are checked per channel.
 Tolerances (float32 path):
   FFT_TOL   = 2e-5  — EncodeIFFT alone. The reference's own fp32 radix-2 structure is 0.2-5e-6 from
                       float64 at N <= 1024 (oracle vs numpy, tests/test_oracle.py); the HIP Stockham
@@ -15,6 +21,16 @@ import numpy as np
 FFT_TOL = 2e-5
 FRAME_TOL = 1e-4
 H0_TOL = 1e-5
+
+
+def channel_err(got: np.ndarray, ref: np.ndarray):
+    out = []
+    for ch in range(got.shape[-1]):
+        r = ref[..., ch].astype(np.float64)
+        scale = np.max(np.abs(r))
+        err = np.max(np.abs(got[..., ch].astype(np.float64) - r))
+        out.append(float(err / scale) if scale > 0 else float(err))
+    return out
 
 
 def lane_err(got: np.ndarray, ref: np.ndarray):

@@ -187,6 +187,23 @@ def test_half_slab_layout_deals_every_strip_once(capi, n, ranks):
         assert slab_layout(n, 0, ranks)[5] < (0.7 if n >= 4096 else 0.8) * full[5]
 
 
+@pytest.mark.parametrize("n,ranks", [(8192, 1), (8192, 2), (8192, 16), (16384, 8), (16384, 16)])
+def test_four_step_slab_layout_deals_every_column_once(capi, n, ranks):
+    """Four-step slabs (ocean_slab_layout half == 2): the N/2 regular kept columns are dealt N/(2P) per
+    rank in order, only the last rank holds the Nyquist column, every block is the same size (equal
+    split), and the exchange is 20 B per point (+ the 16-column pitch pad and the Nyquist-row term)."""
+    from oceansimulation_amd.slab import slab_layout
+
+    lays = [slab_layout(n, r, ranks, half=2) for r in range(ranks)]
+    cols = [c for (u0, k, _, _, _, _) in lays for c in range(u0, u0 + k)]
+    assert cols == list(range(n // 2))
+    assert [l[2] for l in lays] == [0] * (ranks - 1) + [1]
+    assert all(l[3] == n // ranks for l in lays)
+    assert len({l[4] for l in lays}) == 1 and all(l[5] == l[4] * ranks for l in lays)
+    per_point = lays[0][5] / (n * n / ranks)
+    assert 20.0 < per_point < 20.0 * (1 + 17 / (n / (2 * ranks))) + 1.0
+
+
 def test_slab_layout_rejects_bad_geometry(capi):
     from oceansimulation_amd.capi import OceanError
     from oceansimulation_amd.slab import slab_layout
@@ -198,3 +215,5 @@ def test_slab_layout_rejects_bad_geometry(capi):
     with pytest.raises(OceanError):
         slab_layout(512, 0, 2, half=True)
     assert slab_layout(512, 1, 2, half=False)[:2] == (256, 256)
+    with pytest.raises(OceanError):
+        slab_layout(4096, 0, 2, half=2)  # the four-step path serves 8192 / 16384 only

@@ -29,15 +29,20 @@ def _worker(rank, world, port, q):
     b.barrier(w)
     local_elapsed = 1.0 + rank  # rank 1 is the slow one
     el_max = b.max_over_ranks(local_elapsed, w)
-    # per-rank disjoint work: cascades owned by this rank
+    # per-rank disjoint work: cascades owned by this rank in the weak leg (8 each) ...
     owned = [(b.cascade_settings(r, c)["planeSize"],) + tuple(b.cascade_settings(r, c)["seed"]) for c in range(8)]
+    # ... and in the strong-scaling headline (the job's 8 global cascades split 8 / world per rank)
+    strong = [(c,) + (b.cascade_settings(0, c)["planeSize"],) + tuple(b.cascade_settings(0, c)["seed"])
+              for c in b.rank_cascades(8, r, w)]
     import torch.distributed as dist
 
     gathered = [None] * w
     dist.all_gather_object(gathered, owned)
+    gathered_strong = [None] * w
+    dist.all_gather_object(gathered_strong, strong)
     b.barrier(w)
     dist.destroy_process_group()
-    q.put((rank, el_max, gathered))
+    q.put((rank, el_max, gathered, gathered_strong))
 
 
 @pytest.mark.timeout(120)
@@ -52,10 +57,18 @@ def test_world2_max_over_ranks_and_disjoint_cascades():
     for p in procs:
         p.join(timeout=30)
         assert p.exitcode == 0
-    for rank, el_max, gathered in res:
+    spec = importlib.util.spec_from_file_location("bench", os.path.join(ROOT, "bench.py"))
+    b = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(b)
+    one_gpu = [(c,) + (b.cascade_settings(0, c)["planeSize"],) + tuple(b.cascade_settings(0, c)["seed"]) for c in range(8)]
+    for rank, el_max, gathered, gathered_strong in res:
         assert el_max == 2.0  # max over ranks, not rank-local time
         flat = [tuple(k) for ranks in gathered for k in ranks]
         assert len(set(flat)) == len(flat)  # no cascade computed twice across ranks
+        # strong scaling: 4 cascades per rank, disjoint, together exactly the 1-GPU job's 8
+        assert [len(x) for x in gathered_strong] == [4, 4]
+        strong = [tuple(k) for ranks in gathered_strong for k in ranks]
+        assert len(set(strong)) == 8 and sorted(strong) == sorted(one_gpu)
 
 
 def _a2a_worker(rank, world, port, q):

@@ -260,6 +260,50 @@ def test_four_step_whole_grid_matches_dealt_path(ocean, n):
     fft.close()
 
 
+@pytest.mark.parametrize("n", [1024, 8192])
+def test_native_rccl_slab_frames_world1_bit_exact(ocean, n):
+    """The C ABI's own exchange (ocean_generator_slab_frame[_pipelined]: grouped ncclSend / ncclRecv
+    over an RCCL communicator of the C ABI) at world size 1, the exchange forced through RCCL as a
+    self send/receive: serial frames, then pipelined frames + flush, equal the whole-grid generator bit
+    for bit (1024: strip-dealt slab path; 8192: four-step slab path)."""
+    from oceansimulation_amd import capi
+    from oceansimulation_amd.slab import RcclComm, SlabGenerator
+
+    fft = ocean.FFTCalculator(n)
+    whole = ocean.Generator(fft, 1)
+    g = SlabGenerator(fft, 0, 1)
+    for x in (whole.GetOceanSettings(0), g.GetOceanSettings()):
+        ocean.apply_settings(x, planeSize=333.0)
+    comm = RcclComm(0, 1, lambda uid: uid)
+    L = capi.lib()
+
+    def same():
+        fft.synchronize()
+        return all(_dev_equal(int(get(g.handle, 0)), int(get(whole.handle, 0)), n * n * tex)
+                   for get, tex in ((L.ocean_generator_height_map, 16), (L.ocean_generator_displacement_map, 16),
+                                    (L.ocean_generator_jacobian_map, 4)))
+
+    for k, dt in enumerate((0.5, 1.0 / 60.0)):
+        g.frame(comm, dt, update_ocean=(k == 0))
+        whole.CalculateOcean(dt)
+        assert same(), ("serial", k)
+    # pipelined: the maps lag one frame; after flush they hold the last frame
+    steps = [0.25, 1.0 / 30.0, 0.125]
+    for dt in steps:
+        g.frame_pipelined(comm, dt)
+    g.flush()
+    for dt in steps:
+        whole.CalculateOcean(dt)
+    assert same(), "pipelined"
+    # a communicator of the wrong size is refused
+    with pytest.raises(capi.OceanError):
+        SlabGenerator(fft, 0, 2).frame(comm, 0.1)
+    comm.close()
+    g.close()
+    whole.close()
+    fft.close()
+
+
 # ---- bench.py --gpus N on a one-GPU box ---------------------------------------------------------
 def test_bench_gpus_two_shared_gpu_reports_two_ranks(tmp_path):
     """`bench.py --gpus 2 --shared-gpu` (no launcher) starts 2 ranks under torch.distributed.run,

@@ -3,6 +3,7 @@ import importlib.util
 import os
 
 import numpy as np
+import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
@@ -37,6 +38,18 @@ def test_bench_cascade_sharding_is_disjoint():
             assert s["seed"][0] >= 12342 and s["seed"][1] >= 8934
     assert b.cascade_settings(0, 0)["planeSize"] == 5.0
     assert [b.cascade_settings(0, c)["planeSize"] for c in range(3)] == [5.0, 17.0, 101.0]  # Waves.cpp:27
+
+
+def test_strong_scaling_split():
+    """the 8 cascades all on 1 GPU, then 8/P per GPU at P = 2, 4, 8 — disjoint and
+    together the whole job whatever P; an uneven split is refused."""
+    b = _bench()
+    for world in (1, 2, 4, 8):
+        parts = [b.rank_cascades(8, r, world) for r in range(world)]
+        assert all(len(p) == 8 // world for p in parts)
+        assert sorted(c for p in parts for c in p) == list(range(8))
+    with pytest.raises(ValueError):
+        b.rank_cascades(8, 0, 3)
 
 
 def test_lane_err_metric():

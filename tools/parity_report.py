@@ -1,8 +1,8 @@
 #!/usr/bin/env python3
 """GPU-vs-oracle error table for full CalculateOcean frames, including long simulated times.
 
-Metric (tests/parity.py): max |got - ref| / max |ref| per complex lane (worst of the 4 lanes of
-the two maps) and for the Jacobian - 1. Also prints the phase-precision scale eps32 * w_max * t:
+Metrics (tests/parity.py): max |got - ref| / max |ref| per complex lane (worst of the 4 lanes of
+the two maps), per real channel (worst of the 8 channels, and which one), and for the Jacobian - 1. Also prints the phase-precision scale eps32 * w_max * t:
 the fp32 rounding of the phase w*t that the reference itself performs, which bounds how far any
 two fp32 implementations (GLSL, libm, ocml, hardware v_sin) can agree at time t.
 Writes gpurun_out/parity_report.md.  Usage: python tools/parity_report.py
@@ -20,7 +20,7 @@ import numpy as np  # noqa: E402
 
 import oceansimulation_amd as ocean  # noqa: E402
 from oracle import oracle as O  # noqa: E402
-from parity import lane_err, scalar_err  # noqa: E402
+from parity import channel_err, lane_err, scalar_err  # noqa: E402
 
 G = 9.81
 
@@ -45,12 +45,45 @@ def run(n, planes, times):
             r.calculate_ocean(dt)
         t_prev = t
         for c, L in enumerate(planes):
-            e = lane_err(gen.height_map_host(c), refs[c].height) + lane_err(gen.displacement_map_host(c), refs[c].disp)
+            hm, dm = gen.height_map_host(c), gen.displacement_map_host(c)
+            e = lane_err(hm, refs[c].height) + lane_err(dm, refs[c].disp)
+            ec = channel_err(hm, refs[c].height) + channel_err(dm, refs[c].disp)
             ej = scalar_err(gen.jacobian_map_host(c) - 1.0, refs[c].jac - 1.0)
             depth = refs[c].settings.h
             scale = 2.0 ** -23 * omega_max(n, L, depth, refs[c].settings.g) * gen.GetOceanSettings(c).time
-            rows.append((n, L, float(gen.GetOceanSettings(c).time), max(e), ej, scale))
+            rows.append((n, L, float(gen.GetOceanSettings(c).time), max(e), ec, ej, scale))
     return rows
+
+
+CHANNELS = ["h", "dh/dx", "dh/dz", "Dx", "Dz", "dDx/dx", "dDz/dz", "dDx/dz"]
+
+
+def run_sampled(n, plane, dt):
+    """One frame at N (e.g. 16384, too large for the whole-grid CPU oracle): sampled outputs against
+    the oracle's h0 + prepareFFT and a float64 inverse DFT at the sample points (oracle.sampled_frame)."""
+    fft = ocean.FFTCalculator(n)
+    gen = ocean.Generator(fft, 1)
+    ocean.apply_settings(gen.GetOceanSettings(0), planeSize=plane)
+    gen.CalculateOcean(dt)
+    s = O.default_settings(planeSize=plane)
+    s.time = gen.GetOceanSettings(0).time
+    xs, ys = sample_lines(n)
+    h, d, j = O.sampled_frame(s, n, xs, ys)
+    gh = gen.height_map_host(0)[np.ix_(ys, xs)]
+    gd = gen.displacement_map_host(0)[np.ix_(ys, xs)]
+    gj = gen.jacobian_map_host(0)[np.ix_(ys, xs)]
+    e = lane_err(gh, h) + lane_err(gd, d)
+    ec = channel_err(gh, h) + channel_err(gd, d)
+    ej = scalar_err(gj - 1.0, j - 1.0)
+    return [(n, plane, float(s.time), max(e), ec, ej, float("nan"))]
+
+
+def sample_lines(n, extra=10, seed=16384):
+    """Rows / columns 0, 1, N/2 - 1, N/2, N/2 + 1, N - 1 and `extra` random ones (sorted, distinct)."""
+    rng = np.random.default_rng(seed)
+    fixed = [0, 1, n // 2 - 1, n // 2, n // 2 + 1, n - 1]
+    rest = sorted(set(rng.integers(2, n - 2, 4 * extra).tolist()) - set(fixed))[:extra]
+    return np.array(sorted(fixed + rest)), np.array(sorted(fixed + rest))
 
 
 def main():
@@ -58,11 +91,18 @@ def main():
     rows = []
     rows += run(256, [5.0, 17.0, 101.0], [1 / 60, 1.0, 60.0, 600.0, 3600.0])
     rows += run(1024, [40.0], [1.0, 600.0])
-    rows += run(4096, [40.0], [1.0])
+    rows += run(2048, [40.0], [1.0])
+    rows += run(4096, [5.0, 251.0, 4093.0], [1 / 60, 1.0])
+    rows += run(8192, [40.0], [1.0])
+    rows += run_sampled(16384, 40.0, 0.25)
+    rows += run_sampled(16384, 1000.0, 1.0)
     lines = ["# GPU vs CPU oracle, full frames (max |err| / max |ref|)", "",
-             "| N | plane m | t s | maps lane err | Jacobian err | eps32 * w_max * t |", "|---|---|---|---|---|---|"]
-    for n, L, t, e, ej, s in rows:
-        lines.append(f"| {n} | {L:g} | {t:g} | {e:.2e} | {ej:.2e} | {s:.2e} |")
+             "| N | plane m | t s | maps lane err | maps channel err (worst channel) | per channel | Jacobian err | eps32 * w_max * t |",
+             "|---|---|---|---|---|---|---|---|"]
+    for n, L, t, e, ec, ej, s in rows:
+        w = int(np.argmax(ec))
+        per = " ".join(f"{v:.1e}" for v in ec)
+        lines.append(f"| {n} | {L:g} | {t:g} | {e:.2e} | {max(ec):.2e} ({CHANNELS[w]}) | {per} | {ej:.2e} | {s:.2e} |")
     out = os.path.join(ROOT, "gpurun_out")
     os.makedirs(out, exist_ok=True)
     with open(os.path.join(out, "parity_report.md"), "w") as f:

@@ -38,8 +38,9 @@ $(LIB): $(KERNEL_OBJS) $(CSRC)/build/ocean_capi.o
 
 # C++ drop-in layer (Waves::FFTCalculator / Waves::Generator / Vision::RenderDevice shim) over the C ABI.
 WAVES_SRC := $(CSRC)/waves/RenderDevice.cpp $(CSRC)/waves/FFTCalculator.cpp $(CSRC)/waves/Generator.cpp \
-             $(CSRC)/waves/Surface.cpp
+             $(CSRC)/waves/Surface.cpp $(CSRC)/waves/SlabGenerator.cpp
 $(WAVES): $(WAVES_SRC) include/waves/Generator.h include/waves/FFTCalculator.h include/waves/Surface.h \
+          include/waves/SlabGenerator.h \
           include/vision/RenderDevice.h $(LIB)
 	g++ -O2 -std=c++17 -fPIC -shared -Iinclude -I/opt/rocm/include -D__HIP_PLATFORM_AMD__ -o $@ $(WAVES_SRC) \
 	    -L$(PKG) -loceanfft -Wl,-rpath,'$$ORIGIN' -L/opt/rocm/lib -lamdhip64
@@ -58,7 +59,7 @@ $(APP): examples/waveapp_headless.cpp $(WAVES)
 	    -L$(PKG) -lwaves -loceanfft -Wl,-rpath,'$$ORIGIN/../$(PKG)' -L/opt/rocm/lib -lamdhip64
 
 MB := tools/microbench
-microbench: $(MB)/rm16bench $(MB)/gen4bench $(MB)/ifft4bench $(MB)/gridbench $(MB)/halfbench_nohs $(MB)/ifftbench $(MB)/transbench $(MB)/scatterbench $(MB)/halfbench $(MB)/genbench $(MB)/colbench $(MB)/copybench $(MB)/genbench_noxch $(MB)/genbench_nobar $(MB)/layoutbench
+microbench: $(MB)/detbench $(MB)/detbench_soffset $(MB)/rm16bench $(MB)/gen4bench $(MB)/ifft4bench $(MB)/gridbench $(MB)/halfbench_nohs $(MB)/ifftbench $(MB)/transbench $(MB)/scatterbench $(MB)/halfbench $(MB)/genbench $(MB)/colbench $(MB)/copybench $(MB)/genbench_noxch $(MB)/genbench_nobar $(MB)/layoutbench
 MB_DEPS := $(KERNEL_TUS:%=$(CSRC)/%.hip) $(DEVICE_H) $(MB)/ab_kernels.h $(MB)/all_kernels.h
 $(MB)/%: $(MB)/%.hip $(MB_DEPS)
 	$(HIPCC) $(HIPFLAGS) $< -o $@
@@ -67,11 +68,13 @@ $(MB)/genbench_noxch: $(MB)/genbench.hip $(MB_DEPS)
 	$(HIPCC) $(HIPFLAGS) -DOCEAN_ABLATE_EXCHANGE $< -o $@
 $(MB)/halfbench_nohs: $(MB)/halfbench.hip $(MB_DEPS)
 	$(HIPCC) $(HIPFLAGS) -DOCEAN_ABLATE_HS $< -o $@
+$(MB)/detbench_soffset: $(MB)/detbench.hip $(MB_DEPS)
+	$(HIPCC) $(HIPFLAGS) -DOCEAN_SOFFSET_PIECES $< -o $@
 $(MB)/genbench_nobar: $(MB)/genbench.hip $(MB_DEPS)
 	$(HIPCC) $(HIPFLAGS) -DOCEAN_ABLATE_BARRIER $< -o $@
 
 clean:
-	rm -rf $(MB)/rm16bench $(MB)/gen4bench $(MB)/ifft4bench $(MB)/gridbench $(MB)/halfbench_nohs $(MB)/ifftbench $(MB)/transbench $(MB)/scatterbench $(MB)/halfbench $(MB)/genbench $(MB)/colbench $(MB)/copybench $(MB)/genbench_noxch $(MB)/genbench_nobar $(MB)/layoutbench $(CSRC)/build $(LIB) $(WAVES) $(CPPTEST) $(APP)
+	rm -rf $(MB)/detbench $(MB)/detbench_soffset $(MB)/rm16bench $(MB)/gen4bench $(MB)/ifft4bench $(MB)/gridbench $(MB)/halfbench_nohs $(MB)/ifftbench $(MB)/transbench $(MB)/scatterbench $(MB)/halfbench $(MB)/genbench $(MB)/colbench $(MB)/copybench $(MB)/genbench_noxch $(MB)/genbench_nobar $(MB)/layoutbench $(CSRC)/build $(LIB) $(WAVES) $(CPPTEST) $(APP)
 	$(MAKE) -s -C oracle clean
 
 .PHONY: all clean microbench

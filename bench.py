@@ -67,6 +67,9 @@ def parse(argv=None):
     ap.add_argument("--no-ifft", action="store_true", help="skip the EncodeIFFT-only and rocFFT legs")
     ap.add_argument("--no-surface", action="store_true", help="skip the surface-consumer leg")
     ap.add_argument("--no-reseed", action="store_true", help="skip the re-seed-every-frame leg")
+    ap.add_argument("--headline-only", action="store_true",
+                    help="the headline loop alone (every optional leg off): what tools/profile_gpu.sh profiles, "
+                         "so each kernel's launches all cover the headline workload")
     ap.add_argument("--legs-timeout", type=float, default=300.0,
                     help="seconds allowed for the optional legs after the headline measurement; past it the "
                          "line is printed without the unfinished legs and every rank exits")
@@ -85,7 +88,10 @@ def parse(argv=None):
     ap.add_argument("--plumbing-check", action="store_true",
                     help="launcher/rank plumbing only (no GPU work): every rank joins the process group, "
                          "runs the barrier + max-over-ranks protocol, and rank 0 prints a line naming n_gpus")
-    return ap.parse_args(argv)
+    args = ap.parse_args(argv)
+    if args.headline_only:
+        args.no_reseed = args.no_ifft = args.no_slab = args.no_surface = args.no_cpu_baseline = True
+    return args
 
 
 ARGV_ENV = "OCEAN_BENCH_ARGV"  # launch_ranks -> its ranks: the original argument list (JSON)
@@ -891,7 +897,9 @@ def main(argv=None):
     gen.close()
     watchdog = start_legs_watchdog(out, rank, args.legs_timeout)
     try:
-        if world > 1:
+        if args.headline_only:
+            pass
+        elif world > 1:
             out["weak_scaling"] = weak_leg(ocean, fft, args, rank, world, dt)
         else:
             out["strong_scaling"] = one_cascade_leg(ocean, fft, args, dt)

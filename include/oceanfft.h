@@ -203,6 +203,9 @@ int ocean_comm_create(ocean_comm** out, const unsigned char id[OCEAN_COMM_ID_BYT
 /* Use a communicator the caller already has (an ncclComm_t; not destroyed by ocean_comm_destroy). */
 int ocean_comm_wrap(ocean_comm** out, void* nccl_comm, int nranks, int rank);
 int ocean_comm_destroy(ocean_comm* comm);
+/* The equal-split all-to-all of caller device buffers over the communicator (bytes / nranks to each
+ * rank), enqueued on hip_stream: for callers that run ocean_generator_slab_columns / _rows themselves. */
+int ocean_comm_all_to_all(ocean_comm* comm, const void* send, void* recv, size_t bytes, void* hip_stream);
 /* One frame: time += dt, h0 if needed, column pass into the library's send buffer, the all-to-all,
  * row pass — all enqueued on the generator's stream (src/Generator.cpp:45-83 over P ranks). */
 int ocean_generator_slab_frame(ocean_generator* gen, ocean_comm* comm, float timestep, int update_spectrum);

@@ -95,6 +95,7 @@ SIGNATURES = {
     "ocean_comm_create": (_i, [ctypes.POINTER(_vp), _vp, _i, _i]),
     "ocean_comm_wrap": (_i, [ctypes.POINTER(_vp), _vp, _i, _i]),
     "ocean_comm_destroy": (_i, [_vp]),
+    "ocean_comm_all_to_all": (_i, [_vp, _vp, _vp, _sz, _vp]),
     "ocean_generator_slab_frame": (_i, [_vp, _vp, _f, _i]),
     "ocean_generator_slab_frame_pipelined": (_i, [_vp, _vp, _f, _i]),
     "ocean_generator_slab_flush": (_i, [_vp]),

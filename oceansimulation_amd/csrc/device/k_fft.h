@@ -68,7 +68,9 @@ __global__ __launch_bounds__(RowCfg<LOGN>::WG, RowCfg<LOGN>::MIN_WAVES) void k_r
 }
 
 // Column pass in place: strips of C texel columns, transformed along y.
-template <int LOGN>
+// GROUP: consecutive strips on blocks b, b + 8, ... (one XCD, xcd_group_slot), so the partial lines
+// of C-column pieces (C * 16 B) meet in one L2.
+template <int LOGN, int GROUP = 2>
 __global__ __launch_bounds__(ColCfg<LOGN>::WG) void k_cols(int n_images, float4* __restrict__ images,
                                                            const float2* __restrict__ tw_glob)
 {
@@ -82,7 +84,7 @@ __global__ __launch_bounds__(ColCfg<LOGN>::WG) void k_cols(int n_images, float4*
 
   const int c0 = threadIdx.x % C, i0 = threadIdx.x / C;
   const int total = n_images * K::STRIPS;
-  for (int item = xcd_pair_slot(blockIdx.x, gridDim.x); item < total; item += gridDim.x)
+  for (int item = xcd_group_slot<GROUP>(blockIdx.x, gridDim.x); item < total; item += gridDim.x)
   {
     const int c = opaque(c0), i = opaque(i0);
     const int img = item / K::STRIPS, strip = item - img * K::STRIPS;

@@ -170,17 +170,16 @@ __global__ __launch_bounds__(FftShape<LOGN2>::T * CI, CI < ColCfg<LOGN2>::C ? 4 
       v[m] = PAIRS ? raw_pair(r) : to_pair(r);
     }
     fft_run<LOGN2, C, true>(v, i, cc, xch, tw);
-    const int soff = (16 * i * pitch + u) * 16;
-    if (live)
+    // columns past `cols` get an offset past the descriptor's range: the store is dropped (no branch)
+    const int soff = live ? (16 * i * pitch + u) * 16 : kAllBytes;
 #pragma unroll
-      for (int m = 0; m < 16; m++)
-      {
-        const int q = (m * T) / kpb, k2b = m * T - q * kpb;
-        // the block row base is built at its store (sopaque): hoisted, the 16 bases take 32 SGPRs
-        unsigned char* dst = send + sopaque(q * g.blk_bytes + part_off +
-                                            ((size_t)c * g.w + k1 + 16 * k2b) * pitch * 16);
-        st4<kStream>(dst, soff, PAIRS ? pair_raw(v[m]) : from_pair(v[m]));
-      }
+    for (int m = 0; m < 16; m++)
+    {
+      const int q = (m * T) / kpb, k2b = m * T - q * kpb;
+      // the block row base is built at its store (sopaque): hoisted, the 16 bases take 32 SGPRs
+      unsigned char* dst = send + sopaque(q * g.blk_bytes + part_off + ((size_t)c * g.w + k1 + 16 * k2b) * pitch * 16);
+      st4<kStream>(dst, soff, PAIRS ? pair_raw(v[m]) : from_pair(v[m]));
+    }
   }
 }
 

@@ -62,14 +62,21 @@ __device__ __forceinline__ void st1(void* base, int voff_bytes, float v)
   __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), srd(base, kAllBytes), voff_bytes, 0, AUX);
 }
 
-// The same with a wave-uniform byte offset in the instruction's SGPR soffset field: call sites that
-// touch 16 pieces of one buffer per item (m * stride) keep ONE descriptor (4 SGPRs) and pass the
-// piece offset as soffset, instead of building 16 descriptors. k_cols_half built ~50 per item and
-// spilled SGPRs to VGPR lanes (476 v_readlane/v_writelane per item at 112 SGPRs).
+// The same with a second, wave-uniform byte offset (the piece offset m * stride of a call site that
+// touches 16 pieces of one buffer per item): ONE descriptor (4 SGPRs) per buffer, the piece offset
+// added to the lane offset in the VGPR voffset. k_cols_half built one descriptor per piece (~50 per
+// item) and spilled SGPRs to VGPR lanes (476 v_readlane/v_writelane per item at 112 SGPRs).
+// OCEAN_SOFFSET_PIECES (tools/microbench/detbench only) passes the piece offset in the instruction's
+// SGPR soffset field instead: the build round 2 recorded as non-deterministic.
+#if defined(OCEAN_SOFFSET_PIECES)
+#define OCEAN_PIECE(voff, soff) (voff), (soff)
+#else
+#define OCEAN_PIECE(voff, soff) (voff) + (soff), 0
+#endif
 template <int AUX = 0>
 __device__ __forceinline__ float4 ld4s(const void* base, int voff_bytes, int soff_bytes)
 {
-  f4v r = __builtin_amdgcn_raw_buffer_load_b128(srd(base, kAllBytes), voff_bytes + soff_bytes, 0, AUX);
+  f4v r = __builtin_amdgcn_raw_buffer_load_b128(srd(base, kAllBytes), OCEAN_PIECE(voff_bytes, soff_bytes), AUX);
   return make_float4(r.x, r.y, r.z, r.w);
 }
 
@@ -77,13 +84,13 @@ template <int AUX = 0>
 __device__ __forceinline__ void st4s(void* base, int voff_bytes, int soff_bytes, float4 v)
 {
   f4v r = {v.x, v.y, v.z, v.w};
-  __builtin_amdgcn_raw_buffer_store_b128(r, srd(base, kAllBytes), voff_bytes + soff_bytes, 0, AUX);
+  __builtin_amdgcn_raw_buffer_store_b128(r, srd(base, kAllBytes), OCEAN_PIECE(voff_bytes, soff_bytes), AUX);
 }
 
 template <int AUX = 0>
 __device__ __forceinline__ float2 ld2s(const void* base, int voff_bytes, int soff_bytes)
 {
-  u2v r = __builtin_amdgcn_raw_buffer_load_b64(srd(base, kAllBytes), voff_bytes + soff_bytes, 0, AUX);
+  u2v r = __builtin_amdgcn_raw_buffer_load_b64(srd(base, kAllBytes), OCEAN_PIECE(voff_bytes, soff_bytes), AUX);
   return make_float2(__uint_as_float(r.x), __uint_as_float(r.y));
 }
 
@@ -91,7 +98,7 @@ template <int AUX = 0>
 __device__ __forceinline__ void st2s(void* base, int voff_bytes, int soff_bytes, float2 v)
 {
   u2v r = {__float_as_uint(v.x), __float_as_uint(v.y)};
-  __builtin_amdgcn_raw_buffer_store_b64(r, srd(base, kAllBytes), voff_bytes + soff_bytes, 0, AUX);
+  __builtin_amdgcn_raw_buffer_store_b64(r, srd(base, kAllBytes), OCEAN_PIECE(voff_bytes, soff_bytes), AUX);
 }
 
 __device__ __forceinline__ int clamp_bytes(int64_t b)

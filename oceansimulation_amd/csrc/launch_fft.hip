@@ -138,10 +138,10 @@ hipError_t launch_ifft_colfirst(int logn, int n_images, float4* images, float4* 
   constexpr int LOGN = 12;
   using K = ColFirstCfg<LOGN>;
   using S = FftShape<LOGN>;
-  const int tw_bytes = ((S::TW_ENTRIES * 8 + 15) / 16) * 16;
+  constexpr int tw_lds = tw_bytes<S::TW_ENTRIES>();
   {
     auto kern = k_cols_to_blocks<LOGN>;
-    const int lds = tw_bytes + K::LDS1;
+    const int lds = tw_lds + K::LDS1;
     const int grid = persistent_grid(kern, K::WG1, lds, n_images * (S::N / K::B), cus);
     hipLaunchKernelGGL(kern, dim3(grid), dim3(K::WG1), lds, stream, n_images, images, work, tw);
     hipError_t e = hipGetLastError();
@@ -149,7 +149,7 @@ hipError_t launch_ifft_colfirst(int logn, int n_images, float4* images, float4* 
       return e;
   }
   auto kern = k_rows_final<LOGN, true>;
-  const int lds = tw_bytes + K::LDS2;
+  const int lds = tw_lds + K::LDS2;
   const SlabGeom g{0, S::N};
   const int grid = persistent_grid(kern, K::WG2, lds, n_images * (S::N / K::RPW2), cus);
   hipLaunchKernelGGL(kern, dim3(grid), dim3(K::WG2), lds, stream, n_images, g, work, images, (float*)nullptr,

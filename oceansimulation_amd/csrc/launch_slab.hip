@@ -13,6 +13,7 @@
 #include "device/k_gen4.h"
 #include "device/k_half_cols.h"
 #include "device/k_half_rows.h"
+#include "device/k_rows_xs.h"
 #include "device/spectrum.h"
 
 namespace oceanfft
@@ -79,7 +80,9 @@ hipError_t launch_half_slab_columns(int logn, const FrameParams& fp, const HalfS
 // or the four-step path's exchange blocks). N = 16384 (T = 1024, one row per workgroup): the XS x
 // transform (barriers 14 -> 7 per image), which needs tw2, the N/16-point table ocean_fft_create
 // appends for the sizes fourstep_table() names.
-inline int rm_rows_variant = 1;  // tools/microbench A/B: 0 = the plain transform at 16384
+// tools/microbench A/B at 16384: 0 = the plain transform, 1 = XS (k_rows_half), 2 = k_rows_xs, 3 =
+// k_rows_xs with 2 of the next image's 8 field loads in flight during the transform (PF; 4 spill)
+inline int rm_rows_variant = 3;
 
 template <int LOGN>
 hipError_t launch_rm_rows(const FrameParams& fp, const RowSrc& rs, const float4* spec, float4* maps, float* jac,
@@ -92,6 +95,16 @@ hipError_t launch_rm_rows(const FrameParams& fp, const RowSrc& rs, const float4*
     return hipErrorInvalidValue;
   if constexpr (RPW == 1)
   {
+    if (rm_rows_variant >= 2)
+    {
+      if (!tw2)
+        return hipErrorInvalidValue;
+      auto kern = rm_rows_variant == 3 ? k_rows_xs<LOGN, 2> : k_rows_xs<LOGN, 0>;
+      const int lds = XsCfg<LOGN>::LDS;
+      const int grid = persistent_grid(kern, S::T, lds, fp.cascades * rows, cus);
+      hipLaunchKernelGGL(kern, dim3(grid), dim3(S::T), lds, stream, fp, spec, maps, jac, foam, tw, rows, rs, tw2);
+      return hipGetLastError();
+    }
     if (rm_rows_variant != 0)
     {
       if (!tw2)

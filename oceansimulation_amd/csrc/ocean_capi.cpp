@@ -1009,24 +1009,37 @@ int nccl_fail(ncclResult_t r, const char* what)
   return fail(OCEAN_ERR_HIP, std::string(what) + ": " + ncclGetErrorString(r));
 }
 
-// Enqueue this frame's all-to-all (send slot -> recv slot) on `stream`.
-int exchange_blocks(ocean_generator* g, ocean_comm* c, const unsigned char* send, unsigned char* recv,
-                    hipStream_t stream)
+// The equal-split all-to-all of blk bytes per rank pair, enqueued on `stream`: one group of
+// ncclSend / ncclRecv pairs, each block in pieces of at most kExchangePiece bytes (RCCL 2.26 corrupted
+// a single send / receive above 1 GiB in a world-size-1 self exchange: tools/rccl_selfcheck.py,
+// profiles/r03_rccl_selfcheck.log; a whole 8192^2 block is 1.35 GB).
+constexpr size_t kExchangePiece = (size_t)512 << 20;
+
+int exchange_bytes_all_to_all(ocean_comm* c, const unsigned char* send, unsigned char* recv, size_t blk,
+                              hipStream_t stream)
 {
-  const size_t blk = ocean_generator_exchange_bytes(g) / g->ranks;
   ncclResult_t r = ncclGroupStart();
-  for (int q = 0; q < g->ranks && r == ncclSuccess; q++)
-  {
-    r = ncclSend(send + q * blk, blk, ncclUint8, q, c->comm, stream);
-    if (r == ncclSuccess)
-      r = ncclRecv(recv + q * blk, blk, ncclUint8, q, c->comm, stream);
-  }
+  for (int q = 0; q < c->nranks && r == ncclSuccess; q++)
+    for (size_t o = 0; o < blk && r == ncclSuccess; o += kExchangePiece)
+    {
+      const size_t len = std::min(kExchangePiece, blk - o);
+      r = ncclSend(send + q * blk + o, len, ncclUint8, q, c->comm, stream);
+      if (r == ncclSuccess)
+        r = ncclRecv(recv + q * blk + o, len, ncclUint8, q, c->comm, stream);
+    }
   const ncclResult_t e = ncclGroupEnd();
   if (r != ncclSuccess)
     return nccl_fail(r, "slab exchange (ncclSend / ncclRecv)");
   if (e != ncclSuccess)
     return nccl_fail(e, "slab exchange (ncclGroupEnd)");
   return OCEAN_OK;
+}
+
+// Enqueue this frame's all-to-all (send slot -> recv slot) on `stream`.
+int exchange_blocks(ocean_generator* g, ocean_comm* c, const unsigned char* send, unsigned char* recv,
+                    hipStream_t stream)
+{
+  return exchange_bytes_all_to_all(c, send, recv, ocean_generator_exchange_bytes(g) / g->ranks, stream);
 }
 
 // The two exchange slots, the comm stream and its events (first use, or after a path switch that
@@ -1174,6 +1187,14 @@ int ocean_comm_destroy(ocean_comm* comm)
     r = ncclCommDestroy(comm->comm);
   delete comm;
   return r == ncclSuccess ? OCEAN_OK : nccl_fail(r, "ncclCommDestroy");
+}
+
+int ocean_comm_all_to_all(ocean_comm* comm, const void* send, void* recv, size_t bytes, void* hip_stream)
+{
+  if (!comm || !comm->comm || (bytes > 0 && (!send || !recv)) || bytes % comm->nranks != 0)
+    return fail(OCEAN_ERR_INVALID, "ocean_comm_all_to_all: null argument or bytes not a multiple of the rank count");
+  return exchange_bytes_all_to_all(comm, static_cast<const unsigned char*>(send), static_cast<unsigned char*>(recv),
+                                   bytes / comm->nranks, (hipStream_t)hip_stream);
 }
 
 int ocean_generator_slab_frame(ocean_generator* g, ocean_comm* comm, float timestep, int update_spectrum)

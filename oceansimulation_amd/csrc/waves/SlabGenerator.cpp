@@ -1,0 +1,84 @@
+// SlabGenerator.cpp — Waves::SlabComm / Waves::SlabGenerator over the slab C ABI and its RCCL exchange.
+#include "waves/SlabGenerator.h"
+
+#include <stdexcept>
+#include <string>
+
+namespace Waves
+{
+
+static void check(int rc, const char* what)
+{
+  if (rc != OCEAN_OK)
+    throw std::runtime_error(std::string(what) + ": " + ocean_last_error());
+}
+
+SlabComm::UniqueId SlabComm::NewUniqueId()
+{
+  UniqueId id{};
+  check(ocean_comm_unique_id(id.data()), "Waves::SlabComm::NewUniqueId");
+  return id;
+}
+
+SlabComm::SlabComm(const UniqueId& id, int ranks_, int rank_) : ranks(ranks_), rank(rank_)
+{
+  check(ocean_comm_create(&comm, id.data(), ranks, rank), "Waves::SlabComm");
+}
+
+SlabComm::SlabComm(void* ncclComm, int ranks_, int rank_) : ranks(ranks_), rank(rank_)
+{
+  check(ocean_comm_wrap(&comm, ncclComm, ranks, rank), "Waves::SlabComm");
+}
+
+SlabComm::~SlabComm() { ocean_comm_destroy(comm); }
+
+SlabGenerator::SlabGenerator(Vision::RenderDevice* device, FFTCalculator* calc, SlabComm* comm)
+  : renderDevice(device), slabComm(comm)
+{
+  if (!device || !calc || !comm)
+    throw std::runtime_error("Waves::SlabGenerator: null RenderDevice, FFTCalculator or SlabComm");
+  check(ocean_generator_create_slab(&gen, calc->GetPlan(), comm->GetRank(), comm->GetRanks()),
+        "Waves::SlabGenerator");
+  int r = 0, p = 0;
+  if (ocean_generator_slab_info(gen, &r, &p, &row0, &rows) != OCEAN_OK)
+  {
+    ocean_generator_destroy(gen);
+    throw std::runtime_error(std::string("Waves::SlabGenerator: ") + ocean_last_error());
+  }
+  const std::size_t n = calc->GetTextureResolution();
+  heightMap = renderDevice->RegisterTexture2D(ocean_generator_height_map(gen, 0), n, rows,
+                                              Vision::PixelType::RGBA32Float);
+  displacementMap = renderDevice->RegisterTexture2D(ocean_generator_displacement_map(gen, 0), n, rows,
+                                                    Vision::PixelType::RGBA32Float);
+  jacobian = renderDevice->RegisterTexture2D(ocean_generator_jacobian_map(gen, 0), n, rows,
+                                             Vision::PixelType::R32Float);
+}
+
+SlabGenerator::~SlabGenerator()
+{
+  renderDevice->DestroyTexture2D(heightMap);
+  renderDevice->DestroyTexture2D(displacementMap);
+  renderDevice->DestroyTexture2D(jacobian);
+  ocean_generator_destroy(gen);
+}
+
+GeneratorSettings& SlabGenerator::GetOceanSettings()
+{
+  return *reinterpret_cast<GeneratorSettings*>(ocean_generator_settings(gen, 0));
+}
+
+void SlabGenerator::CalculateOcean(float timestep, bool updateOcean)
+{
+  check(ocean_generator_slab_frame(gen, slabComm->GetHandle(), timestep, updateOcean ? 1 : 0),
+        "Waves::SlabGenerator::CalculateOcean");
+}
+
+void SlabGenerator::CalculateOceanPipelined(float timestep, bool updateOcean)
+{
+  check(ocean_generator_slab_frame_pipelined(gen, slabComm->GetHandle(), timestep, updateOcean ? 1 : 0),
+        "Waves::SlabGenerator::CalculateOceanPipelined");
+}
+
+void SlabGenerator::Flush() { check(ocean_generator_slab_flush(gen), "Waves::SlabGenerator::Flush"); }
+
+}  // namespace Waves

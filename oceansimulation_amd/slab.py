@@ -150,6 +150,11 @@ class RcclComm:
     def handle(self):
         return self._h
 
+    def all_to_all(self, send_ptr: int, recv_ptr: int, nbytes: int, stream: int | None = None) -> None:
+        """Equal-split all-to-all of device buffers (ocean_comm_all_to_all), enqueued on `stream`."""
+        check(lib().ocean_comm_all_to_all(self._h, ctypes.c_void_p(send_ptr), ctypes.c_void_p(recv_ptr), nbytes,
+                                          ctypes.c_void_p(stream or 0)), "ocean_comm_all_to_all")
+
     def close(self) -> None:
         if self._h:
             lib().ocean_comm_destroy(self._h)

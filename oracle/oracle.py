@@ -155,7 +155,7 @@ def prepare_fft_rows(s: OracleSettings, n: int, y0: int, h0_rows: np.ndarray):
     return height, disp
 
 
-def sampled_frame(s: OracleSettings, n: int, xs, ys, chunk: int = 256):
+def sampled_frame(s: OracleSettings, n: int, xs, ys, chunk: int = 256, progress: bool = False):
     """The frame's maps at the sample points (xs x ys) without a full-size transform: the oracle's h0
     and prepareFFT (fp32, the reference's arithmetic) on spectrum rows in chunks, then the 2D inverse
     DFT of EncodeIFFT (N^2 ifft2(ifftshift), src/FFTCalculator.cpp:73-114) evaluated in float64 at
@@ -167,6 +167,8 @@ def sampled_frame(s: OracleSettings, n: int, xs, ys, chunk: int = 256):
     ey = np.exp(2j * np.pi * np.outer(idx, ys) / n)  # [N, Y]
     acc = np.zeros((4, len(ys), n), np.complex128)   # lanes: height xy, zw; disp xy, zw
     for y0 in range(0, n, chunk):
+        if progress and y0 % (16 * chunk) == 0:
+            print(f"sampled_frame: spectrum rows {y0} / {n}", flush=True)
         rows = min(chunk, n - y0)
         h, d = prepare_fft_rows(s, n, y0, spectrum_rows(s, n, y0, rows))
         for k, (img, lane) in enumerate(((h, 0), (h, 1), (d, 0), (d, 1))):

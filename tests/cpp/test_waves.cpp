@@ -4,7 +4,9 @@
 // Scene = WaveApp's (src/Waves.cpp:14-39): one FFTCalculator shared by 3 Generators, plane sizes
 // 5/17/101 m, boundWavelength = 1, wavelength bounds; per frame CalculateOcean(dt, true) for
 // every generator (src/Waves.cpp:90-91: updateSpectrum is never cleared). Also checks
-// FFTCalculator::EncodeIFFT on a random image. Exit code 0 = all within tolerance.
+// FFTCalculator::EncodeIFFT on a random image, and Waves::SlabGenerator at world size 1 (the RCCL
+// exchange with one rank, pipelined and not) against a whole-grid Waves::Generator, bit for bit.
+// Usage: test_waves [n] [frames] [slab n, 0 = skip]. Exit code 0 = all within tolerance.
 #include <hip/hip_runtime_api.h>
 
 #include <cmath>
@@ -17,6 +19,7 @@
 #include "ocean_oracle.h"
 #include "waves/FFTCalculator.h"
 #include "waves/Generator.h"
+#include "waves/SlabGenerator.h"
 
 static double rel_err(const std::vector<float>& got, const std::vector<float>& ref, int stride, int ch)
 {
@@ -29,10 +32,58 @@ static double rel_err(const std::vector<float>& got, const std::vector<float>& r
   return maxref > 0 ? maxerr / maxref : maxerr;
 }
 
+// Waves::SlabGenerator over a one-rank communicator (the library's RCCL all-to-all, pipelined and
+// not) against Waves::Generator on the whole grid: the same kernels on the same columns, so the maps
+// must agree bit for bit.
+static int slab_world1(Vision::RenderDevice& device, int n, int frames)
+{
+  int failures = 0;
+  Waves::FFTCalculator fft(&device, n);
+  Waves::SlabComm comm(Waves::SlabComm::NewUniqueId(), 1, 0);
+  Waves::Generator whole(&device, &fft);
+  Waves::SlabGenerator serial(&device, &fft, &comm), piped(&device, &fft, &comm);
+  if (serial.GetFirstRow() != 0 || serial.GetRows() != n)
+  {
+    std::printf("slab n=%d: row slab %d + %d, expected 0 + %d\n", n, serial.GetFirstRow(), serial.GetRows(), n);
+    return 1;
+  }
+  for (auto* s : {&serial.GetOceanSettings(), &piped.GetOceanSettings()})
+    *s = whole.GetOceanSettings();
+  const float dt = 1.0f / 60.0f;
+  for (int f = 0; f < frames; f++)
+  {
+    whole.CalculateOcean(dt, f == 0);
+    serial.CalculateOcean(dt, f == 0);
+    piped.CalculateOceanPipelined(dt, f == 0);
+  }
+  piped.Flush();
+  const size_t texels = (size_t)n * n;
+  std::vector<float> a(texels * 4), b(texels * 4), c(texels * 4);
+  const Vision::ID ids[3][3] = {{whole.GetHeightMap(), serial.GetHeightMap(), piped.GetHeightMap()},
+                                {whole.GetDisplacementMap(), serial.GetDisplacementMap(), piped.GetDisplacementMap()},
+                                {whole.GetJacobianMap(), serial.GetJacobianMap(), piped.GetJacobianMap()}};
+  static const char* names[3] = {"heightMap", "displacementMap", "jacobian"};
+  for (int m = 0; m < 3; m++)
+  {
+    const size_t bytes = texels * (m == 2 ? 4 : 16);
+    device.GetTexture2DDataRaw(ids[m][0], a.data());
+    device.GetTexture2DDataRaw(ids[m][1], b.data());
+    device.GetTexture2DDataRaw(ids[m][2], c.data());
+    const bool ok_s = std::memcmp(a.data(), b.data(), bytes) == 0, ok_p = std::memcmp(a.data(), c.data(), bytes) == 0;
+    std::printf("slab n=%d world 1 %s: serial %s, pipelined %s\n", n, names[m], ok_s ? "bit-exact" : "DIFFERS",
+                ok_p ? "bit-exact" : "DIFFERS");
+    failures += !ok_s + !ok_p;
+  }
+  if (serial.GetOceanSettings().time != whole.GetOceanSettings().time)
+    failures++;
+  return failures;
+}
+
 int main(int argc, char** argv)
 {
   const int n = argc > 1 ? std::atoi(argv[1]) : 256;
   const int frames = argc > 2 ? std::atoi(argv[2]) : 3;
+  const int slab_n = argc > 3 ? std::atoi(argv[3]) : 1024;
   int failures = 0;
 
   Vision::RenderDevice device;  // default stream
@@ -123,6 +174,8 @@ int main(int argc, char** argv)
   }
   for (auto* g : generators)
     delete g;
+  if (slab_n > 0)
+    failures += slab_world1(device, slab_n, frames);
   std::printf("%s (%d failures)\n", failures ? "FAIL" : "PASS", failures);
   return failures ? 1 : 0;
 }

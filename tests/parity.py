@@ -20,6 +20,7 @@ import numpy as np
 
 FFT_TOL = 2e-5
 FRAME_TOL = 1e-4
+FRAME_TOL_GPU = 1e-5
 H0_TOL = 1e-5
 
 

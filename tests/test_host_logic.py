@@ -153,9 +153,7 @@ def test_traffic_attribution_needs_same_device_code(tmp_path, monkeypatch):
     import shutil
 
     b = _bench()
-    src = open(os.path.join(ROOT, "tools", "parse_rocprof.py")).read().split("src, tag =")[0]
-    g = {"__file__": os.path.join(ROOT, "tools", "parse_rocprof.py"), "__name__": "parse_rocprof"}
-    exec(src, g)
+    g = vars(_parse_rocprof())
     assert g["device_source_sha256"]() == b.device_source_sha256()
     assert g["base_name"]("void oceanfft::k_rows_half<12, 0, 2>(oceanfft::FrameParams, float*)") == "k_rows_half"
     # a fake tree: same device code, one matching and one stale summary
@@ -171,3 +169,73 @@ def test_traffic_attribution_needs_same_device_code(tmp_path, monkeypatch):
     (root / "profiles" / "r01_same_rocprof.json").write_text(json.dumps(dict(rec, device_source_sha256=sha)))
     got = b.measured_traffic("k_rows_half", 4096, 8)
     assert got["hbm_traffic_bytes"] == 123.0 and "r01_same_rocprof.json" in got["source"]
+
+
+def _parse_rocprof():
+    import importlib.util
+
+    spec = importlib.util.spec_from_file_location("parse_rocprof", os.path.join(ROOT, "tools", "parse_rocprof.py"))
+    m = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(m)
+    return m
+
+
+def _write_csv(path, header, rows):
+    import csv
+
+    path.parent.mkdir(parents=True, exist_ok=True)
+    with open(path, "w", newline="") as f:
+        w = csv.writer(f, quoting=csv.QUOTE_NONNUMERIC)
+        w.writerow(header)
+        w.writerows(rows)
+
+
+def _fake_profile(tmp_path, rows_ms):
+    """A gpurun_out-like directory: kernel trace + FETCH_SIZE + WRITE_SIZE CSVs in rocprofv3's columns.
+    rows_ms: [(symbol, grid threads, workgroup threads, duration ms, FETCH_SIZE KB, WRITE_SIZE KB)]."""
+    th = ["Kind", "Dispatch_Id", "Kernel_Name", "Start_Timestamp", "End_Timestamp", "Workgroup_Size_X",
+          "Workgroup_Size_Y", "Workgroup_Size_Z", "Grid_Size_X", "Grid_Size_Y", "Grid_Size_Z"]
+    ch = ["Dispatch_Id", "Grid_Size", "Kernel_Name", "Workgroup_Size", "Counter_Name", "Counter_Value"]
+    trace, fetch, write = [], [], []
+    for d, (sym, grid, wg, ms, fe, wr) in enumerate(rows_ms):
+        trace.append(["KERNEL_DISPATCH", d, sym, 1000, 1000 + int(ms * 1e6), wg, 1, 1, grid, 1, 1])
+        fetch.append([d, grid, sym, wg, "FETCH_SIZE", fe])
+        write.append([d, grid, sym, wg, "WRITE_SIZE", wr])
+    _write_csv(tmp_path / "p_trace" / "t_kernel_trace.csv", th, trace)
+    _write_csv(tmp_path / "p_fetch" / "f_counter_collection.csv", ch, fetch)
+    _write_csv(tmp_path / "p_write" / "w_counter_collection.csv", ch, write)
+
+
+def test_parse_rocprof_keys_by_geometry_and_size(tmp_path, monkeypatch):
+    """tools/parse_rocprof.py: durations and counters keyed by (kernel at its size, grid, workgroup); the
+    workload's algorithmic bytes only for the workload's size; "-" for kernels with no figure."""
+    import json
+
+    m = _parse_rocprof()
+    rows = "void oceanfft::k_rows_half<12, 1, 2>(oceanfft::FrameParams)"
+    other = "void oceanfft::k_rows_half<14, 1, 2>(oceanfft::FrameParams)"
+    nyq = "void oceanfft::k_half_nyquist<12>(oceanfft::FrameParams)"
+    _fake_profile(tmp_path, [(rows, 262144, 512, 1.4, 3e6, 4.5e6), (rows, 262144, 512, 1.4, 3e6, 4.5e6),
+                             (other, 262144, 1024, 4.0, 1e6, 1e6), (nyq, 8192, 256, 0.01, 10, 10)])
+    monkeypatch.chdir(tmp_path)
+    m.main(["parse_rocprof.py", str(tmp_path), "t", "4096", "8", "p"])
+    prof = json.load(open(tmp_path / "profiles" / "t_rocprof.json"))
+    rec = prof["kernels"]["k_rows_half"]
+    kept = (2048 + 4) / 4096
+    assert rec["calls"] == 2 and rec["algorithmic_bytes"] == int((40 * kept + 36) * 4096 * 4096 * 8)
+    assert rec["hbm_traffic_bytes"] == 3e6 * 2048 + 4.5e6 * 1024
+    assert prof["kernels"]["k_rows_half<14>"]["algorithmic_bytes"] is None  # another size: no borrowed bytes
+    assert prof["kernels"]["k_half_nyquist"]["algorithmic_bytes"] is None
+    md = open(tmp_path / "profiles" / "t_rocprof.md").read()
+    assert "| k_rows_half<14> | 256 x 1024 | 1 | 4.000 | - |" in md
+
+
+def test_parse_rocprof_refuses_above_peak(tmp_path, monkeypatch):
+    """A launch whose algorithmic rate would exceed the HBM peak covers less work than the workload the
+    bytes assume (e.g. a one-cascade launch of the same persistent grid): the parser refuses it."""
+    m = _parse_rocprof()
+    rows = "void oceanfft::k_rows_half<12, 1, 2>(oceanfft::FrameParams)"
+    _fake_profile(tmp_path, [(rows, 262144, 512, 0.18, 1, 1)])  # 8 cascades' bytes in a 1-cascade time
+    monkeypatch.chdir(tmp_path)
+    with pytest.raises(SystemExit, match="exceeds"):
+        m.main(["parse_rocprof.py", str(tmp_path), "t", "4096", "8", "p"])

@@ -416,4 +416,141 @@ hipError_t launch_policy_variant(int pass, int policy, const FrameParams& fp, co
   return hipGetLastError();
 }
 
+// Round 2's step 1 (whole grids only, compile-time pitch; its h0 descriptor per lane became a
+// waterfall loop per load): the same-box reference for k_gen4_step1 (gen4bench)
+template <int LOGN>
+struct Gen4CfgR2
+{
+  static constexpr int N = 1 << LOGN, N2 = N / 16, B = ColFirstCfg<LOGN>::B, KP = N / 2 + B;
+  static constexpr int PITCH = (KP + 15) / 16 * 16;
+};
+
+template <int LOGN, int MINW = 1>
+__global__ __launch_bounds__(256, MINW) void k_gen4_step1_r2(FrameParams fp, const float4* __restrict__ h0,
+                                                    unsigned char* __restrict__ parts, const float2* __restrict__ tw_glob)
+{
+  using S = FftShape<LOGN>;
+  using G = Gen4CfgR2<LOGN>;
+  constexpr int N = G::N, N2 = G::N2, KP = G::KP, PITCH = G::PITCH, XB = (KP + 63) / 64;
+  __shared__ float2 tw[S::TW_ENTRIES];
+  load_twiddles<LOGN>(tw, tw_glob);
+  const size_t part = (size_t)fp.cascades * N * PITCH;  // texels per part
+  float4* gab = reinterpret_cast<float4*>(parts);
+  float4* gde = gab + part;
+  float2* gc = reinterpret_cast<float2*>(gde + part);
+  const int total = fp.cascades * XB * (N2 / 4);
+  const float dim = (float)N;
+  for (int item = blockIdx.x; item < total; item += gridDim.x)
+  {
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    int t = item;
+    const int xbk = t % XB;
+    t /= XB;
+    const int n2 = (t % (N2 / 4)) * 4 + wv, c = t / (N2 / 4);
+    const int u = xbk * 64 + lane;
+    const bool live = u < KP;
+    const int uc = live ? u : KP - 1;  // columns past the last: loads clamped, nothing stored
+    const int x = uc < N / 2 ? N / 2 + uc : uc - N / 2;
+    const CascadeFrame f = fp.c[c];
+    // one descriptor for the item's h0 strip (uniform: 64 lanes = one 64-column block)
+    const float4* src = h0 + ((size_t)c * (N / kGen4Block) + x / kGen4Block) * N * kGen4Block;
+    const int loff = (n2 * kGen4Block + (x % kGen4Block)) * 16;
+    float2 H[16];
+    {
+      float4 a[16];
+#pragma unroll
+      for (int n1 = 0; n1 < 16; n1++)
+        a[n1] = ld4s<kStream>(src, loff, N2 * ((n1 + 8) & 15) * kGen4Block * 16);
+#pragma unroll
+      for (int n1 = 0; n1 < 16; n1++)
+        H[n1] = evolve(a[n1], make_kvec(x, N2 * ((n1 + 8) & 15) + n2, dim, f.dk).k, f);
+    }
+    // output row N2 k1 + n2 of the cascade: two descriptors per part (k1 < 8, k1 >= 8) keep the
+    // 32-bit offsets below 2 GiB
+    const size_t cb = (size_t)c * N * PITCH;
+    const int soff = (n2 * PITCH + u) * 16;
+#pragma unroll
+    for (int round = 0; round < 2; round++)
+    {
+      const int xr = opaque(x), n2r = opaque(n2);
+      CPair v[16];
+#pragma unroll
+      for (int n1 = 0; n1 < 16; n1++)
+      {
+        const KVec q = make_kvec(xr, N2 * ((n1 + 8) & 15) + n2r, dim, f.dk);
+        const float2 h = H[n1];
+        if (round == 0)  // (A, B) = (H, kz H)
+          v[n1] = CPair{f2v{h.x, q.kz * h.x}, f2v{h.y, q.kz * h.y}};
+        else  // (D, E) = (kz H / |k|, kz^2 H / |k|)
+        {
+          const float e = q.kz * q.dirz;
+          v[n1] = CPair{f2v{q.dirz * h.x, e * h.x}, f2v{q.dirz * h.y, e * h.y}};
+        }
+      }
+      idft16(v);
+      apply_stage_twiddles<LOGN>(v, n2r, tw);
+      float4* d0 = (round == 0 ? gab : gde) + cb;
+      float4* d1 = d0 + (size_t)8 * N2 * PITCH;
+      if (live)
+#pragma unroll
+        for (int k1 = 0; k1 < 16; k1++)
+          st4s<kStream>(k1 < 8 ? d0 : d1, soff, (k1 & 7) * N2 * PITCH * 16, pair_raw(v[k1]));
+    }
+    {
+      const int xr = opaque(x), n2r = opaque(n2);
+      float2 w[16];  // C = H / |k|, one complex lane
+#pragma unroll
+      for (int n1 = 0; n1 < 16; n1++)
+      {
+        const float inv = make_kvec(xr, N2 * ((n1 + 8) & 15) + n2r, dim, f.dk).inv;
+        w[n1] = make_float2(inv * H[n1].x, inv * H[n1].y);
+      }
+      idft16(w);
+      apply_stage_twiddles<LOGN>(w, n2r, tw);
+      float2* d0 = gc + cb;
+      if (live)
+#pragma unroll
+        for (int k1 = 0; k1 < 16; k1++)
+          st2s<kStream>(d0, soff / 2, k1 * N2 * PITCH * 8, w[k1]);
+    }
+  }
+}
+
+
+// The in-place column pass with GROUP strips per XCD group (ifft4bench)
+template <int GROUP>
+hipError_t launch_cols_group(int logn, int n_images, float4* images, const float2* tw, hipStream_t stream, int cus)
+{
+  return with_logn(logn, [&](auto L) -> hipError_t {
+    constexpr int LOGN = decltype(L)::value;
+    using K = ColCfg<LOGN>;
+    int lds = lds_bytes_cols<LOGN>();
+    auto kern = k_cols<LOGN, GROUP>;
+    int grid = persistent_grid(kern, K::WG, lds, n_images * K::STRIPS, cus);
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(K::WG), lds, stream, n_images, images, tw);
+    return hipGetLastError();
+  });
+}
+
+// Column-first EncodeIFFT at N = 8192 (B = 2: 32-B strided pieces, GROUP strips per XCD group) through a
+// work image, then the blocked row pass (ifft4bench)
+template <int GROUP>
+hipError_t launch_ifft_colfirst13(int n_images, float4* images, float4* work, const float2* tw, hipStream_t stream,
+                                  int cus)
+{
+  constexpr int LOGN = 13;
+  using K = ColFirstCfg<LOGN>;
+  using S = FftShape<LOGN>;
+  constexpr int tw_lds = tw_bytes<S::TW_ENTRIES>();
+  auto ka = k_cols_to_blocks<LOGN, 0, GROUP>;
+  const int grid = persistent_grid(ka, K::WG1, tw_lds + K::LDS1, n_images * (S::N / K::B), cus);
+  hipLaunchKernelGGL(ka, dim3(grid), dim3(K::WG1), tw_lds + K::LDS1, stream, n_images, images, work, tw);
+  auto kb = k_rows_final<LOGN, true>;
+  const SlabGeom g{0, S::N};
+  const int grid2 = persistent_grid(kb, K::WG2, tw_lds + K::LDS2, n_images * (S::N / K::RPW2), cus);
+  hipLaunchKernelGGL(kb, dim3(grid2), dim3(K::WG2), tw_lds + K::LDS2, stream, n_images, g, work, images,
+                     (float*)nullptr, FoamParams{}, tw);
+  return hipGetLastError();
+}
+
 }  // namespace oceanfft

@@ -121,8 +121,12 @@ int main()
     std::vector<float> t;
   };
   const double pts = (double)N * N;
+  auto s1r2 = [&](auto kern) {
+    return [=] { hipLaunchKernelGGL(kern, dim3(items1), dim3(256), 0, 0, fp, h0, buf, tw); };
+  };
   std::vector<V> vs = {
       {"step 1, launch bound 1 (production)", s1(k_gen4_step1<LOGN, 1>), 28 * pts, {}},
+      {"step 1 of round 2 (waterfall loads)", s1r2(k_gen4_step1_r2<LOGN, 1>), 28 * pts, {}},
       {"step 1, min 2 waves/SIMD", s1(k_gen4_step1<LOGN, 2>), 28 * pts, {}},
       {"step 1, min 3 waves/SIMD", s1(k_gen4_step1<LOGN, 3>), 28 * pts, {}},
       {"step 1, min 4 waves/SIMD", s1(k_gen4_step1<LOGN, 4>), 28 * pts, {}},
@@ -139,17 +143,17 @@ int main()
   vs[0].run();
   CHECK(hipDeviceSynchronize());
   auto ref1 = snap(buf, 40 * part);
-  for (int k = 1; k < 4; k++)
+  for (int k = 1; k < 5; k++)
   {
     CHECK(hipMemset(buf, 0, 40 * part));
     vs[k].run();
     CHECK(hipDeviceSynchronize());
     std::printf("%s: parts %s\n", vs[k].name.c_str(), snap(buf, 40 * part) == ref1 ? "bit-identical" : "DIFFER");
   }
-  vs[4].run();
+  vs[5].run();
   CHECK(hipDeviceSynchronize());
   auto ref2 = snap(rab, rt * 16);
-  for (int k = 5; k < 7; k++)
+  for (int k = 6; k < 8; k++)
   {
     CHECK(hipMemset(rab, 0, rt * 16));
     vs[k].run();

@@ -76,7 +76,7 @@ int main()
     float4 *img, *ref, *work;
     CHECK(hipMalloc(&img, tex * 16));
     CHECK(hipMalloc(&ref, tex * 16));
-    CHECK(hipMalloc(&work, ifft_fourstep_work_texels(logn, n) * 16));
+    CHECK(hipMalloc(&work, std::max(ifft_fourstep_work_texels(logn, n), tex) * 16));
     auto t1 = table(logn), t2 = table(logn - 4);
     float2 *tw, *tw2;
     CHECK(hipMalloc(&tw, t1.size() * 8));
@@ -119,6 +119,35 @@ int main()
     {
       names.push_back("rows + four-step cols, wc " + std::to_string(wc));
       runs.push_back([&, wc] { return launch_ifft_fourstep(logn, imgs, img, work, wc, tw, tw2, 0, cus); });
+    }
+    // in-place columns with more strips per XCD group (their partial lines meet in one L2)
+    names.push_back("in place rows + cols, 4 strips per XCD group");
+    runs.push_back([&] {
+      hipError_t e = launch_rows_ifft(logn, imgs, img, tw, 0, cus);
+      return e == hipSuccess ? launch_cols_group<4>(logn, imgs, img, tw, 0, cus) : e;
+    });
+    names.push_back("in place rows + cols, 8 strips per XCD group");
+    runs.push_back([&] {
+      hipError_t e = launch_rows_ifft(logn, imgs, img, tw, 0, cus);
+      return e == hipSuccess ? launch_cols_group<8>(logn, imgs, img, tw, 0, cus) : e;
+    });
+    names.push_back("cols only in place (production group)");
+    runs.push_back([&] { return launch_cols(logn, imgs, img, tw, 0, cus); });
+    names.push_back("cols only, 4 strips per XCD group");
+    runs.push_back([&] { return launch_cols_group<4>(logn, imgs, img, tw, 0, cus); });
+    names.push_back("cols only, 8 strips per XCD group");
+    runs.push_back([&] { return launch_cols_group<8>(logn, imgs, img, tw, 0, cus); });
+    if (logn == 13)
+    {
+      for (int grp : {2, 4, 8})
+      {
+        names.push_back("column-first via work image, group " + std::to_string(grp));
+        runs.push_back([&, grp] {
+          return grp == 2 ? launch_ifft_colfirst13<2>(imgs, img, work, tw, 0, cus)
+                          : grp == 4 ? launch_ifft_colfirst13<4>(imgs, img, work, tw, 0, cus)
+                                     : launch_ifft_colfirst13<8>(imgs, img, work, tw, 0, cus);
+        });
+      }
     }
     std::vector<std::vector<float>> t(runs.size());
     for (int r = 0; r < 5; r++)

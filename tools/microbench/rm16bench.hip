@@ -124,6 +124,12 @@ int main()
                          N, rs, tw2);
     };
   };
+  auto mkn = [&](auto kern) {  // k_rows_xs (spec, maps, jac, foam, tw, rows, rs, tw2)
+    CHECK(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, XsCfg<LOGN>::LDS));
+    return [=] {
+      hipLaunchKernelGGL(kern, dim3(C * N), dim3(S::T), XsCfg<LOGN>::LDS, 0, fp, spec, maps, jac, foam, tw, N, rs, tw2);
+    };
+  };
   std::vector<V> vs = {
       {"row pass, plain transform (round 2)", mk(k_rows_half<LOGN, kStream, kStream, 0, 1, true, true>), {}},
       {"XS (four-step x transform)", mkx(k_rows_half<LOGN, kStream, kStream, 0, 1, true, true, 1, 1, 4, 2, true, true>), {}},
@@ -131,6 +137,9 @@ int main()
       {"XS ABL 1: no HBM loads", mkx(k_rows_half<LOGN, kStream, kStream, 1, 1, true, true, 1, 1, 4, 2, true, true>), {}},
       {"ABL 1: no HBM loads", mk(k_rows_half<LOGN, kStream, kStream, 1, 1, true, true>), {}},
       {"ABL 2: no x transform", mk(k_rows_half<LOGN, kStream, kStream, 2, 1, true, true>), {}},
+      {"k_rows_xs (C loaded per image)", mkn(k_rows_xs<LOGN, 0>), {}},
+      {"k_rows_xs, 2 of 8 loads prefetched", mkn(k_rows_xs<LOGN, 2>), {}},
+      {"k_rows_xs, 3 of 8 loads prefetched", mkn(k_rows_xs<LOGN, 3>), {}},
   };
   // XS vs the plain transform: same lanes, different rounding order (max |diff| vs max |value|)
   auto snapf = [&](const void* p, size_t n) {
@@ -163,6 +172,9 @@ int main()
                 m0 == m1 && j0 == j1 ? " (bit-identical)" : "");
   };
   compare(0, 1, "XS vs plain");
+  compare(1, 6, "k_rows_xs vs XS");
+  compare(1, 7, "k_rows_xs PF 2 vs XS");
+  compare(1, 8, "k_rows_xs PF 3 vs XS");
   compare(1, 2, "XS streamed vs default-policy loads");
   for (int r = 0; r < 5; r++)
     for (auto& v : vs)

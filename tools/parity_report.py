@@ -52,6 +52,7 @@ def run(n, planes, times):
             depth = refs[c].settings.h
             scale = 2.0 ** -23 * omega_max(n, L, depth, refs[c].settings.g) * gen.GetOceanSettings(c).time
             rows.append((n, L, float(gen.GetOceanSettings(c).time), max(e), ec, ej, scale))
+            print(f"N={n} L={L:g} t={rows[-1][2]:g}: lane {max(e):.2e} channel {max(ec):.2e} jac {ej:.2e}", flush=True)
     return rows
 
 
@@ -68,13 +69,14 @@ def run_sampled(n, plane, dt):
     s = O.default_settings(planeSize=plane)
     s.time = gen.GetOceanSettings(0).time
     xs, ys = sample_lines(n)
-    h, d, j = O.sampled_frame(s, n, xs, ys)
+    h, d, j = O.sampled_frame(s, n, xs, ys, progress=True)
     gh = gen.height_map_host(0)[np.ix_(ys, xs)]
     gd = gen.displacement_map_host(0)[np.ix_(ys, xs)]
     gj = gen.jacobian_map_host(0)[np.ix_(ys, xs)]
     e = lane_err(gh, h) + lane_err(gd, d)
     ec = channel_err(gh, h) + channel_err(gd, d)
     ej = scalar_err(gj - 1.0, j - 1.0)
+    print(f"N={n} L={plane:g} sampled: lane {max(e):.2e} channel {max(ec):.2e} jac {ej:.2e}", flush=True)
     return [(n, plane, float(s.time), max(e), ec, ej, float("nan"))]
 
 

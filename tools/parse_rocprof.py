@@ -30,97 +30,132 @@ def device_source_sha256(root=ROOT):
     return h.hexdigest()
 
 
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E peak
+
+
 def base_name(symbol):
     """k_rows_half from 'void oceanfft::k_rows_half<12, 0, ...>(oceanfft::FrameParams, ...)'."""
     s = symbol.split("(")[0].replace("void ", "").replace("oceanfft::", "").strip()
     return s.split("<")[0]
 
 
+def first_arg(symbol):
+    """The first template argument (log2 N of every frame kernel), or None."""
+    s = symbol.split("(")[0]
+    return s.split("<", 1)[1].split(",")[0].split(">")[0].strip() if "<" in s else None
+
+
 def size_key(symbol, logn):
     """The summary key: the base name for instantiations at the workload's log2 N (what bench.py
     looks up), else base<first template argument> (other sizes: k_rows_half<14>, k_gen4_step2<10>)."""
-    s = symbol.split("(")[0].replace("void ", "").replace("oceanfft::", "").strip()
-    if "<" not in s:
-        return s
-    first = s.split("<", 1)[1].split(",")[0].split(">")[0].strip()
-    return s.split("<")[0] if first == str(logn) else f"{s.split('<')[0]}<{first}>"
-
-src, tag = sys.argv[1], sys.argv[2]
-n = int(sys.argv[3]) if len(sys.argv) > 3 else 4096
-cascades = int(sys.argv[4]) if len(sys.argv) > 4 else 8
-prefix = sys.argv[5] if len(sys.argv) > 5 else "prof"  # tools/profile_gpu.sh PREFIX
-mode = sys.argv[6] if len(sys.argv) > 6 else "frame"  # frame | ifft (EncodeIFFT chunks of 8 images)
-pts = n * n * cascades
-kept = (n // 2 + 4) / n  # half-spectrum path: columns u in [0, N/2) plus the 4-wide Nyquist strip
-ALGO = {"k_cols_evolve": 48 * pts, "k_rows_final": 68 * pts, "k_generate_spectrum": 16 * n * n,
-        "k_generate_spectrum_pairs": 16 * n * n,
-        "k_cols_half": int((16 + 40) * kept * pts), "k_rows_half": int((40 * kept + 36) * pts),
-        "k_gen4_step1": int((16 + 40) * kept * pts)}
-if mode == "ifft":  # standalone EncodeIFFT at 4096: work-image chunks of 8 images, 32 B per texel per pass
-    ALGO["k_cols_to_blocks"] = ALGO["k_rows_final"] = 32 * 8 * n * n
+    first = first_arg(symbol)
+    return base_name(symbol) if first in (None, str(logn)) else f"{base_name(symbol)}<{first}>"
 
 
-def read_csv(path):
-    with open(path) as f:
-        return list(csv.DictReader(f))
+def algorithmic_bytes(key, n, cascades, mode):
+    """Algorithmic HBM bytes of ONE launch of `key` at the profiled workload (DESIGN.md §4 figures,
+    the same as ocean_generator_frame_bytes), or None where no figure is defined: printed "-", never
+    guessed. Keyed by the size-qualified name, so another size's instantiation (k_rows_half<14> in a
+    4096 profile) never borrows this workload's bytes."""
+    pts = n * n * cascades
+    logn = n.bit_length() - 1
+    if mode == "ifft":  # standalone EncodeIFFT: work-image chunks of 8 images, 32 B per texel per pass
+        return {"k_cols_to_blocks": 32 * 8 * n * n, "k_rows_final": 32 * 8 * n * n}.get(key)
+    if logn in (13, 14):  # four-step whole grid: kept columns [0, N/2) + the Nyquist column
+        kept = (n // 2 + 1) / n
+        table = {"k_gen4_step1": (16 + 40) * kept, "k_rows_xs": 40 * kept + 36, "k_rows_half": 40 * kept + 36}
+    else:
+        kept = (n // 2 + 4) / n  # columns [0, N/2) plus the 4-wide Nyquist strip
+        table = {"k_cols_evolve": 48, "k_rows_final": 68, "k_cols_half": (16 + 40) * kept,
+                 "k_rows_half": 40 * kept + 36}
+    if key in ("k_generate_spectrum", "k_generate_spectrum_pairs"):
+        return 16 * n * n  # one cascade's h0 per launch
+    return int(table[key] * pts) if key in table else None
 
 
-def find(sub, suffix):
-    d = os.path.join(src, sub)
-    for fn in os.listdir(d):
-        if fn.endswith(suffix):
-            return os.path.join(d, fn)
-    raise FileNotFoundError(f"{d}/*{suffix}")
+def main(argv):
+    src, tag = argv[1], argv[2]
+    n = int(argv[3]) if len(argv) > 3 else 4096
+    cascades = int(argv[4]) if len(argv) > 4 else 8
+    prefix = argv[5] if len(argv) > 5 else "prof"  # tools/profile_gpu.sh PREFIX
+    mode = argv[6] if len(argv) > 6 else "frame"  # frame | ifft (EncodeIFFT chunks of 8 images)
+    logn = n.bit_length() - 1
+
+    def read_csv(path):
+        with open(path) as f:
+            return list(csv.DictReader(f))
+
+    def find(sub, suffix):
+        d = os.path.join(src, sub)
+        for fn in os.listdir(d):
+            if fn.endswith(suffix):
+                return os.path.join(d, fn)
+        raise FileNotFoundError(f"{d}/*{suffix}")
+
+    # per dispatch: (size key, grid threads, workgroup threads) -> durations. A persistent grid has the
+    # same geometry for every cascade count, so tools/profile_gpu.sh profiles bench.py --headline-only
+    # (no one-cascade or re-seed legs): each key then holds the workload's launches only.
+    durs = {}
+    for r in read_csv(find(prefix + "_trace", "kernel_trace.csv")):
+        grid = int(r["Grid_Size_X"]) * int(r["Grid_Size_Y"]) * int(r["Grid_Size_Z"])
+        wg = int(r["Workgroup_Size_X"]) * int(r["Workgroup_Size_Y"]) * int(r["Workgroup_Size_Z"])
+        k = (size_key(r["Kernel_Name"], logn), grid, wg)
+        durs.setdefault(k, {"ns": [], "symbols": set()})
+        durs[k]["ns"].append(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
+        durs[k]["symbols"].add(r["Kernel_Name"])
+    counters = {}
+    for sub, name in ((prefix + "_fetch", "FETCH_SIZE"), (prefix + "_write", "WRITE_SIZE")):
+        for r in read_csv(find(sub, "counter_collection.csv")):
+            if r["Counter_Name"] == name:
+                k = (size_key(r["Kernel_Name"], logn), int(r["Grid_Size"]), int(r["Workgroup_Size"]))
+                counters.setdefault(k, {}).setdefault(name, []).append(float(r["Counter_Value"]))
+
+    out = {"tag": tag, "n": n, "cascades": cascades, "device_source_sha256": device_source_sha256(), "kernels": {},
+           "by_geometry": []}
+    lines = [f"# rocprofv3 summary — {tag}", "",
+             f"Workload: bench.py --headline-only, {cascades} cascades of {n}x{n} per launch. Durations: "
+             "`--kernel-trace --stats` (per dispatch, keyed by kernel, grid and workgroup size). Traffic: separate "
+             "`--pmc FETCH_SIZE` and `--pmc WRITE_SIZE` passes; read = 2 x FETCH_SIZE (gfx950 half-count "
+             "correction), write = WRITE_SIZE; KB = 1024 B. Algorithmic bytes: DESIGN.md §4 per-point figures "
+             "x the points of one launch; \"-\" where no figure is defined.", "",
+             "| kernel | grid x wg | calls | avg ms | algorithmic GB/launch | measured HBM GB/launch (read + write) "
+             "| traffic / algorithmic | achieved GB/s (algorithmic) |",
+             "|---|---|---|---|---|---|---|---|"]
+    fmt = lambda v: "-" if v is None else f"{v / 1e9:.3f}"
+    for k in sorted(durs):
+        name, grid, wg = k
+        ns = durs[k]["ns"]
+        avg_ms = statistics.mean(ns) / 1e6
+        fe, wr_ = counters.get(k, {}).get("FETCH_SIZE", []), counters.get(k, {}).get("WRITE_SIZE", [])
+        rd = statistics.median(fe) * 1024 * 2 if fe else None
+        wr = statistics.median(wr_) * 1024 if wr_ else None
+        traffic = (rd + wr) if (rd is not None and wr is not None) else None
+        algo = algorithmic_bytes(name, n, cascades, mode)
+        achieved = algo / (avg_ms * 1e-3) / 1e9 if algo else None
+        if achieved is not None and achieved > HBM_PEAK_GBS:
+            raise SystemExit(f"{name} grid {grid}: {achieved:.0f} GB/s algorithmic exceeds the {HBM_PEAK_GBS:.0f} GB/s "
+                             "HBM peak: the launch does not cover the workload the bytes assume (profile with "
+                             "bench.py --headline-only)")
+        rec = {"kernel": name, "grid_threads": grid, "workgroup_threads": wg, "calls": len(ns), "avg_ms": avg_ms,
+               "algorithmic_bytes": algo, "hbm_read_bytes": rd, "hbm_write_bytes": wr, "hbm_traffic_bytes": traffic,
+               "achieved_GBps_algorithmic": achieved, "symbols": sorted(durs[k]["symbols"])}
+        out["by_geometry"].append(rec)
+        # bench.py's lookup: the workload's kernel by name (its most-called geometry)
+        if name not in out["kernels"] or out["kernels"][name]["calls"] < len(ns):
+            out["kernels"][name] = rec
+        ratio = f"{traffic / algo:.3f}" if (traffic and algo) else "-"
+        ach = "-" if achieved is None else f"{achieved:.0f}"
+        lines.append(f"| {name} | {grid // wg} x {wg} | {len(ns)} | {avg_ms:.3f} | {fmt(algo)} | {fmt(rd)} + {fmt(wr)} "
+                     f"| {ratio} | {ach} |")
+    lines += ["", f"Device source sha256: `{out['device_source_sha256']}` (bench.py uses this summary's traffic only for "
+              "the same device code)."]
+    os.makedirs("profiles", exist_ok=True)
+    with open(f"profiles/{tag}_rocprof.json", "w") as fh:
+        json.dump(out, fh, indent=1)
+    with open(f"profiles/{tag}_rocprof.md", "w") as fh:
+        fh.write("\n".join(lines) + "\n")
+    print("\n".join(lines))
 
 
-stats = {}
-for r in read_csv(find(prefix + "_trace", "kernel_stats.csv")):
-    stats[r["Name"]] = r
-counters = {}
-for sub, name in ((prefix + "_fetch", "FETCH_SIZE"), (prefix + "_write", "WRITE_SIZE")):
-    for r in read_csv(find(sub, "counter_collection.csv")):
-        if r["Counter_Name"] == name:
-            counters.setdefault(r["Kernel_Name"], {}).setdefault(name, []).append(float(r["Counter_Value"]))
-# full symbols (no -T): aggregate per base name, keeping the symbols each base name covered
-by_base = {}
-logn = n.bit_length() - 1
-for sym in list(stats) + list(counters):
-    by_base.setdefault(size_key(sym, logn), set()).add(sym)
-
-out = {"tag": tag, "n": n, "cascades": cascades, "device_source_sha256": device_source_sha256(), "kernels": {}}
-lines = [f"# rocprofv3 summary — {tag}", "",
-         f"Workload: bench.py, {cascades} cascades of {n}x{n} per launch. Durations: `--kernel-trace --stats`. "
-         "Traffic: separate `--pmc FETCH_SIZE` and `--pmc WRITE_SIZE` passes; read = 2 x FETCH_SIZE (gfx950 "
-         "half-count correction), write = WRITE_SIZE; KB = 1024 B.", "",
-         "| kernel | calls | avg ms | algorithmic GB/launch | measured HBM GB/launch (read + write) | traffic / algorithmic | achieved GB/s (algorithmic) |",
-         "|---|---|---|---|---|---|---|"]
-for name in sorted(by_base):
-    syms = by_base[name]
-    st_list = [stats[sy] for sy in syms if sy in stats]
-    if not st_list:
-        continue
-    calls = sum(int(st["Calls"]) for st in st_list)
-    avg_ms = sum(float(st["AverageNs"]) * int(st["Calls"]) for st in st_list) / calls / 1e6
-    fe = [v for sy in syms for v in counters.get(sy, {}).get("FETCH_SIZE", [])]
-    wr_ = [v for sy in syms for v in counters.get(sy, {}).get("WRITE_SIZE", [])]
-    rd = statistics.median(fe) * 1024 * 2 if fe else None
-    wr = statistics.median(wr_) * 1024 if wr_ else None
-    algo = ALGO.get(name)
-    traffic = (rd + wr) if (rd is not None and wr is not None) else None
-    rec = {"calls": calls, "avg_ms": avg_ms, "algorithmic_bytes": algo, "hbm_read_bytes": rd,
-           "hbm_write_bytes": wr, "hbm_traffic_bytes": traffic, "symbols": sorted(syms)}
-    if algo:
-        rec["achieved_GBps_algorithmic"] = algo / (avg_ms * 1e-3) / 1e9
-    out["kernels"][name] = rec
-    f = lambda v: "-" if v is None else f"{v / 1e9:.3f}"
-    ratio = f"{traffic / algo:.3f}" if (traffic and algo) else "-"
-    ach = f"{rec['achieved_GBps_algorithmic']:.0f}" if algo else "-"
-    lines.append(f"| {name} | {calls} | {avg_ms:.3f} | {f(algo)} | {f(rd)} + {f(wr)} | {ratio} | {ach} |")
-lines += ["", f"Device source sha256: `{out['device_source_sha256']}` (bench.py uses this summary's traffic only for "
-          "the same device code)."]
-os.makedirs("profiles", exist_ok=True)
-with open(f"profiles/{tag}_rocprof.json", "w") as fh:
-    json.dump(out, fh, indent=1)
-with open(f"profiles/{tag}_rocprof.md", "w") as fh:
-    fh.write("\n".join(lines) + "\n")
-print("\n".join(lines))
+if __name__ == "__main__":
+    main(sys.argv)

@@ -6,8 +6,8 @@
 # Counters are never combined with tracing domains (pool rule), and each step has its own limit.
 set -u
 cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
-ARGS=${BENCH_ARGS:-"--steps 20 --warmup 3 --no-cpu-baseline --no-slab --no-ifft --no-surface --no-reseed"}
-KRE=${KERNEL_REGEX:-"k_cols_evolve|k_rows_final|k_rows_ifft|k_rows_half|k_cols|k_generate_spectrum|k_half_nyquist"}
+ARGS=${BENCH_ARGS:-"--steps 20 --warmup 3 --headline-only"}
+KRE=${KERNEL_REGEX:-"k_cols_evolve|k_rows_final|k_rows_ifft|k_rows_half|k_rows_xs|k_cols|k_gen4|k_generate_spectrum|k_half_nyquist"}
 P=${PREFIX:-prof}  # output directories gpurun_out/${P}_trace, _fetch, _write
 mkdir -p gpurun_out
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/${P}_trace -o trace --output-format csv \

@@ -127,8 +127,9 @@ __global__ __launch_bounds__(FftShape<LOGN>::T * RPW_) void k_rows_half(
     for (int m = 0; m < 8; m++)
     {
       const int u = m * T + i;               // >= 0, column x = N/2 + u
-      const int src = RM ? __builtin_amdgcn_readfirstlane(u / rs.cpr) : 0;  // source block (wave-uniform)
-      const int off = RM ? r * rs.lp + (u - src * rs.cpr) : half_group_offset<LOGN, RG, FB>(y, u / FB, u % FB);
+      // source block (wave-uniform; cpr a power of two, launch_rm_rows): a shift, not a division
+      const int src = RM ? __builtin_amdgcn_readfirstlane(u >> (31 - __builtin_clz(rs.cpr))) : 0;
+      const int off = RM ? r * rs.lp + (u & (rs.cpr - 1)) : half_group_offset<LOGN, RG, FB>(y, u / FB, u % FB);
       const int offc = RM ? off : half_group_offset<LOGN, RGC, FB>(y, u / FB, u % FB);
       const float4* fab = RM ? reinterpret_cast<const float4*>(rs.ab + src * rs.src_stride) + base : gab + base;
       const float4* fde = RM ? reinterpret_cast<const float4*>(rs.de + src * rs.src_stride) + base : gde + base;

@@ -45,6 +45,11 @@ __global__ __launch_bounds__(1024) void k_rows_xs(FrameParams fp, const float4* 
 
   const int total = fp.cascades * rows;
   const float dim = (float)N;
+  // Source block of column u: u >> lcpr (cpr a power of two, launch_rm_rows), wave-uniform because
+  // cpr is a multiple of 64: computed on the scalar unit from the wave's first column, so a load's
+  // address costs one VALU mask instead of a division.
+  const int lcpr = 31 - __builtin_clz(rs.cpr), cmask = rs.cpr - 1;
+  const int wave0 = __builtin_amdgcn_readfirstlane((int)threadIdx.x & ~63);
   // the 8 kept elements u = m T + tid of one image: (A, B) or (D, E)
   float4 fp4[8], nx4[8];
   auto issue = [&](int item, int img, float4* p4, int m0, int m1) __attribute__((always_inline)) {
@@ -54,11 +59,10 @@ __global__ __launch_bounds__(1024) void k_rows_xs(FrameParams fp, const float4* 
 #pragma unroll
     for (int m = m0; m < m1; m++)
     {
-      const int u = m * T + i;
-      const int src = __builtin_amdgcn_readfirstlane(u / rs.cpr);  // source block (wave-uniform)
-      const int col = u - src * rs.cpr;
+      const int src = (m * T + sopaque(wave0)) >> lcpr;  // source block (scalar, computed here: not hoisted)
       const size_t sb = (size_t)src * rs.src_stride;
-      p4[m] = ld4<kStream>(reinterpret_cast<const float4*>((img == 0 ? rs.ab : rs.de) + sb) + base, col * 16);
+      p4[m] = ld4<kStream>(reinterpret_cast<const float4*>((img == 0 ? rs.ab : rs.de) + sb) + base,
+                           ((m * T + i) & cmask) * 16);
     }
   };
   int item = blockIdx.x;
@@ -84,9 +88,9 @@ __global__ __launch_bounds__(1024) void k_rows_xs(FrameParams fp, const float4* 
         const int u = m * T + i;
         const float kx = (float)u * dk;
         const float4 s4 = ld4<0>(sp, (N / 2 - u) * 16);  // the -u column's Nyquist-row term (x = N/2 - u)
-        const int src = __builtin_amdgcn_readfirstlane(u / rs.cpr);
+        const int src = (m * T + sopaque(wave0)) >> lcpr;
         const float2 cc = ld2<0>(reinterpret_cast<const float2*>(rs.c + (size_t)src * rs.src_stride) + base,
-                                 (u - src * rs.cpr) * 8);  // C
+                                 (u & cmask) * 8);  // C
         if (img == 0)
         {
           const CPair p = raw_pair(fp4[m]);  // (A, B)

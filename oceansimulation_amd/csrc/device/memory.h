@@ -122,4 +122,10 @@ __device__ __forceinline__ size_t sopaque(size_t v)
   return v;
 }
 
+__device__ __forceinline__ int sopaque(int v)
+{
+  asm volatile("" : "+s"(v));
+  return v;
+}
+
 }  // namespace oceanfft

@@ -91,7 +91,8 @@ hipError_t launch_rm_rows(const FrameParams& fp, const RowSrc& rs, const float4*
 {
   using S = FftShape<LOGN>;
   constexpr int RPW = S::T >= 1024 ? 1 : 2;
-  if (rs.cpr % 64 != 0 || rows % RPW != 0)  // the block index of a wave's loads must be wave-uniform
+  // the block index of a wave's loads must be wave-uniform, and is taken with a shift
+  if (rs.cpr < 64 || (rs.cpr & (rs.cpr - 1)) != 0 || rows % RPW != 0)
     return hipErrorInvalidValue;
   if constexpr (RPW == 1)
   {

@@ -19,7 +19,7 @@ import sys
 import numpy as np
 import pytest
 
-from parity import FRAME_TOL, H0_TOL, lane_err, scalar_err
+from parity import FRAME_TOL, FRAME_TOL_GPU, H0_TOL, channel_err, lane_err, scalar_err
 
 pytestmark = pytest.mark.gpu
 
@@ -61,7 +61,8 @@ def _dev_equal(ptr_a: int, ptr_b: int, nbytes: int) -> bool:
 # ---- configs[3]: 8 independent 4096^2 cascades, as bench.py times them ---------------------------
 def test_headline_batch_vs_oracle(ocean, oracle):
     """bench.py's step (rank 0's 8 cascades of 4096^2, plane sizes 5..4093 m) against the oracle
-    after three frames (the first seeds h0): cascades 0, 3 and 7 at FRAME_TOL; and every cascade of
+    after three frames (the first seeds h0): cascades 0, 3 and 7 at FRAME_TOL, and per channel at
+    FRAME_TOL_GPU against the float64 transform of the oracle's spectrum; and every cascade of
     the 8-cascade launch bit-exact against the same cascade in a one-cascade generator, so the
     many-cascade item mapping is exercised (src/Generator.cpp:45-83)."""
     b = _bench()
@@ -79,10 +80,19 @@ def test_headline_batch_vs_oracle(ocean, oracle):
         ref = oracle.OracleGenerator(n, oracle.default_settings(**s))
         for dt in steps:
             ref.calculate_ocean(dt)
-        e = lane_err(gen.height_map_host(c), ref.height) + lane_err(gen.displacement_map_host(c), ref.disp)
-        ej = scalar_err(gen.jacobian_map_host(c) - 1.0, ref.jac - 1.0)
+        gh, gd, gj = gen.height_map_host(c), gen.displacement_map_host(c), gen.jacobian_map_host(c)
+        e = lane_err(gh, ref.height) + lane_err(gd, ref.disp)
+        ej = scalar_err(gj - 1.0, ref.jac - 1.0)
         assert max(e) <= FRAME_TOL and ej <= FRAME_TOL, (c, e, ej)
-        del ref
+        # per channel against the float64 transform of the oracle's spectrum (tests/parity.py)
+        import numpy_ref as R
+
+        hp, dp = oracle.prepare_fft(ref.settings, n, ref.h0)
+        h64, d64 = R.encode_ifft(hp), R.encode_ifft(dp)
+        ec = channel_err(gh, h64) + channel_err(gd, d64)
+        ej64 = scalar_err(gj - 1.0, R.compute_foam(ref.settings, d64) - 1.0)
+        assert max(ec) <= FRAME_TOL_GPU and ej64 <= FRAME_TOL_GPU, (c, ec, ej64)
+        del ref, hp, dp, h64, d64
     for c in range(C):
         one = ocean.Generator(fft, 1)
         ocean.apply_settings(one.GetOceanSettings(0), **b.cascade_settings(0, c))

@@ -207,10 +207,27 @@ def test_property_parseval_linearity_hermitian(ocean, n):
 
 
 # ---- Full CalculateOcean frames (src/Generator.cpp:45-83) -----------------------------------
+def _f64_frame(o):
+    """The frame of OracleGenerator o with its FFT in float64: the oracle's fp32 h0 and prepareFFT at
+    o's time (the reference's arithmetic), N^2 ifft2(ifftshift) in float64 (the meaning of
+    src/FFTCalculator.cpp:73-114), foam from those maps (spectrum.compute:246-259)."""
+    from oracle import oracle as O
+
+    hp, dp = O.prepare_fft(o.settings, o.n, o.h0)
+    h64, d64 = R.encode_ifft(hp), R.encode_ifft(dp)
+    return h64, d64, R.compute_foam(o.settings, d64)
+
+
 def _frame_check(got_h, got_d, got_j, o):
+    """Against the oracle per lane (FRAME_TOL), and per channel against the float64 transform of the
+    oracle's spectrum (FRAME_TOL_GPU; tests/parity.py)."""
     eh, ed = lane_err(got_h, o.height), lane_err(got_d, o.disp)
     ej = scalar_err(got_j - 1.0, o.jac - 1.0)
     assert max(eh + ed) <= FRAME_TOL and ej <= FRAME_TOL, (eh, ed, ej)
+    h64, d64, j64 = _f64_frame(o)
+    ec = channel_err(got_h, h64) + channel_err(got_d, d64)
+    ej64 = scalar_err(got_j - 1.0, j64 - 1.0)
+    assert max(ec) <= FRAME_TOL_GPU and ej64 <= FRAME_TOL_GPU, (ec, ej64)
 
 
 @pytest.mark.parametrize("n", [64, 256, 1024])
@@ -279,9 +296,9 @@ def test_calculate_ocean_8192_vs_float64(ocean, oracle, half):
     s.time = 1.25
     hp, dp = oracle.prepare_fft(s, n, oracle.generate_spectrum(s, n))
     h64, d64 = R.encode_ifft(hp), R.encode_ifft(dp)
-    assert max(lane_err(gen.height_map_host(0), h64)) <= FRAME_TOL
-    assert max(lane_err(gen.displacement_map_host(0), d64)) <= FRAME_TOL
-    assert scalar_err(gen.jacobian_map_host(0) - 1.0, R.compute_foam(s, d64) - 1.0) <= FRAME_TOL
+    ec = channel_err(gen.height_map_host(0), h64) + channel_err(gen.displacement_map_host(0), d64)
+    assert max(ec) <= FRAME_TOL_GPU, ec
+    assert scalar_err(gen.jacobian_map_host(0) - 1.0, R.compute_foam(s, d64) - 1.0) <= FRAME_TOL_GPU
 
 
 @pytest.mark.parametrize("n", [1024, 2048, 4096])
@@ -308,6 +325,27 @@ def test_half_spectrum_path_matches_full_path_and_oracle(ocean, oracle, n):
             a, b = getattr(gh, get)(c), getattr(gf, get)(c)
             assert max(lane_err(a, b)) <= 1e-5, (c, get, lane_err(a, b))
         _frame_check(gh.height_map_host(c), gh.displacement_map_host(c), gh.jacobian_map_host(c), refs[c])
+
+
+def test_frames_deterministic_run_twice(ocean):
+    """The same frames computed twice (two generators, the bench's 8 x 4096^2 batch: persistent
+    grids, the H scratch shared by the workgroups of a CU slot) are bit-identical: no result depends on
+    scheduling. A build that passed the column pass's piece offsets in the buffer instructions' SGPR
+    offset field differed in ~3 % of the floats from run to run (tools/microbench/detbench,
+    profiles/r03_detbench_*.log); production folds them into the VGPR offset."""
+    n, planes = 4096, [5.0, 17.0, 101.0, 251.0, 509.0, 1021.0, 2039.0, 4093.0]
+    fft = ocean.FFTCalculator(n)
+    runs = []
+    for _ in range(2):
+        gen = ocean.Generator(fft, len(planes))
+        for c, L in enumerate(planes):
+            ocean.apply_settings(gen.GetOceanSettings(c), planeSize=L)
+        for dt in (0.5, 1.0 / 60.0):
+            gen.CalculateOcean(dt)
+        runs.append(gen)
+    for c in range(len(planes)):
+        for get in ("height_map_host", "displacement_map_host", "jacobian_map_host"):
+            assert np.array_equal(getattr(runs[0], get)(c), getattr(runs[1], get)(c)), (c, get)
 
 
 def test_sixty_four_cascades_in_one_launch(ocean):

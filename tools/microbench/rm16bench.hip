@@ -140,6 +140,7 @@ int main()
       {"k_rows_xs (C loaded per image)", mkn(k_rows_xs<LOGN, 0>), {}},
       {"k_rows_xs, 2 of 8 loads prefetched", mkn(k_rows_xs<LOGN, 2>), {}},
       {"k_rows_xs, 3 of 8 loads prefetched", mkn(k_rows_xs<LOGN, 3>), {}},
+      {"k_rows_xs PF 2, block index by division (before)", mkn(k_rows_xs_div<LOGN, 2>), {}},
   };
   // XS vs the plain transform: same lanes, different rounding order (max |diff| vs max |value|)
   auto snapf = [&](const void* p, size_t n) {
@@ -175,6 +176,7 @@ int main()
   compare(1, 6, "k_rows_xs vs XS");
   compare(1, 7, "k_rows_xs PF 2 vs XS");
   compare(1, 8, "k_rows_xs PF 3 vs XS");
+  compare(7, 9, "k_rows_xs PF 2: shift vs division");
   compare(1, 2, "XS streamed vs default-policy loads");
   for (int r = 0; r < 5; r++)
     for (auto& v : vs)

@@ -154,10 +154,14 @@ __device__ __forceinline__ float2 spectrum_amplitude(const SpectrumConsts& q, fl
   const float2 u = hash_uniform((uint32_t)(int64_t)(tx + q.seed_x), (uint32_t)(int64_t)(ty + q.seed_y));
   // accurate logf: for u near 1 the hardware log2's absolute error is a large relative error
   const float rad = __builtin_amdgcn_sqrtf(-2.0f * logf(u.x));
-  // sin/cos(2 pi u.y) with u.y in [0, 1): the hardware v_sin_f32 / v_cos_f32 take revolutions, so
-  // u.y goes in unreduced (absolute error ~3e-7, the size of the fp32 rounding of the reference's
-  // own argument 2 pi u.y, whose ulp is up to 4.8e-7)
-  const float sn = __builtin_amdgcn_sinf(u.y), cs = __builtin_amdgcn_cosf(u.y);
+  // sin/cos of the reference's own fp32 argument 2 pi u.y (spectrum.compute:153), accurate (ocml's
+  // small-argument path): the hardware v_sin_f32 / v_cos_f32 on u.y in revolutions are as close to
+  // the exact values, but their errors are biased, and a bias in every texel's phase adds up over
+  // the N^2 texels where the frame sums them in phase (the grid origin, each image row 0 / column 0)
+  // while the signal adds up incoherently: 1.3e-4 of the origin's value in a slope channel's spectrum
+  // sum at 4096^2, 1.5-1.9e-5 in the frame (tools/parity_probe.py).
+  const float th = 2.0f * OCEAN_PI * u.y;
+  const float sn = sinf(th), cs = cosf(th);
   const float amp = __builtin_amdgcn_sqrtf(2.0f * Sj * d * chain);
   return make_float2(q.c * (rad * cs) * amp, q.c * (rad * sn) * amp);
 }

@@ -18,7 +18,7 @@ Tolerances (float32 path):
   FRAME_TOL_GPU = 1e-5 — full frames, per channel, against the oracle's own fp32 spectrum (h0 and
                       prepareFFT at the frame's time, the reference's arithmetic) transformed in
                       float64: the GPU's error with the oracle's FFT rounding taken out. Observed
-                      1-4e-6 (profiles/r03_parity_report.md).
+                      0.4-5.7e-6 over N = 256 .. 16384, t up to 3600 s (profiles/r03_parity_report.md).
   H0_TOL    = 1e-5  — generateSpectrum (relative to max |h0| per lane).
   Hash: bit-exact.
 """

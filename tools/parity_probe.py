@@ -41,6 +41,29 @@ def main():
         dh0 = np.abs(h0 - ref.h0)
         print(f"{'half' if half else 'full'}: h0 max|diff| / max|h0| = {dh0.max() / np.abs(ref.h0).max():.2e} "
               f"at {np.unravel_index(np.argmax(dh0.max(-1)), dh0.shape[:2])}", flush=True)
+        if half:
+            gpu_h0 = g.initial_spectrum_host(0)
+    # h0 texel by texel: relative error where |h0| is not negligible, and |k|^2-weighted (slope-like)
+    mag = np.abs(ref.h0.astype(np.float64)).max(-1)
+    rel = np.abs(gpu_h0.astype(np.float64) - ref.h0).max(-1) / np.maximum(mag, 1e-30)
+    kk2 = np.add.outer((np.arange(n) - n // 2) ** 2, (np.arange(n) - n // 2) ** 2).astype(np.float64)
+    for thr in (1e-2, 1e-4, 1e-6):
+        m = mag > thr * mag.max()
+        t = np.argmax(np.where(m, rel, 0))
+        y, x = np.unravel_index(t, rel.shape)
+        print(f"h0 texels with |h0| > {thr:g} max: worst relative error {rel[y, x]:.2e} at (x={x}, y={y}) "
+              f"(u={x - n // 2}, v={y - n // 2}), |h0| {mag[y, x]:.2e}", flush=True)
+    wk = np.abs(gpu_h0.astype(np.float64) - ref.h0).max(-1) * kk2
+    print(f"h0 |k|^2-weighted: max |k|^2 |dh0| / max |k|^2 |h0| = {wk.max() / (mag * kk2).max():.2e}", flush=True)
+    # the spectrum from the GPU's own h0 through the oracle's prepareFFT: splits h0 error from the rest
+    hpg, dpg = O.prepare_fft(s, n, gpu_h0)
+    spec_g = np.concatenate([hpg, dpg], -1).astype(np.float64)
+    spec_o = np.concatenate([hp, dp], -1).astype(np.float64)
+    for lane, what in ((0, "h + i dh/dx"), (4, "Dz + i dDx/dx")):
+        a = spec_g[..., lane] + 1j * spec_g[..., lane + 1]
+        b = spec_o[..., lane] + 1j * spec_o[..., lane + 1]
+        print(f"prepareFFT(GPU h0) vs prepareFFT(oracle h0), lane '{what}': |sum dX| / |sum X| "
+              f"{abs((a - b).sum()) / abs(b.sum()):.2e}", flush=True)
     outs["oracle"] = orc
     # the spectrum each output implies (forward transform in float64, the inverse of EncodeIFFT's
     # convention) against the oracle's prepareFFT spectrum: where the frame's error comes from
@@ -64,8 +87,8 @@ def main():
                 m = (kk >= lo) & (kk < hi)
                 parts.append(f"[{lo},{hi}) {abs((X - R0)[m].sum()) / abs(R0.sum()):.1e}")
             print("    origin error by |k| band: " + " ".join(parts), flush=True)
-            for t in top:
-                j, i = np.unravel_index(t, d.shape)
+            for tt in top:
+                j, i = np.unravel_index(tt, d.shape)
                 print(f"    (u={i - n // 2}, v={j - n // 2}) |dX| {d[j, i]:.3e} |X| {abs(R0[j, i]):.3e} "
                       f"X_gpu {X[j, i]:.4e} X_ref {R0[j, i]:.4e}", flush=True)
     for name, a in outs.items():

@@ -31,6 +31,9 @@ def omega_max(n, plane, depth, g=G):
     return math.sqrt((g * k + 0.074 / 1000.0 * k ** 3) * math.tanh(min(k * depth, 20.0)))
 
 
+CHANNELS = ["h", "dh/dx", "dh/dz", "Dx", "Dz", "dDx/dx", "dDz/dz", "dDx/dz"]
+
+
 def f64_frame(ref, t):
     """The oracle's fp32 h0 and prepareFFT (the reference's arithmetic) at time t, transformed in
     float64 (N^2 ifft2(ifftshift), the meaning of src/FFTCalculator.cpp:73-114), foam from those maps:

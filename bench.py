@@ -36,15 +36,30 @@ PLANES = [5.0, 17.0, 101.0, 251.0, 509.0, 1021.0, 2039.0, 4093.0]
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md, chip-level parameters)
 
 
-def frame_bytes_per_point(n: int, half: bool):
+def frame_path(n: int, full_spectrum: bool = False) -> str:
+    """The whole-grid generator's frame path at N (ocean_generator_create defaults): "full" below
+    1024 or when the full spectrum is requested, "four-step" at 8192 / 16384, else "half"."""
+    if full_spectrum or n < 1024:
+        return "full"
+    return "four-step" if n >= 8192 else "half"
+
+
+def frame_bytes_per_point(n: int, path):
     """Algorithmic HBM bytes per height-field point of (column pass, row pass); the
     generator reports the same through ocean_generator_frame_bytes (checked at run time).
-    Full spectrum: h0 16 + intermediate 32 | intermediate 32 + maps 32 + Jacobian 4 = 48 | 68.
-    Half spectrum (default for whole grids of 1024..4096): only the kept columns u in [0, N/2) plus
-    the 4-wide Nyquist strip, kept = (N/2 + 4)/N of the grid: h0 16 + 5 fields 40 per kept texel |
-    5 fields 40 per kept texel + maps 32 + Jacobian 4 (~28 | ~56)."""
-    if not half:
-        return 48.0, 68.0
+    Full spectrum: h0 16 + intermediate 32 | intermediate 32 + maps 32 + Jacobian 4 = 48 | 68 (+ 64
+    for the B = 1 transpose at 16384).
+    Half spectrum (whole grids of 1024..4096): only the kept columns u in [0, N/2) plus the 4-wide
+    Nyquist strip, kept = (N/2 + 4)/N of the grid: h0 16 + 5 fields 40 per kept texel | 5 fields 40
+    per kept texel + maps 32 + Jacobian 4 (~28 | ~56).
+    Four-step (whole grids of 8192 / 16384): kept = (N/2 + 1)/N: h0 16 + step 1's 5 fields 40 + step 2
+    reading and writing them 80 | 40 per kept texel + 36 (~68 | ~56). path True / False = half / full."""
+    path = {True: "half", False: "full"}.get(path, path)
+    if path == "full":
+        return 48.0, 68.0 + (64.0 if n >= 16384 else 0.0)
+    if path == "four-step":
+        kept = (n / 2 + 1) / n
+        return (16.0 + 40.0 + 80.0) * kept, 40.0 * kept + 36.0
     kept = (n / 2 + 4) / n
     return 16.0 * kept + 40.0 * kept, 40.0 * kept + 36.0
 
@@ -761,8 +776,9 @@ def main(argv=None):
     if args.full_spectrum:
         gen.set_half_spectrum(False)
     pass_bytes = gen.frame_bytes()
-    half = pass_bytes[0] < 48.0
-    assert tuple(pass_bytes) == frame_bytes_per_point(n, half), (pass_bytes, n, half)
+    path = frame_path(n, args.full_spectrum)
+    half = path != "full"
+    assert tuple(pass_bytes) == frame_bytes_per_point(n, path), (pass_bytes, n, path)
 
     dt = 1.0 / 60.0
     # h0 seeding, timed separately (time-independent; the reference API regenerates only on change)
@@ -837,7 +853,8 @@ def main(argv=None):
             "cascades_per_gpu": C,
             "plane_sizes_m": [PLANES[c % len(PLANES)] for c in range(total)],
             "parallelism": f"the {total} cascades split {C} per GPU over {world} GPU(s) (strong scaling), no collective",
-            "frame_path": "half spectrum" if half else "full spectrum",
+            "frame_path": {"half": "half spectrum", "full": "full spectrum",
+                           "four-step": "half spectrum, four-step column pass"}[path],
             "frame_hbm_bytes_per_point": pass_bytes[0] + pass_bytes[1],
         },
     }
@@ -858,9 +875,11 @@ def main(argv=None):
         p1_ms, p2_ms = ms[1] / cnt[1], ms[2] / cnt[2]
         per_launch_pts = float(n) * n * C
         kernels = {
-            ("column_pass_k_cols_half" if half else "column_pass_k_cols_evolve"):
+            {"half": "column_pass_k_cols_half", "full": "column_pass_k_cols_evolve",
+             "four-step": "column_pass_k_gen4_step1+2"}[path]:
                 {"avg_ms": p1_ms, "bytes": pass_bytes[0] * per_launch_pts},
-            ("row_pass_k_rows_half" if half else "row_pass_k_rows_final"):
+            {"half": "row_pass_k_rows_half", "full": "row_pass_k_rows_final",
+             "four-step": "row_pass_k_rows_xs" if n >= 16384 else "row_pass_k_rows_half"}[path]:
                 {"avg_ms": p2_ms, "bytes": pass_bytes[1] * per_launch_pts},
         }
         dom_name = max(kernels, key=lambda k: kernels[k]["avg_ms"])

@@ -22,6 +22,14 @@ def test_bench_byte_accounting():
     kept = (2048 + 4) / 4096
     assert p1 == 16.0 * kept + 40.0 * kept and p2 == 40.0 * kept + 36.0
     assert 84.0 < p1 + p2 < 84.1  # 8 + 20 | 20 + 36 per grid point, plus the Nyquist strip
+    # the whole-grid paths ocean_generator_create picks, and the four-step bytes at 8192 / 16384
+    assert [b.frame_path(n) for n in (256, 1024, 4096, 8192, 16384)] == ["full", "half", "half", "four-step",
+                                                                         "four-step"]
+    assert b.frame_path(4096, full_spectrum=True) == "full"
+    q1, q2 = b.frame_bytes_per_point(16384, "four-step")
+    kept = (8192 + 1) / 16384
+    assert q1 == 136.0 * kept and q2 == 40.0 * kept + 36.0 and 124.0 < q1 + q2 < 124.1
+    assert b.frame_bytes_per_point(16384, "full") == (48.0, 132.0)  # + the B = 1 transpose
 
 
 def test_bench_cascade_sharding_is_disjoint():

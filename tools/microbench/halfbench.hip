@@ -190,6 +190,79 @@ int main(int argc, char** argv)
     std::printf("rows, row layout (round 1)              median %7.3f ms  bit-identical %s\n", tr[1][4], same ? "yes" : "NO");
     return 0;
   }
+  if (argc > 3 && std::strcmp(argv[3], "rg") == 0 && logn == 12)
+  {
+    // the gab / gde row-group size RG (gc keeps RGC = 4) with the production row pass (one row per
+    // 256-thread workgroup, 4 rows per XCD group, so a 128-B line's two rows stay on one XCD for any
+    // RG >= 2): pass 1's store pieces are RG x 64 B. Same arithmetic, so the maps must be identical.
+    using K = ColFirstCfg<12>;
+    using S = FftShape<12>;
+    const int clds = ((S::TW_ENTRIES * 8 + 15) / 16) * 16 + K::LDS1 + kHalfHL * K::WG1 * 16;
+    const int rlds = ((S::TW_ENTRIES * 8 + 15) / 16) * 16 + lds_row_slots<12>(1) * 8;
+    auto cols = [&](auto kern) {
+      return [=] {
+        hipError_t e = launch_half_nyquist(fp, n, K::B, h0, spec, nullptr, 1, 0, nullptr, 0, cus);
+        if (e != hipSuccess)
+          return e;
+        int grid = persistent_grid(kern, K::WG1, clds, fp.cascades * HalfCfg<12>::STRIPS, cus);
+        grid = grid > cus ? cus : grid;
+        hipLaunchKernelGGL(kern, dim3(grid), dim3(K::WG1), clds, 0, fp, h0, gab, gcd, ge, tw, hs, HalfSlab{},
+                           (unsigned char*)nullptr, 1, nullptr);
+        return hipGetLastError();
+      };
+    };
+    auto rows = [&](auto kern) {
+      return [=] {
+        const int grid = persistent_grid(kern, S::T, rlds, fp.cascades * S::N, cus);
+        hipLaunchKernelGGL(kern, dim3(grid), dim3(S::T), rlds, 0, fp, gab, gcd, ge, spec, maps, jac, foam, tw, S::N,
+                           RowSrc{}, (const float2*)nullptr);
+        return hipGetLastError();
+      };
+    };
+    std::vector<std::function<hipError_t()>> vc = {
+        cols(k_cols_half<12, kStream, kStream, true, false, false, 2, 4, 4, true, false, kHalfHL, kHalfHK>),
+        cols(k_cols_half<12, kStream, kStream, true, false, false, 4, 4, 4, true, false, kHalfHL, kHalfHK>),
+        cols(k_cols_half<12, kStream, kStream, true, false, false, 8, 4, 4, true, false, kHalfHL, kHalfHK>),
+        cols(k_cols_half<12, kStream, kStream, true, false, false, 16, 4, 4, true, false, kHalfHL, kHalfHK>)};
+    std::vector<std::function<hipError_t()>> vr = {
+        rows(k_rows_half<12, 0, kStream, 0, 1, true, false, 2, 4, 4, 4>),
+        rows(k_rows_half<12, 0, kStream, 0, 1, true, false, 4, 4, 4, 4>),
+        rows(k_rows_half<12, 0, kStream, 0, 1, true, false, 8, 4, 4, 4>),
+        rows(k_rows_half<12, 0, kStream, 0, 1, true, false, 16, 4, 4, 4>)};
+    const int rgs[4] = {2, 4, 8, 16};
+    CHECK(vc[0]());
+    CHECK(vr[0]());
+    CHECK(hipDeviceSynchronize());
+    auto pm = snap(maps, mb), pj = snap(jac, jb);
+    bool same[4] = {true, true, true, true};
+    for (int k = 1; k < 4; k++)
+    {
+      CHECK(hipMemset(maps, 0, mb));
+      CHECK(vc[k]());
+      CHECK(vr[k]());
+      CHECK(hipDeviceSynchronize());
+      std::printf("RG %d vs RG 2: maps, jacobian\n", rgs[k]);
+      same[k] = (int)diff(snap(maps, mb), pm) & (int)diff(snap(jac, jb), pj);
+    }
+    std::vector<std::vector<float>> tc(4), tr(4), tf(4);
+    for (int r = 0; r < 9; r++)
+      for (int k = 0; k < 4; k++)
+      {
+        tc[k].push_back(time_ms(vc[k], 10));
+        tr[k].push_back(time_ms(vr[k], 10));
+        auto fr = [&] { CHECK(vc[k]()); return vr[k](); };
+        tf[k].push_back(time_ms(fr, 10));
+      }
+    for (int k = 0; k < 4; k++)
+    {
+      std::sort(tc[k].begin(), tc[k].end());
+      std::sort(tr[k].begin(), tr[k].end());
+      std::sort(tf[k].begin(), tf[k].end());
+      std::printf("RG %2d (gab/gde pieces %4d B)  cols %7.3f  rows %7.3f  frame %7.3f ms  bit-identical %s%s\n", rgs[k],
+                  rgs[k] * 64, tc[k][4], tr[k][4], tf[k][4], same[k] ? "yes" : "NO", k == 0 ? " (production)" : "");
+    }
+    return 0;
+  }
   if (argc > 3 && std::strcmp(argv[3], "hpair") == 0)
   {
     // pass 1 with the H scratch in 8-B entries (variant 23, round 2) against production (16-B pairs):

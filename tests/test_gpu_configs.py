@@ -337,3 +337,23 @@ def test_bench_gpus_two_shared_gpu_reports_two_ranks(tmp_path):
         r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2"], capture_output=True,
                            text=True, timeout=120, env=env, cwd=ROOT)
         assert r.returncode == 2 and "GPU(s) are visible" in r.stderr, (r.returncode, r.stderr[-2000:])
+
+
+def test_rccl_all_to_all_large_pieces_world1(ocean):
+    """ocean_comm_all_to_all at world size 1 with single transfers above 1 GiB, which RCCL 2.26 got
+    wrong in one send/recv pair (profiles/r03_rccl_selfcheck.log): the C ABI cuts each pair into
+    512-MiB pieces, so 1.4 GB (two pieces and a ragged third) copies exactly."""
+    import torch
+
+    from oceansimulation_amd.slab import RcclComm
+
+    comm = RcclComm(0, 1, lambda uid: uid)
+    n = 1400 << 20
+    a = torch.randint(0, 255, (n,), dtype=torch.uint8, device="cuda")
+    b = torch.zeros_like(a)
+    comm.all_to_all(a.data_ptr(), b.data_ptr(), n, 0)
+    torch.cuda.synchronize()
+    assert torch.equal(a, b)
+    del a, b
+    torch.cuda.empty_cache()
+    comm.close()

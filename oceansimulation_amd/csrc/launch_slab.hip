@@ -163,7 +163,8 @@ hipError_t launch_half_slab_rows(int logn, const FrameParams& fp, const HalfSlab
 }
 
 // ---- the four-step column pass (N = 8192 / 16384): whole grids and slabs (device/k_gen4.h) ----
-bool gen4_supported(int logn) { return logn == 13 || logn == 14; }
+// the four-step paths read the N/16-point table ocean_fft_create appends under the same predicate
+bool gen4_supported(int logn) { return fourstep_table(logn); }
 
 int gen4_h0_block() { return kGen4Block; }
 

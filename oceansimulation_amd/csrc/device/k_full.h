@@ -111,7 +111,10 @@ __global__ __launch_bounds__(ColFirstCfg<LOGN>::WG1) void k_cols_evolve(
 // k_blocks_to_rows, used when B == 1).
 // ABL: timing ablations for tools/microbench (results wrong by construction): 1 = no HBM traffic,
 // 2 = no FFT (memory traffic and stores only).
-template <int LOGN, bool BLOCKED, int LA = kStream, int SA = kStream, int RPW_ = ColFirstCfg<LOGN>::RPW2, int ABL = 0>
+// GRPR (blocked input): consecutive items run on one XCD in groups of GRPR (xcd_group_slot), for a
+// block width whose 128-B lines span more rows than one item reads (B = 2, RPW = 2: a line is 4 rows).
+template <int LOGN, bool BLOCKED, int LA = kStream, int SA = kStream, int RPW_ = ColFirstCfg<LOGN>::RPW2, int ABL = 0,
+          int GRPR = 1>
 __global__ __launch_bounds__(FftShape<LOGN>::T * RPW_) void k_rows_final(
     int images, SlabGeom g, const float4* __restrict__ inter, float4* __restrict__ maps, float* __restrict__ jac,
     FoamParams foam, const float2* __restrict__ tw_glob)
@@ -134,7 +137,8 @@ __global__ __launch_bounds__(FftShape<LOGN>::T * RPW_) void k_rows_final(
   const int i20 = threadIdx.x % T, r20 = threadIdx.x / T;
   constexpr bool REMAP = BLOCKED && S::NSTAGE > 1;
   const int total = images * blocks;  // images = 2 per cascade (height, displacement)
-  for (int item = blockIdx.x; item < total; item += gridDim.x)
+  for (int item = GRPR > 1 ? xcd_group_slot<GRPR>(blockIdx.x, gridDim.x) : blockIdx.x; item < total;
+       item += gridDim.x)
   {
     int i, r;
     if constexpr (BLOCKED)

@@ -128,33 +128,47 @@ hipError_t launch_ifft_fourstep(int logn, int n_images, float4* images, float4* 
   });
 }
 
-bool ifft_colfirst_supported(int logn) { return logn == 12; }
+// Column-first EncodeIFFT through a work image: 4096 (B = 4) and 8192 (B = 2: the strided pass only
+// reads the 32-B pieces, which L2 merges, and writes whole strips; the in-place column pass wrote
+// them back as partial lines, 1.67 x algorithmic). At 8192 a 128-B line of the work image holds 4
+// rows = 2 row items, run as pairs on one XCD (GRPR 2): 4 x 8192^2 in 4.39 ms against 5.06 ungrouped
+// and 4.77 in place (tools/microbench/ifft4bench, profiles/r03_ifft4bench.log).
+bool ifft_colfirst_supported(int logn) { return logn == 12 || logn == 13; }
 
 hipError_t launch_ifft_colfirst(int logn, int n_images, float4* images, float4* work, const float2* tw,
                                 hipStream_t stream, int cus)
 {
   if (!ifft_colfirst_supported(logn))
     return hipErrorInvalidValue;
-  constexpr int LOGN = 12;
-  using K = ColFirstCfg<LOGN>;
-  using S = FftShape<LOGN>;
-  constexpr int tw_lds = tw_bytes<S::TW_ENTRIES>();
-  {
-    auto kern = k_cols_to_blocks<LOGN>;
-    const int lds = tw_lds + K::LDS1;
-    const int grid = persistent_grid(kern, K::WG1, lds, n_images * (S::N / K::B), cus);
-    hipLaunchKernelGGL(kern, dim3(grid), dim3(K::WG1), lds, stream, n_images, images, work, tw);
-    hipError_t e = hipGetLastError();
-    if (e != hipSuccess)
-      return e;
-  }
-  auto kern = k_rows_final<LOGN, true>;
-  const int lds = tw_lds + K::LDS2;
-  const SlabGeom g{0, S::N};
-  const int grid = persistent_grid(kern, K::WG2, lds, n_images * (S::N / K::RPW2), cus);
-  hipLaunchKernelGGL(kern, dim3(grid), dim3(K::WG2), lds, stream, n_images, g, work, images, (float*)nullptr,
-                     FoamParams{}, tw);
-  return hipGetLastError();
+  return with_logn(logn, [&](auto L) -> hipError_t {
+    constexpr int LOGN = decltype(L)::value;
+    if constexpr (LOGN != 12 && LOGN != 13)
+      return hipErrorInvalidValue;
+    else
+    {
+      using K = ColFirstCfg<LOGN>;
+      using S = FftShape<LOGN>;
+      constexpr int tw_lds = tw_bytes<S::TW_ENTRIES>();
+      {
+        auto kern = k_cols_to_blocks<LOGN>;
+        const int lds = tw_lds + K::LDS1;
+        const int grid = persistent_grid(kern, K::WG1, lds, n_images * (S::N / K::B), cus);
+        hipLaunchKernelGGL(kern, dim3(grid), dim3(K::WG1), lds, stream, n_images, images, work, tw);
+        hipError_t e = hipGetLastError();
+        if (e != hipSuccess)
+          return e;
+      }
+      // row items sharing one 128-B line (8 texels) of the work image: B x RPW2 texels per item each
+      constexpr int GRPR = K::B * K::RPW2 >= 8 ? 1 : 8 / (K::B * K::RPW2);
+      auto kern = k_rows_final<LOGN, true, kStream, kStream, K::RPW2, 0, GRPR>;
+      const int lds = tw_lds + K::LDS2;
+      const SlabGeom g{0, S::N};
+      const int grid = persistent_grid(kern, K::WG2, lds, n_images * (S::N / K::RPW2), cus);
+      hipLaunchKernelGGL(kern, dim3(grid), dim3(K::WG2), lds, stream, n_images, g, work, images, (float*)nullptr,
+                         FoamParams{}, tw);
+      return hipGetLastError();
+    }
+  });
 }
 
 hipError_t launch_rows_final(int logn, int cascades, const SlabGeom& g, const float4* inter, float4* scratch,

@@ -279,9 +279,9 @@ int ocean_fft_encode_ifft_batch(ocean_fft* fft, float* images, int n_images)
   auto* img = reinterpret_cast<float4*>(images);
   if (ifft_colfirst_supported(fft->logn))
   {
-    // column-first through a work image of up to kIfftChunk images (2 GiB at N = 4096)
-    constexpr int kIfftChunk = 8;
-    const int want = n_images < kIfftChunk ? n_images : kIfftChunk;
+    // column-first through a work image of up to 2 GiB (8 images at N = 4096, 2 at 8192)
+    const int chunk = std::max(1, (int)(((size_t)2 << 30) / ((size_t)fft->n * fft->n * sizeof(float4))));
+    const int want = n_images < chunk ? n_images : chunk;
     if (fft->work_images < want)
     {
       float4* w = nullptr;

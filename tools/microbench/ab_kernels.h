@@ -534,7 +534,7 @@ hipError_t launch_cols_group(int logn, int n_images, float4* images, const float
 
 // Column-first EncodeIFFT at N = 8192 (B = 2: 32-B strided pieces, GROUP strips per XCD group) through a
 // work image, then the blocked row pass (ifft4bench)
-template <int GROUP>
+template <int GROUP, int GRPR = 1>
 hipError_t launch_ifft_colfirst13(int n_images, float4* images, float4* work, const float2* tw, hipStream_t stream,
                                   int cus)
 {
@@ -545,7 +545,7 @@ hipError_t launch_ifft_colfirst13(int n_images, float4* images, float4* work, co
   auto ka = k_cols_to_blocks<LOGN, 0, GROUP>;
   const int grid = persistent_grid(ka, K::WG1, tw_lds + K::LDS1, n_images * (S::N / K::B), cus);
   hipLaunchKernelGGL(ka, dim3(grid), dim3(K::WG1), tw_lds + K::LDS1, stream, n_images, images, work, tw);
-  auto kb = k_rows_final<LOGN, true>;
+  auto kb = k_rows_final<LOGN, true, kStream, kStream, K::RPW2, 0, GRPR>;
   const SlabGeom g{0, S::N};
   const int grid2 = persistent_grid(kb, K::WG2, tw_lds + K::LDS2, n_images * (S::N / K::RPW2), cus);
   hipLaunchKernelGGL(kb, dim3(grid2), dim3(K::WG2), tw_lds + K::LDS2, stream, n_images, g, work, images,

@@ -139,13 +139,32 @@ int main()
     runs.push_back([&] { return launch_cols_group<8>(logn, imgs, img, tw, 0, cus); });
     if (logn == 13)
     {
-      for (int grp : {2, 4, 8})
+      // column-first through a work image (the strided pass only reads 32-B pieces, which L2
+      // merges; it writes whole strips), then the blocked row pass, whose 128-B lines hold 4 rows =
+      // 2 items: GRPR items per XCD group read them together
+      for (int grpr : {1, 2, 4})
       {
-        names.push_back("column-first via work image, group " + std::to_string(grp));
-        runs.push_back([&, grp] {
-          return grp == 2 ? launch_ifft_colfirst13<2>(imgs, img, work, tw, 0, cus)
-                          : grp == 4 ? launch_ifft_colfirst13<4>(imgs, img, work, tw, 0, cus)
-                                     : launch_ifft_colfirst13<8>(imgs, img, work, tw, 0, cus);
+        CHECK(hipMemcpy(img, h.data(), tex * 16, hipMemcpyHostToDevice));
+        hipError_t ec = grpr == 1 ? launch_ifft_colfirst13<2, 1>(imgs, img, work, tw, 0, cus)
+                        : grpr == 2 ? launch_ifft_colfirst13<2, 2>(imgs, img, work, tw, 0, cus)
+                                    : launch_ifft_colfirst13<2, 4>(imgs, img, work, tw, 0, cus);
+        CHECK(ec);
+        CHECK(hipDeviceSynchronize());
+        CHECK(hipMemcpy(b.data(), img, tex * 16, hipMemcpyDeviceToHost));
+        double mx = 0, er = 0;
+        for (size_t k = 0; k < tex; k++)
+          for (int j = 0; j < 4; j++)
+          {
+            mx = std::max(mx, (double)std::fabs((&a[k].x)[j]));
+            er = std::max(er, (double)std::fabs((&a[k].x)[j] - (&b[k].x)[j]));
+          }
+        std::printf("N=%d column-first, row items grouped %d: vs in-place max |diff| / max |x| = %.3g\n", n, grpr,
+                    er / mx);
+        names.push_back("column-first via work image, row items grouped " + std::to_string(grpr));
+        runs.push_back([&, grpr] {
+          return grpr == 1 ? launch_ifft_colfirst13<2, 1>(imgs, img, work, tw, 0, cus)
+                           : grpr == 2 ? launch_ifft_colfirst13<2, 2>(imgs, img, work, tw, 0, cus)
+                                       : launch_ifft_colfirst13<2, 4>(imgs, img, work, tw, 0, cus);
         });
       }
     }

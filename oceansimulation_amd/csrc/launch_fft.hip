@@ -200,7 +200,9 @@ hipError_t launch_rows_final(int logn, int cascades, const SlabGeom& g, const fl
     }
     else
     {
-      auto kern = k_rows_final<LOGN, true>;
+      // B x RPW2 texels per item and strip; items sharing a 128-B line run together on one XCD (8192)
+      constexpr int GRPR = K::B * K::RPW2 >= 8 ? 1 : 8 / (K::B * K::RPW2);
+      auto kern = k_rows_final<LOGN, true, kStream, kStream, K::RPW2, 0, GRPR>;
       const int grid = persistent_grid(kern, K::WG2, lds, items, cus);
       hipLaunchKernelGGL(kern, dim3(grid), dim3(K::WG2), lds, stream, 2 * cascades, g, inter, maps, jac, foam, tw);
     }

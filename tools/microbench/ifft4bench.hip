@@ -57,13 +57,13 @@ static std::vector<float2> table(int logn)
   return tab;
 }
 
-int main()
+int main(int argc, char** argv)
 {
   int cus = 0;
   CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0));
   for (int logn : {13, 14})
   {
-    const int n = 1 << logn, imgs = logn == 13 ? 4 : 1;
+    const int n = 1 << logn, imgs = logn == 13 ? (argc > 1 ? std::atoi(argv[1]) : 4) : 1;
     const size_t tex = (size_t)n * n * imgs;
     std::vector<float4> h(tex);
     uint32_t st = 12345;

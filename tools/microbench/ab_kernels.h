@@ -553,6 +553,29 @@ hipError_t launch_ifft_colfirst13(int n_images, float4* images, float4* work, co
   return hipGetLastError();
 }
 
+// Column-first EncodeIFFT at any N (ifft4bench): the strided pass with GROUPC strips per XCD group
+// (their partial-line reads meet in one L2), the blocked row pass with GRPR row items per XCD group
+template <int LOGN, int GROUPC, int GRPR>
+hipError_t launch_ifft_colfirst_ab(int n_images, float4* images, float4* work, const float2* tw, hipStream_t stream,
+                                   int cus)
+{
+  using K = ColFirstCfg<LOGN>;
+  using S = FftShape<LOGN>;
+  constexpr int tw_lds = tw_bytes<S::TW_ENTRIES>();
+  auto ka = k_cols_to_blocks<LOGN, 0, GROUPC>;
+  const int grid = persistent_grid(ka, K::WG1, tw_lds + K::LDS1, n_images * (S::N / K::B), cus);
+  hipLaunchKernelGGL(ka, dim3(grid), dim3(K::WG1), tw_lds + K::LDS1, stream, n_images, images, work, tw);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess)
+    return e;
+  auto kb = k_rows_final<LOGN, true, kStream, kStream, K::RPW2, 0, GRPR>;
+  const SlabGeom g{0, S::N};
+  const int grid2 = persistent_grid(kb, K::WG2, tw_lds + K::LDS2, n_images * (S::N / K::RPW2), cus);
+  hipLaunchKernelGGL(kb, dim3(grid2), dim3(K::WG2), tw_lds + K::LDS2, stream, n_images, g, work, images,
+                     (float*)nullptr, FoamParams{}, tw);
+  return hipGetLastError();
+}
+
 // k_rows_xs before the scalar source-block shift (a division per field load): same-box A/B reference
 // for rm16bench. Results are bit-identical to production's.
 template <int LOGN, int PF>

@@ -168,6 +168,37 @@ int main(int argc, char** argv)
         });
       }
     }
+    if (logn == 14)
+    {
+      // column-first through a work image at 16384 (one-column strided items: 16-B read pieces,
+      // 8 strips per line; whole strips written), blocked rows with 8 row items per XCD group
+      CHECK(hipFree(work));
+      CHECK(hipMalloc(&work, tex * 16));
+      for (int v = 0; v < 3; v++)
+      {
+        auto run = [&, v] {
+          return v == 0 ? launch_ifft_colfirst_ab<14, 8, 8>(imgs, img, work, tw, 0, cus)
+                 : v == 1 ? launch_ifft_colfirst_ab<14, 8, 1>(imgs, img, work, tw, 0, cus)
+                          : launch_ifft_colfirst_ab<14, 2, 8>(imgs, img, work, tw, 0, cus);
+        };
+        CHECK(hipMemcpy(img, h.data(), tex * 16, hipMemcpyHostToDevice));
+        CHECK(run());
+        CHECK(hipDeviceSynchronize());
+        CHECK(hipMemcpy(b.data(), img, tex * 16, hipMemcpyDeviceToHost));
+        double mx = 0, er = 0;
+        for (size_t k = 0; k < tex; k++)
+          for (int j = 0; j < 4; j++)
+          {
+            mx = std::max(mx, (double)std::fabs((&a[k].x)[j]));
+            er = std::max(er, (double)std::fabs((&a[k].x)[j] - (&b[k].x)[j]));
+          }
+        const char* nm[3] = {"column-first, col group 8, row group 8", "column-first, col group 8, rows ungrouped",
+                             "column-first, col group 2, row group 8"};
+        std::printf("N=%d %s: vs in-place max |diff| / max |x| = %.3g\n", n, nm[v], er / mx);
+        names.push_back(nm[v]);
+        runs.push_back(run);
+      }
+    }
     std::vector<std::vector<float>> t(runs.size());
     for (int r = 0; r < 5; r++)
       for (size_t k = 0; k < runs.size(); k++)

@@ -1,0 +1,14 @@
+#!/bin/bash
+# Round-3 final measurement on one GPU box (frozen device code): smoke, the GPU suite, the default
+# bench line, and the rocprofv3 collections (trace + separate FETCH_SIZE / WRITE_SIZE passes) of the
+# headline, the 16384^2 whole grid and the EncodeIFFT legs. The first failure ends the script.
+set -u
+mkdir -p gpurun_out
+tools/gpu_step.sh f_smoke 300 python -u -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" || exit 1
+tools/gpu_step.sh f_suite 900 python -u -m pytest tests/ -m gpu -v --timeout 300 --timeout-method thread || exit 1
+tools/gpu_step.sh f_bench 900 python -u bench.py || exit 1
+PREFIX=r03f tools/profile_gpu.sh || exit 1
+PREFIX=r03f_16k BENCH_ARGS="--n 16384 --cascades 1 --steps 10 --warmup 2 --headline-only" tools/profile_gpu.sh || exit 1
+PREFIX=r03f_ifft BENCH_ARGS="--steps 3 --warmup 1 --no-slab --no-surface --no-reseed --no-cpu-baseline" \
+  KERNEL_REGEX="k_cols_to_blocks|k_rows_final|k_cols|k_rows_ifft|k_cols4" tools/profile_gpu.sh || exit 1
+echo "final measurements done"

@@ -219,11 +219,14 @@ def _f64_frame(o):
 
 
 def _frame_check(got_h, got_d, got_j, o):
-    """Against the oracle per lane (FRAME_TOL), and per channel against the float64 transform of the
-    oracle's spectrum (FRAME_TOL_GPU; tests/parity.py)."""
+    """Against the oracle per lane and per channel (FRAME_TOL), and per channel against the float64
+    transform of the oracle's spectrum (FRAME_TOL_GPU; tests/parity.py)."""
     eh, ed = lane_err(got_h, o.height), lane_err(got_d, o.disp)
     ej = scalar_err(got_j - 1.0, o.jac - 1.0)
     assert max(eh + ed) <= FRAME_TOL and ej <= FRAME_TOL, (eh, ed, ej)
+    # SURVEY §8(c)'s bar for the full pipeline: per channel against the oracle
+    eo = channel_err(got_h, o.height) + channel_err(got_d, o.disp)
+    assert max(eo) <= FRAME_TOL, eo
     h64, d64, j64 = _f64_frame(o)
     ec = channel_err(got_h, h64) + channel_err(got_d, d64)
     ej64 = scalar_err(got_j - 1.0, j64 - 1.0)

@@ -1,0 +1,9 @@
+#!/bin/bash
+# Round-3 final measurement, part B: rocprofv3 collections (trace + separate FETCH_SIZE / WRITE_SIZE
+# passes) of the headline, the 16384^2 whole grid and the EncodeIFFT legs.
+set -u
+PREFIX=r03f tools/profile_gpu.sh || exit 1
+PREFIX=r03f_16k BENCH_ARGS="--n 16384 --cascades 1 --steps 10 --warmup 2 --headline-only" tools/profile_gpu.sh || exit 1
+PREFIX=r03f_ifft BENCH_ARGS="--steps 3 --warmup 1 --no-slab --no-surface --no-reseed --no-cpu-baseline" \
+  KERNEL_REGEX="k_cols_to_blocks|k_rows_final|k_cols|k_rows_ifft|k_cols4" tools/profile_gpu.sh || exit 1
+echo "part B done"

@@ -341,7 +341,9 @@ hipError_t launch_half_rows_ab(int logn, const FrameParams& fp, const float4* ga
       // CU, the 4 rows of a gc line on one XCD (GRP 4): 1.407 -> 1.377 ms per 8 x 4096^2, maps
       // bit-identical (halfbench rowv 16); 17 = the two-row workgroups (production below 4096)
       constexpr bool ONE_ROW = LOGN == 12;
-      const int rpw = ablation == 4 ? R4 : (ablation == 5 || ablation == 16 || (ablation == 0 && ONE_ROW)) ? 1 : 2;
+      const int rpw = ablation == 4 ? R4
+                      : (ablation == 5 || ablation == 16 || ablation == 18 || ablation == 19 || (ablation == 0 && ONE_ROW)) ? 1
+                                                                                                             : 2;
       const int per_item = (ablation <= 3 || ablation >= 7) ? 1 : 2;
       // production loads use the default policy: C's 128-B lines are shared by the paired items
       // (xcd_pair_slot) and streamed loads lost them before the partner's read (-5 %,
@@ -352,6 +354,10 @@ hipError_t launch_half_rows_ab(int logn, const FrameParams& fp, const float4* ga
       auto kern = ablation == 0 && ONE_ROW ? k_rows_half<LOGN, 0, kStream, 0, 1, true, false, RG, RGC, 4, 4>
                   : ablation == 0 || ablation == 17 ? k_rows_half<LOGN, 0, kStream, 0, 2, true, false, RG, RGC>
                   : ablation == 16 ? k_rows_half<LOGN, 0, kStream, 0, 1, true, false, RG, RGC, 4, 4>
+                  // 18 / 19: one row per 256-thread workgroup on the half-strip layouts of pass-1 variants
+                  // 12 / 14 (FB 2: gab/gde RG 4; gc RGC 8 / 4), the 4 rows of a 128-B line on one XCD
+                  : ablation == 18 ? k_rows_half<LOGN, 0, kStream, 0, 1, true, false, 4, 8, 2, 4>
+                  : ablation == 19 ? k_rows_half<LOGN, 0, kStream, 0, 1, true, false, 4, 4, 2, 4>
                   : ablation == 8 ? k_rows_half<LOGN, 0, kStream, 0, 2, true, false, 2, 2>
                   : ablation == 9 ? k_rows_half<LOGN, 0, kStream, 0, 2, true, false, 2, 4>
                   : ablation == 10 ? k_rows_half<LOGN, 0, kStream, 0, 2, true, false, 4, 4>
@@ -555,23 +561,26 @@ hipError_t launch_ifft_colfirst13(int n_images, float4* images, float4* work, co
 
 // Column-first EncodeIFFT at any N (ifft4bench): the strided pass with GROUPC strips per XCD group
 // (their partial-line reads meet in one L2), the blocked row pass with GRPR row items per XCD group
-template <int LOGN, int GROUPC, int GRPR>
+// RPW: rows per row-pass item (default ColFirstCfg's; 1 at 8192 halves the workgroup's LDS, so two
+// workgroups share a CU)
+template <int LOGN, int GROUPC, int GRPR, int RPW = ColFirstCfg<LOGN>::RPW2>
 hipError_t launch_ifft_colfirst_ab(int n_images, float4* images, float4* work, const float2* tw, hipStream_t stream,
                                    int cus)
 {
   using K = ColFirstCfg<LOGN>;
   using S = FftShape<LOGN>;
   constexpr int tw_lds = tw_bytes<S::TW_ENTRIES>();
+  constexpr int LDS2 = lds_row_slots<LOGN>(RPW) * 8;
   auto ka = k_cols_to_blocks<LOGN, 0, GROUPC>;
   const int grid = persistent_grid(ka, K::WG1, tw_lds + K::LDS1, n_images * (S::N / K::B), cus);
   hipLaunchKernelGGL(ka, dim3(grid), dim3(K::WG1), tw_lds + K::LDS1, stream, n_images, images, work, tw);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess)
     return e;
-  auto kb = k_rows_final<LOGN, true, kStream, kStream, K::RPW2, 0, GRPR>;
+  auto kb = k_rows_final<LOGN, true, kStream, kStream, RPW, 0, GRPR>;
   const SlabGeom g{0, S::N};
-  const int grid2 = persistent_grid(kb, K::WG2, tw_lds + K::LDS2, n_images * (S::N / K::RPW2), cus);
-  hipLaunchKernelGGL(kb, dim3(grid2), dim3(K::WG2), tw_lds + K::LDS2, stream, n_images, g, work, images,
+  const int grid2 = persistent_grid(kb, S::T * RPW, tw_lds + LDS2, n_images * (S::N / RPW), cus);
+  hipLaunchKernelGGL(kb, dim3(grid2), dim3(S::T * RPW), tw_lds + LDS2, stream, n_images, g, work, images,
                      (float*)nullptr, FoamParams{}, tw);
   return hipGetLastError();
 }

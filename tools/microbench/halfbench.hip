@@ -387,6 +387,72 @@ int main(int argc, char** argv)
     }
     return 0;
   }
+  if (argc > 3 && std::strcmp(argv[3], "fb2") == 0)
+  {
+    // half-strip pass 1 (k_cols_half2: 2 columns per 512-thread item, H in VGPRs, no H scratch) with
+    // the one-row pass 2 on the FB = 2 layouts (rows variants 18 / 19), against production
+    const int BIG = 1 << 20;
+    CHECK(c1());
+    CHECK(r1());
+    CHECK(hipDeviceSynchronize());
+    auto pm = snap(maps, mb), pj = snap(jac, jb);
+    struct V
+    {
+      const char* name;
+      int cv, rv, cus;
+    };
+    const V vs[] = {{"production", 0, 0, 0},
+                    {"half2 RG4/RGC8 persistent + rows 18", 12, 18, cus},
+                    {"half2 RG4/RGC8 one-shot + rows 18", 12, 18, BIG},
+                    {"half2 RG4/RGC4 persistent + rows 19", 14, 19, cus},
+                    {"half2 RG4/RGC8 persistent + rows 12 (2-row)", 12, 12, cus}};
+    const int NV = sizeof(vs) / sizeof(vs[0]);
+    auto cl = [&](const V& v) {
+      return [&, v] {
+        return v.cv == 0 ? c1() : launch_half_columns_ab(logn, fp, h0, gab, gcd, ge, spec, tw, 0, v.cus, nullptr, 0, nullptr, v.cv);
+      };
+    };
+    auto rl = [&](const V& v) {
+      return [&, v] { return v.rv == 0 ? r1() : launch_half_rows_ab(logn, fp, gab, gcd, ge, spec, maps, jac, foam, tw, 0, cus, v.rv); };
+    };
+    for (int k = 1; k < NV; k++)
+    {
+      CHECK(hipMemset(maps, 0, mb));
+      CHECK(hipMemset(jac, 0, jb));
+      CHECK(cl(vs[k])());
+      CHECK(rl(vs[k])());
+      CHECK(hipDeviceSynchronize());
+      auto m = snap(maps, mb), j = snap(jac, jb);
+      const float* a = reinterpret_cast<const float*>(m.data());
+      const float* b = reinterpret_cast<const float*>(pm.data());
+      double mx = 0, dm = 0;
+      for (size_t e = 0; e < mb / 4; e++)
+      {
+        mx = std::max(mx, (double)std::fabs(b[e]));
+        dm = std::max(dm, (double)std::fabs(a[e] - b[e]));
+      }
+      std::printf("%s vs production: maps max|diff| %g of max %g (%.2e)\n", vs[k].name, dm, mx, dm / mx);
+      diff(j, pj);
+    }
+    std::vector<std::vector<float>> tc(NV), tr(NV), tf(NV);
+    for (int r = 0; r < 7; r++)
+      for (int k = 0; k < NV; k++)
+      {
+        auto c = cl(vs[k]);
+        auto w = rl(vs[k]);
+        tc[k].push_back(time_ms(c, 10));
+        tr[k].push_back(time_ms(w, 10));
+        tf[k].push_back(time_ms([&] { hipError_t e = c(); return e == hipSuccess ? w() : e; }, 10));
+      }
+    for (int k = 0; k < NV; k++)
+    {
+      std::sort(tc[k].begin(), tc[k].end());
+      std::sort(tr[k].begin(), tr[k].end());
+      std::sort(tf[k].begin(), tf[k].end());
+      std::printf("%-46s cols %7.3f  rows %7.3f  frame %7.3f ms (median)\n", vs[k].name, tc[k][3], tr[k][3], tf[k][3]);
+    }
+    return 0;
+  }
   if (argc > 3 && std::strcmp(argv[3], "layout2") == 0)
   {
     // field layouts (RG, RGC) re-measured with production's pass 1 (5 of 8 H pairs out of the

@@ -167,6 +167,30 @@ int main(int argc, char** argv)
                                        : launch_ifft_colfirst13<2, 4>(imgs, img, work, tw, 0, cus);
         });
       }
+      // one row per row-pass item (512 threads, half the LDS: two workgroups per CU), the 4 items of a
+      // line grouped on one XCD (4) or 8 items (two lines of a strip piece)
+      for (int grpr : {4, 8})
+      {
+        auto run = [&, grpr] {
+          return grpr == 4 ? launch_ifft_colfirst_ab<13, 2, 4, 1>(imgs, img, work, tw, 0, cus)
+                           : launch_ifft_colfirst_ab<13, 2, 8, 1>(imgs, img, work, tw, 0, cus);
+        };
+        CHECK(hipMemcpy(img, h.data(), tex * 16, hipMemcpyHostToDevice));
+        CHECK(run());
+        CHECK(hipDeviceSynchronize());
+        CHECK(hipMemcpy(b.data(), img, tex * 16, hipMemcpyDeviceToHost));
+        double mx = 0, er = 0;
+        for (size_t k = 0; k < tex; k++)
+          for (int j = 0; j < 4; j++)
+          {
+            mx = std::max(mx, (double)std::fabs((&a[k].x)[j]));
+            er = std::max(er, (double)std::fabs((&a[k].x)[j] - (&b[k].x)[j]));
+          }
+        std::printf("N=%d column-first, one-row items grouped %d: vs in-place max |diff| / max |x| = %.3g\n", n, grpr,
+                    er / mx);
+        names.push_back("column-first, one-row items grouped " + std::to_string(grpr));
+        runs.push_back(run);
+      }
     }
     if (logn == 14)
     {

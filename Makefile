@@ -59,7 +59,7 @@ $(APP): examples/waveapp_headless.cpp $(WAVES)
 	    -L$(PKG) -lwaves -loceanfft -Wl,-rpath,'$$ORIGIN/../$(PKG)' -L/opt/rocm/lib -lamdhip64
 
 MB := tools/microbench
-microbench: $(MB)/detbench $(MB)/detbench_soffset $(MB)/rm16bench $(MB)/gen4bench $(MB)/ifft4bench $(MB)/gridbench $(MB)/halfbench_nohs $(MB)/ifftbench $(MB)/transbench $(MB)/scatterbench $(MB)/halfbench $(MB)/genbench $(MB)/colbench $(MB)/copybench $(MB)/genbench_noxch $(MB)/genbench_nobar $(MB)/layoutbench
+microbench: $(MB)/prebench $(MB)/detbench $(MB)/detbench_soffset $(MB)/rm16bench $(MB)/gen4bench $(MB)/ifft4bench $(MB)/gridbench $(MB)/halfbench_nohs $(MB)/ifftbench $(MB)/transbench $(MB)/scatterbench $(MB)/halfbench $(MB)/genbench $(MB)/colbench $(MB)/copybench $(MB)/genbench_noxch $(MB)/genbench_nobar $(MB)/layoutbench
 MB_DEPS := $(KERNEL_TUS:%=$(CSRC)/%.hip) $(DEVICE_H) $(MB)/ab_kernels.h $(MB)/all_kernels.h
 $(MB)/%: $(MB)/%.hip $(MB_DEPS)
 	$(HIPCC) $(HIPFLAGS) $< -o $@

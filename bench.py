@@ -473,7 +473,8 @@ def ifft_legs(n: int, cascades: int, calls: int = 6) -> dict:
 
 def large_ifft_legs(calls: int = 3) -> dict:
     """Standalone EncodeIFFT at the sizes the frame path runs slabs at: 2 packed 8192^2 images (one
-    cascade: column-first through a work image, rows grouped per 128-B line) and 2 packed 16384^2 images (rows, then the
+    cascade: the radix-2 pre-stage column pass through a work image, then the permuted blocked rows) and 2 packed
+    16384^2 images (rows, then the
     four-step column transform through an N x 2048 work slab). 64 algorithmic B per texel as above;
     the four-step order moves 96."""
     import torch
@@ -495,7 +496,8 @@ def large_ifft_legs(calls: int = 3) -> dict:
         texels = imgs * n * n
         out[str(n)] = {"workload": f"EncodeIFFT of {imgs} packed RGBA32F {n}x{n} images (1 cascade x 2), in place",
                        "order": ("rows + four-step columns (work slab)" if n == 16384 else
-                                 "columns through a work image (whole strips written), then the blocked rows"),
+                                 "radix-2 pre-stage columns (4-column strips, two 4096-point halves) through a work "
+                                 "image, then the permuted blocked rows"),
                        "ms_per_call": ms, "height_field_points_per_s": n * n / (ms * 1e-3),
                        "GB_per_s_algorithmic": 64.0 * texels / (ms * 1e-3) / 1e9}
         fft.close()

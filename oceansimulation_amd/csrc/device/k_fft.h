@@ -154,6 +154,142 @@ __global__ __launch_bounds__(ColFirstCfg<LOGN>::WG1) void k_cols_to_blocks(int i
   }
 }
 
+// Standalone EncodeIFFT at N = R M, M = 4096 (R = 2: 8192, R = 4: 16384), column-first with a
+// radix-R pre-stage, so that a column item is the 4096 pass's shape (a strip of B = 4 columns, 64-B
+// pieces, 256 KiB of CPairs) instead of one or two whole columns (16/32-B pieces). With y index
+// q = n + M j and k = R k' + r:
+//   X[R k' + r] = sum_n W_M^(n k') [W_N^(n r) sum_j x[n + M j] W_R^(j r)],
+// so item (strip, r) forms y_r[n] = W_N^(n r) sum_j x[n + M j] W_R^(j r) from R loads per point and
+// runs the 4096-point transform, which leaves X[R k' + r] at k' = i + m T. The R items of a strip
+// read the same lines and the two strips of a 128-B line share them: the 2R items run together on
+// one XCD (xcd_group_slot), so HBM serves each line once and L2 the rest.
+// WL (work layout): 0 = [img][strip][r][k'][B] split planes (each item writes one contiguous 256-KiB
+// run; the row pass reads stored row r M + k' and writes image row R k' + r: k_rows_final PR); 1 =
+// row-major [img][y][x] reference texels (64-B pieces of rows R k' + r; k_rows_ifft_out).
+// The pre-stage sum in the wave-uniform r, branch-free (c = (-1)^r, w = i^r computed once per item):
+// R = 2: x0 + c x1; R = 4: (x0 + c x2) + w (x1 + c x3) (inverse: W_4 = +i).
+template <int R>
+__device__ __forceinline__ CPair prestage_sum(const CPair* x, float c, float2 w)
+{
+  const f2v cc = {c, c};
+  if constexpr (R == 2)
+    return {x[0].re + cc * x[1].re, x[0].im + cc * x[1].im};
+  else
+  {
+    static_assert(R == 4, "pre-stage radix 2 or 4");
+    const CPair s02 = {x[0].re + cc * x[2].re, x[0].im + cc * x[2].im};
+    const CPair t13 = {x[1].re + cc * x[3].re, x[1].im + cc * x[3].im};
+    return s02 + cmul(t13, w);
+  }
+}
+
+struct PreCfg
+{
+  static constexpr int LOGM = 12, M = 4096, T = 256, B = 4, WG = 1024;
+  static constexpr int TWM = ((FftShape<LOGM>::TW_ENTRIES * 8 + 15) / 16) * 16;
+  static constexpr int XCH = B * FftShape<LOGM>::PADDED * 8;
+};
+
+template <int LOGN, int LA = 0, int WL = 0, int LB = 2>
+__global__ __launch_bounds__(PreCfg::WG) void k_cols_pre(int images, const float4* __restrict__ src_images,
+                                                         float4* __restrict__ work, const float2* __restrict__ twn_glob,
+                                                         const float2* __restrict__ twm_glob)
+{
+  using P = PreCfg;
+  using SN = FftShape<LOGN>;
+  constexpr int N = SN::N, M = P::M, R = N / M, T = P::T, B = P::B;
+  static_assert(R == 2 || R == 4, "N = 8192 or 16384");
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  float2* twm = reinterpret_cast<float2*>(smem);
+  float2* twn = reinterpret_cast<float2*>(smem + P::TWM);
+  void* xch = smem + P::TWM + ((SN::TW_ENTRIES * 8 + 15) / 16) * 16;
+  for (int e = threadIdx.x; e < SN::TW_ENTRIES; e += blockDim.x)
+    twn[e] = twn_glob[e];
+  load_twiddles<P::LOGM>(twm, twm_glob);
+  const int strips = N / B;
+  const int total = images * strips * R;
+  // item = ((img strips/2 + strip pair) R + r) 2 + strip & 1: the 2R items sharing lines are consecutive
+  for (int item = xcd_group_slot<2 * R>(blockIdx.x, gridDim.x); item < total; item += gridDim.x)
+  {
+    const int tid = opaque((int)threadIdx.x);
+    const int b = tid & (B - 1), i = tid / B;
+    const int it = __builtin_amdgcn_readfirstlane(item);  // keep the item math scalar (no waterfall loops)
+    int t = it >> 1;
+    const int r = t % R;
+    t /= R;
+    const int sp = t % (strips / 2), img = t / (strips / 2);
+    const int xb = sp * 2 + (it & 1);
+    const float c = (r & 1) ? -1.0f : 1.0f;
+    const float2 w = make_float2((r & 1) ? 0.0f : c * (1.0f - (float)(r & 2)), (r & 1) ? 1.0f - (float)(r & 2) : 0.0f);
+    const float4* src = src_images + ((size_t)img << (2 * LOGN)) + (size_t)xb * B;
+    const int voff = ((i << LOGN) + b) * 16;
+    CPair v[16];
+#pragma unroll
+    for (int m = 0; m < 16; m++)
+    {
+      CPair x[R];
+#pragma unroll
+      for (int j = 0; j < R; j++)  // q = i + m T + M j sits in row (q + N/2) mod N: fftShift on y
+      {
+        // one descriptor per image (64 per-piece descriptors spill SGPRs, then VGPRs): the row offset
+        // joins the lane offset as an unsigned 32-bit byte offset (< 4 GiB = one 16384^2 image)
+        const unsigned row = (unsigned)((m * T + j * M + N / 2) & (N - 1));
+        x[j] = to_pair(ld4<LA>(src, (int)((unsigned)voff + (row << (LOGN + 4))), -1));
+      }
+      v[m] = cmul(prestage_sum<R>(x, c, w), twiddle<LOGN>((i + m * T) * r, twn));
+      if (LB > 0 && (m & (LB - 1)) == LB - 1)
+        asm volatile("" ::: "memory");  // LB points' loads in flight
+    }
+    fft_run<P::LOGM, B, true>(v, i, b, xch, twm);  // v[m] = X[R (i + m T) + r]
+    if constexpr (WL == 0)
+    {
+      float4* dst = work + ((size_t)img << (2 * LOGN)) + (size_t)(xb * R + r) * M * B;
+      const int soff = (i * B + b) * 16;
+#pragma unroll
+      for (int m = 0; m < 16; m++)
+        st4<kStream>(dst + m * T * B, soff, pair_raw(v[m]));
+    }
+    else
+    {
+      float4* dst = work + ((size_t)img << (2 * LOGN)) + (size_t)xb * B;
+      const int soff = (((R * i) << LOGN) + b) * 16;
+#pragma unroll
+      for (int m = 0; m < 16; m++)
+        st4<kStream>(dst + ((size_t)(R * m * T + r) << LOGN), soff, from_pair(v[m]));
+    }
+  }
+}
+
+// Row pass from a row-major work image to the caller's image (WL = 1 above): k_rows_ifft with
+// separate source and destination.
+template <int LOGN>
+__global__ __launch_bounds__(RowCfg<LOGN>::WG, RowCfg<LOGN>::MIN_WAVES) void k_rows_ifft_out(
+    int rows, const float4* __restrict__ src, float4* __restrict__ dst, const float2* __restrict__ tw_glob)
+{
+  using S = FftShape<LOGN>;
+  using R = RowCfg<LOGN>;
+  constexpr int T = S::T;
+  static_assert(R::RPW == 1, "one row per item");
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  float2* tw = reinterpret_cast<float2*>(smem);
+  void* xch = smem + ((S::TW_ENTRIES * 8 + 15) / 16) * 16;
+  load_twiddles<LOGN>(tw, tw_glob);
+  for (int row = blockIdx.x; row < rows; row += gridDim.x)
+  {
+    const int i = opaque((int)threadIdx.x % T);
+    const float4* in = src + ((size_t)row << LOGN);
+    float4* out = dst + ((size_t)row << LOGN);
+    CPair v[16];
+#pragma unroll
+    for (int m = 0; m < 16; m++)
+      v[m] = to_pair(ld4<kStream>(in + ((m + 8) & 15) * T, i * 16));  // fftShift on x
+    fft_run<LOGN, 0, R::SPLIT>(v, i, 0, xch, tw);
+#pragma unroll
+    for (int m = 0; m < 16; m++)
+      st4<kStream>(out + m * T, i * 16, from_pair(v[m]));
+  }
+}
+
 // Standalone EncodeIFFT at N >= 8192: the column transform in four steps (N = 16 N2), so that no
 // access is a 16- or 32-byte column piece (one 16384-row column is 256 KiB: an in-place column
 // item holds one or two columns and reads 16-32-B pieces, 1.3-2.8 TB/s). For y index n = N2 n1 + n2

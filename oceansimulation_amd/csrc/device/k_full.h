@@ -113,15 +113,18 @@ __global__ __launch_bounds__(ColFirstCfg<LOGN>::WG1) void k_cols_evolve(
 // 2 = no FFT (memory traffic and stores only).
 // GRPR (blocked input): consecutive items run on one XCD in groups of GRPR (xcd_group_slot), for a
 // block width whose 128-B lines span more rows than one item reads (B = 2, RPW = 2: a line is 4 rows).
+// BO: block width override (0: ColFirstCfg's B). PR > 1 (EncodeIFFT with k_cols_pre, WL = 0): stored
+// row y' = r M + k' (M = N / PR) is image row PR k' + r.
 template <int LOGN, bool BLOCKED, int LA = kStream, int SA = kStream, int RPW_ = ColFirstCfg<LOGN>::RPW2, int ABL = 0,
-          int GRPR = 1>
+          int GRPR = 1, int BO = 0, int PR = 1>
 __global__ __launch_bounds__(FftShape<LOGN>::T * RPW_) void k_rows_final(
     int images, SlabGeom g, const float4* __restrict__ inter, float4* __restrict__ maps, float* __restrict__ jac,
     FoamParams foam, const float2* __restrict__ tw_glob)
 {
   using S = FftShape<LOGN>;
   using K = ColFirstCfg<LOGN>;
-  constexpr int N = S::N, T = S::T, B = BLOCKED ? K::B : 1, RPW = RPW_;
+  constexpr int N = S::N, T = S::T, B = BLOCKED ? (BO ? BO : K::B) : 1, RPW = RPW_;
+  static_assert(PR == 1 || (BLOCKED && (N / PR) % RPW == 0), "PR: blocked input, items inside one r block");
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   float2* tw = reinterpret_cast<float2*>(smem);
   void* xch = smem + ((S::TW_ENTRIES * 8 + 15) / 16) * 16;
@@ -183,8 +186,9 @@ __global__ __launch_bounds__(FftShape<LOGN>::T * RPW_) void k_rows_final(
     }
     if constexpr (ABL != 2)
       fft_run<LOGN, 0, true>(v, i, r, i2, r2, xch, tw);
-    float4* dst = maps + ((size_t)cimg * w + y0) * N;
-    const int woff = ((r2 << LOGN) + i2) * 16;
+    // PR: rows y0 + r2 of one r block are image rows PR (y0 mod M + r2) + y0 / M
+    float4* dst = maps + ((size_t)cimg * w + (PR > 1 ? (y0 % (N / PR)) * PR + y0 / (N / PR) : y0)) * N;
+    const int woff = (((r2 * PR) << LOGN) + i2) * 16;
 #pragma unroll
     for (int m = 0; m < 16; m++)
       if constexpr (ABL == 1)

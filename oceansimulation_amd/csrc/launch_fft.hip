@@ -171,6 +171,65 @@ hipError_t launch_ifft_colfirst(int logn, int n_images, float4* images, float4* 
   });
 }
 
+// EncodeIFFT at N = 8192 / 16384 with the radix-R pre-stage column pass (k_cols_pre) through a work
+// image, then the row pass. WL 0: blocked work, k_rows_final with the row permutation (GRPR row items
+// sharing a 128-B line of the B = 4 blocks on one XCD: 1 at 8192, where an item reads 2 rows = whole
+// lines, 2 at 16384); WL 1: row-major work, k_rows_ifft_out. twm: the 4096-point table.
+template <int LOGN, int WL, int LA = 0, int LAR = kStream, int RPW = (LOGN == 13 ? 2 : 1), int LB = 2>
+hipError_t launch_ifft_pre_t(int n_images, float4* images, float4* work, const float2* twn, const float2* twm,
+                             hipStream_t stream, int cus)
+{
+  using S = FftShape<LOGN>;
+  using P = PreCfg;
+  constexpr int R = S::N / P::M;
+  {
+    auto kern = k_cols_pre<LOGN, LA, WL, LB>;  // 8 loads in flight per batch
+    const int lds = P::TWM + tw_bytes<S::TW_ENTRIES>() + P::XCH;
+    const int grid = persistent_grid(kern, P::WG, lds, n_images * (S::N / P::B) * R, cus);
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(P::WG), lds, stream, n_images, images, work, twn, twm);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess)
+      return e;
+  }
+  constexpr int tw_lds = tw_bytes<S::TW_ENTRIES>();
+  if constexpr (WL == 0)
+  {
+    constexpr int GRPR = P::B * RPW >= 8 ? 1 : 8 / (P::B * RPW);
+    auto kern = k_rows_final<LOGN, true, LAR, kStream, RPW, 0, GRPR, P::B, R>;
+    const int lds = tw_lds + lds_row_slots<LOGN>(RPW) * 8;
+    const SlabGeom g{0, S::N};
+    const int grid = persistent_grid(kern, S::T * RPW, lds, n_images * (S::N / RPW), cus);
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(S::T * RPW), lds, stream, n_images, g, work, images, (float*)nullptr,
+                       FoamParams{}, twn);
+  }
+  else
+  {
+    using RC = RowCfg<LOGN>;
+    auto kern = k_rows_ifft_out<LOGN>;
+    const int lds = tw_lds + RC::LDS_BYTES;
+    const int grid = persistent_grid(kern, RC::WG, lds, n_images << LOGN, cus);
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(RC::WG), lds, stream, n_images << LOGN, (const float4*)work, images,
+                       twn);
+  }
+  return hipGetLastError();
+}
+
+bool ifft_pre_supported(int logn) { return logn == 13; }
+
+hipError_t launch_ifft_pre(int logn, int n_images, float4* images, float4* work, const float2* twn, const float2* twm,
+                           hipStream_t stream, int cus)
+{
+  // 8192: one-row row items (512 threads, two workgroups per CU), the two items of each 128-B line
+  // on one XCD with default-policy loads so the partner's half is an L2 hit. 2 x 8192^2 (prebench,
+  // profiles/r03_prebench.log): 2.231 ms (production column-first) -> 1.860 ms; the two-row items
+  // 2.043, streamed row loads 1.975, row-major work 2.104. At 16384 the R = 4 pass (6.1 ms for 2
+  // images: each item reads its strip 4 times, 48 us per item) plus the blocked row pass (4.6 ms)
+  // lose to the four-step order (9.7 vs 10.6 ms): not used there.
+  if (logn == 13)
+    return launch_ifft_pre_t<13, 0, 0, 0, 1>(n_images, images, work, twn, twm, stream, cus);
+  return hipErrorInvalidValue;
+}
+
 hipError_t launch_rows_final(int logn, int cascades, const SlabGeom& g, const float4* inter, float4* scratch,
                              float4* maps, float* jac, const FoamParams& foam, const float2* tw, hipStream_t stream,
                              int cus)

@@ -69,6 +69,7 @@ struct ocean_fft
   hipStream_t stream = nullptr;
   float2* twiddles = nullptr;  // two-level table, see FftShape in device/fft.h
   float2* tw2 = nullptr;       // the N/16-point table after it (fourstep_table sizes), else null
+  float2* twm = nullptr;       // the 4096-point table after that (ifft_pre_supported sizes), else null
   float4* work = nullptr;      // column-first EncodeIFFT work image (the reference's workImage)
   int work_images = 0;
   size_t work_texels = 0;      // four-step EncodeIFFT (N = 16384): work slab of N x kFourStepSlab texels
@@ -230,6 +231,9 @@ int ocean_fft_create(ocean_fft** out, size_t texture_size, void* hip_stream)
   const size_t tw2_at = tab.size();
   if (fourstep_table(logn))
     append_table(logn - 4);
+  const size_t twm_at = tab.size();
+  if (ifft_pre_supported(logn))
+    append_table(12);
   e = hipMalloc(&f->twiddles, tab.size() * sizeof(float2));
   if (e == hipSuccess)
     e = hipMemcpy(f->twiddles, tab.data(), tab.size() * sizeof(float2), hipMemcpyHostToDevice);
@@ -242,6 +246,8 @@ int ocean_fft_create(ocean_fft** out, size_t texture_size, void* hip_stream)
   }
   if (fourstep_table(logn))
     f->tw2 = f->twiddles + tw2_at;
+  if (ifft_pre_supported(logn))
+    f->twm = f->twiddles + twm_at;
   *out = f;
   return OCEAN_OK;
 }
@@ -277,7 +283,8 @@ int ocean_fft_encode_ifft_batch(ocean_fft* fft, float* images, int n_images)
   if (!fft || !images || n_images < 1)
     return fail(OCEAN_ERR_INVALID, "ocean_fft_encode_ifft_batch: null plan/image or n_images < 1");
   auto* img = reinterpret_cast<float4*>(images);
-  if (ifft_colfirst_supported(fft->logn))
+  const bool pre = fft->logn == 13 && fft->twm != nullptr;  // 8192: the radix-2 pre-stage column pass
+  if (ifft_colfirst_supported(fft->logn) || pre)
   {
     // column-first through a work image of up to 2 GiB (8 images at N = 4096, 2 at 8192)
     const int chunk = std::max(1, (int)(((size_t)2 << 30) / ((size_t)fft->n * fft->n * sizeof(float4))));
@@ -301,9 +308,13 @@ int ocean_fft_encode_ifft_batch(ocean_fft* fft, float* images, int n_images)
       for (int first = 0; first < n_images; first += fft->work_images)
       {
         const int count = n_images - first < fft->work_images ? n_images - first : fft->work_images;
-        HIP_TRY(launch_ifft_colfirst(fft->logn, count, img + (size_t)first * fft->n * fft->n, fft->work, fft->twiddles,
-                                     fft->stream, fft->cus),
-                "column-first EncodeIFFT");
+        float4* first_img = img + (size_t)first * fft->n * fft->n;
+        if (pre)
+          HIP_TRY(launch_ifft_pre(fft->logn, count, first_img, fft->work, fft->twiddles, fft->twm, fft->stream, fft->cus),
+                  "pre-stage EncodeIFFT");
+        else
+          HIP_TRY(launch_ifft_colfirst(fft->logn, count, first_img, fft->work, fft->twiddles, fft->stream, fft->cus),
+                  "column-first EncodeIFFT");
       }
       return OCEAN_OK;
     }

@@ -208,6 +208,13 @@ hipError_t launch_ifft_fourstep(int logn, int n_images, float4* images, float4* 
 bool ifft_colfirst_supported(int logn);
 hipError_t launch_ifft_colfirst(int logn, int n_images, float4* images, float4* work, const float2* tw,
                                 hipStream_t stream, int cus);
+// Standalone EncodeIFFT at N = 8192: the radix-2 pre-stage column pass into a work image of
+// n_images * N^2 texels, then the row pass back into the images (16384: kernels for microbench A/B
+// only, launch_ifft_pre_t). twn: the N-point twiddle table; twm: the 4096-point table
+// (ocean_fft_create appends it for the ifft_pre_supported sizes).
+bool ifft_pre_supported(int logn);
+hipError_t launch_ifft_pre(int logn, int n_images, float4* images, float4* work, const float2* twn, const float2* twm,
+                           hipStream_t stream, int cus);
 hipError_t launch_surface(const SurfaceParams& p, const SurfacePlane& plane, const float2* xz, int64_t count,
                           float4* out, hipStream_t stream, int cus);
 hipError_t launch_hash(const uint32_t* xy, int count, uint32_t* raw, float2* uv, hipStream_t stream);

@@ -603,6 +603,79 @@ int main(int argc, char** argv)
     }
     return 0;
   }
+  if (argc > 3 && std::strcmp(argv[3], "xframe") == 0)
+  {
+    // frames pipelined over two field slots: frame f+1's pass 1 (depends on h0 and t only) on
+    // stream A beside frame f's pass 2 on stream B; pass 2 of every frame stays in order on B, so
+    // the maps are written frame after frame as before. Against both passes per frame on one stream.
+    float4 *gab2, *gcd2, *spec2;
+    float2* ge2;
+    CHECK(hipMalloc(&gab2, ht * sizeof(float4)));
+    CHECK(hipMalloc(&gcd2, ht * sizeof(float4)));
+    CHECK(hipMalloc(&ge2, ht * sizeof(float2)));
+    CHECK(hipMalloc(&spec2, (size_t)C * 2 * n * sizeof(float4)));
+    float4* sab[2] = {gab, gab2};
+    float4* sde[2] = {gcd, gcd2};
+    float2* sc[2] = {ge, ge2};
+    float4* ssp[2] = {spec, spec2};
+    hipStream_t sa, sb;
+    CHECK(hipStreamCreateWithFlags(&sa, hipStreamNonBlocking));
+    CHECK(hipStreamCreateWithFlags(&sb, hipStreamNonBlocking));
+    hipEvent_t evc[2], evr[2], e0;
+    for (int k = 0; k < 2; k++)
+    {
+      CHECK(hipEventCreateWithFlags(&evc[k], hipEventDisableTiming));
+      CHECK(hipEventCreateWithFlags(&evr[k], hipEventDisableTiming));
+      CHECK(hipEventRecord(evr[k], 0));
+    }
+    CHECK(hipEventCreateWithFlags(&e0, hipEventDisableTiming));
+    const int F = 20;
+    auto serial = [&] {
+      for (int f = 0; f < F; f++)
+      {
+        CHECK(c1());
+        CHECK(r1());
+      }
+      return hipSuccess;
+    };
+    auto piped = [&] {
+      CHECK(hipEventRecord(e0, 0));
+      CHECK(hipStreamWaitEvent(sa, e0, 0));
+      CHECK(hipStreamWaitEvent(sb, e0, 0));
+      for (int f = 0; f < F; f++)
+      {
+        const int s = f & 1;
+        CHECK(hipStreamWaitEvent(sa, evr[s], 0));
+        CHECK(launch_half_columns_ab(logn, fp, h0, sab[s], sde[s], sc[s], ssp[s], tw, sa, cus, hs, cus));
+        CHECK(hipEventRecord(evc[s], sa));
+        CHECK(hipStreamWaitEvent(sb, evc[s], 0));
+        CHECK(launch_half_rows_ab(logn, fp, sab[s], sde[s], sc[s], ssp[s], maps, jac, foam, tw, sb, cus));
+        CHECK(hipEventRecord(evr[s], sb));
+      }
+      CHECK(hipStreamWaitEvent(0, evr[(F - 1) & 1], 0));
+      return hipSuccess;
+    };
+    CHECK(serial());
+    CHECK(hipDeviceSynchronize());
+    auto bm = snap(maps, mb), bj = snap(jac, jb);
+    CHECK(hipMemset(maps, 0, mb));
+    CHECK(piped());
+    CHECK(hipDeviceSynchronize());
+    std::printf("pipelined vs serial frames:\n");
+    const bool same = (int)diff(snap(maps, mb), bm) & (int)diff(snap(jac, jb), bj);
+    std::vector<float> ts, tp;
+    for (int r = 0; r < 7; r++)
+    {
+      ts.push_back(time_ms(serial, 1) / F);
+      tp.push_back(time_ms(piped, 1) / F);
+    }
+    std::sort(ts.begin(), ts.end());
+    std::sort(tp.begin(), tp.end());
+    std::printf("C=%d frame, both passes on one stream     median %7.3f ms (%d frames)\n", C, ts[3], F);
+    std::printf("C=%d frame, pass 1 of f+1 beside pass 2 of f median %7.3f ms  bit-identical %s\n", C, tp[3],
+                same ? "yes" : "NO");
+    return 0;
+  }
   if (argc > 3 && std::strcmp(argv[3], "overlap") == 0)
   {
     // cascade groups pipelined over two streams: pass 1 of group g+1 (VALU-bound) beside pass 2 of

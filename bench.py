@@ -88,6 +88,9 @@ def parse(argv=None):
     ap.add_argument("--legs-timeout", type=float, default=300.0,
                     help="seconds allowed for the optional legs after the headline measurement; past it the "
                          "line is printed without the unfinished legs and every rank exits")
+    ap.add_argument("--frame-overlap", choices=("auto", "on", "off"), default="auto",
+                    help="ocean_generator_set_frame_overlap (frame f+1's column pass beside frame f's row pass): "
+                         "auto = on at <= 2 cascades per GPU on the half-spectrum path (8 x 4096^2: slower)")
     ap.add_argument("--full-spectrum", action="store_true",
                     help="time the full-spectrum frame path instead of the default half-spectrum one")
     ap.add_argument("--slab-n", type=int, default=16384, help="side of the single slab-decomposed grid")
@@ -402,17 +405,34 @@ def weak_leg(ocean, fft, args, rank: int, world: int, dt: float) -> dict:
             "ms_per_step": 1000.0 * el / args.steps, "points_per_s": float(n) * n * C * world * args.steps / el}
 
 
+def use_frame_overlap(args, cascades: int, path: str) -> bool:
+    """The headline's frame-overlap mode: on at <= 2 cascades per GPU (the 4- and 8-GPU strong-scaling
+    shares) on the blocked half-spectrum path, where the passes' launch tails dominate."""
+    if args.frame_overlap != "auto":
+        return args.frame_overlap == "on" and path == "half"
+    return path == "half" and cascades <= 2
+
+
 def one_cascade_leg(ocean, fft, args, dt: float) -> dict:
     """The P = 8 point of the strong-scaling headline on one GPU: ONE 4096^2 cascade per frame (what
     each of 8 GPUs runs when the 8 cascades are split 1 per GPU; src/Waves.cpp:20-39 runs one generator
-    per cascade). Launch tails weigh more than in the 8-cascade batch."""
+    per cascade). Launch tails weigh more than in the 8-cascade batch; the headline runs this share
+    with frame overlap (use_frame_overlap), the serial frame is reported beside it."""
     n = args.n
     gen = ocean.Generator(fft, 1)
     ocean.apply_settings(gen.GetOceanSettings(0), **cascade_settings(0, 0))
     for _ in range(max(args.warmup, 2)):
         gen.CalculateOcean(dt)
     steps = max(args.steps, 20)
-    el = timed_frames(gen, steps, dt, 1)
+    overlap = use_frame_overlap(args, 1, frame_path(n, args.full_spectrum))
+    el_serial = timed_frames(gen, steps, dt, 1)
+    el = el_serial
+    if overlap:
+        gen.set_frame_overlap(True)
+        for _ in range(2):
+            gen.CalculateOcean(dt)
+        el = timed_frames(gen, steps, dt, 1)
+        gen.set_frame_overlap(False)
     gen.set_profiling(True)
     gen.kernel_times()
     for _ in range(steps):
@@ -423,7 +443,8 @@ def one_cascade_leg(ocean, fft, args, dt: float) -> dict:
     frame_ms = 1000.0 * el / steps
     passes_ms = ms[1] / max(cnt[1], 1) + ms[2] / max(cnt[2], 1)
     return {"what": f"1 cascade of {n}^2 per frame (the per-GPU share at 8 GPUs)",
-            "one_cascade_ms": frame_ms, "one_cascade_passes_ms": passes_ms,
+            "one_cascade_ms": frame_ms, "frame_overlap": overlap,
+            "one_cascade_serial_ms": 1000.0 * el_serial / steps, "one_cascade_passes_ms": passes_ms,
             "points_per_s": float(n) * n / (frame_ms * 1e-3),
             "frac_hbm_peak": b * n * n / (frame_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
             "frame_hbm_bytes_per_point": b}
@@ -809,6 +830,9 @@ def main(argv=None):
         gen.GenerateSpectrum()
     ms, cnt = gen.kernel_times()
     h0_ms = ms[0] / reps  # all cascades, per regeneration
+    overlap = use_frame_overlap(args, C, path)
+    if overlap:
+        gen.set_frame_overlap(True)
     for _ in range(args.warmup):
         gen.CalculateOcean(dt)
     gen.set_profiling(not args.no_profile)
@@ -875,6 +899,7 @@ def main(argv=None):
             "frame_path": {"half": "half spectrum", "full": "full spectrum",
                            "four-step": "half spectrum, four-step column pass"}[path],
             "frame_hbm_bytes_per_point": pass_bytes[0] + pass_bytes[1],
+            "frame_overlap": overlap,
         },
     }
     if el_reseed is not None:

@@ -158,6 +158,17 @@ int ocean_generator_set_four_step(ocean_generator* gen, int enable);
  * since the caller may have written h0 through it. enable = 0 re-seeds on every request, as the
  * reference does. Default 1. No reference counterpart. */
 int ocean_generator_set_h0_memo(ocean_generator* gen, int enable);
+/* Frame overlap (whole grids of N = 1024 .. 4096 on the half-spectrum path): frame f + 1's column
+ * pass, which depends only on h0 and the time, runs on an internal stream into a second set of field
+ * buffers while frame f's row pass still runs on the generator's stream, so the two passes' launch
+ * tails overlap when the caller issues frames back to back. Row passes, maps and Jacobian stay in
+ * order on the generator's stream, and the results are bit-identical. The internal stream waits for
+ * the generator's stream whenever the library writes h0 (seeding, re-seeds) and after the h0 pointer
+ * is handed out (ocean_generator_initial_spectrum); other work the caller enqueues on that stream
+ * between frames is not waited for, so it must not write the generator's buffers. Costs 20 B of
+ * device memory per point. Pays at 1-2 cascades per generator (8 x 4096^2: slower, leave it off).
+ * Default 0. No reference counterpart (the reference barriers after every dispatch). */
+int ocean_generator_set_frame_overlap(ocean_generator* gen, int enable);
 /* Algorithmic HBM bytes per height-field point of the column pass [0] and the row pass [1] of the
  * generator's current path (what bench.py prices the roofline with). */
 int ocean_generator_frame_bytes(const ocean_generator* gen, double per_point[2]);

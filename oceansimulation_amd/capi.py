@@ -89,6 +89,7 @@ SIGNATURES = {
     "ocean_generator_set_half_spectrum": (_i, [_vp, _i]),
     "ocean_generator_set_four_step": (_i, [_vp, _i]),
     "ocean_generator_set_h0_memo": (_i, [_vp, _i]),
+    "ocean_generator_set_frame_overlap": (_i, [_vp, _i]),
     "ocean_generator_frame_bytes": (_i, [_vp, _vp]),
     "ocean_slab_layout": (_i, [_sz, _i, _i, _i, ctypes.POINTER(ctypes.c_int64)]),
     "ocean_comm_unique_id": (_i, [_vp]),

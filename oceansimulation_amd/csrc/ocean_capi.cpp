@@ -138,6 +138,16 @@ struct ocean_generator
   int pending_slot = -1;           // slot whose row pass is still to be issued
   FrameParams slot_frame[2]{};     // the column pass's per-cascade values of the frame in each slot
   int64_t frames_issued = 0;
+  // ocean_generator_set_frame_overlap (blocked half path): frame f's column pass on `side` into field
+  // slot f % 2, beside frame f - 1's row pass on the generator's stream
+  bool overlap = false;
+  hipStream_t side = nullptr;
+  float4 *gab2 = nullptr, *gcd2 = nullptr, *spec2 = nullptr;
+  float2* ge2 = nullptr;
+  hipEvent_t ocols[2] = {nullptr, nullptr}, orows[2] = {nullptr, nullptr}, oh0 = nullptr;
+  bool orows_valid[2] = {false, false};
+  int oslot = 0;
+  bool h0_dirty = false;  // h0 (or the fused re-seed constants) written on the generator's stream since the side stream last waited
   bool profiling = false;
   std::vector<EventPair> pending;
   std::vector<hipEvent_t> pool;
@@ -380,18 +390,20 @@ hipEvent_t take_event(ocean_generator* g)
 
 // Runs `launch` bracketed by events when profiling is on.
 template <typename F>
-hipError_t timed(ocean_generator* g, int kind, F&& launch)
+hipError_t timed(ocean_generator* g, int kind, F&& launch, hipStream_t stream = nullptr)
 {
   if (!g->profiling)
     return launch();
+  if (!stream)
+    stream = g->fft->stream;
   EventPair p{kind, take_event(g), take_event(g)};
-  hipError_t e = hipEventRecord(p.a, g->fft->stream);
+  hipError_t e = hipEventRecord(p.a, stream);
   if (e != hipSuccess)
     return e;
   e = launch();
   if (e != hipSuccess)
     return e;
-  e = hipEventRecord(p.b, g->fft->stream);
+  e = hipEventRecord(p.b, stream);
   g->pending.push_back(p);
   return e;
 }
@@ -623,6 +635,17 @@ int ocean_generator_destroy(ocean_generator* g)
   }
   if (g->comm_stream)
     (void)hipStreamDestroy(g->comm_stream);
+  if (g->side)
+  {
+    (void)hipStreamSynchronize(g->side);
+    (void)hipStreamDestroy(g->side);
+  }
+  for (hipEvent_t ev : {g->ocols[0], g->ocols[1], g->orows[0], g->orows[1], g->oh0})
+    if (ev)
+      (void)hipEventDestroy(ev);
+  for (void* p : {(void*)g->gab2, (void*)g->gcd2, (void*)g->ge2, (void*)g->spec2})
+    if (p)
+      (void)hipFree(p);
   for (void* p : {(void*)g->gab, (void*)g->gcd, (void*)g->ge, (void*)g->spec, (void*)g->hs, (void*)g->h0row, g->seedc,
                   (void*)g->rm_ab, (void*)g->rm_de, (void*)g->rm_c, (void*)g->parts, (void*)g->xbuf})
     if (p)
@@ -648,6 +671,7 @@ ocean_settings* ocean_generator_settings(ocean_generator* g, int c)
 // frame evaluated h0 with, when that h0 image is materialised later)
 static int generate_spectrum_with(ocean_generator* g, const std::vector<ocean_settings>& settings)
 {
+  g->h0_dirty = true;
   g->h0_stale = false;
   g->h0_block = h0_block(g);
   g->h0_settings = settings;
@@ -776,6 +800,7 @@ static int generator_columns(ocean_generator* g, float timestep, int update_spec
         g->seedc_host.swap(host);
       }
       seed = g->seedc;
+      g->h0_dirty = true;
       g->h0_stale = true;
       g->seed_settings = g->settings;
       g->seeded = g->settings;
@@ -830,6 +855,27 @@ static int generator_columns(ocean_generator* g, float timestep, int update_spec
                                               g->hs, f->device_cus);
             }),
             "column pass (half spectrum, strip-dealt)");
+  else if (g->half && g->overlap)
+  {
+    // frame overlap: this column pass on the side stream into field slot oslot, after the row pass
+    // that last read the slot, and after any h0 / seed-constant writes on the generator's stream
+    const int s = g->oslot;
+    if (g->h0_dirty)
+    {
+      HIP_TRY(hipEventRecord(g->oh0, f->stream), "overlap: h0 event");
+      HIP_TRY(hipStreamWaitEvent(g->side, g->oh0, 0), "overlap: h0 wait");
+      g->h0_dirty = false;
+    }
+    if (g->orows_valid[s])
+      HIP_TRY(hipStreamWaitEvent(g->side, g->orows[s], 0), "overlap: slot wait");
+    HIP_TRY(timed(g, 1, [&] {
+              return launch_half_columns(f->logn, fp, g->h0, s ? g->gab2 : g->gab, s ? g->gcd2 : g->gcd,
+                                         s ? g->ge2 : g->ge, s ? g->spec2 : g->spec, f->twiddles, g->side, f->cus,
+                                         g->hs, f->device_cus, seed);
+            }, g->side),
+            "column pass (half spectrum, overlapped)");
+    HIP_TRY(hipEventRecord(g->ocols[s], g->side), "overlap: column event");
+  }
   else if (g->half)
     HIP_TRY(timed(g, 1, [&] {
               return launch_half_columns(f->logn, fp, g->h0, g->gab, g->gcd, g->ge, g->spec, f->twiddles, f->stream,
@@ -866,6 +912,20 @@ static int generator_rows(ocean_generator* g, const float4* in)
                                            f->tw2, f->stream, f->cus);
             }),
             "row pass (half spectrum, strip-dealt)");
+  else if (g->half && g->overlap)
+  {
+    const int s = g->oslot;
+    HIP_TRY(hipStreamWaitEvent(f->stream, g->ocols[s], 0), "overlap: column wait");
+    HIP_TRY(timed(g, 2, [&] {
+              return launch_half_rows(f->logn, g->frame, s ? g->gab2 : g->gab, s ? g->gcd2 : g->gcd,
+                                      s ? g->ge2 : g->ge, s ? g->spec2 : g->spec, g->maps, g->jac, foam, f->twiddles,
+                                      f->stream, f->cus);
+            }),
+            "row pass (half spectrum, overlapped)");
+    HIP_TRY(hipEventRecord(g->orows[s], f->stream), "overlap: row event");
+    g->orows_valid[s] = true;
+    g->oslot = s ^ 1;
+  }
   else if (g->half)
     HIP_TRY(timed(g, 2, [&] {
               return launch_half_rows(f->logn, g->frame, g->gab, g->gcd, g->ge, g->spec, g->maps, g->jac, foam,
@@ -885,6 +945,12 @@ int ocean_generator_set_half_spectrum(ocean_generator* g, int enable)
 {
   if (!g)
     return fail(OCEAN_ERR_INVALID, "ocean_generator_set_half_spectrum: null generator");
+  if (!enable && g->overlap)
+  {
+    const int rc = ocean_generator_set_frame_overlap(g, 0);
+    if (rc != OCEAN_OK)
+      return rc;
+  }
   const int logn = g->fft->logn;
   const bool blocked = !g->slab && half_spectrum_supported(logn);
   const bool dealt = !blocked && half_slab_supported(logn) && (g->slab || logn > 12);
@@ -909,6 +975,57 @@ int ocean_generator_set_half_spectrum(ocean_generator* g, int enable)
   }
   if ((was_hslab && g->ranks > 1) != (g->hslab && g->ranks > 1))
     g->update_spectrum = true;  // a slab's h0 layout changes (its strips or columns <-> its column slab)
+  return OCEAN_OK;
+}
+
+int ocean_generator_set_frame_overlap(ocean_generator* g, int enable)
+{
+  if (!g)
+    return fail(OCEAN_ERR_INVALID, "ocean_generator_set_frame_overlap: null generator");
+  if (enable && !g->half)
+    return fail(OCEAN_ERR_INVALID, "ocean_generator_set_frame_overlap: whole grids of N = 1024 .. 4096 on the "
+                                   "half-spectrum path only");
+  ocean_fft* f = g->fft;
+  if (enable && !g->overlap)
+  {
+    const size_t t = half_field_texels(f->logn) * g->cascades;
+    hipError_t e = hipSuccess;
+    if (!g->side)
+      e = hipStreamCreateWithFlags(&g->side, hipStreamNonBlocking);
+    for (hipEvent_t* ev : {&g->ocols[0], &g->ocols[1], &g->orows[0], &g->orows[1], &g->oh0})
+      if (e == hipSuccess && !*ev)
+        e = hipEventCreateWithFlags(ev, hipEventDisableTiming);
+    if (e == hipSuccess && !g->gab2)
+      e = hipMalloc(&g->gab2, t * sizeof(float4));
+    if (e == hipSuccess && !g->gcd2)
+      e = hipMalloc(&g->gcd2, t * sizeof(float4));
+    if (e == hipSuccess && !g->ge2)
+      e = hipMalloc(&g->ge2, t * sizeof(float2));
+    if (e == hipSuccess && !g->spec2)
+      e = hipMalloc(&g->spec2, (size_t)g->cascades * 2 * f->n * sizeof(float4));
+    // the side stream starts after everything issued so far (the last column pass used slot 0 and hs)
+    if (e == hipSuccess)
+      e = hipEventRecord(g->oh0, f->stream);
+    if (e == hipSuccess)
+      e = hipStreamWaitEvent(g->side, g->oh0, 0);
+    if (e != hipSuccess)
+      return fail(e == hipErrorOutOfMemory ? OCEAN_ERR_OOM : OCEAN_ERR_HIP,
+                  std::string("ocean_generator_set_frame_overlap: ") + hipGetErrorString(e));
+    g->orows_valid[0] = g->orows_valid[1] = false;
+    g->oslot = 0;
+    g->h0_dirty = false;
+    g->overlap = true;
+  }
+  else if (!enable && g->overlap)
+  {
+    // later frames run on the generator's stream in slot 0: after every overlapped pass
+    for (int s = 0; s < 2; s++)
+      if (g->orows_valid[s])
+        HIP_TRY(hipStreamWaitEvent(f->stream, g->orows[s], 0), "ocean_generator_set_frame_overlap");
+    HIP_TRY(hipEventRecord(g->oh0, g->side), "ocean_generator_set_frame_overlap");
+    HIP_TRY(hipStreamWaitEvent(f->stream, g->oh0, 0), "ocean_generator_set_frame_overlap");
+    g->overlap = false;
+  }
   return OCEAN_OK;
 }
 
@@ -1397,6 +1514,7 @@ float* ocean_generator_initial_spectrum(ocean_generator* g, int c)
   // the caller may write h0 through this pointer: the next requested re-seed must regenerate it, as
   // the reference does on every request (src/Generator.cpp:55-59), so the h0 memo forgets its inputs
   g->seeded.clear();
+  g->h0_dirty = true;  // frame overlap: the next column pass waits for the caller's stream (its h0 writes)
   return reinterpret_cast<float*>(g->h0 + h0_texels(g) * c);
 }
 

@@ -111,6 +111,12 @@ class Generator:
         """Skip requested re-seeds whose h0 inputs are unchanged (default) or re-seed every time."""
         check(lib().ocean_generator_set_h0_memo(self._h, 1 if enable else 0), "ocean_generator_set_h0_memo")
 
+    def set_frame_overlap(self, enable: bool) -> None:
+        """Run frame f + 1's column pass beside frame f's row pass (whole grids of 1024..4096, half
+        spectrum; bit-identical results; pays at 1-2 cascades)."""
+        check(lib().ocean_generator_set_frame_overlap(self._h, 1 if enable else 0),
+              "ocean_generator_set_frame_overlap")
+
     def frame_bytes(self):
         """Algorithmic HBM bytes per point of the column and row pass of the current path."""
         out = (ctypes.c_double * 2)()

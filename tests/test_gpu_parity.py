@@ -147,10 +147,11 @@ def test_encode_ifft_separable_vs_float64(ocean, n):
         assert err <= FFT_TOL, (n, lane, err)
 
 
-@pytest.mark.parametrize("n,b", [(512, 5), (4096, 10)])
+@pytest.mark.parametrize("n,b", [(512, 5), (4096, 10), (8192, 3)])
 def test_encode_ifft_batch_matches_single(ocean, n, b):
     """Batched == one image at a time, bit for bit (at 4096: the column-first path through its
-    work image, in chunks of 8 images, so 10 images cross a chunk boundary)."""
+    work image, in chunks of 8 images, so 10 images cross a chunk boundary; at 8192: the pre-stage
+    path, chunks of 2)."""
     from oceansimulation_amd.hip import DeviceBuffer
 
     imgs = np.stack([_rand_image(n, 100 + i) for i in range(b)])
@@ -459,6 +460,60 @@ def test_fused_reseed_frames(ocean, oracle):
     fused.CalculateOcean(0.0, update_ocean=True)  # getter after a fused frame: the new settings
     ref = oracle.generate_spectrum(oracle.default_settings(U_10=20.0, planeSize=5.0), n)
     assert max(lane_err(fused.initial_spectrum_host(0), ref)) <= H0_TOL
+
+
+@pytest.mark.parametrize("n,cascades", [(1024, 3), (4096, 1)])
+def test_frame_overlap_bit_identical(ocean, n, cascades):
+    """ocean_generator_set_frame_overlap: frame f + 1's column pass runs on an internal stream into a
+    second field slot beside frame f's row pass. Frames issued back to back without synchronising —
+    plain frames, the reference app's fused re-seeds (src/Waves.cpp:91-94, memo off), an h0 edit
+    with the update flag, h0 written through the getter's pointer, and the mode switched off and on
+    again — give the serial generator's bits (maps and Jacobian), frame for frame."""
+    fft = ocean.FFTCalculator(n)
+    ov, ser = ocean.Generator(fft, cascades), ocean.Generator(fft, cascades)
+    for g in (ov, ser):
+        g.set_h0_memo(False)
+        for c in range(cascades):
+            ocean.apply_settings(g.GetOceanSettings(c), planeSize=[5.0, 17.0, 101.0][c % 3] * (1 + c // 3))
+    ov.set_frame_overlap(True)
+
+    def same(tag):
+        for c in range(cascades):
+            for get in ("height_map_host", "displacement_map_host", "jacobian_map_host"):
+                assert np.array_equal(getattr(ov, get)(c), getattr(ser, get)(c)), (tag, c, get)
+
+    script = [(1.0 / 60.0, False), (0.5, False), (1.0 / 60.0, True), (1.0 / 60.0, False), (2.0, True),
+              (1.0 / 60.0, False), (1.0 / 60.0, False)]
+    for k, (dt, upd) in enumerate(script):
+        if k == 4:
+            for g in (ov, ser):
+                ocean.apply_settings(g.GetOceanSettings(0), U_10=25.0)
+        for g in (ov, ser):
+            g.CalculateOcean(dt, update_ocean=upd)
+        if k in (1, 4, 6):
+            same(("frame", k))
+    # the h0 getter (the caller may write through its pointer): the next column pass waits for it
+    h0 = ov.initial_spectrum_host(0)
+    for g in (ov, ser):
+        g.CalculateOcean(1.0 / 60.0)
+        g.CalculateOcean(1.0 / 60.0)
+    same("after getter")
+    ov.set_frame_overlap(False)
+    for g in (ov, ser):
+        g.CalculateOcean(1.0 / 60.0, update_ocean=True)
+        g.CalculateOcean(1.0 / 60.0)
+    same("overlap off")
+    ov.set_frame_overlap(True)
+    for _ in range(3):
+        for g in (ov, ser):
+            g.CalculateOcean(1.0 / 30.0)
+    same("overlap on again")
+    assert h0.shape[0] > 0
+    # the mode exists on the blocked half path only
+    full = ocean.Generator(fft, 1)
+    full.set_half_spectrum(False)
+    with pytest.raises(RuntimeError):
+        full.set_frame_overlap(True)
 
 
 def test_h0_memo_skips_identical_reseeds(ocean, oracle):

@@ -60,6 +60,18 @@ def test_strong_scaling_split():
         b.rank_cascades(8, 0, 3)
 
 
+def test_frame_overlap_mode_choice():
+    """The strong-scaling headline overlaps frames (ocean_generator_set_frame_overlap) only at <= 2
+    cascades per GPU on the blocked half path; --frame-overlap on/off overrides, never on other paths."""
+    b = _bench()
+    auto = b.parse([])
+    assert [b.use_frame_overlap(auto, c, "half") for c in (8, 4, 2, 1)] == [False, False, True, True]
+    assert not b.use_frame_overlap(auto, 1, "full") and not b.use_frame_overlap(auto, 1, "four-step")
+    assert b.use_frame_overlap(b.parse(["--frame-overlap", "on"]), 8, "half")
+    assert not b.use_frame_overlap(b.parse(["--frame-overlap", "on"]), 8, "full")
+    assert not b.use_frame_overlap(b.parse(["--frame-overlap", "off"]), 1, "half")
+
+
 def test_lane_err_metric():
     from parity import lane_err, scalar_err
 

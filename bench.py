@@ -425,14 +425,17 @@ def one_cascade_leg(ocean, fft, args, dt: float) -> dict:
         gen.CalculateOcean(dt)
     steps = max(args.steps, 20)
     overlap = use_frame_overlap(args, 1, frame_path(n, args.full_spectrum))
-    el_serial = timed_frames(gen, steps, dt, 1)
-    el = el_serial
-    if overlap:
-        gen.set_frame_overlap(True)
-        for _ in range(2):
-            gen.CalculateOcean(dt)
-        el = timed_frames(gen, steps, dt, 1)
-        gen.set_frame_overlap(False)
+    # serial and overlapped frames interleaved (3 runs each, median), so clock drift hits both alike
+    runs = {False: [], True: []}
+    for _ in range(3):
+        for mode in ((False, True) if overlap else (False,)):
+            gen.set_frame_overlap(mode)
+            for _ in range(2):
+                gen.CalculateOcean(dt)
+            runs[mode].append(timed_frames(gen, steps, dt, 1))
+    gen.set_frame_overlap(False)
+    el_serial = sorted(runs[False])[1]
+    el = sorted(runs[True])[1] if overlap else el_serial
     gen.set_profiling(True)
     gen.kernel_times()
     for _ in range(steps):

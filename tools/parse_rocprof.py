@@ -59,8 +59,10 @@ def algorithmic_bytes(key, n, cascades, mode):
     4096 profile) never borrows this workload's bytes."""
     pts = n * n * cascades
     logn = n.bit_length() - 1
-    if mode == "ifft":  # standalone EncodeIFFT: work-image chunks of 8 images, 32 B per texel per pass
-        return {"k_cols_to_blocks": 32 * 8 * n * n, "k_rows_final": 32 * 8 * n * n}.get(key)
+    if mode == "ifft":  # standalone EncodeIFFT: work-image chunks of 8 images, 32 B per texel per pass;
+        # the bench's 8192 leg (2 images per call, one launch per pass: the pre-stage column pass and its row pass)
+        return {"k_cols_to_blocks": 32 * 8 * n * n, "k_rows_final": 32 * 8 * n * n,
+                "k_cols_pre<13>": 32 * 2 * 8192 ** 2, "k_rows_final<13>": 32 * 2 * 8192 ** 2}.get(key)
     if logn in (13, 14):  # four-step whole grid: kept columns [0, N/2) + the Nyquist column
         kept = (n // 2 + 1) / n
         table = {"k_gen4_step1": (16 + 40) * kept, "k_rows_xs": 40 * kept + 36, "k_rows_half": 40 * kept + 36}

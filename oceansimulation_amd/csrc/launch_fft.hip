@@ -158,13 +158,17 @@ hipError_t launch_ifft_colfirst(int logn, int n_images, float4* images, float4* 
         if (e != hipSuccess)
           return e;
       }
-      // row items sharing one 128-B line (8 texels) of the work image: B x RPW2 texels per item each
-      constexpr int GRPR = K::B * K::RPW2 >= 8 ? 1 : 8 / (K::B * K::RPW2);
-      auto kern = k_rows_final<LOGN, true, kStream, kStream, K::RPW2, 0, GRPR>;
-      const int lds = tw_lds + K::LDS2;
+      // row items sharing one 128-B line (8 texels) of the work image: B x RPW texels per item each.
+      // 4096: one row per 256-thread item (four workgroups per CU instead of one 4-row workgroup),
+      // the two items of each line on one XCD with default-policy loads, as at 8192: 8 x 4096^2
+      // 1.779 -> 1.697 ms (tools/microbench/prebench, profiles/r03_prebench_4096.log)
+      constexpr int RPW = LOGN == 12 ? 1 : K::RPW2, LAR = LOGN == 12 ? 0 : kStream;
+      constexpr int GRPR = K::B * RPW >= 8 ? 1 : 8 / (K::B * RPW);
+      auto kern = k_rows_final<LOGN, true, LAR, kStream, RPW, 0, GRPR>;
+      const int lds = tw_lds + lds_row_slots<LOGN>(RPW) * 8;
       const SlabGeom g{0, S::N};
-      const int grid = persistent_grid(kern, K::WG2, lds, n_images * (S::N / K::RPW2), cus);
-      hipLaunchKernelGGL(kern, dim3(grid), dim3(K::WG2), lds, stream, n_images, g, work, images, (float*)nullptr,
+      const int grid = persistent_grid(kern, S::T * RPW, lds, n_images * (S::N / RPW), cus);
+      hipLaunchKernelGGL(kern, dim3(grid), dim3(S::T * RPW), lds, stream, n_images, g, work, images, (float*)nullptr,
                          FoamParams{}, tw);
       return hipGetLastError();
     }

@@ -563,7 +563,7 @@ hipError_t launch_ifft_colfirst13(int n_images, float4* images, float4* work, co
 // (their partial-line reads meet in one L2), the blocked row pass with GRPR row items per XCD group
 // RPW: rows per row-pass item (default ColFirstCfg's; 1 at 8192 halves the workgroup's LDS, so two
 // workgroups share a CU)
-template <int LOGN, int GROUPC, int GRPR, int RPW = ColFirstCfg<LOGN>::RPW2>
+template <int LOGN, int GROUPC, int GRPR, int RPW = ColFirstCfg<LOGN>::RPW2, int LAR = kStream>
 hipError_t launch_ifft_colfirst_ab(int n_images, float4* images, float4* work, const float2* tw, hipStream_t stream,
                                    int cus)
 {
@@ -577,7 +577,7 @@ hipError_t launch_ifft_colfirst_ab(int n_images, float4* images, float4* work, c
   hipError_t e = hipGetLastError();
   if (e != hipSuccess)
     return e;
-  auto kb = k_rows_final<LOGN, true, kStream, kStream, RPW, 0, GRPR>;
+  auto kb = k_rows_final<LOGN, true, LAR, kStream, RPW, 0, GRPR>;
   const SlabGeom g{0, S::N};
   const int grid2 = persistent_grid(kb, S::T * RPW, tw_lds + LDS2, n_images * (S::N / RPW), cus);
   hipLaunchKernelGGL(kb, dim3(grid2), dim3(S::T * RPW), tw_lds + LDS2, stream, n_images, g, work, images,

@@ -69,8 +69,11 @@ int main(int argc, char** argv)
   int cus = 0;
   CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0));
   const int imgs = argc > 1 ? std::atoi(argv[1]) : 2;
-  for (int logn : {13, 14})
+  const int only = argc > 2 ? std::atoi(argv[2]) : 0;  // 12, 13 or 14: that size only
+  for (int logn : {12, 13, 14})
   {
+    if (only ? logn != only : logn == 12)
+      continue;
     const int n = 1 << logn;
     const size_t tex = (size_t)n * n * imgs;
     std::vector<float4> h(tex);
@@ -95,7 +98,24 @@ int main(int argc, char** argv)
 
     std::vector<std::string> names;
     std::vector<std::function<hipError_t()>> runs;
-    if (logn == 13)
+    if (logn == 12)
+    {
+      // 4096: the column-first production (4-row row items, one 1024-thread workgroup per CU, streamed
+      // loads) against fewer rows per item (more workgroups per CU) and default-policy row loads
+      names.push_back("production: column-first, 4-row row items");
+      runs.push_back([&] { return launch_ifft_colfirst(12, imgs, img, work, twn, 0, cus); });
+      names.push_back("4-row row items, default-policy row loads");
+      runs.push_back([&] { return launch_ifft_colfirst_ab<12, 2, 1, 4, 0>(imgs, img, work, twn, 0, cus); });
+      names.push_back("2-row row items (512 threads)");
+      runs.push_back([&] { return launch_ifft_colfirst_ab<12, 2, 1, 2>(imgs, img, work, twn, 0, cus); });
+      names.push_back("2-row row items, default-policy row loads");
+      runs.push_back([&] { return launch_ifft_colfirst_ab<12, 2, 1, 2, 0>(imgs, img, work, twn, 0, cus); });
+      names.push_back("1-row row items (256 threads), pairs per line");
+      runs.push_back([&] { return launch_ifft_colfirst_ab<12, 2, 2, 1>(imgs, img, work, twn, 0, cus); });
+      names.push_back("1-row row items, pairs per line, default-policy row loads");
+      runs.push_back([&] { return launch_ifft_colfirst_ab<12, 2, 2, 1, 0>(imgs, img, work, twn, 0, cus); });
+    }
+    else if (logn == 13)
     {
       names.push_back("production: column-first (2-column items) + blocked rows");
       runs.push_back([&] { return launch_ifft_colfirst(13, imgs, img, work, twn, 0, cus); });

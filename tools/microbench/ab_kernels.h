@@ -761,4 +761,98 @@ __global__ __launch_bounds__(1024) void k_rows_xs_div(FrameParams fp, const floa
 }
 
 
+
+// EncodeIFFT at 16384 with the radix-4 pre-stage on TWO columns per item and the residue pair
+// (rp, rp + 2), which share their four loads: y_{rp} = s02 + w t13, y_{rp+2} = s02 - w t13 with
+// s02 = x0 + (-1)^rp x2, t13 = x1 + (-1)^rp x3, w = i^rp (half the L2 reads per output of
+// k_cols_pre<14>). Transform b4 = (column c = b4 & 1, s = b4 >> 1), residue r = rp + 2 s. Work
+// layout [img][strip2][r][k'][2] (two 128-KiB runs per item); the row pass is k_rows_final with
+// BO = 2, PR = 4 (32-B pieces, 4 stored rows per 128-B line on one XCD). prebench only.
+template <int LA = 0>
+__global__ __launch_bounds__(1024) void k_cols_pre_pair14(int images, const float4* __restrict__ src_images,
+                                                          float4* __restrict__ work, const float2* __restrict__ twn_glob,
+                                                          const float2* __restrict__ twm_glob)
+{
+  constexpr int LOGN = 14;
+  using P = PreCfg;
+  using SN = FftShape<LOGN>;
+  constexpr int N = SN::N, M = P::M, R = 4, T = P::T, B = 2;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  float2* twm = reinterpret_cast<float2*>(smem);
+  float2* twn = reinterpret_cast<float2*>(smem + P::TWM);
+  void* xch = smem + P::TWM + ((SN::TW_ENTRIES * 8 + 15) / 16) * 16;
+  for (int e = threadIdx.x; e < SN::TW_ENTRIES; e += blockDim.x)
+    twn[e] = twn_glob[e];
+  load_twiddles<P::LOGM>(twm, twm_glob);
+  const int strips = N / B;  // 2-column strips
+  const int total = images * strips * 2;
+  // item = ((img strips/4 + group) 2 + rp) 4 + strip & 3: the 8 items sharing lines are consecutive
+  for (int item = xcd_group_slot<8>(blockIdx.x, gridDim.x); item < total; item += gridDim.x)
+  {
+    const int tid = opaque((int)threadIdx.x);
+    const int b4 = tid & 3, i = tid >> 2, c = b4 & 1, s = b4 >> 1;
+    const int it = __builtin_amdgcn_readfirstlane(item);
+    int t = it >> 2;
+    const int rp = t & 1;
+    t >>= 1;
+    const int grp = t % (strips / 4), img = t / (strips / 4);
+    const int xb = grp * 4 + (it & 3);
+    const int r = rp + 2 * s;  // per lane
+    const float cs = rp ? -1.0f : 1.0f, sg = s ? -1.0f : 1.0f;
+    const float2 w = make_float2(rp ? 0.0f : sg, rp ? sg : 0.0f);  // (-1)^s i^rp
+    const float4* src = src_images + ((size_t)img << (2 * LOGN)) + (size_t)xb * B;
+    const int voff = ((i << LOGN) + c) * 16;
+    CPair v[16];
+#pragma unroll
+    for (int m = 0; m < 16; m++)
+    {
+      CPair x[R];
+#pragma unroll
+      for (int j = 0; j < R; j++)
+      {
+        const unsigned row = (unsigned)((m * T + j * M + N / 2) & (N - 1));
+        x[j] = to_pair(ld4<LA>(src, (int)((unsigned)voff + (row << (LOGN + 4))), -1));
+      }
+      const f2v cc = {cs, cs};
+      const CPair s02 = {x[0].re + cc * x[2].re, x[0].im + cc * x[2].im};
+      const CPair t13 = {x[1].re + cc * x[3].re, x[1].im + cc * x[3].im};
+      v[m] = cmul(s02 + cmul(t13, w), twiddle<LOGN>((i + m * T) * r, twn));
+      if ((m & 1) == 1)
+        asm volatile("" ::: "memory");
+    }
+    fft_run<P::LOGM, 4, true>(v, i, b4, xch, twm);  // v[m] = X[4 (i + m T) + r] of column c
+    // run (xb, r) = (xb, rp) + 2 s runs: a wave-uniform base, the residue's run in the lane offset
+    float4* dst = work + ((size_t)img << (2 * LOGN)) + (size_t)(xb * R + rp) * M * B;
+    const int soff = (i * B + c) * 16 + s * (2 * M * B * 16);
+#pragma unroll
+    for (int m = 0; m < 16; m++)
+      st4<kStream>(dst + m * T * B, soff, pair_raw(v[m]));
+  }
+}
+
+template <int LAR = 0>
+hipError_t launch_ifft_pre_pair14(int n_images, float4* images, float4* work, const float2* twn, const float2* twm,
+                                  hipStream_t stream, int cus)
+{
+  constexpr int LOGN = 14;
+  using S = FftShape<LOGN>;
+  using P = PreCfg;
+  {
+    auto kern = k_cols_pre_pair14<0>;
+    const int lds = P::TWM + tw_bytes<S::TW_ENTRIES>() + P::XCH;
+    const int grid = persistent_grid(kern, P::WG, lds, n_images * (S::N / 2) * 2, cus);
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(P::WG), lds, stream, n_images, images, work, twn, twm);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess)
+      return e;
+  }
+  auto kern = k_rows_final<LOGN, true, LAR, kStream, 1, 0, 4, 2, 4>;
+  const int lds = tw_bytes<S::TW_ENTRIES>() + lds_row_slots<LOGN>(1) * 8;
+  const SlabGeom g{0, S::N};
+  const int grid = persistent_grid(kern, S::T, lds, n_images * S::N, cus);
+  hipLaunchKernelGGL(kern, dim3(grid), dim3(S::T), lds, stream, n_images, g, work, images, (float*)nullptr,
+                     FoamParams{}, twn);
+  return hipGetLastError();
+}
+
 }  // namespace oceanfft

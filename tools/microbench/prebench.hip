@@ -144,10 +144,10 @@ int main(int argc, char** argv)
       runs.push_back([&] { return launch_ifft_pre_t<14, 0>(imgs, img, work, twn, twm, 0, cus); });
       names.push_back("pre-stage R=4, WL 1 (row-major work)");
       runs.push_back([&] { return launch_ifft_pre_t<14, 1>(imgs, img, work, twn, twm, 0, cus); });
-      names.push_back("pre-stage R=4, WL 0, column loads in batches of 4 points");
-      runs.push_back([&] { return launch_ifft_pre_t<14, 0, 0, kStream, 1, 4>(imgs, img, work, twn, twm, 0, cus); });
-      names.push_back("pre-stage R=4, WL 0, column loads in batches of 1 point");
-      runs.push_back([&] { return launch_ifft_pre_t<14, 0, 0, kStream, 1, 1>(imgs, img, work, twn, twm, 0, cus); });
+      names.push_back("pre-stage R=4, residue pairs on 2-column strips");
+      runs.push_back([&] { return launch_ifft_pre_pair14<0>(imgs, img, work, twn, twm, 0, cus); });
+      names.push_back("pre-stage R=4, residue pairs, streamed row loads");
+      runs.push_back([&] { return launch_ifft_pre_pair14<kStream>(imgs, img, work, twn, twm, 0, cus); });
     }
     // the four-step slab uses `work` as its slab (N x 2048 texels fit in the image-sized buffer)
     for (size_t k = 0; k < runs.size(); k++)

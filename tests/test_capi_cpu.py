@@ -69,6 +69,9 @@ def test_invalid_arguments_fail_without_touching_a_device(capi):
     assert L.ocean_fft_texture_resolution(None) == 0
     assert L.ocean_debug_hash(None, 4, None, None, None) == capi.OCEAN_ERR_INVALID
     assert L.ocean_fft_set_cu_budget(None, 0) == capi.OCEAN_ERR_INVALID
+    for switch in ("ocean_generator_set_frame_overlap", "ocean_generator_set_h0_memo",
+                   "ocean_generator_set_half_spectrum", "ocean_generator_set_four_step"):
+        assert getattr(L, switch)(None, 1) == capi.OCEAN_ERR_INVALID, switch
 
 
 def test_no_cpu_fallback_without_gpu(capi):

@@ -590,7 +590,8 @@ def slab_grid(args, rank: int, world: int, local: int) -> dict:
     With an exchange, serial frames (columns, all-to-all, rows) and pipelined frames (frame f's
     all-to-all beside frame f+1's column pass and frame f-1's row pass, passes sized for all CUs but
     --slab-reserve-cus) are timed; the headline is the better of the two. The all-to-all alone is timed
-    with torch's all_to_all_single of the same size (the achieved per-rank exchange rate)."""
+    through the library's ocean_comm_all_to_all (torch's all_to_all_single in the gloo rehearsal): the
+    achieved per-rank exchange rate."""
     import torch
     import torch.distributed as dist
 
@@ -607,11 +608,25 @@ def slab_grid(args, rank: int, world: int, local: int) -> dict:
     if args.full_spectrum:
         g.set_half_spectrum(False)
     comm, native_error = None, None
+
+    def all_ranks_ok(ok: bool) -> bool:
+        """every rank's verdict (MIN over ranks): no rank switches exchange path alone"""
+        if world == 1:
+            return ok
+        t = torch.tensor([1 if ok else 0], dtype=torch.int32, device=device)
+        dist.all_reduce(t, op=dist.ReduceOp.MIN)
+        return bool(t.item())
+
     if native:
         try:
             comm = RcclComm(rank, world, torch_share_id)
         except Exception as e:  # reported; the exchange then runs through torch.distributed
-            native, native_error = False, f"{type(e).__name__}: {e}"
+            native_error = f"{type(e).__name__}: {e}"
+        if not all_ranks_ok(comm is not None):
+            if comm is not None:
+                comm.close()
+                native_error = native_error or "another rank could not create its RCCL communicator"
+            native, comm = False, None
 
     def timed(run_steps):
         sync()
@@ -638,15 +653,20 @@ def slab_grid(args, rank: int, world: int, local: int) -> dict:
             ex()
             g.rows_pass(ex.recv.data_ptr())
 
+    first_error = None
     try:
         frame(1.0 / 60.0, update=True)  # seeds this rank's h0 columns
     except Exception as e:
         if comm is None:
             raise
-        # the library's exchange failed on this node: fall back to torch.distributed's all-to-all
-        native, native_error, comm = False, f"{type(e).__name__}: {e}", None
-        ex = TorchExchange(g.exchange_bytes, device)
-        frame(1.0 / 60.0, update=True)
+        first_error = f"{type(e).__name__}: {e}"
+    if comm is not None and not all_ranks_ok(first_error is None):
+        # The library's exchange failed on some rank. The frame is enqueued asynchronously, so a rank
+        # whose own call succeeded may hold sends its failed peer never matches: no rank falls back to
+        # torch alone (the all-reduce above makes every rank take the same branch), and the leg ends
+        # here with the error rather than waiting in RCCL.
+        raise RuntimeError("slab leg: the library's RCCL exchange failed on a rank: " +
+                           (first_error or "(on another rank)"))
     frame(1.0 / 60.0)
     g.set_profiling(True)
     g.kernel_times()
@@ -679,18 +699,28 @@ def slab_grid(args, rank: int, world: int, local: int) -> dict:
         out["native_exchange_error"] = native_error
         out["exchange"] = f"{dist.get_backend()} all_to_all_single (torch.distributed; the library's exchange failed)"
     if exchange:
-        # the all-to-all alone (no passes): the achieved per-rank exchange rate over xGMI
-        xo = ex if ex is not None else TorchExchange(g.exchange_bytes, device)
+        # the all-to-all alone (no passes): the achieved per-rank exchange rate over xGMI, through the
+        # library's own exchange (ocean_comm_all_to_all on the C ABI) when it runs the frames
+        if comm is not None:
+            xo = TorchExchange(g.exchange_bytes, device)  # buffers only
+            stream = torch.cuda.current_stream(device).cuda_stream
+            run_exchange = lambda: comm.all_to_all(xo.send.data_ptr(), xo.recv.data_ptr(), g.exchange_bytes,  # noqa: E731
+                                                   stream)
+            out["exchange_only_via"] = "ocean_comm_all_to_all (C ABI, grouped ncclSend / ncclRecv)"
+        else:
+            xo = ex if ex is not None else TorchExchange(g.exchange_bytes, device)
+            run_exchange = xo
+            out["exchange_only_via"] = f"torch.distributed all_to_all_single ({dist.get_backend()})"
 
         def exchange_steps():
             for _ in range(per):
-                xo()
+                run_exchange()
 
         el = timed(exchange_steps)
         out["exchange_only_ms"] = 1000.0 * el / per
         moved = g.exchange_bytes * (world - 1) // world if world > 1 else g.exchange_bytes
         out["exchange_GBps_per_rank"] = moved / (el / per) / 1e9
-        del xo
+        del xo, run_exchange
     del ex
     torch.cuda.empty_cache()
 
@@ -732,57 +762,151 @@ def slab_grid(args, rank: int, world: int, local: int) -> dict:
     return out
 
 
+# MI355X xGMI: 7 Infinity Fabric links per GPU at 153.6 GB/s each, counted over both directions
+# (SURVEY.md §7 "≈7×153 GB/s ≈ 1.07 TB/s" aggregate), i.e. 76.8 GB/s per link and direction. In the
+# 8-GPU all-to-all every peer pair has its own link, so one rank's sends leave over 7 links at once.
+XGMI_LINKS = 7
+XGMI_LINK_GBS_BIDIR = 153.6
+XGMI_ONE_WAY_GBS = XGMI_LINKS * XGMI_LINK_GBS_BIDIR / 2.0  # 537.6 GB/s per rank, one direction
+
+
 def p8_rank_projection(args, one_gpu_frame_ms: float, ranks: int = 8) -> dict:
-    """The per-rank cost of BASELINE configs[4] (the 16384^2 grid over 8 GPUs) measured on ONE GPU:
-    all 8 ranks' SlabGenerators in this process, frames emulated with the equal-split all-to-all as
-    device copies (oceansimulation_amd.slab.emulate_frame), each rank's column and row passes timed with
-    HIP events on their stream. On 8 GPUs every rank runs the same kernels on its own device, so
-    max(passes) bounds the pipelined 8-GPU frame from below when the exchange hides behind it; the
-    exchange itself is not measurable here (one device), so its bytes and the xGMI rate that would
-    hide it are reported instead."""
+    """The per-rank cost of BASELINE configs[4] (the 16384^2 grid over 8 GPUs) measured on ONE GPU, and
+    the 8-GPU frame it implies. All 8 ranks' SlabGenerators run in this process on one compute stream;
+    frames are emulated with the equal-split all-to-all as device copies (slab.emulate_frame) and each
+    rank's column and row passes are timed with HIP events on that stream, three ways:
+      1. on all CUs;
+      2. under the CU budget the pipelined 8-GPU path uses (all but --slab-reserve-cus, left to RCCL);
+      3. under that budget with the rank's exchange volume moved concurrently through the C ABI's own
+         exchange (ocean_comm_all_to_all over a one-rank RCCL communicator: RCCL's kernels reading and
+         writing the same bytes in HBM that the 8-rank exchange reads from and writes into this GPU's
+         HBM), issued beside each rank's passes on a second stream, as the pipelined frame issues
+         frame f's exchange beside frame f+1's column pass and frame f-1's row pass.
+    The xGMI leg itself cannot run on one GPU: it is priced at XGMI_ONE_WAY_GBS (stated source above).
+    The 8-GPU frame is bounded below by max(passes under contention, exchange at that rate); the
+    projected speed-up is the one-GPU frame over that bound."""
+    import torch
+
     import oceansimulation_amd as ocean
     from oceansimulation_amd.hip import DeviceBuffer
-    from oceansimulation_amd.slab import SlabGenerator, emulate_frame
+    from oceansimulation_amd.slab import RcclComm, SlabGenerator, emulate_frame
 
-    n, dt = args.slab_n, 1.0 / 60.0
-    fft = ocean.FFTCalculator(n)
+    n, dt, steps = args.slab_n, 1.0 / 60.0, args.slab_steps
+    comp = torch.cuda.Stream()  # the generators' stream (non-blocking, so the exchange stream runs beside it)
+    side = torch.cuda.Stream()
+    fft = ocean.FFTCalculator(n, stream=comp.cuda_stream)
     slabs = [SlabGenerator(fft, r, ranks) for r in range(ranks)]
+    xbytes = slabs[0].exchange_bytes
     sends = [DeviceBuffer(g.exchange_bytes) for g in slabs]
     recvs = [DeviceBuffer(g.exchange_bytes) for g in slabs]
-    try:
-        emulate_frame(slabs, sends, recvs, dt, update_ocean=True)
-        emulate_frame(slabs, sends, recvs, dt)
+    xdst = DeviceBuffer(xbytes)
+    comm = None
+    reserve = max(0, min(args.slab_reserve_cus, fft.cus - 1))
+
+    def passes(contend: bool):
+        """per-rank (column, row) pass ms over `steps` emulated frames, and the mean wall ms per rank frame"""
         for g in slabs:
             g.set_profiling(True)
             g.kernel_times()
-        for _ in range(args.slab_steps):
-            emulate_frame(slabs, sends, recvs, dt)
+        ev_go, ev_x = torch.cuda.Event(), torch.cuda.Event()
+        t0, t1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        torch.cuda.synchronize()
+        t0.record(comp)
+        for _ in range(steps):
+            for r, g in enumerate(slabs):
+                if contend:
+                    ev_go.record(comp)
+                    side.wait_event(ev_go)
+                    comm.all_to_all(sends[r].ptr, xdst.ptr, xbytes, side.cuda_stream)
+                    ev_x.record(side)
+                g.columns(dt, False, sends[r].ptr)
+                g.rows_pass(recvs[r].ptr)
+                if contend:
+                    comp.wait_event(ev_x)  # this rank's frame ends when both its passes and its exchange have
+        t1.record(comp)
+        torch.cuda.synchronize()
         cols, rows = [], []
         for g in slabs:
             ms, cnt = g.kernel_times()
+            g.set_profiling(False)
             cols.append(ms[1] / max(cnt[1], 1))
             rows.append(ms[2] / max(cnt[2], 1))
-        passes = [c + r for c, r in zip(cols, rows)]
-        worst = max(passes)
-        moved = slabs[0].exchange_bytes * (ranks - 1) // ranks
+        return cols, rows, t0.elapsed_time(t1) / (steps * ranks)
+
+    try:
+        emulate_frame(slabs, sends, recvs, dt, update_ocean=True)
+        emulate_frame(slabs, sends, recvs, dt)
+        torch.cuda.synchronize()
+        cols, rows, _ = passes(False)
+        fft.set_cu_budget(fft.cus - reserve)
+        cols_b, rows_b, _ = passes(False)
+        worst = max(c + r for c, r in zip(cols, rows))
+        worst_b = max(c + r for c, r in zip(cols_b, rows_b))
+        moved = xbytes * (ranks - 1) // ranks
         per_point = sum(slabs[0].frame_bytes())
         out = {
-            "what": f"{ranks} slab ranks of the single {n}x{n} grid emulated on one GPU (exchange as device copies, "
-                    "not timed); per-rank column pass (four-step, destination-block order) + row pass",
+            "what": f"{ranks} slab ranks of the single {n}x{n} grid emulated on one GPU (exchange as device copies); "
+                    "per-rank column pass (four-step, destination-block order) + row pass",
             "ranks": ranks,
             "column_pass_ms": cols,
             "row_pass_ms": rows,
             "passes_ms": worst,
-            "passes_ms_mean": sum(passes) / ranks,
+            "passes_ms_mean": sum(c + r for c, r in zip(cols, rows)) / ranks,
             "frac_hbm_peak": per_point * n * n / ranks / (worst * 1e-3) / 1e9 / HBM_PEAK_GBS,
             "frame_hbm_bytes_per_point": per_point,
             "one_gpu_frame_ms": one_gpu_frame_ms,
-            "projected_speedup_vs_1gpu": one_gpu_frame_ms / worst,
+            "passes_only_speedup_vs_1gpu": one_gpu_frame_ms / worst,
+            "reserved_cus": reserve,
+            "passes_budget_ms": worst_b,
+            "column_pass_budget_ms": cols_b,
+            "row_pass_budget_ms": rows_b,
             "exchange_bytes_per_rank": moved,
+            "exchange_local_hbm_bytes_per_rank": 2 * xbytes,
             "xgmi_GBps_per_rank_to_hide_exchange": moved / (worst * 1e-3) / 1e9,
+            "xgmi_rate_GBps_one_way": XGMI_ONE_WAY_GBS,
+            "xgmi_rate_source": f"{XGMI_LINKS} xGMI links x {XGMI_LINK_GBS_BIDIR} GB/s per link over both directions "
+                                "(SURVEY.md §7), so half of that per direction; every peer pair of the 8-GPU "
+                                "all-to-all on its own link",
+            "exchange_ms_at_rate": moved / (XGMI_ONE_WAY_GBS * 1e9) * 1e3,
         }
+        try:
+            comm = RcclComm(0, 1, lambda u: u)
+            # the exchange alone, through the C ABI (ocean_comm_all_to_all; at one rank RCCL's local copy)
+            comm.all_to_all(sends[0].ptr, xdst.ptr, xbytes, side.cuda_stream)
+            torch.cuda.synchronize()
+            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            a.record(side)
+            for _ in range(steps):
+                comm.all_to_all(sends[0].ptr, xdst.ptr, xbytes, side.cuda_stream)
+            b.record(side)
+            torch.cuda.synchronize()
+            out["exchange_only_ms_local"] = a.elapsed_time(b) / steps
+            out["exchange_only_what"] = ("ocean_comm_all_to_all of one rank's exchange bytes over a one-rank RCCL "
+                                         "communicator: RCCL's own kernels moving them HBM to HBM (no xGMI)")
+            cols_c, rows_c, frame_c = passes(True)
+            worst_c = max(c + r for c, r in zip(cols_c, rows_c))
+            out.update({
+                "column_pass_contended_ms": cols_c,
+                "row_pass_contended_ms": rows_c,
+                "passes_contended_ms": worst_c,
+                "rank_frame_contended_ms_mean": frame_c,
+            })
+        except Exception as e:  # reported; the projection then rests on the budgeted passes
+            out["contended_error"] = f"{type(e).__name__}: {e}"
+            worst_c = worst_b
+        bound = max(worst_c, out["exchange_ms_at_rate"])
+        out["frame_bound_ms"] = bound
+        out["bounding_term"] = "passes under contention" if worst_c >= out["exchange_ms_at_rate"] else \
+            "exchange at the xGMI rate"
+        out["projected_speedup_vs_1gpu"] = one_gpu_frame_ms / bound
+        out["projected_speedup_note"] = ("one-GPU frame / max(per-rank passes under the CU budget with the exchange's "
+                                         "HBM traffic concurrent, exchange bytes at the one-way xGMI rate): assumes the "
+                                         "pipelined frame overlaps the two perfectly")
     finally:
-        for b in sends + recvs:
+        fft.set_cu_budget(0)
+        if comm is not None:
+            comm.close()
+        for b in sends + recvs + [xdst]:
             b.free()
         for g in slabs:
             g.close()

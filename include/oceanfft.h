@@ -211,7 +211,10 @@ typedef struct ocean_comm ocean_comm;
 int ocean_comm_unique_id(unsigned char id[OCEAN_COMM_ID_BYTES]);
 /* ncclCommInitRank(nranks, id, rank) on the current device; collective over the nranks processes. */
 int ocean_comm_create(ocean_comm** out, const unsigned char id[OCEAN_COMM_ID_BYTES], int nranks, int rank);
-/* Use a communicator the caller already has (an ncclComm_t; not destroyed by ocean_comm_destroy). */
+/* Use a communicator the caller already has (an ncclComm_t; not destroyed by ocean_comm_destroy).
+ * nranks / rank must be the communicator's own (ncclCommCount / ncclCommUserRank), else
+ * OCEAN_ERR_INVALID. A communicator must outlive every generator whose frames used it: destroying
+ * a generator drains its exchange stream but does not issue a pending pipelined frame's row pass. */
 int ocean_comm_wrap(ocean_comm** out, void* nccl_comm, int nranks, int rank);
 int ocean_comm_destroy(ocean_comm* comm);
 /* The equal-split all-to-all of caller device buffers over the communicator (bytes / nranks to each

@@ -137,6 +137,7 @@ struct ocean_generator
   bool rows_recorded[2] = {false, false};
   int pending_slot = -1;           // slot whose row pass is still to be issued
   FrameParams slot_frame[2]{};     // the column pass's per-cascade values of the frame in each slot
+  FoamParams slot_foam[2]{};       // and the settings' displacement its row pass uses
   int64_t frames_issued = 0;
   // ocean_generator_set_frame_overlap (blocked half path): frame f's column pass on `side` into field
   // slot f % 2, beside frame f - 1's row pass on the generator's stream
@@ -546,7 +547,19 @@ static int generator_alloc(ocean_generator** out, ocean_fft* fft, int cascades, 
   g->hslab = !g->half && half_slab_supported(fft->logn) && (is_slab || fft->logn > 12);
   g->hsl = half_slab_geom(fft->logn, rank, ranks);
   if (gen4_supported(fft->logn))
+  {
     g->g4 = gen4_geom(fft->logn, cascades, rank, ranks, ranks == 1);
+    // one h0 cascade stride for every writer and reader (generate_spectrum_with, k_gen4,
+    // ocean_generator_initial_spectrum): the largest of the layouts, as allocated
+    g->g4.h0_cstride = h0_texels(g);
+  }
+  // the strip-dealt column pass reads cascade c's strips at (c * nstrips + s) * N * B, which equals
+  // h0_texels(g) * c only for one cascade: slabs are single-grid (ocean_generator_create_slab)
+  if (is_slab && cascades != 1)
+  {
+    delete g;
+    return fail(OCEAN_ERR_INVALID, "generator allocation: a slab generator holds exactly one cascade");
+  }
   hipError_t e = hipMalloc(&g->h0, h0_texels(g) * cascades * sizeof(float4));
   if (e == hipSuccess && !g->half && !g->hslab)
     e = full_buffers(g);
@@ -605,6 +618,10 @@ int ocean_generator_destroy(ocean_generator* g)
 {
   if (!g)
     return OCEAN_OK;
+  // A pipelined slab frame still in flight: its exchange may be running on comm_stream (the
+  // communicator must outlive the generator, include/oceanfft.h). Drain it before the slots go.
+  if (g->comm_stream)
+    (void)hipStreamSynchronize(g->comm_stream);
   if (g->fft)
     (void)hipStreamSynchronize(g->fft->stream);
   for (auto& p : g->pending)
@@ -892,13 +909,20 @@ static int generator_columns(ocean_generator* g, float timestep, int update_spec
   return OCEAN_OK;
 }
 
-// Second half: the x direction of both EncodeIFFTs + computeFoam (src/Generator.cpp:71-80).
-static int generator_rows(ocean_generator* g, const float4* in)
+static FoamParams current_foam(const ocean_generator* g)
 {
-  ocean_fft* f = g->fft;
   FoamParams foam{};
   for (int c = 0; c < g->cascades; c++)
     foam.displacement[c] = g->settings[c].displacement;
+  return foam;
+}
+
+// Second half: the x direction of both EncodeIFFTs + computeFoam (src/Generator.cpp:71-80). `frame_foam`:
+// the displacement of a pipelined slab frame's own settings (null: the current settings).
+static int generator_rows(ocean_generator* g, const float4* in, const FoamParams* frame_foam = nullptr)
+{
+  ocean_fft* f = g->fft;
+  const FoamParams foam = frame_foam ? *frame_foam : current_foam(g);
   if (uses_gen4(g))
     HIP_TRY(timed(g, 2, [&] {
               return launch_gen4_rows(f->logn, g->frame, g->g4, in ? (const void*)in : (const void*)g->xbuf, g->maps,
@@ -945,6 +969,14 @@ int ocean_generator_set_half_spectrum(ocean_generator* g, int enable)
 {
   if (!g)
     return fail(OCEAN_ERR_INVALID, "ocean_generator_set_half_spectrum: null generator");
+  if (g->pending_slot >= 0)
+  {
+    // a pipelined slab frame's column pass wrote its blocks in the current path's layout: its row
+    // pass runs before the switch
+    const int rc = ocean_generator_slab_flush(g);
+    if (rc != OCEAN_OK)
+      return rc;
+  }
   if (!enable && g->overlap)
   {
     const int rc = ocean_generator_set_frame_overlap(g, 0);
@@ -1041,6 +1073,12 @@ int ocean_generator_set_four_step(ocean_generator* g, int enable)
 {
   if (!g)
     return fail(OCEAN_ERR_INVALID, "ocean_generator_set_four_step: null generator");
+  if (g->pending_slot >= 0)
+  {
+    const int rc = ocean_generator_slab_flush(g);  // as in ocean_generator_set_half_spectrum
+    if (rc != OCEAN_OK)
+      return rc;
+  }
   g->four_step = enable != 0;  // h0 is re-laid out by the next frame if its strip width changes
   if (g->hslab)
   {
@@ -1223,7 +1261,7 @@ int slot_rows(ocean_generator* g, int s)
   HIP_TRY(hipStreamWaitEvent(f->stream, g->xchg_done[s], 0), "slab frame: wait for the exchange");
   const FrameParams newest = g->frame;
   g->frame = g->slot_frame[s];
-  const int rc = generator_rows(g, reinterpret_cast<const float4*>(g->xrecv[s]));
+  const int rc = generator_rows(g, reinterpret_cast<const float4*>(g->xrecv[s]), &g->slot_foam[s]);
   g->frame = newest;
   if (rc != OCEAN_OK)
     return rc;
@@ -1241,6 +1279,7 @@ int slot_columns_and_exchange(ocean_generator* g, ocean_comm* c, float timestep,
   if (rc != OCEAN_OK)
     return rc;
   g->slot_frame[s] = g->frame;
+  g->slot_foam[s] = current_foam(g);
   HIP_TRY(hipEventRecord(g->cols_done[s], f->stream), "slab frame: events");
   HIP_TRY(hipStreamWaitEvent(g->comm_stream, g->cols_done[s], 0), "slab frame: stream order");
   if (g->rows_recorded[s])  // frame f - 2's row pass has finished reading recv[s]
@@ -1298,8 +1337,21 @@ int ocean_comm_wrap(ocean_comm** out, void* nccl_comm, int nranks, int rank)
 {
   if (!out || !nccl_comm || nranks < 1 || rank < 0 || rank >= nranks)
     return fail(OCEAN_ERR_INVALID, "ocean_comm_wrap: null argument or rank outside [0, nranks)");
+  *out = nullptr;
+  // the exchange addresses peers by these values: they must be the communicator's own
+  const ncclComm_t nc = static_cast<ncclComm_t>(nccl_comm);
+  int count = 0, user_rank = 0;
+  ncclResult_t r = ncclCommCount(nc, &count);
+  if (r == ncclSuccess)
+    r = ncclCommUserRank(nc, &user_rank);
+  if (r != ncclSuccess)
+    return nccl_fail(r, "ocean_comm_wrap: ncclCommCount / ncclCommUserRank");
+  if (count != nranks || user_rank != rank)
+    return fail(OCEAN_ERR_INVALID, "ocean_comm_wrap: the communicator is rank " + std::to_string(user_rank) + " of " +
+                                       std::to_string(count) + ", not rank " + std::to_string(rank) + " of " +
+                                       std::to_string(nranks));
   auto* c = new ocean_comm();
-  c->comm = static_cast<ncclComm_t>(nccl_comm);
+  c->comm = nc;
   c->nranks = nranks;
   c->rank = rank;
   *out = c;

@@ -314,6 +314,46 @@ def test_native_rccl_slab_frames_world1_bit_exact(ocean, n):
     fft.close()
 
 
+@pytest.mark.gpu
+def test_path_switch_lands_pending_pipelined_frame(ocean):
+    """A path switch with a pipelined slab frame in flight (ocean_generator_set_four_step) first issues
+    that frame's row pass in the layout its column pass wrote, with the displacement of the settings it
+    was issued with (a later edit must not leak into its Jacobian); frames after the switch run the
+    strip-dealt path. Both are checked bit for bit against the whole-grid generator on the same path."""
+    from oceansimulation_amd import capi
+    from oceansimulation_amd.slab import RcclComm, SlabGenerator
+
+    n = 8192
+    fft = ocean.FFTCalculator(n)
+    whole = ocean.Generator(fft, 1)
+    g = SlabGenerator(fft, 0, 1)
+    for x in (whole.GetOceanSettings(0), g.GetOceanSettings()):
+        ocean.apply_settings(x, planeSize=333.0)
+    comm = RcclComm(0, 1, lambda uid: uid)
+    L = capi.lib()
+
+    def same():
+        fft.synchronize()
+        return all(_dev_equal(int(get(g.handle, 0)), int(get(whole.handle, 0)), n * n * tex)
+                   for get, tex in ((L.ocean_generator_height_map, 16), (L.ocean_generator_displacement_map, 16),
+                                    (L.ocean_generator_jacobian_map, 4)))
+
+    g.frame_pipelined(comm, 0.25, update_ocean=True)  # pending: four-step blocks, displacement 0.4
+    ocean.apply_settings(g.GetOceanSettings(), displacement=0.9)
+    g.set_four_step(False)  # lands the pending frame first
+    whole.CalculateOcean(0.25)
+    assert same(), "pending frame after the switch"
+    whole.set_four_step(False)
+    ocean.apply_settings(whole.GetOceanSettings(0), displacement=0.9)
+    g.frame(comm, 0.1)
+    whole.CalculateOcean(0.1)
+    assert same(), "strip-dealt frame after the switch"
+    comm.close()
+    g.close()
+    whole.close()
+    fft.close()
+
+
 # ---- bench.py --gpus N on a one-GPU box ---------------------------------------------------------
 def test_bench_gpus_two_shared_gpu_reports_two_ranks(tmp_path):
     """`bench.py --gpus 2 --shared-gpu` (no launcher) starts 2 ranks under torch.distributed.run,

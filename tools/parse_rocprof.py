@@ -45,10 +45,20 @@ def first_arg(symbol):
     return s.split("<", 1)[1].split(",")[0].split(">")[0].strip() if "<" in s else None
 
 
+def template_args(symbol):
+    s = symbol.split("(")[0]
+    return [a.strip() for a in s.split("<", 1)[1].rsplit(">", 1)[0].split(",")] if "<" in s else []
+
+
 def size_key(symbol, logn):
     """The summary key: the base name for instantiations at the workload's log2 N (what bench.py
-    looks up), else base<first template argument> (other sizes: k_rows_half<14>, k_gen4_step2<10>)."""
+    looks up), else base<first template argument> (other sizes: k_rows_half<14>). k_gen4_step2 runs
+    three launches per frame, two over 16-B field texels (second argument true: gab, gde) and one
+    over gc's 8-B texels as column pairs (false), so its key carries both arguments."""
     first = first_arg(symbol)
+    if base_name(symbol) == "k_gen4_step2":
+        args = template_args(symbol)
+        return f"k_gen4_step2<{args[0]},{args[1]}>"
     return base_name(symbol) if first in (None, str(logn)) else f"{base_name(symbol)}<{first}>"
 
 
@@ -61,11 +71,20 @@ def algorithmic_bytes(key, n, cascades, mode):
     logn = n.bit_length() - 1
     if mode == "ifft":  # standalone EncodeIFFT: work-image chunks of 8 images, 32 B per texel per pass;
         # the bench's 8192 leg (2 images per call, one launch per pass: the pre-stage column pass and its row pass)
+        # the 16384 leg (2 images per call): rows in place over both images in one launch, then per
+        # image and 2048-column work slab one step-1 launch (image -> slab) and one step-2 launch (slab
+        # -> image), each reading and writing its 16384 x 2048 texels once (launch_ifft_fourstep)
         return {"k_cols_to_blocks": 32 * 8 * n * n, "k_rows_final": 32 * 8 * n * n,
-                "k_cols_pre<13>": 32 * 2 * 8192 ** 2, "k_rows_final<13>": 32 * 2 * 8192 ** 2}.get(key)
+                "k_cols_pre<13>": 32 * 2 * 8192 ** 2, "k_rows_final<13>": 32 * 2 * 8192 ** 2,
+                "k_rows_ifft<14>": 32 * 2 * 16384 ** 2, "k_cols4_step1<14>": 32 * 16384 * 2048,
+                "k_cols4_step2<10>": 32 * 16384 * 2048}.get(key)
     if logn in (13, 14):  # four-step whole grid: kept columns [0, N/2) + the Nyquist column
         kept = (n // 2 + 1) / n
-        table = {"k_gen4_step1": (16 + 40) * kept, "k_rows_xs": 40 * kept + 36, "k_rows_half": 40 * kept + 36}
+        # step 2 (the N/16-point step) reads step 1's parts and writes the row pass's fields, one launch
+        # per field: gab and gde 16 + 16 per kept texel each, gc 8 + 8 (40 + 40 in all)
+        table = {"k_gen4_step1": (16 + 40) * kept, f"k_gen4_step2<{logn - 4},true>": 32 * kept,
+                 f"k_gen4_step2<{logn - 4},false>": 16 * kept,
+                 "k_rows_xs": 40 * kept + 36, "k_rows_half": 40 * kept + 36}
     else:
         kept = (n // 2 + 4) / n  # columns [0, N/2) plus the 4-wide Nyquist strip
         table = {"k_cols_evolve": 48, "k_rows_final": 68, "k_cols_half": (16 + 40) * kept,

@@ -1,0 +1,192 @@
+// device/k_rows_hp.h — the half-spectrum row pass of whole 4096^2 grids (blocked field layout) with
+// the x transform split 16 x 256: one LDS transposition T_in that also does the mirror exchange, the
+// 256-point sub-transforms inside the wave (lane_xchg.h: v_permlane16/32_swap + DPP), a second
+// transposition T_out, a 16-point DFT in registers. Production k_rows_half moves the -u lanes through
+// the LDS, then runs fft_run<12> with two split exchanges: 2.5 LDS round trips and 10 barriers per
+// image against 2 and 7 here.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "ocean_internal.h"
+#include "device/fft.h"
+#include "device/grid.h"
+#include "device/k_half_cols.h"
+#include "device/lane_xchg.h"
+#include "device/memory.h"
+
+namespace oceanfft
+{
+
+// x index n = n1 + 16 n2 (n1 < 16, n2 < 256), output k = k2 + 256 k1:
+//   X(k2 + 256 k1) = sum_n1 W_16^(n1 k1) [W_N^(n1 k2) Y_n1(k2)],  Y_n1(k2) = sum_n2 x(n1 + 16 n2) W_256^(n2 k2).
+// LDS slot of (n1, j), 8-B halves: n1 RS + (j ^ ((n1 >> 2) & 3)), RS = 4 (mod 16), as k_rows_xp.
+struct HpCfg
+{
+  static constexpr int LOGN = 12, RS = 260;
+  static constexpr int TW = ((FftShape<LOGN>::TW_ENTRIES * 8 + 15) / 16) * 16;
+  static constexpr int LDS = TW + 16 * RS * 8;
+};
+
+__device__ __forceinline__ int hp_slot(int n1, int j) { return n1 * HpCfg::RS + (j ^ ((n1 >> 2) & 3)); }
+
+// One row (both images; C loaded once, kept for image 1) per 256-thread workgroup, four per CU, the
+// 4 rows of a gc line on one XCD; default-policy loads, streamed stores (production k_rows_half's
+// item shape at 4096).
+//   T_in: thread (w, s, p) = (tid >> 6, tid & 3, (tid >> 2) & 15) receives x(n1 + 16 (p + 16 m)),
+//         n1 = 4 w + s (four 256-point sub-transforms per wave).
+//   sub-transform as k_rows_xp: v[b] = Y_n1(p + 16 b), then x W_N^(n1 (p + 16 b)).
+//   T_out: thread k2 = tid receives Z_n1(k2), n1 < 16; DFT-16: v[k1] = X(tid + 256 k1).
+template <int RG, int RGC>
+__global__ __launch_bounds__(256, 4) void k_rows_hp(FrameParams fp, const float4* __restrict__ gab,
+                                                 const float4* __restrict__ gde, const float2* __restrict__ gc,
+                                                 const float4* __restrict__ spec, float4* __restrict__ maps,
+                                                 float* __restrict__ jac, FoamParams foam,
+                                                 const float2* __restrict__ tw_glob)
+{
+  constexpr int LOGN = HpCfg::LOGN, RS = HpCfg::RS;
+  using S = FftShape<LOGN>;
+  using HC = HalfCfg<LOGN>;
+  constexpr int N = S::N, T = S::T, B = 4, STRIPS = HC::STRIPS;
+  static_assert(T == 256, "one 4-wave row per workgroup");
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  float2* tw = reinterpret_cast<float2*>(smem);
+  float2* xs = reinterpret_cast<float2*>(smem + HpCfg::TW);
+  load_twiddles<LOGN>(tw, tw_glob);
+
+  const int total = fp.cascades * N;
+  const float dim = (float)N;
+  for (int item = xcd_group_slot<4>(blockIdx.x, gridDim.x); item < total; item += gridDim.x)
+  {
+    const int c = item / N, y = item - c * N;
+    const float dk = fp.c[c].dk;
+    const size_t base = (size_t)c * STRIPS * N * B;
+    const float sgy = (y & 1) ? -1.0f : 1.0f;
+    float2 ckeep[8], cnyq;
+#pragma unroll
+    for (int img = 0; img < 2; img++)
+    {
+      const int cimg = c * 2 + img;
+      const float4* sp = spec + (size_t)cimg * N;
+      const int tid = opaque((int)threadIdx.x), i = tid;
+      CPair v[16];  // own lanes in v[m], the -u lanes in v[m + 8] until T_in
+#pragma unroll
+      for (int m = 0; m < 8; m++)
+      {
+        const int u = m * T + i;
+        const int off = half_group_offset<LOGN, RG>(y, u / B, u % B);
+        const int offc = half_group_offset<LOGN, RGC>(y, u / B, u % B);
+        const float kx = (float)u * dk;
+        const float4 s4 = ld4<0>(sp, (N / 2 - u) * 16);
+        if (img == 0)
+        {
+          const CPair p = raw_pair(ld4<0>(gab + base, off * 16));
+          const float2 cc = ld2<0>(gc + base, offc * 8);
+          ckeep[m] = cc;
+          const float Ar = p.re.x, Ai = p.im.x, Br = p.re.y, Bi = p.im.y, Cr = cc.x, Ci = cc.y;
+          v[m] = CPair{f2v{(1.0f - kx) * Ar, -Bi - kx * Cr}, f2v{(1.0f - kx) * Ai, Br - kx * Ci}};
+          v[m + 8] = CPair{f2v{(1.0f + kx) * Ar + sgy * s4.x, -Bi + kx * Cr + sgy * s4.z},
+                           f2v{-(1.0f + kx) * Ai + sgy * s4.y, -Br - kx * Ci + sgy * s4.w}};
+        }
+        else
+        {
+          const CPair q = raw_pair(ld4<0>(gde + base, off * 16));
+          const float2 cc = ckeep[m];
+          const float Cr = cc.x, Ci = cc.y, Dr = q.re.x, Di = q.im.x, Er = q.re.y, Ei = q.im.y;
+          const float kx2 = kx * kx;
+          v[m] = CPair{f2v{-(Di - kx2 * Ci), -Er + kx * Di}, f2v{Dr - kx2 * Cr, -Ei - kx * Dr}};
+          v[m + 8] = CPair{f2v{-(Di + kx2 * Ci) + sgy * s4.x, -Er - kx * Di + sgy * s4.z},
+                           f2v{-Dr - kx2 * Cr + sgy * s4.y, Ei - kx * Dr + sgy * s4.w}};
+        }
+      }
+      if (i == 0)
+      {
+        // the Nyquist column u = -N/2 (first column of the last strip) replaces the unused -u lane of u = 0
+        const int off = half_group_offset<LOGN, RG>(y, N / 2 / B);
+        const int offc = half_group_offset<LOGN, RGC>(y, N / 2 / B);
+        const float kx = -(dim / 2.0f) * dk;
+        if (img == 0)
+          cnyq = ld2<0>(gc + base, offc * 8);
+        const float2 cc = cnyq;
+        if (img == 0)
+        {
+          const CPair p = raw_pair(ld4<0>(gab + base, off * 16));
+          v[8] = CPair{f2v{(1.0f - kx) * p.re.x, -p.im.y - kx * cc.x}, f2v{(1.0f - kx) * p.im.x, p.re.y - kx * cc.y}};
+        }
+        else
+        {
+          const CPair q = raw_pair(ld4<0>(gde + base, off * 16));
+          const float kx2 = kx * kx;
+          v[8] = CPair{f2v{-(q.im.x - kx2 * cc.y), -q.re.y + kx * q.im.x}, f2v{q.re.x - kx2 * cc.x, -q.im.y - kx * q.re.x}};
+        }
+      }
+      // ---- T_in (own lanes at n = i + m T, the -u lanes at N - n, thread 0's v[8] at N/2)
+      const int w = tid >> 6, l = tid & 63, s = l & 3, p = l >> 2;
+      const int n1r = 4 * w + s;
+      const int rd = n1r * RS + (p ^ (w & 3));  // + 16 m: x(n1r + 16 (p + 16 m))
+      const int wo = hp_slot(i & 15, i >> 4);   // + 16 m
+      const int nm = N - i;
+      const int wm = hp_slot(nm & 15, nm >> 4);  // - 16 m
+      const int wm0 = i == 0 ? hp_slot(0, (N / 2) >> 4) : wm;
+      __syncthreads();  // the previous image's T_out reads are done
+#pragma unroll
+      for (int h = 0; h < 2; h++)
+      {
+        if (h)
+          __syncthreads();
+#pragma unroll
+        for (int m = 0; m < 8; m++)
+        {
+          xs[wo + 16 * m] = half_of(v[m], h);
+          xs[(m == 0 ? wm0 : wm) - 16 * m] = half_of(v[m + 8], h);
+        }
+        __syncthreads();
+#pragma unroll
+        for (int m = 0; m < 16; m++)
+          set_half(v[m], h, xs[rd + 16 * m]);
+      }
+      // ---- the 256-point sub-transform of n1r in the wave's registers
+      idft16(v);
+      apply_stage_twiddles<LOGN>(v, 16 * p, tw);  // x W_256^(p a) = W_N^(16 p a)
+      transpose_reg_lanes_2_5(v);
+      idft16(v);                                  // v[b] = Y_n1r(p + 16 b)
+      const float2 base_w = twiddle<LOGN>(n1r * p, tw);
+#pragma unroll
+      for (int m = 0; m < 16; m++)
+        v[m] = cmul(v[m], base_w);
+      apply_stage_twiddles<LOGN>(v, 16 * n1r, tw);  // x W_N^(n1r (p + 16 b))
+      // ---- T_out: thread k2 = tid gathers Z_n1(k2)
+#pragma unroll
+      for (int h = 0; h < 2; h++)
+      {
+        if (h)
+          __syncthreads();
+#pragma unroll
+        for (int m = 0; m < 16; m++)
+          xs[rd + 16 * m] = half_of(v[m], h);
+        __syncthreads();
+#pragma unroll
+        for (int n1 = 0; n1 < 16; n1++)
+          set_half(v[n1], h, xs[n1 * RS + (tid ^ ((n1 >> 2) & 3))]);
+      }
+      idft16(v);  // v[k1] = X(tid + T k1)
+      float4* dst = maps + ((size_t)cimg * N + y) * N;
+#pragma unroll
+      for (int m = 0; m < 16; m++)
+        st4<kStream>(dst + m * T, tid * 16, from_pair(v[m]));
+      if (img == 1)
+      {
+        const float lam = foam.displacement[c];
+        float* jb = jac + ((size_t)c * N + y) * N;
+#pragma unroll
+        for (int m = 0; m < 16; m++)
+          st1<kStream>(jb + m * T, tid * 4,
+                       (1.0f + lam * v[m].im.x) * (1.0f + lam * v[m].re.y) - lam * lam * v[m].im.y * v[m].im.y);
+      }
+    }
+  }
+}
+
+}  // namespace oceanfft

@@ -190,6 +190,57 @@ int main(int argc, char** argv)
     std::printf("rows, row layout (round 1)              median %7.3f ms  bit-identical %s\n", tr[1][4], same ? "yes" : "NO");
     return 0;
   }
+  if (argc > 3 && std::strcmp(argv[3], "hp") == 0 && logn == 12)
+  {
+    // row pass: production (k_rows_half, mirror exchange + fft_run<12>) against k_rows_hp (T_in with
+    // the mirror, 256-point sub-transforms in the wave through permlane / DPP swaps, T_out). Different
+    // radix order, so the maps agree to rounding, not bit for bit.
+    CHECK(c1());
+    CHECK(r1());
+    CHECK(hipDeviceSynchronize());
+    auto pm = snap(maps, mb), pj = snap(jac, jb);
+    CHECK(hipMemset(maps, 0, mb));
+    CHECK(hipMemset(jac, 0, jb));
+    auto hpk = k_rows_hp<kHalfRG, kHalfRGC>;
+    CHECK(hipFuncSetAttribute((const void*)hpk, hipFuncAttributeMaxDynamicSharedMemorySize, HpCfg::LDS));
+    const int hgrid = persistent_grid(hpk, 256, HpCfg::LDS, C * n, cus);
+    auto rhp = [&] {
+      hipLaunchKernelGGL(hpk, dim3(hgrid), dim3(256), HpCfg::LDS, 0, fp, gab, gcd, ge, spec, maps, jac, foam, tw);
+      return hipGetLastError();
+    };
+    CHECK(rhp());
+    CHECK(hipDeviceSynchronize());
+    const auto hm = snap(maps, mb), hj = snap(jac, jb);
+    const float* a = reinterpret_cast<const float*>(pm.data());
+    const float* b = reinterpret_cast<const float*>(hm.data());
+    double dm = 0, am = 0;
+    for (size_t k = 0; k < mb / 4; k++)
+    {
+      dm = std::max(dm, (double)std::fabs(a[k] - b[k]));
+      am = std::max(am, (double)std::fabs(a[k]));
+    }
+    const float* ja = reinterpret_cast<const float*>(pj.data());
+    const float* jb2 = reinterpret_cast<const float*>(hj.data());
+    double dj = 0, aj = 0;
+    for (size_t k = 0; k < jb / 4; k++)
+    {
+      dj = std::max(dj, (double)std::fabs(ja[k] - jb2[k]));
+      aj = std::max(aj, (double)std::fabs(ja[k]));
+    }
+    std::printf("k_rows_hp vs production rows: maps max|diff| %.3g of max %.3g (%.2g), jacobian %.3g of %.3g (grid %d)\n", dm, am,
+                dm / am, dj, aj, hgrid);
+    std::vector<std::vector<float>> tr(2);
+    for (int r = 0; r < 9; r++)
+    {
+      tr[0].push_back(time_ms(r1, 10));
+      tr[1].push_back(time_ms(rhp, 10));
+    }
+    for (int k = 0; k < 2; k++)
+      std::sort(tr[k].begin(), tr[k].end());
+    std::printf("rows, production k_rows_half   median %7.3f ms  %7.1f GB/s at 56 B/pt\n", tr[0][4], 56.04 * pts / tr[0][4] / 1e6);
+    std::printf("rows, k_rows_hp (permlane/DPP) median %7.3f ms  %7.1f GB/s at 56 B/pt\n", tr[1][4], 56.04 * pts / tr[1][4] / 1e6);
+    return 0;
+  }
   if (argc > 3 && std::strcmp(argv[3], "rg") == 0 && logn == 12)
   {
     // the gab / gde row-group size RG (gc keeps RGC = 4) with the production row pass (one row per

@@ -59,6 +59,35 @@ __global__ void fill(float* p, size_t n, unsigned salt)
   }
 }
 
+// lane_xchg.h check: element e = 64 m + lane; after transpose_reg_lanes_2_5 the value at (m, lane) must
+// be the element whose register bits 0..3 and lane bits 2..5 are exchanged; after the two permlane
+// swaps (register bits 2, 3 <-> lane bits 4, 5) likewise. Counts mismatches.
+__global__ void k_check_lane_xchg(int* bad)
+{
+  const int lane = threadIdx.x;
+  CPair v[16], u[16];
+  for (int m = 0; m < 16; m++)
+  {
+    const float e = (float)(64 * m + lane);
+    v[m] = CPair{f2v{e, e + 0.25f}, f2v{e + 0.5f, e + 0.75f}};
+    u[m] = v[m];
+  }
+  transpose_reg_lanes_2_5(v);
+  swap_reg_lane_bit<2, 4>(u);
+  swap_reg_lane_bit<3, 5>(u);
+  int nb = 0;
+  for (int m = 0; m < 16; m++)
+  {
+    const int om = (lane >> 2) & 15, ol = (lane & 3) | (m << 2);  // full 4 x 4 transposition
+    const float e = (float)(64 * om + ol);
+    nb += v[m].re.x != e || v[m].re.y != e + 0.25f || v[m].im.x != e + 0.5f || v[m].im.y != e + 0.75f;
+    const int pm = (m & 3) | (((lane >> 4) & 3) << 2), pl = (lane & 15) | (((m >> 2) & 3) << 4);
+    const float f = (float)(64 * pm + pl);
+    nb += u[m].re.x != f || u[m].im.y != f + 0.75f;
+  }
+  atomicAdd(bad, nb);
+}
+
 static float2* table(int logn)
 {
   const int n = 1 << logn, lb = logn / 2, tb = 1 << lb, ta = 1 << (logn - lb);
@@ -130,6 +159,22 @@ int main()
       hipLaunchKernelGGL(kern, dim3(C * N), dim3(S::T), XsCfg<LOGN>::LDS, 0, fp, spec, maps, jac, foam, tw, N, rs, tw2);
     };
   };
+  auto mkp = [&](auto kern) {  // k_rows_xp (spec, maps, jac, foam, tw, rows, rs)
+    CHECK(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, XpCfg<LOGN>::LDS));
+    return [=] {
+      hipLaunchKernelGGL(kern, dim3(C * N), dim3(S::T), XpCfg<LOGN>::LDS, 0, fp, spec, maps, jac, foam, tw, N, rs);
+    };
+  };
+  {
+    int* bad;
+    CHECK(hipMalloc(&bad, 4));
+    CHECK(hipMemset(bad, 0, 4));
+    hipLaunchKernelGGL(k_check_lane_xchg, dim3(1), dim3(64), 0, 0, bad);
+    int hb = -1;
+    CHECK(hipMemcpy(&hb, bad, 4, hipMemcpyDeviceToHost));
+    std::printf("lane_xchg check: %d mismatching values%s\n", hb, hb ? " (WRONG)" : " (exact)");
+    CHECK(hipFree(bad));
+  }
   std::vector<V> vs = {
       {"row pass, plain transform (round 2)", mk(k_rows_half<LOGN, kStream, kStream, 0, 1, true, true>), {}},
       {"XS (four-step x transform)", mkx(k_rows_half<LOGN, kStream, kStream, 0, 1, true, true, 1, 1, 4, 2, true, true>), {}},
@@ -141,6 +186,9 @@ int main()
       {"k_rows_xs, 2 of 8 loads prefetched", mkn(k_rows_xs<LOGN, 2>), {}},
       {"k_rows_xs, 3 of 8 loads prefetched", mkn(k_rows_xs<LOGN, 3>), {}},
       {"k_rows_xs PF 2, block index by division (before)", mkn(k_rows_xs_div<LOGN, 2>), {}},
+      {"k_rows_xp (64 x 256, permlane/DPP), PF 0", mkp(k_rows_xp<LOGN, 0>), {}},
+      {"k_rows_xp PF 2", mkp(k_rows_xp<LOGN, 2>), {}},
+      {"k_rows_xp PF 3", mkp(k_rows_xp<LOGN, 3>), {}},
   };
   // XS vs the plain transform: same lanes, different rounding order (max |diff| vs max |value|)
   auto snapf = [&](const void* p, size_t n) {
@@ -178,6 +226,9 @@ int main()
   compare(1, 8, "k_rows_xs PF 3 vs XS");
   compare(7, 9, "k_rows_xs PF 2: shift vs division");
   compare(1, 2, "XS streamed vs default-policy loads");
+  compare(7, 10, "k_rows_xp PF 0 vs k_rows_xs PF 2");
+  compare(7, 11, "k_rows_xp PF 2 vs k_rows_xs PF 2");
+  compare(10, 12, "k_rows_xp PF 3 vs PF 0");
   for (int r = 0; r < 5; r++)
     for (auto& v : vs)
       v.t.push_back(time_ms(v.run, 3));

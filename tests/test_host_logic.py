@@ -259,3 +259,16 @@ def test_parse_rocprof_refuses_above_peak(tmp_path, monkeypatch):
     monkeypatch.chdir(tmp_path)
     with pytest.raises(SystemExit, match="exceeds"):
         m.main(["parse_rocprof.py", str(tmp_path), "t", "4096", "8", "p"])
+
+
+def test_xp_hp_index_model():
+    """tools/xp_model.py plays k_rows_xp's (16384) and k_rows_hp's (4096) LDS slots, in-wave
+    register <-> lane bit transpositions, twiddles and output layout on the host: both must be the
+    unnormalised inverse DFT (the T_in write slots must also cover every x index exactly once)."""
+    import importlib.util
+
+    spec = importlib.util.spec_from_file_location("xp_model", os.path.join(ROOT, "tools", "xp_model.py"))
+    m = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(m)
+    assert m.model_xp() < 1e-12
+    assert m.model_hp() < 1e-12

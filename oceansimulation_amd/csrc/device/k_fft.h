@@ -298,7 +298,9 @@ __global__ __launch_bounds__(RowCfg<LOGN>::WG, RowCfg<LOGN>::MIN_WAVES) void k_r
 // on y folded into n1: row (n + N/2) mod N = N2 ((n1 + 8) mod 16) + n2), times W_N^(n2 k1), into the
 // work slab at row N2 k1 + n2, split planes. Lanes run along x: every load and store of a wave is one
 // 1-KiB row piece, and there is no LDS exchange. The work slab holds columns [x0, x0 + wc).
-template <int LOGN>
+// WNT: the work slab's stores (here) and loads (step 2) non-temporal; false: default policy, so a slab
+// small enough stays in the Infinity Cache between the two steps and its lines are rewritten there.
+template <int LOGN, bool WNT = true>
 __global__ __launch_bounds__(256) void k_cols4_step1(int images, int x0, int wc, const float4* __restrict__ img,
                                                      float4* __restrict__ work, const float2* __restrict__ tw_glob)
 {
@@ -331,7 +333,10 @@ __global__ __launch_bounds__(256) void k_cols4_step1(int images, int x0, int wc,
     for (int k1 = 0; k1 < 16; k1++)
     {
       const float4 o = pair_raw(v[k1]);
-      __builtin_nontemporal_store(f4v{o.x, o.y, o.z, o.w}, reinterpret_cast<f4v*>(dst + (size_t)(N2 * k1 + n2) * wc));
+      if constexpr (WNT)
+        __builtin_nontemporal_store(f4v{o.x, o.y, o.z, o.w}, reinterpret_cast<f4v*>(dst + (size_t)(N2 * k1 + n2) * wc));
+      else
+        dst[(size_t)(N2 * k1 + n2) * wc] = o;
     }
   }
 }
@@ -339,7 +344,7 @@ __global__ __launch_bounds__(256) void k_cols4_step1(int images, int x0, int wc,
 // Step 2, per (image, k1, strip of C slab columns): the N2-point inverse FFT along the work slab's
 // contiguous rows N2 k1 + n2 (n2 = i + m T), output X[k1 + 16 k2] to image row k1 + 16 k2 in the
 // reference layout. Loads and stores are C * 16 = 256-byte row pieces. tw_glob: the N2-point table.
-template <int LOGN2>
+template <int LOGN2, bool WNT = true>
 __global__ __launch_bounds__(ColCfg<LOGN2>::WG) void k_cols4_step2(int images, int x0, int wc,
                                                                  const float4* __restrict__ work, float4* __restrict__ img,
                                                                  const float2* __restrict__ tw_glob)
@@ -364,8 +369,13 @@ __global__ __launch_bounds__(ColCfg<LOGN2>::WG) void k_cols4_step2(int images, i
 #pragma unroll
     for (int m = 0; m < 16; m++)
     {
-      const f4v r = __builtin_nontemporal_load(reinterpret_cast<const f4v*>(src + (size_t)(i + m * T) * wc));
-      v[m] = raw_pair(make_float4(r.x, r.y, r.z, r.w));
+      if constexpr (WNT)
+      {
+        const f4v r = __builtin_nontemporal_load(reinterpret_cast<const f4v*>(src + (size_t)(i + m * T) * wc));
+        v[m] = raw_pair(make_float4(r.x, r.y, r.z, r.w));
+      }
+      else
+        v[m] = raw_pair(src[(size_t)(i + m * T) * wc]);
     }
     fft_run<LOGN2, C, true>(v, i, c, xch, tw);
     float4* dst = img + ((size_t)im << (2 * LOGN)) + (size_t)k1 * N + x0 + xl;

@@ -12,6 +12,7 @@
 #include "device/grid.h"
 #include "device/k_half_cols.h"
 #include "device/k_half_rows.h"
+#include "device/k_rows_hp.h"
 #include "device/spectrum.h"
 
 namespace oceanfft
@@ -74,6 +75,10 @@ hipError_t launch_half_columns(int logn, const FrameParams& fp, const float4* h0
   });
 }
 
+// 4096 row pass: 0 = k_rows_half (the mirror exchange, then fft_run<12>), 1 = k_rows_hp (T_in with the
+// mirror, 256-point sub-transforms in the wave, T_out: device/k_rows_hp.h)
+inline int half_rows_variant = 0;
+
 hipError_t launch_half_rows(int logn, const FrameParams& fp, const float4* gab, const float4* gcd, const float2* ge,
                             const float4* rcorr, float4* maps, float* jac, const FoamParams& foam, const float2* tw,
                             hipStream_t stream, int cus)
@@ -91,6 +96,16 @@ hipError_t launch_half_rows(int logn, const FrameParams& fp, const float4* gab, 
       // workgroup, four per CU, the 4 rows of a gc line grouped on one XCD: 1.407 -> 1.377 ms per
       // 8 x 4096^2 against two-row workgroups (halfbench rowv 16), which stay below 4096.
       constexpr int RG = kHalfRG, RGC = kHalfRGC;
+      if constexpr (LOGN == 12)
+      {
+        if (half_rows_variant == 1)
+        {
+          auto kern = k_rows_hp<RG, RGC>;
+          const int grid = persistent_grid(kern, 256, HpCfg::LDS, fp.cascades * S::N, cus);
+          hipLaunchKernelGGL(kern, dim3(grid), dim3(256), HpCfg::LDS, stream, fp, gab, gcd, ge, rcorr, maps, jac, foam, tw);
+          return hipGetLastError();
+        }
+      }
       constexpr int RPW = LOGN == 12 ? 1 : 2, GRP = LOGN == 12 ? 4 : 2;
       auto kern = k_rows_half<LOGN, 0, kStream, 0, RPW, true, false, RG, RGC, 4, GRP>;
       const int lds = ((S::TW_ENTRIES * 8 + 15) / 16) * 16 + lds_row_slots<LOGN>(RPW) * 8;

@@ -202,8 +202,9 @@ bool fourstep_table(int logn);
 // N/16-point twiddle table.
 bool ifft_fourstep_supported(int logn);
 size_t ifft_fourstep_work_texels(int logn, int wc);
+// work_nt: the slab's accesses non-temporal (false: default policy, k_cols4_step1/2 WNT).
 hipError_t launch_ifft_fourstep(int logn, int n_images, float4* images, float4* work, int wc, const float2* tw,
-                                const float2* tw2, hipStream_t stream, int cus);
+                                const float2* tw2, hipStream_t stream, int cus, bool work_nt = true);
 // Standalone EncodeIFFT, column-first through a work image of n_images * N^2 texels (N = 4096).
 bool ifft_colfirst_supported(int logn);
 hipError_t launch_ifft_colfirst(int logn, int n_images, float4* images, float4* work, const float2* tw,

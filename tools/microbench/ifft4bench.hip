@@ -9,6 +9,7 @@
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
+#include <cstring>
 #include <functional>
 #include <string>
 #include <vector>
@@ -57,10 +58,74 @@ static std::vector<float2> table(int logn)
   return tab;
 }
 
+__global__ void fill_img(float4* p, size_t n)
+{
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
+  {
+    unsigned h = (unsigned)i * 2654435761u;
+    h ^= h >> 15;
+    h *= 2246822519u;
+    h ^= h >> 13;
+    const float a = ((float)(h & 0xffff) - 32768.0f) * (1.0f / 32768.0f);
+    p[i] = make_float4(a, 0.5f * a, -0.25f * a, 0.125f * a);
+  }
+}
+
+// "mall": 2 images of 16384^2 (the bench's EncodeIFFT leg), rows + four-step columns through work slabs
+// of 256 .. 2048 columns with the slab's accesses non-temporal (production) or default-policy: a slab
+// of <= 128 MiB may stay in the 256 MiB Infinity Cache between step 1's stores and step 2's loads.
+static int mall_mode(int cus)
+{
+  constexpr int logn = 14, n = 1 << logn, imgs = 2;
+  const size_t tex = (size_t)n * n * imgs;
+  float4 *img, *work;
+  CHECK(hipMalloc(&img, tex * 16));
+  CHECK(hipMalloc(&work, ifft_fourstep_work_texels(logn, 2048) * 16));
+  hipLaunchKernelGGL(fill_img, dim3(4096), dim3(256), 0, 0, img, tex);
+  auto t1 = table(logn), t2 = table(logn - 4);
+  float2 *tw, *tw2;
+  CHECK(hipMalloc(&tw, t1.size() * 8));
+  CHECK(hipMalloc(&tw2, t2.size() * 8));
+  CHECK(hipMemcpy(tw, t1.data(), t1.size() * 8, hipMemcpyHostToDevice));
+  CHECK(hipMemcpy(tw2, t2.data(), t2.size() * 8, hipMemcpyHostToDevice));
+  std::vector<float4> base(tex);
+  CHECK(hipDeviceSynchronize());
+  CHECK(hipMemcpy(base.data(), img, tex * 16, hipMemcpyDeviceToHost));
+  struct R { int wc; bool nt; std::vector<float> t; };
+  std::vector<R> rs;
+  for (int wc : {256, 512, 1024, 2048})
+    for (bool nt : {true, false})
+      rs.push_back({wc, nt, {}});
+  // every variant must give the production result bit for bit (same arithmetic, only the policy / slab width)
+  std::vector<float4> ref(tex), got(tex);
+  for (size_t k = 0; k < rs.size(); k++)
+  {
+    CHECK(hipMemcpy(img, base.data(), tex * 16, hipMemcpyHostToDevice));
+    CHECK(launch_ifft_fourstep(logn, imgs, img, work, rs[k].wc, tw, tw2, 0, cus, rs[k].nt));
+    CHECK(hipDeviceSynchronize());
+    CHECK(hipMemcpy(k == 0 ? ref.data() : got.data(), img, tex * 16, hipMemcpyDeviceToHost));
+    if (k > 0)
+      std::printf("wc %4d %s: %s\n", rs[k].wc, rs[k].nt ? "nt     " : "default",
+                  std::memcmp(ref.data(), got.data(), tex * 16) == 0 ? "bit-identical to wc 256 nt" : "DIFFERS");
+  }
+  for (int r = 0; r < 5; r++)
+    for (auto& v : rs)
+      v.t.push_back(time_ms([&] { return launch_ifft_fourstep(logn, imgs, img, work, v.wc, tw, tw2, 0, cus, v.nt); }, 3));
+  for (auto& v : rs)
+  {
+    std::sort(v.t.begin(), v.t.end());
+    std::printf("2 x 16384^2 EncodeIFFT, slab %4d columns, slab %s  median %7.3f ms  %7.1f GB/s at 64 B/texel\n", v.wc,
+                v.nt ? "nt     " : "default", v.t[2], 64.0 * tex / v.t[2] / 1e6);
+  }
+  return 0;
+}
+
 int main(int argc, char** argv)
 {
   int cus = 0;
   CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0));
+  if (argc > 1 && std::strcmp(argv[1], "mall") == 0)
+    return mall_mode(cus);
   for (int logn : {13, 14})
   {
     const int n = 1 << logn, imgs = logn == 13 ? (argc > 1 ? std::atoi(argv[1]) : 4) : 1;

@@ -6,6 +6,7 @@ set -u
 export PYTHONUNBUFFERED=1
 tools/gpu_step.sh r04a_rm16bench 150 tools/microbench/rm16bench || exit 1
 tools/gpu_step.sh r04a_halfbench_hp 150 tools/microbench/halfbench 12 8 hp || exit 1
+tools/gpu_step.sh r04a_ifft4bench_mall 150 tools/microbench/ifft4bench mall || exit 1
 tools/gpu_step.sh r04a_tests 300 python -u -m pytest tests/test_gpu_configs.py -x -v --timeout 240 --timeout-method thread \
   -k "path_switch or native_rccl" || exit 1
 tools/gpu_step.sh r04a_rccl_rocm 200 tools/rccl_repro/rccl_big_sendrecv_rocm; rc1=$?

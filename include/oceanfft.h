@@ -241,6 +241,10 @@ int ocean_generator_kernel_times(ocean_generator* gen, double ms_total[3], int64
 /* Device Hash (resources/spectrum.compute:109-117) of count (x, y) pairs in device memory:
  * raw[i] = uint32 n, uv[2i..2i+1] = the two uniforms. For bit-exact parity tests. */
 int ocean_debug_hash(const uint32_t* xy, int count, uint32_t* raw, float* uv, void* hip_stream);
+/* Copy `bytes` (a multiple of 16, 16-B aligned device pointers) with exactly `workgroups` 256-thread
+ * workgroups on hip_stream: a rate-limited HBM read + write stream (bench.py prices a slab rank's
+ * exchange traffic with it on one GPU). No reference counterpart. */
+int ocean_debug_copy(void* dst, const void* src, size_t bytes, int workgroups, void* hip_stream);
 
 /* ---- Surface consumer: the renderer's use of the maps -------------------
  * resources/waveShader.glsl evaluated per mesh vertex on the maps of `count` (generator, cascade)

@@ -84,6 +84,7 @@ SIGNATURES = {
     "ocean_generator_set_profiling": (_i, [_vp, _i]),
     "ocean_generator_kernel_times": (_i, [_vp, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int64)]),
     "ocean_debug_hash": (_i, [_vp, _i, _vp, _vp, _vp]),
+    "ocean_debug_copy": (_i, [_vp, _vp, _sz, _i, _vp]),
     "ocean_surface_sample": (_i, [_vp, _vp, _i, _vp, ctypes.c_int64, _vp]),
     "ocean_surface_sample_plane": (_i, [_vp, _vp, _i, _vp, _i, _vp]),
     "ocean_generator_set_half_spectrum": (_i, [_vp, _i]),

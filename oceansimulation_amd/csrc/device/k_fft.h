@@ -298,8 +298,10 @@ __global__ __launch_bounds__(RowCfg<LOGN>::WG, RowCfg<LOGN>::MIN_WAVES) void k_r
 // on y folded into n1: row (n + N/2) mod N = N2 ((n1 + 8) mod 16) + n2), times W_N^(n2 k1), into the
 // work slab at row N2 k1 + n2, split planes. Lanes run along x: every load and store of a wave is one
 // 1-KiB row piece, and there is no LDS exchange. The work slab holds columns [x0, x0 + wc).
-// WNT: the work slab's stores (here) and loads (step 2) non-temporal; false: default policy, so a slab
-// small enough stays in the Infinity Cache between the two steps and its lines are rewritten there.
+// WNT: the work slab's stores (here) and loads (step 2) non-temporal (production). false: default
+// policy, so that a slab of <= 128 MiB could stay in the Infinity Cache between the two steps: measured
+// and not kept (2 x 16384^2: 10.02 ms at best, slab 1024 columns, against 10.00 for 2048 nt;
+// profiles/r04_ifft4bench_mall.log).
 template <int LOGN, bool WNT = true>
 __global__ __launch_bounds__(256) void k_cols4_step1(int images, int x0, int wc, const float4* __restrict__ img,
                                                      float4* __restrict__ work, const float2* __restrict__ tw_glob)

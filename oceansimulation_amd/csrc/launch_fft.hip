@@ -90,7 +90,7 @@ size_t ifft_fourstep_work_texels(int logn, int wc) { return ((size_t)1 << logn) 
 // columns per item, 32-B pieces) stays ahead, 4.78 vs 4.96 ms for 4 images.
 
 hipError_t launch_ifft_fourstep(int logn, int n_images, float4* images, float4* work, int wc, const float2* tw,
-                                const float2* tw2, hipStream_t stream, int cus, bool work_nt)
+                                const float2* tw2, hipStream_t stream, int cus)
 {
   if (!ifft_fourstep_supported(logn) || !tw2)
     return hipErrorInvalidValue;
@@ -108,8 +108,8 @@ hipError_t launch_ifft_fourstep(int logn, int n_images, float4* images, float4* 
     {
       constexpr int LOGN2 = LOGN - 4;
       using K2 = ColCfg<LOGN2>;
-      auto k1 = work_nt ? k_cols4_step1<LOGN, true> : k_cols4_step1<LOGN, false>;
-      auto k2 = work_nt ? k_cols4_step2<LOGN2, true> : k_cols4_step2<LOGN2, false>;
+      auto k1 = k_cols4_step1<LOGN>;
+      auto k2 = k_cols4_step2<LOGN2>;
       const int lds2 = lds_bytes_cols<LOGN2>();
       for (int im = 0; im < n_images; im++)
         for (int x0 = 0; x0 < n; x0 += wc)

@@ -14,7 +14,6 @@
 #include "device/k_half_cols.h"
 #include "device/k_half_rows.h"
 #include "device/k_rows_xs.h"
-#include "device/k_rows_xp.h"
 #include "device/spectrum.h"
 
 namespace oceanfft
@@ -82,8 +81,9 @@ hipError_t launch_half_slab_columns(int logn, const FrameParams& fp, const HalfS
 // transform (barriers 14 -> 7 per image), which needs tw2, the N/16-point table ocean_fft_create
 // appends for the sizes fourstep_table() names.
 // tools/microbench A/B at 16384: 0 = the plain transform, 1 = XS (k_rows_half), 2 = k_rows_xs, 3 =
-// k_rows_xs with 2 of the next image's 8 field loads in flight during the transform (PF; 4 spill), 4 =
-// k_rows_xp (64 x 256 split, the sub-transforms' exchanges in the wave: device/k_rows_xp.h), PF 2
+// k_rows_xs with 2 of the next image's 8 field loads in flight during the transform (PF; 4 spill).
+// Measured and not kept: k_rows_xp (tools/microbench/k_rows_xp.h, the 64 x 256 split with the
+// sub-transforms' exchanges in the wave), 3.80-3.83 against 3.74 ms (profiles/r04_rm16bench_xp.log).
 inline int rm_rows_variant = 3;
 
 template <int LOGN>
@@ -98,14 +98,6 @@ hipError_t launch_rm_rows(const FrameParams& fp, const RowSrc& rs, const float4*
     return hipErrorInvalidValue;
   if constexpr (RPW == 1)
   {
-    if (rm_rows_variant == 4)
-    {
-      auto kern = k_rows_xp<LOGN, 2>;
-      const int lds = XpCfg<LOGN>::LDS;
-      const int grid = persistent_grid(kern, S::T, lds, fp.cascades * rows, cus);
-      hipLaunchKernelGGL(kern, dim3(grid), dim3(S::T), lds, stream, fp, spec, maps, jac, foam, tw, rows, rs);
-      return hipGetLastError();
-    }
     if (rm_rows_variant >= 2)
     {
       if (!tw2)

@@ -1610,6 +1610,18 @@ int ocean_generator_kernel_times(ocean_generator* g, double ms_total[3], int64_t
   return OCEAN_OK;
 }
 
+int ocean_debug_copy(void* dst, const void* src, size_t bytes, int workgroups, void* hip_stream)
+{
+  if ((bytes > 0 && (!dst || !src)) || bytes % 16 != 0 || workgroups < 1 || workgroups > 65536 ||
+      (reinterpret_cast<uintptr_t>(dst) | reinterpret_cast<uintptr_t>(src)) % 16 != 0)
+    return fail(OCEAN_ERR_INVALID, "ocean_debug_copy: null or unaligned pointer, bytes not a multiple of 16, or "
+                                   "workgroups outside [1, 65536]");
+  if (bytes == 0)
+    return OCEAN_OK;
+  HIP_TRY(launch_debug_copy(dst, src, bytes, workgroups, (hipStream_t)hip_stream), "debug copy");
+  return OCEAN_OK;
+}
+
 int ocean_debug_hash(const uint32_t* xy, int count, uint32_t* raw, float* uv, void* hip_stream)
 {
   if (!xy || !raw || !uv || count < 0)

@@ -202,9 +202,8 @@ bool fourstep_table(int logn);
 // N/16-point twiddle table.
 bool ifft_fourstep_supported(int logn);
 size_t ifft_fourstep_work_texels(int logn, int wc);
-// work_nt: the slab's accesses non-temporal (false: default policy, k_cols4_step1/2 WNT).
 hipError_t launch_ifft_fourstep(int logn, int n_images, float4* images, float4* work, int wc, const float2* tw,
-                                const float2* tw2, hipStream_t stream, int cus, bool work_nt = true);
+                                const float2* tw2, hipStream_t stream, int cus);
 // Standalone EncodeIFFT, column-first through a work image of n_images * N^2 texels (N = 4096).
 bool ifft_colfirst_supported(int logn);
 hipError_t launch_ifft_colfirst(int logn, int n_images, float4* images, float4* work, const float2* tw,
@@ -219,6 +218,7 @@ hipError_t launch_ifft_pre(int logn, int n_images, float4* images, float4* work,
 hipError_t launch_surface(const SurfaceParams& p, const SurfacePlane& plane, const float2* xz, int64_t count,
                           float4* out, hipStream_t stream, int cus);
 hipError_t launch_hash(const uint32_t* xy, int count, uint32_t* raw, float2* uv, hipStream_t stream);
+hipError_t launch_debug_copy(void* dst, const void* src, size_t bytes, int workgroups, hipStream_t stream);
 // Generator frame: pass 1 (evolve + y iFFT, destination-block-ordered output), pass 2 (x iFFT +
 // maps + Jacobian). keep: evolved amplitudes kept live between the two packed images (0, 8, 16).
 hipError_t launch_cols_evolve(int logn, const FrameParams& fp, const SlabGeom& g, const float4* h0, float4* inter,

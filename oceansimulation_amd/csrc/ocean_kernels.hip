@@ -341,6 +341,21 @@ hipError_t launch_surface(const SurfaceParams& p, const SurfacePlane& plane, con
   return hipGetLastError();
 }
 
+// A plain 16-B copy on a fixed number of 256-thread workgroups (ocean_debug_copy): bench.py paces the
+// one-GPU emulation of a slab rank's exchange traffic with it (the workgroup count sets the rate).
+__global__ __launch_bounds__(256) void k_debug_copy(const float4* __restrict__ src, float4* __restrict__ dst, size_t n16)
+{
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n16; i += (size_t)gridDim.x * blockDim.x)
+    dst[i] = src[i];
+}
+
+hipError_t launch_debug_copy(void* dst, const void* src, size_t bytes, int workgroups, hipStream_t stream)
+{
+  hipLaunchKernelGGL(k_debug_copy, dim3(workgroups), dim3(256), 0, stream, static_cast<const float4*>(src),
+                     static_cast<float4*>(dst), bytes / 16);
+  return hipGetLastError();
+}
+
 hipError_t launch_hash(const uint32_t* xy, int count, uint32_t* raw, float2* uv, hipStream_t stream)
 {
   hipLaunchKernelGGL(k_hash, dim3((count + 255) / 256), dim3(256), 0, stream, xy, count, raw, uv);

@@ -195,6 +195,12 @@ class Generator:
             pass
 
 
+def debug_copy(dst_ptr: int, src_ptr: int, nbytes: int, workgroups: int, stream: int | None = None) -> None:
+    """ocean_debug_copy: a copy on exactly `workgroups` 256-thread workgroups (a rate-limited HBM stream)."""
+    check(lib().ocean_debug_copy(ctypes.c_void_p(dst_ptr), ctypes.c_void_p(src_ptr), nbytes, workgroups,
+                                 ctypes.c_void_p(stream or 0)), "ocean_debug_copy")
+
+
 def debug_hash(xy_dev_ptr: int, count: int, raw_dev_ptr: int, uv_dev_ptr: int, stream: int | None = None) -> None:
     check(lib().ocean_debug_hash(ctypes.c_void_p(xy_dev_ptr), count, ctypes.c_void_p(raw_dev_ptr),
                                  ctypes.c_void_p(uv_dev_ptr), ctypes.c_void_p(stream or 0)), "ocean_debug_hash")

@@ -855,4 +855,34 @@ hipError_t launch_ifft_pre_pair14(int n_images, float4* images, float4* work, co
   return hipGetLastError();
 }
 
+// The four-step EncodeIFFT (launch_ifft_fourstep) with the work slab's cache policy selectable
+// (k_cols4_step1/2 WNT): ifft4bench mall.
+inline hipError_t launch_ifft_fourstep_ab(int logn, int n_images, float4* images, float4* work, int wc, const float2* tw,
+                                          const float2* tw2, hipStream_t stream, int cus, bool work_nt)
+{
+  if (logn != 14 || !tw2 || wc < 64 || (1 << logn) % wc != 0 || (wc & 63) != 0)
+    return hipErrorInvalidValue;
+  hipError_t e = launch_rows_ifft(logn, n_images, images, tw, stream, cus);
+  if (e != hipSuccess)
+    return e;
+  constexpr int LOGN = 14, LOGN2 = 10, n = 1 << LOGN;
+  using K2 = ColCfg<LOGN2>;
+  auto k1 = work_nt ? k_cols4_step1<LOGN, true> : k_cols4_step1<LOGN, false>;
+  auto k2 = work_nt ? k_cols4_step2<LOGN2, true> : k_cols4_step2<LOGN2, false>;
+  const int lds2 = lds_bytes_cols<LOGN2>();
+  for (int im = 0; im < n_images; im++)
+    for (int x0 = 0; x0 < n; x0 += wc)
+    {
+      float4* img = images + ((size_t)im << (2 * LOGN));
+      const int g1 = persistent_grid(k1, 256, 0, (wc / 64) * ((n / 16) / 4), cus);
+      hipLaunchKernelGGL(k1, dim3(g1), dim3(256), 0, stream, 1, x0, wc, img, work, tw);
+      const int g2 = persistent_grid(k2, K2::WG, lds2, 16 * (wc / K2::C), cus);
+      hipLaunchKernelGGL(k2, dim3(g2), dim3(K2::WG), lds2, stream, 1, x0, wc, work, img, tw2);
+      e = hipGetLastError();
+      if (e != hipSuccess)
+        return e;
+    }
+  return hipSuccess;
+}
+
 }  // namespace oceanfft

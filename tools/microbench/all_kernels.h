@@ -6,6 +6,6 @@
 #include "../../oceansimulation_amd/csrc/launch_half.hip"
 #include "../../oceansimulation_amd/csrc/launch_slab.hip"
 #include "../../oceansimulation_amd/csrc/launch_fft.hip"
-#include "../../oceansimulation_amd/csrc/device/k_rows_xp.h"
+#include "k_rows_xp.h"
 #include "../../oceansimulation_amd/csrc/device/k_rows_hp.h"
 #include "ab_kernels.h"

@@ -101,7 +101,7 @@ static int mall_mode(int cus)
   for (size_t k = 0; k < rs.size(); k++)
   {
     CHECK(hipMemcpy(img, base.data(), tex * 16, hipMemcpyHostToDevice));
-    CHECK(launch_ifft_fourstep(logn, imgs, img, work, rs[k].wc, tw, tw2, 0, cus, rs[k].nt));
+    CHECK(launch_ifft_fourstep_ab(logn, imgs, img, work, rs[k].wc, tw, tw2, 0, cus, rs[k].nt));
     CHECK(hipDeviceSynchronize());
     CHECK(hipMemcpy(k == 0 ? ref.data() : got.data(), img, tex * 16, hipMemcpyDeviceToHost));
     if (k > 0)
@@ -110,7 +110,7 @@ static int mall_mode(int cus)
   }
   for (int r = 0; r < 5; r++)
     for (auto& v : rs)
-      v.t.push_back(time_ms([&] { return launch_ifft_fourstep(logn, imgs, img, work, v.wc, tw, tw2, 0, cus, v.nt); }, 3));
+      v.t.push_back(time_ms([&] { return launch_ifft_fourstep_ab(logn, imgs, img, work, v.wc, tw, tw2, 0, cus, v.nt); }, 3));
   for (auto& v : rs)
   {
     std::sort(v.t.begin(), v.t.end());

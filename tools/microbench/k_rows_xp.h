@@ -1,4 +1,4 @@
-// device/k_rows_xp.h — the row pass of N = 16384 with the x transform split 64 x 256 and the
+// k_rows_xp.h (microbenchmark A/B, not in the library) — the row pass of N = 16384 with the x transform split 64 x 256 and the
 // sub-transforms' exchanges done inside the wave (lane_xchg.h: v_permlane16/32_swap + DPP), so the
 // LDS carries only the two transpositions (k_rows_xs: the two transpositions plus two exchanges of
 // every 1024-point sub-transform, half of its LDS traffic).
@@ -8,11 +8,11 @@
 
 #include <cstdint>
 
-#include "ocean_internal.h"
-#include "device/fft.h"
-#include "device/grid.h"
-#include "device/lane_xchg.h"
-#include "device/memory.h"
+#include "../../oceansimulation_amd/csrc/ocean_internal.h"
+#include "../../oceansimulation_amd/csrc/device/fft.h"
+#include "../../oceansimulation_amd/csrc/device/grid.h"
+#include "../../oceansimulation_amd/csrc/device/lane_xchg.h"
+#include "../../oceansimulation_amd/csrc/device/memory.h"
 
 namespace oceanfft
 {

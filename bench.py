@@ -1088,7 +1088,8 @@ def main(argv=None):
             {"half": "column_pass_k_cols_half", "full": "column_pass_k_cols_evolve",
              "four-step": "column_pass_k_gen4_step1+2"}[path]:
                 {"avg_ms": p1_ms, "bytes": pass_bytes[0] * per_launch_pts},
-            {"half": "row_pass_k_rows_half", "full": "row_pass_k_rows_final",
+            # the whole-grid 4096 row pass is k_rows_hp (launch_half_rows); 1024 / 2048 keep k_rows_half
+            {"half": "row_pass_k_rows_hp" if n == 4096 else "row_pass_k_rows_half", "full": "row_pass_k_rows_final",
              "four-step": "row_pass_k_rows_xs" if n >= 16384 else "row_pass_k_rows_half"}[path]:
                 {"avg_ms": p2_ms, "bytes": pass_bytes[1] * per_launch_pts},
         }

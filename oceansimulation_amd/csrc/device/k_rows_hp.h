@@ -34,17 +34,19 @@ __device__ __forceinline__ int hp_slot(int n1, int j) { return n1 * HpCfg::RS + 
 
 // One row (both images; C loaded once, kept for image 1) per 256-thread workgroup, four per CU, the
 // 4 rows of a gc line on one XCD; default-policy loads, streamed stores (production k_rows_half's
-// item shape at 4096).
+// item shape at 4096). RM: the fields are row-major behind a RowSrc (the strip-dealt slabs' row pass,
+// rows = the rank's rows; streamed loads, C loaded per image, one row per workgroup in order), so slab
+// frames stay bit-identical to whole grids.
 //   T_in: thread (w, s, p) = (tid >> 6, tid & 3, (tid >> 2) & 15) receives x(n1 + 16 (p + 16 m)),
 //         n1 = 4 w + s (four 256-point sub-transforms per wave).
 //   sub-transform as k_rows_xp: v[b] = Y_n1(p + 16 b), then x W_N^(n1 (p + 16 b)).
 //   T_out: thread k2 = tid receives Z_n1(k2), n1 < 16; DFT-16: v[k1] = X(tid + 256 k1).
-template <int RG, int RGC>
+template <int RG, int RGC, bool RM = false>
 __global__ __launch_bounds__(256, 4) void k_rows_hp(FrameParams fp, const float4* __restrict__ gab,
                                                  const float4* __restrict__ gde, const float2* __restrict__ gc,
                                                  const float4* __restrict__ spec, float4* __restrict__ maps,
                                                  float* __restrict__ jac, FoamParams foam,
-                                                 const float2* __restrict__ tw_glob)
+                                                 const float2* __restrict__ tw_glob, int rows, RowSrc rs)
 {
   constexpr int LOGN = HpCfg::LOGN, RS = HpCfg::RS;
   using S = FftShape<LOGN>;
@@ -56,13 +58,17 @@ __global__ __launch_bounds__(256, 4) void k_rows_hp(FrameParams fp, const float4
   float2* xs = reinterpret_cast<float2*>(smem + HpCfg::TW);
   load_twiddles<LOGN>(tw, tw_glob);
 
-  const int total = fp.cascades * N;
+  const int nrows = RM ? rows : N;
+  const int total = fp.cascades * nrows;
   const float dim = (float)N;
-  for (int item = xcd_group_slot<4>(blockIdx.x, gridDim.x); item < total; item += gridDim.x)
+  constexpr int LA = RM ? kStream : 0;
+  const int lcpr = RM ? 31 - __builtin_clz(rs.cpr) : 0, cmask = RM ? rs.cpr - 1 : 0;
+  const int wave0 = __builtin_amdgcn_readfirstlane((int)threadIdx.x & ~63);
+  for (int item = RM ? (int)blockIdx.x : xcd_group_slot<4>(blockIdx.x, gridDim.x); item < total; item += gridDim.x)
   {
-    const int c = item / N, y = item - c * N;
+    const int c = item / nrows, y = item - c * nrows;  // RM: y is the local row (slabs start at an even row)
     const float dk = fp.c[c].dk;
-    const size_t base = (size_t)c * STRIPS * N * B;
+    const size_t base = RM ? ((size_t)c * rows + y) * rs.lp : (size_t)c * STRIPS * N * B;
     const float sgy = (y & 1) ? -1.0f : 1.0f;
     float2 ckeep[8], cnyq;
 #pragma unroll
@@ -76,15 +82,21 @@ __global__ __launch_bounds__(256, 4) void k_rows_hp(FrameParams fp, const float4
       for (int m = 0; m < 8; m++)
       {
         const int u = m * T + i;
-        const int off = half_group_offset<LOGN, RG>(y, u / B, u % B);
-        const int offc = half_group_offset<LOGN, RGC>(y, u / B, u % B);
+        // RM: source block of column u (wave-uniform, a scalar shift) and the element in its row
+        const int src = RM ? (m * T + sopaque(wave0)) >> lcpr : 0;
+        const int off = RM ? (u & cmask) : half_group_offset<LOGN, RG>(y, u / B, u % B);
+        const int offc = RM ? off : half_group_offset<LOGN, RGC>(y, u / B, u % B);
+        const float4* fab = RM ? reinterpret_cast<const float4*>(rs.ab + (size_t)src * rs.src_stride) : gab;
+        const float4* fde = RM ? reinterpret_cast<const float4*>(rs.de + (size_t)src * rs.src_stride) : gde;
+        const float2* fc = RM ? reinterpret_cast<const float2*>(rs.c + (size_t)src * rs.src_stride) : gc;
         const float kx = (float)u * dk;
         const float4 s4 = ld4<0>(sp, (N / 2 - u) * 16);
         if (img == 0)
         {
-          const CPair p = raw_pair(ld4<0>(gab + base, off * 16));
-          const float2 cc = ld2<0>(gc + base, offc * 8);
-          ckeep[m] = cc;
+          const CPair p = raw_pair(ld4<LA>(fab + base, off * 16));
+          const float2 cc = ld2<0>(fc + base, offc * 8);
+          if constexpr (!RM)
+            ckeep[m] = cc;
           const float Ar = p.re.x, Ai = p.im.x, Br = p.re.y, Bi = p.im.y, Cr = cc.x, Ci = cc.y;
           v[m] = CPair{f2v{(1.0f - kx) * Ar, -Bi - kx * Cr}, f2v{(1.0f - kx) * Ai, Br - kx * Ci}};
           v[m + 8] = CPair{f2v{(1.0f + kx) * Ar + sgy * s4.x, -Bi + kx * Cr + sgy * s4.z},
@@ -92,8 +104,14 @@ __global__ __launch_bounds__(256, 4) void k_rows_hp(FrameParams fp, const float4
         }
         else
         {
-          const CPair q = raw_pair(ld4<0>(gde + base, off * 16));
-          const float2 cc = ckeep[m];
+          const CPair q = raw_pair(ld4<LA>(fde + base, off * 16));
+          // RM: C again (its second read, a few microseconds after the first, comes from L2): keeping
+          // it beside the source-block addressing spills
+          float2 cc;
+          if constexpr (RM)
+            cc = ld2<0>(fc + base, offc * 8);
+          else
+            cc = ckeep[m];
           const float Cr = cc.x, Ci = cc.y, Dr = q.re.x, Di = q.im.x, Er = q.re.y, Ei = q.im.y;
           const float kx2 = kx * kx;
           v[m] = CPair{f2v{-(Di - kx2 * Ci), -Er + kx * Di}, f2v{Dr - kx2 * Cr, -Ei - kx * Dr}};
@@ -103,21 +121,26 @@ __global__ __launch_bounds__(256, 4) void k_rows_hp(FrameParams fp, const float4
       }
       if (i == 0)
       {
-        // the Nyquist column u = -N/2 (first column of the last strip) replaces the unused -u lane of u = 0
-        const int off = half_group_offset<LOGN, RG>(y, N / 2 / B);
-        const int offc = half_group_offset<LOGN, RGC>(y, N / 2 / B);
+        // the Nyquist column u = -N/2 (first column of the last strip; RM: block nyq_src, column cpr)
+        // replaces the unused -u lane of u = 0
+        const int off = RM ? rs.cpr : half_group_offset<LOGN, RG>(y, N / 2 / B);
+        const int offc = RM ? off : half_group_offset<LOGN, RGC>(y, N / 2 / B);
+        const size_t ns = RM ? (size_t)rs.nyq_src * rs.src_stride : 0;
+        const float4* fab = RM ? reinterpret_cast<const float4*>(rs.ab + ns) : gab;
+        const float4* fde = RM ? reinterpret_cast<const float4*>(rs.de + ns) : gde;
+        const float2* fc = RM ? reinterpret_cast<const float2*>(rs.c + ns) : gc;
         const float kx = -(dim / 2.0f) * dk;
-        if (img == 0)
-          cnyq = ld2<0>(gc + base, offc * 8);
+        if (RM || img == 0)
+          cnyq = ld2<0>(fc + base, offc * 8);
         const float2 cc = cnyq;
         if (img == 0)
         {
-          const CPair p = raw_pair(ld4<0>(gab + base, off * 16));
+          const CPair p = raw_pair(ld4<LA>(fab + base, off * 16));
           v[8] = CPair{f2v{(1.0f - kx) * p.re.x, -p.im.y - kx * cc.x}, f2v{(1.0f - kx) * p.im.x, p.re.y - kx * cc.y}};
         }
         else
         {
-          const CPair q = raw_pair(ld4<0>(gde + base, off * 16));
+          const CPair q = raw_pair(ld4<LA>(fde + base, off * 16));
           const float kx2 = kx * kx;
           v[8] = CPair{f2v{-(q.im.x - kx2 * cc.y), -q.re.y + kx * q.im.x}, f2v{q.re.x - kx2 * cc.x, -q.im.y - kx * q.re.x}};
         }
@@ -172,14 +195,14 @@ __global__ __launch_bounds__(256, 4) void k_rows_hp(FrameParams fp, const float4
           set_half(v[n1], h, xs[n1 * RS + (tid ^ ((n1 >> 2) & 3))]);
       }
       idft16(v);  // v[k1] = X(tid + T k1)
-      float4* dst = maps + ((size_t)cimg * N + y) * N;
+      float4* dst = maps + ((size_t)cimg * nrows + y) * N;
 #pragma unroll
       for (int m = 0; m < 16; m++)
         st4<kStream>(dst + m * T, tid * 16, from_pair(v[m]));
       if (img == 1)
       {
         const float lam = foam.displacement[c];
-        float* jb = jac + ((size_t)c * N + y) * N;
+        float* jb = jac + ((size_t)c * nrows + y) * N;
 #pragma unroll
         for (int m = 0; m < 16; m++)
           st1<kStream>(jb + m * T, tid * 4,

@@ -59,6 +59,13 @@ inline int device_cu_count()
 
 inline bool g_force_persistent = false;  // tools/microbench A/B only
 
+// 4096 row pass (whole grids, launch_half_rows, and the strip-dealt slabs' row-major fields,
+// launch_rm_rows): 1 = k_rows_hp (production: T_in with the mirror, 256-point sub-transforms in the
+// wave through permlane / DPP swaps, T_out; device/k_rows_hp.h), 0 = k_rows_half (the mirror
+// exchange, then fft_run<12>). 8 x 4096^2: 1.377 -> 1.360 ms, maps within 1e-6 of max
+// (profiles/r04_halfbench_hp.log). Both paths switch together, so slabs stay bit-identical to whole grids.
+inline int half_rows_variant = 1;
+
 inline bool one_shot_grids(int cus)
 {
   const int d = device_cu_count();

@@ -75,11 +75,6 @@ hipError_t launch_half_columns(int logn, const FrameParams& fp, const float4* h0
   });
 }
 
-// 4096 row pass: 1 = k_rows_hp (production: T_in with the mirror, 256-point sub-transforms in the wave
-// through permlane / DPP swaps, T_out; device/k_rows_hp.h), 0 = k_rows_half (the mirror exchange, then
-// fft_run<12>). 8 x 4096^2: 1.377 -> 1.360 ms, maps within 4e-7 of max (profiles/r04_halfbench_hp.log).
-inline int half_rows_variant = 1;
-
 hipError_t launch_half_rows(int logn, const FrameParams& fp, const float4* gab, const float4* gcd, const float2* ge,
                             const float4* rcorr, float4* maps, float* jac, const FoamParams& foam, const float2* tw,
                             hipStream_t stream, int cus)
@@ -103,7 +98,8 @@ hipError_t launch_half_rows(int logn, const FrameParams& fp, const float4* gab, 
         {
           auto kern = k_rows_hp<RG, RGC>;
           const int grid = persistent_grid(kern, 256, HpCfg::LDS, fp.cascades * S::N, cus);
-          hipLaunchKernelGGL(kern, dim3(grid), dim3(256), HpCfg::LDS, stream, fp, gab, gcd, ge, rcorr, maps, jac, foam, tw);
+          hipLaunchKernelGGL(kern, dim3(grid), dim3(256), HpCfg::LDS, stream, fp, gab, gcd, ge, rcorr, maps, jac, foam, tw, 0,
+                             RowSrc{});
           return hipGetLastError();
         }
       }

@@ -13,6 +13,7 @@
 #include "device/k_gen4.h"
 #include "device/k_half_cols.h"
 #include "device/k_half_rows.h"
+#include "device/k_rows_hp.h"
 #include "device/k_rows_xs.h"
 #include "device/spectrum.h"
 
@@ -96,6 +97,19 @@ hipError_t launch_rm_rows(const FrameParams& fp, const RowSrc& rs, const float4*
   // the block index of a wave's loads must be wave-uniform, and is taken with a shift
   if (rs.cpr < 64 || (rs.cpr & (rs.cpr - 1)) != 0 || rows % RPW != 0)
     return hipErrorInvalidValue;
+  if constexpr (LOGN == 12)
+  {
+    // the strip-dealt slabs at 4096: the whole grid's row pass (k_rows_hp, launch_half_rows) on
+    // row-major fields, so slab frames stay bit-identical to whole grids
+    if (half_rows_variant == 1)
+    {
+      auto kern = k_rows_hp<1, 1, true>;
+      const int grid = persistent_grid(kern, 256, HpCfg::LDS, fp.cascades * rows, cus);
+      hipLaunchKernelGGL(kern, dim3(grid), dim3(256), HpCfg::LDS, stream, fp, (const float4*)nullptr,
+                         (const float4*)nullptr, (const float2*)nullptr, spec, maps, jac, foam, tw, rows, rs);
+      return hipGetLastError();
+    }
+  }
   if constexpr (RPW == 1)
   {
     if (rm_rows_variant >= 2)

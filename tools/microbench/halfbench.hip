@@ -205,7 +205,8 @@ int main(int argc, char** argv)
     CHECK(hipFuncSetAttribute((const void*)hpk, hipFuncAttributeMaxDynamicSharedMemorySize, HpCfg::LDS));
     const int hgrid = persistent_grid(hpk, 256, HpCfg::LDS, C * n, cus);
     auto rhp = [&] {
-      hipLaunchKernelGGL(hpk, dim3(hgrid), dim3(256), HpCfg::LDS, 0, fp, gab, gcd, ge, spec, maps, jac, foam, tw);
+      hipLaunchKernelGGL(hpk, dim3(hgrid), dim3(256), HpCfg::LDS, 0, fp, gab, gcd, ge, spec, maps, jac, foam, tw, 0,
+                         RowSrc{});
       return hipGetLastError();
     };
     CHECK(rhp());

@@ -56,6 +56,8 @@ def size_key(symbol, logn):
     three launches per frame, two over 16-B field texels (second argument true: gab, gde) and one
     over gc's 8-B texels as column pairs (false), so its key carries both arguments."""
     first = first_arg(symbol)
+    if base_name(symbol) == "k_rows_hp":  # 4096 only; its template arguments are the field layout
+        return "k_rows_hp" if logn == 12 else "k_rows_hp<12>"
     if base_name(symbol) == "k_gen4_step2":
         args = template_args(symbol)
         return f"k_gen4_step2<{args[0]},{args[1]}>"
@@ -88,7 +90,7 @@ def algorithmic_bytes(key, n, cascades, mode):
     else:
         kept = (n // 2 + 4) / n  # columns [0, N/2) plus the 4-wide Nyquist strip
         table = {"k_cols_evolve": 48, "k_rows_final": 68, "k_cols_half": (16 + 40) * kept,
-                 "k_rows_half": 40 * kept + 36}
+                 "k_rows_half": 40 * kept + 36, "k_rows_hp": 40 * kept + 36}
     if key in ("k_generate_spectrum", "k_generate_spectrum_pairs"):
         return 16 * n * n  # one cascade's h0 per launch
     return int(table[key] * pts) if key in table else None

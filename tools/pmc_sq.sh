@@ -8,7 +8,7 @@
 set -u
 cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
 ARGS=${BENCH_ARGS:-"--steps 5 --warmup 2 --no-cpu-baseline --no-slab --no-ifft --no-surface --no-reseed --no-profile"}
-KRE=${KERNEL_REGEX:-"k_rows_half|k_cols_half"}
+KRE=${KERNEL_REGEX:-"k_rows_half|k_rows_hp|k_cols_half"}
 P=${PREFIX:-pmc_sq}
 SETS=(
   "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS"

@@ -7,7 +7,7 @@
 set -u
 cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
 ARGS=${BENCH_ARGS:-"--steps 20 --warmup 3 --headline-only"}
-KRE=${KERNEL_REGEX:-"k_cols_evolve|k_rows_final|k_rows_ifft|k_rows_half|k_rows_xs|k_cols|k_gen4|k_generate_spectrum|k_half_nyquist"}
+KRE=${KERNEL_REGEX:-"k_cols_evolve|k_rows_final|k_rows_ifft|k_rows_half|k_rows_hp|k_rows_xs|k_cols|k_gen4|k_generate_spectrum|k_half_nyquist"}
 P=${PREFIX:-prof}  # output directories gpurun_out/${P}_trace, _fetch, _write
 mkdir -p gpurun_out
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/${P}_trace -o trace --output-format csv \

@@ -772,7 +772,7 @@ XGMI_LINK_GBS_BIDIR = 153.6
 XGMI_ONE_WAY_GBS = XGMI_LINKS * XGMI_LINK_GBS_BIDIR / 2.0  # 537.6 GB/s per rank, one direction
 
 
-def p8_rank_projection(args, one_gpu_frame_ms: float, ranks: int = 8) -> dict:
+def p8_rank_projection(args, one_gpu_frame_ms: float, ranks: int = 8, masked: bool = False) -> dict:
     """The per-rank cost of BASELINE configs[4] (the 16384^2 grid over 8 GPUs) measured on ONE GPU, and
     the 8-GPU frame it implies. All 8 ranks' SlabGenerators run in this process on one compute stream;
     frames are emulated with the equal-split all-to-all as device copies (slab.emulate_frame) and each
@@ -792,7 +792,9 @@ def p8_rank_projection(args, one_gpu_frame_ms: float, ranks: int = 8) -> dict:
     The xGMI leg itself cannot run on one GPU: it is priced at XGMI_ONE_WAY_GBS (stated source above).
     The 8-GPU frame is bounded below by max(passes under contention, exchange at that rate); the
     projected speed-up is the one-GPU frame over that bound (paced contention; the RCCL-copy bound is
-    reported beside it)."""
+    reported beside it). masked: the compute stream and the exchange stream carry disjoint CU masks
+    (hipExtStreamCreateWithCUMask: the passes on all but the reserved CUs, the exchange traffic on the
+    reserved ones), so the exchange's workgroups cannot take CUs from the passes."""
     import torch
 
     import oceansimulation_amd as ocean
@@ -800,9 +802,19 @@ def p8_rank_projection(args, one_gpu_frame_ms: float, ranks: int = 8) -> dict:
     from oceansimulation_amd.slab import RcclComm, SlabGenerator, emulate_frame
     from oceansimulation_amd.waves import debug_copy
 
+    from oceansimulation_amd.hip import stream_destroy, stream_with_cu_mask
+
     n, dt, steps = args.slab_n, 1.0 / 60.0, args.slab_steps
-    comp = torch.cuda.Stream()  # the generators' stream (non-blocking, so the exchange stream runs beside it)
-    side = torch.cuda.Stream()
+    dev_cus = torch.cuda.get_device_properties(torch.cuda.current_device()).multi_processor_count
+    reserve = max(0, min(args.slab_reserve_cus, dev_cus - 1))
+    raw_streams = []
+    if masked:
+        raw_streams = [stream_with_cu_mask(range(0, dev_cus - reserve), dev_cus),
+                       stream_with_cu_mask(range(dev_cus - reserve, dev_cus), dev_cus)]
+        comp, side = (torch.cuda.ExternalStream(h) for h in raw_streams)
+    else:
+        comp = torch.cuda.Stream()  # the generators' stream (non-blocking, so the exchange stream runs beside it)
+        side = torch.cuda.Stream()
     fft = ocean.FFTCalculator(n, stream=comp.cuda_stream)
     slabs = [SlabGenerator(fft, r, ranks) for r in range(ranks)]
     xbytes = slabs[0].exchange_bytes
@@ -810,7 +822,6 @@ def p8_rank_projection(args, one_gpu_frame_ms: float, ranks: int = 8) -> dict:
     recvs = [DeviceBuffer(g.exchange_bytes) for g in slabs]
     xdst = DeviceBuffer(xbytes)
     comm = None
-    reserve = max(0, min(args.slab_reserve_cus, fft.cus - 1))
 
     def passes(contend):
         """per-rank (column, row) pass ms over `steps` emulated frames, and the mean wall ms per rank frame;
@@ -941,6 +952,9 @@ def p8_rank_projection(args, one_gpu_frame_ms: float, ranks: int = 8) -> dict:
                                          "rate): assumes the pipelined frame overlaps the two perfectly; "
                                          "projected_speedup_rccl_copy_contention uses the RCCL self-copy at HBM speed "
                                          "(the upper bound on contention) instead")
+        if masked:
+            out["cu_masks"] = (f"passes on logical CUs [0, {dev_cus - reserve}), exchange traffic on "
+                               f"[{dev_cus - reserve}, {dev_cus})")
     finally:
         fft.set_cu_budget(0)
         if comm is not None:
@@ -950,6 +964,9 @@ def p8_rank_projection(args, one_gpu_frame_ms: float, ranks: int = 8) -> dict:
         for g in slabs:
             g.close()
         fft.close()
+        torch.cuda.synchronize()
+        for h in raw_streams:
+            stream_destroy(h)
     return out
 
 
@@ -1162,6 +1179,10 @@ def main(argv=None):
                 one = sl["ms_per_frame"] if sl.get("exchange_bytes_per_rank", 0) == 0 and "exchange_only_ms" not in sl \
                     else sl["column_pass_ms"] + sl["row_pass_ms"]
                 sl["p8_rank_projection"] = p8_rank_projection(args, one)
+                try:
+                    sl["p8_rank_projection_cu_masked"] = p8_rank_projection(args, one, masked=True)
+                except Exception as e:  # reported, never fatal
+                    sl["p8_rank_projection_cu_masked"] = {"error": f"{type(e).__name__}: {e}"}
         except Exception as e:  # reported, never fatal to the headline measurement
             out["slab"] = dict(out.get("slab", {}), error=f"{type(e).__name__}: {e}")
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

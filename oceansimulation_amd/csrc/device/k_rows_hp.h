@@ -22,15 +22,21 @@ namespace oceanfft
 
 // x index n = n1 + 16 n2 (n1 < 16, n2 < 256), output k = k2 + 256 k1:
 //   X(k2 + 256 k1) = sum_n1 W_16^(n1 k1) [W_N^(n1 k2) Y_n1(k2)],  Y_n1(k2) = sum_n2 x(n1 + 16 n2) W_256^(n2 k2).
-// LDS slot of (n1, j), 8-B halves: n1 RS + (j ^ ((n1 >> 2) & 3)), RS = 4 (mod 16), as k_rows_xp.
+// LDS slot of (n1, j), 8-B halves: n1 RS + (j ^ g(n1)), RS = 8 (mod 32), g(n1) = ((n1 >> 1) & 7) ^
+// (((n1 >> 1) & 1) << 2). MI355X_MICROARCH.md §LDS banks ds_write_b64 in 16-lane groups (8-B slot mod 16)
+// and ds_read_b64 in 32-lane groups (slot mod 32); with this layout all four access shapes are
+// conflict-free: T_in's writes (16 consecutive n1 at one j), T_in's reads and T_out's writes (4 n1 of
+// one wave x 8 or 4 consecutive j), T_out's reads (32 consecutive j at one n1). (RS = 260 with the XOR
+// of (n1 >> 2) & 3 left T_in's reads 2-way; tools/xp_model.py checks the bank multiplicities.)
 struct HpCfg
 {
-  static constexpr int LOGN = 12, RS = 260;
+  static constexpr int LOGN = 12, RS = 264;
   static constexpr int TW = ((FftShape<LOGN>::TW_ENTRIES * 8 + 15) / 16) * 16;
   static constexpr int LDS = TW + 16 * RS * 8;
 };
 
-__device__ __forceinline__ int hp_slot(int n1, int j) { return n1 * HpCfg::RS + (j ^ ((n1 >> 2) & 3)); }
+__device__ __forceinline__ int hp_swz(int n1) { return ((n1 >> 1) & 7) ^ (((n1 >> 1) & 1) << 2); }
+__device__ __forceinline__ int hp_slot(int n1, int j) { return n1 * HpCfg::RS + (j ^ hp_swz(n1)); }
 
 // One row (both images; C loaded once, kept for image 1) per 256-thread workgroup, four per CU, the
 // 4 rows of a gc line on one XCD; default-policy loads, streamed stores (production k_rows_half's
@@ -148,7 +154,7 @@ __global__ __launch_bounds__(256, 4) void k_rows_hp(FrameParams fp, const float4
       // ---- T_in (own lanes at n = i + m T, the -u lanes at N - n, thread 0's v[8] at N/2)
       const int w = tid >> 6, l = tid & 63, s = l & 3, p = l >> 2;
       const int n1r = 4 * w + s;
-      const int rd = n1r * RS + (p ^ (w & 3));  // + 16 m: x(n1r + 16 (p + 16 m))
+      const int rd = n1r * RS + (p ^ hp_swz(n1r));  // + 16 m: x(n1r + 16 (p + 16 m))
       const int wo = hp_slot(i & 15, i >> 4);   // + 16 m
       const int nm = N - i;
       const int wm = hp_slot(nm & 15, nm >> 4);  // - 16 m
@@ -192,7 +198,7 @@ __global__ __launch_bounds__(256, 4) void k_rows_hp(FrameParams fp, const float4
         __syncthreads();
 #pragma unroll
         for (int n1 = 0; n1 < 16; n1++)
-          set_half(v[n1], h, xs[n1 * RS + (tid ^ ((n1 >> 2) & 3))]);
+          set_half(v[n1], h, xs[n1 * RS + (tid ^ hp_swz(n1))]);
       }
       idft16(v);  // v[k1] = X(tid + T k1)
       float4* dst = maps + ((size_t)cimg * nrows + y) * N;

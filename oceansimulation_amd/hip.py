@@ -45,6 +45,30 @@ def from_host(dev_ptr: int, arr: np.ndarray) -> None:
     _check(hip().hipMemcpy(ctypes.c_void_p(dev_ptr), arr.ctypes.data, arr.nbytes, H2D), "hipMemcpy H2D")
 
 
+def stream_with_cu_mask(cus, n_cus: int) -> int:
+    """hipExtStreamCreateWithCUMask: a non-default stream whose kernels run only on the CUs listed in
+    `cus` (logical CU indices < n_cus). Returns the hipStream_t as an int (wrap it with
+    torch.cuda.ExternalStream); release with stream_destroy."""
+    h = hip()
+    words = (n_cus + 31) // 32
+    mask = (ctypes.c_uint32 * words)()
+    for c in cus:
+        mask[c // 32] |= 1 << (c % 32)
+    h.hipExtStreamCreateWithCUMask.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_uint32,
+                                               ctypes.POINTER(ctypes.c_uint32)]
+    h.hipExtStreamCreateWithCUMask.restype = ctypes.c_int
+    s = ctypes.c_void_p()
+    _check(h.hipExtStreamCreateWithCUMask(ctypes.byref(s), words, mask), "hipExtStreamCreateWithCUMask")
+    return int(s.value)
+
+
+def stream_destroy(stream: int) -> None:
+    h = hip()
+    h.hipStreamDestroy.argtypes = [ctypes.c_void_p]
+    h.hipStreamDestroy.restype = ctypes.c_int
+    _check(h.hipStreamDestroy(ctypes.c_void_p(stream)), "hipStreamDestroy")
+
+
 def synchronize() -> None:
     _check(hip().hipDeviceSynchronize(), "hipDeviceSynchronize")
 

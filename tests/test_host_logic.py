@@ -272,3 +272,4 @@ def test_xp_hp_index_model():
     spec.loader.exec_module(m)
     assert m.model_xp() < 1e-12
     assert m.model_hp() < 1e-12
+    assert m.hp_bank_multiplicity() == 1  # k_rows_hp's four LDS access shapes are conflict-free

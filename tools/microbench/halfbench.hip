@@ -228,7 +228,7 @@ int main(int argc, char** argv)
       dj = std::max(dj, (double)std::fabs(ja[k] - jb2[k]));
       aj = std::max(aj, (double)std::fabs(ja[k]));
     }
-    std::printf("k_rows_hp vs production rows: maps max|diff| %.3g of max %.3g (%.2g), jacobian %.3g of %.3g (grid %d)\n", dm, am,
+    std::printf("k_rows_hp vs k_rows_half: maps max|diff| %.3g of max %.3g (%.2g), jacobian %.3g of %.3g (grid %d)\n", dm, am,
                 dm / am, dj, aj, hgrid);
     std::vector<std::vector<float>> tr(2);
     for (int r = 0; r < 9; r++)
@@ -238,7 +238,7 @@ int main(int argc, char** argv)
     }
     for (int k = 0; k < 2; k++)
       std::sort(tr[k].begin(), tr[k].end());
-    std::printf("rows, production k_rows_half   median %7.3f ms  %7.1f GB/s at 56 B/pt\n", tr[0][4], 56.04 * pts / tr[0][4] / 1e6);
+    std::printf("rows, k_rows_half (round 3)     median %7.3f ms  %7.1f GB/s at 56 B/pt\n", tr[0][4], 56.04 * pts / tr[0][4] / 1e6);
     std::printf("rows, k_rows_hp (permlane/DPP) median %7.3f ms  %7.1f GB/s at 56 B/pt\n", tr[1][4], 56.04 * pts / tr[1][4] / 1e6);
     return 0;
   }

@@ -8,11 +8,20 @@ permlane / DPP swaps are checked on the GPU by tools/microbench/rm16bench (lane_
 Usage: python tools/xp_model.py"""
 import numpy as np
 
-RS = 260
+RS = 260  # k_rows_xp
+RS_HP = 264  # k_rows_hp
 
 
 def slot(n1, j):
     return n1 * RS + (j ^ ((n1 >> 2) & 3))
+
+
+def hp_swz(n1):
+    return ((n1 >> 1) & 7) ^ (((n1 >> 1) & 1) << 2)
+
+
+def slot_hp(n1, j):
+    return n1 * RS_HP + (j ^ hp_swz(n1))
 
 
 def W(e, n):
@@ -38,7 +47,7 @@ def swap_reg_lane(v, rb, lb):
     return out
 
 
-def fill_tin(x, N, T, sub_bits):
+def fill_tin(x, N, T, sub_bits, slot=slot):
     """T_in writes as the kernels do (own lanes at i + m T, mirror lanes at N - i - m T, thread 0's
     m = 0 mirror at N/2) and checks every slot holds x(n) at slot(n mod 2^sub_bits, n >> sub_bits)"""
     nsub = 1 << sub_bits
@@ -112,13 +121,13 @@ def model_hp(seed=2):
     N, T = 4096, 256
     rng = np.random.default_rng(seed)
     x = rng.standard_normal(N) + 1j * rng.standard_normal(N)
-    lds = fill_tin(x, N, T, 4)
+    lds = fill_tin(x, N, T, 4, slot_hp)
     v = np.zeros((T, 16), complex)
     tid = np.arange(T)
     w, l = tid >> 6, tid & 63
     s, p = l & 3, l >> 2
     n1r = 4 * w + s
-    rd = n1r * RS + (p ^ (w & 3))
+    rd = n1r * RS_HP + (p ^ hp_swz(n1r))
     for t in range(T):
         for m in range(16):
             v[t, m] = lds[rd[t] + 16 * m]
@@ -134,7 +143,7 @@ def model_hp(seed=2):
             lds2[rd[t] + 16 * m] = v[t, m]
     for t in range(T):
         for n1 in range(16):
-            v[t, n1] = lds2[n1 * RS + (t ^ ((n1 >> 2) & 3))]
+            v[t, n1] = lds2[n1 * RS_HP + (t ^ hp_swz(n1))]
     v = idft(v, 1)
     X = np.zeros(N, complex)
     for t in range(T):
@@ -144,6 +153,23 @@ def model_hp(seed=2):
     return np.max(np.abs(X - ref)) / np.max(np.abs(ref))
 
 
+def hp_bank_multiplicity():
+    """Worst bank multiplicity of k_rows_hp's four LDS access shapes (MI355X_MICROARCH.md §LDS:
+    ds_write_b64 in 16-lane groups, bank of 8-B slot mod 16; ds_read_b64 in 32-lane groups, mod 32):
+    T_in writes (16 consecutive n1, one j), T_in reads (lanes s + 4 p: n1 = 4 w + s, j = p + 16 m),
+    T_out writes (the same slots, 16-lane groups), T_out reads (32 consecutive j, one n1). 1 = conflict-free."""
+    def mult(v):
+        return max(v.count(a) for a in v)
+    w1 = max(mult([slot_hp(t, j) % 16 for t in range(16)]) for j in range(256))
+    r1 = max(mult([slot_hp(4 * w + s, p + 8 * hh + 16 * m) % 32 for p in range(8) for s in range(4)])
+             for w in range(4) for m in range(16) for hh in range(2))
+    w2 = max(mult([slot_hp(4 * w + s, p + 4 * q + 16 * m) % 16 for p in range(4) for s in range(4)])
+             for w in range(4) for m in range(16) for q in range(4))
+    r2 = max(mult([slot_hp(n1, k0 + k) % 32 for k in range(32)]) for n1 in range(16) for k0 in range(0, 256, 32))
+    return max(w1, r1, w2, r2)
+
+
 if __name__ == "__main__":
+    print(f"k_rows_hp LDS bank multiplicity (1 = conflict-free): {hp_bank_multiplicity()}")
     print(f"k_rows_xp model (16384): max |X - N ifft(x)| / max = {model_xp():.2e}")
     print(f"k_rows_hp model (4096):  max |X - N ifft(x)| / max = {model_hp():.2e}")

@@ -99,6 +99,8 @@ def parse(argv=None):
                     help="CUs left free for RCCL's copy kernels while the slab passes overlap the all-to-all "
                          "(28: a P = 8 rank's 2048 rows of 16384 run in 9 rounds of one-row workgroups on 228 CUs, "
                          "10 on 224)")
+    ap.add_argument("--slab-mask-layouts", default="",
+                    help="comma-separated reserved-CU layouts (top, xcd, stride) for extra CU-masked 8-rank projections")
     ap.add_argument("--shared-gpu", action="store_true",
                     help="rehearsal: every rank on GPU 0 with gloo collectives and host-staged exchanges "
                          "(exercises the N > 1 paths on a one-GPU machine; not a measurement)")
@@ -772,7 +774,22 @@ XGMI_LINK_GBS_BIDIR = 153.6
 XGMI_ONE_WAY_GBS = XGMI_LINKS * XGMI_LINK_GBS_BIDIR / 2.0  # 537.6 GB/s per rank, one direction
 
 
-def p8_rank_projection(args, one_gpu_frame_ms: float, ranks: int = 8, masked: bool = False) -> dict:
+def reserved_cu_set(layout: str, dev_cus: int, reserve: int):
+    """The logical CU indices (hipExtStreamCreateWithCUMask bits) left to the exchange: "top" = the last
+    `reserve`; "xcd" = the same number at the top of every 32-CU block (one block per XCD if the logical
+    numbering is XCD-major); "stride" = every (dev_cus / reserve)-th CU (one per XCD per step if the
+    numbering interleaves the XCDs)."""
+    if layout == "top":
+        return list(range(dev_cus - reserve, dev_cus))
+    if layout == "xcd":
+        blocks = max(1, dev_cus // 32)
+        per = max(1, reserve // blocks)
+        return [b * 32 + 32 - 1 - k for b in range(blocks) for k in range(per)]
+    step = max(1, dev_cus // reserve)
+    return list(range(step - 1, dev_cus, step))[:reserve]
+
+
+def p8_rank_projection(args, one_gpu_frame_ms: float, ranks: int = 8, masked: str = "") -> dict:
     """The per-rank cost of BASELINE configs[4] (the 16384^2 grid over 8 GPUs) measured on ONE GPU, and
     the 8-GPU frame it implies. All 8 ranks' SlabGenerators run in this process on one compute stream;
     frames are emulated with the equal-split all-to-all as device copies (slab.emulate_frame) and each
@@ -809,8 +826,10 @@ def p8_rank_projection(args, one_gpu_frame_ms: float, ranks: int = 8, masked: bo
     reserve = max(0, min(args.slab_reserve_cus, dev_cus - 1))
     raw_streams = []
     if masked:
-        raw_streams = [stream_with_cu_mask(range(0, dev_cus - reserve), dev_cus),
-                       stream_with_cu_mask(range(dev_cus - reserve, dev_cus), dev_cus)]
+        res = set(reserved_cu_set(masked, dev_cus, reserve))
+        reserve = len(res)
+        raw_streams = [stream_with_cu_mask([c for c in range(dev_cus) if c not in res], dev_cus),
+                       stream_with_cu_mask(sorted(res), dev_cus)]
         comp, side = (torch.cuda.ExternalStream(h) for h in raw_streams)
     else:
         comp = torch.cuda.Stream()  # the generators' stream (non-blocking, so the exchange stream runs beside it)
@@ -953,8 +972,7 @@ def p8_rank_projection(args, one_gpu_frame_ms: float, ranks: int = 8, masked: bo
                                          "projected_speedup_rccl_copy_contention uses the RCCL self-copy at HBM speed "
                                          "(the upper bound on contention) instead")
         if masked:
-            out["cu_masks"] = (f"passes on logical CUs [0, {dev_cus - reserve}), exchange traffic on "
-                               f"[{dev_cus - reserve}, {dev_cus})")
+            out["cu_masks"] = f"layout {masked}: exchange traffic on logical CUs {sorted(res)}, the passes on the rest"
     finally:
         fft.set_cu_budget(0)
         if comm is not None:
@@ -1179,10 +1197,11 @@ def main(argv=None):
                 one = sl["ms_per_frame"] if sl.get("exchange_bytes_per_rank", 0) == 0 and "exchange_only_ms" not in sl \
                     else sl["column_pass_ms"] + sl["row_pass_ms"]
                 sl["p8_rank_projection"] = p8_rank_projection(args, one)
-                try:
-                    sl["p8_rank_projection_cu_masked"] = p8_rank_projection(args, one, masked=True)
-                except Exception as e:  # reported, never fatal
-                    sl["p8_rank_projection_cu_masked"] = {"error": f"{type(e).__name__}: {e}"}
+                for lay in args.slab_mask_layouts.split(",") if args.slab_mask_layouts else []:
+                    try:
+                        sl[f"p8_rank_projection_cu_masked_{lay}"] = p8_rank_projection(args, one, masked=lay)
+                    except Exception as e:  # reported, never fatal
+                        sl[f"p8_rank_projection_cu_masked_{lay}"] = {"error": f"{type(e).__name__}: {e}"}
         except Exception as e:  # reported, never fatal to the headline measurement
             out["slab"] = dict(out.get("slab", {}), error=f"{type(e).__name__}: {e}")
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

@@ -885,4 +885,179 @@ inline hipError_t launch_ifft_fourstep_ab(int logn, int n_images, float4* images
   return hipSuccess;
 }
 
+// k_rows_xs with a streaming T_in (round 4 A/B): each of the 8 kept elements' own and -u CPairs is formed
+// and its re-half written to the LDS at once (the slots are free after the first barrier); only the
+// im-halves stay in registers (32 VGPRs instead of the 16 CPairs' 64) until the second T_in half. The
+// registers freed carry a deeper prefetch of the next image's field loads (PF up to 6 of 8).
+template <int LOGN, int PF>
+__global__ __launch_bounds__(1024) void k_rows_xs2(FrameParams fp, const float4* __restrict__ spec, float4* __restrict__ maps,
+                                                   float* __restrict__ jac, FoamParams foam,
+                                                   const float2* __restrict__ tw_glob, int rows, RowSrc rs,
+                                                   const float2* __restrict__ tw2_glob)
+{
+  using S = FftShape<LOGN>;
+  using X = XsCfg<LOGN>;
+  constexpr int N = S::N, T = S::T, L2 = X::L2, RS = X::RS;
+  static_assert(T == 1024, "one 16-wave row per workgroup");
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  float2* tw = reinterpret_cast<float2*>(smem);
+  float2* tw2 = reinterpret_cast<float2*>(smem + X::TW1);
+  float2* xs = reinterpret_cast<float2*>(smem + X::TW1 + X::TW2);
+  for (int e = threadIdx.x; e < FftShape<L2>::TW_ENTRIES; e += blockDim.x)
+    tw2[e] = tw2_glob[e];
+  load_twiddles<LOGN>(tw, tw_glob);
+
+  const int total = fp.cascades * rows;
+  const float dim = (float)N;
+  const int lcpr = 31 - __builtin_clz(rs.cpr), cmask = rs.cpr - 1;
+  const int wave0 = __builtin_amdgcn_readfirstlane((int)threadIdx.x & ~63);
+  float4 fp4[8], nx4[8];
+  auto issue = [&](int item, int img, float4* p4, int m0, int m1) __attribute__((always_inline)) {
+    const int c = item / rows, yl = item - c * rows;
+    const size_t base = ((size_t)c * rows + yl) * rs.lp;
+    const int i = opaque((int)threadIdx.x);
+#pragma unroll
+    for (int m = m0; m < m1; m++)
+    {
+      const int src = (m * T + sopaque(wave0)) >> lcpr;
+      const size_t sb = (size_t)src * rs.src_stride;
+      p4[m] = ld4<kStream>(reinterpret_cast<const float4*>((img == 0 ? rs.ab : rs.de) + sb) + base,
+                           ((m * T + i) & cmask) * 16);
+    }
+  };
+  int item = blockIdx.x;
+  if (PF > 0 && item < total)
+    issue(item, 0, fp4, 0, PF);
+  for (; item < total; item += gridDim.x)
+  {
+    const int c = item / rows, yl = item - c * rows;
+    const float dk = fp.c[c].dk;
+    const float sgy = (yl & 1) ? -1.0f : 1.0f;
+    const size_t base = ((size_t)c * rows + yl) * rs.lp;
+#pragma unroll
+    for (int img = 0; img < 2; img++)
+    {
+      const int cimg = c * 2 + img;
+      const int tid = opaque((int)threadIdx.x), i = tid;
+      const float4* sp = spec + (size_t)cimg * N;
+      issue(item, img, fp4, PF, 8);
+      auto pslot = [&](int n) { return (n & 15) * RS + (n >> 4); };
+      // thread 0: the Nyquist column (u = -N/2) takes the -u lane of u = 0 (T_in slot N/2)
+      CPair nyq{};
+      if (i == 0)
+      {
+        const size_t ns = (size_t)rs.nyq_src * rs.src_stride;
+        const float kx = -(dim / 2.0f) * dk;
+        const float2 cc = ld2<kStream>(reinterpret_cast<const float2*>(rs.c + ns) + base, rs.cpr * 8);
+        const float4 t = ld4<kStream>(reinterpret_cast<const float4*>((img == 0 ? rs.ab : rs.de) + ns) + base,
+                                      rs.cpr * 16);
+        const CPair p = raw_pair(t);
+        if (img == 0)
+          nyq = CPair{f2v{(1.0f - kx) * p.re.x, -p.im.y - kx * cc.x}, f2v{(1.0f - kx) * p.im.x, p.re.y - kx * cc.y}};
+        else
+        {
+          const float kx2 = kx * kx;
+          nyq = CPair{f2v{-(p.im.x - kx2 * cc.y), -p.re.y + kx * p.im.x}, f2v{p.re.x - kx2 * cc.x, -p.im.y - kx * p.re.x}};
+        }
+      }
+      __syncthreads();  // the previous image's T_out reads are done: T_in's first half streams in now
+      float2 ho[8], hn[8];  // the im halves of the own and -u lanes, written after the first half
+#pragma unroll
+      for (int m = 0; m < 8; m++)
+      {
+        const int u = m * T + i;
+        const float kx = (float)u * dk;
+        const float4 s4 = ld4<0>(sp, (N / 2 - u) * 16);
+        const int src = (m * T + sopaque(wave0)) >> lcpr;
+        const float2 cc = ld2<0>(reinterpret_cast<const float2*>(rs.c + (size_t)src * rs.src_stride) + base,
+                                 (u & cmask) * 8);
+        CPair own, neg;
+        if (img == 0)
+        {
+          const CPair p = raw_pair(fp4[m]);
+          const float Ar = p.re.x, Ai = p.im.x, Br = p.re.y, Bi = p.im.y, Cr = cc.x, Ci = cc.y;
+          own = CPair{f2v{(1.0f - kx) * Ar, -Bi - kx * Cr}, f2v{(1.0f - kx) * Ai, Br - kx * Ci}};
+          neg = CPair{f2v{(1.0f + kx) * Ar + sgy * s4.x, -Bi + kx * Cr + sgy * s4.z},
+                      f2v{-(1.0f + kx) * Ai + sgy * s4.y, -Br - kx * Ci + sgy * s4.w}};
+        }
+        else
+        {
+          const CPair q = raw_pair(fp4[m]);
+          const float Cr = cc.x, Ci = cc.y, Dr = q.re.x, Di = q.im.x, Er = q.re.y, Ei = q.im.y;
+          const float kx2 = kx * kx;
+          own = CPair{f2v{-(Di - kx2 * Ci), -Er + kx * Di}, f2v{Dr - kx2 * Cr, -Ei - kx * Dr}};
+          neg = CPair{f2v{-(Di + kx2 * Ci) + sgy * s4.x, -Er - kx * Di + sgy * s4.z},
+                      f2v{-Dr - kx2 * Cr + sgy * s4.y, Ei - kx * Dr + sgy * s4.w}};
+        }
+        if (m == 0 && i == 0)
+          neg = nyq;
+        xs[pslot(i + m * T)] = half_of(own, 0);
+        xs[pslot(m == 0 && i == 0 ? N / 2 : N - i - m * T)] = half_of(neg, 0);
+        ho[m] = half_of(own, 1);
+        hn[m] = half_of(neg, 1);
+      }
+      if constexpr (PF > 0)
+      {
+        if (img == 0)
+          issue(item, 1, nx4, 0, PF);
+        else if (item + (int)gridDim.x < total)
+          issue(item + gridDim.x, 0, nx4, 0, PF);
+      }
+      const int w = tid >> 6, l = tid & 63;
+      CPair v[16];
+      __syncthreads();
+#pragma unroll
+      for (int m = 0; m < 16; m++)
+        set_half(v[m], 0, xs[w * RS + l + 64 * m]);
+      __syncthreads();
+#pragma unroll
+      for (int m = 0; m < 8; m++)
+      {
+        xs[pslot(i + m * T)] = ho[m];
+        xs[pslot(m == 0 && i == 0 ? N / 2 : N - i - m * T)] = hn[m];
+      }
+      __syncthreads();
+#pragma unroll
+      for (int m = 0; m < 16; m++)
+        set_half(v[m], 1, xs[w * RS + l + 64 * m]);
+      fft_run<L2, 0, true, true>(v, l, 0, l, 0, xs + w * RS, tw2);
+      const float2 base_w = twiddle<LOGN>(w * l, tw);
+#pragma unroll
+      for (int m = 0; m < 16; m++)
+        v[m] = cmul(v[m], base_w);
+      apply_stage_twiddles<LOGN>(v, 64 * w, tw);
+#pragma unroll
+      for (int h = 0; h < 2; h++)
+      {
+        if (h)
+          __syncthreads();
+#pragma unroll
+        for (int m = 0; m < 16; m++)
+          xs[w * RS + l + 64 * m] = half_of(v[m], h);
+        __syncthreads();
+#pragma unroll
+        for (int n1 = 0; n1 < 16; n1++)
+          set_half(v[n1], h, xs[n1 * RS + tid]);
+      }
+      idft16(v);
+      float4* dst = maps + ((size_t)cimg * rows + yl) * N;
+#pragma unroll
+      for (int m = 0; m < 16; m++)
+        st4<kStream>(dst + m * T, tid * 16, from_pair(v[m]));
+      if (img == 1)
+      {
+        const float lam = foam.displacement[c];
+        float* jb = jac + ((size_t)c * rows + yl) * N;
+#pragma unroll
+        for (int m = 0; m < 16; m++)
+          st1<kStream>(jb + m * T, tid * 4,
+                       (1.0f + lam * v[m].im.x) * (1.0f + lam * v[m].re.y) - lam * lam * v[m].im.y * v[m].im.y);
+      }
+#pragma unroll
+      for (int m = 0; m < PF; m++)
+        fp4[m] = nx4[m];
+    }
+  }
+}
+
 }  // namespace oceanfft

@@ -260,6 +260,9 @@ hipError_t launch_half_columns_ab(int logn, const FrameParams& fp, const float4*
                        : variant == 34 ? k_cols_half<LOGN, kStream, kStream, true, false, false, 2, 2, K::B, true, false, kHalfHL, kHalfHK>
                        : variant == 35 ? k_cols_half<LOGN, kStream, kStream, true, false, false, 4, 4, K::B, true, false, kHalfHL, kHalfHK>
                        : variant == 36 ? k_cols_half<LOGN, kStream, kStream, true, false, false, 1, 1, K::B, true, false, kHalfHL, kHalfHK>
+                       // 44 / 45: the next item's first 4 / 8 h0 chunks fetched into the LDS during round 2 (LPF)
+                       : variant == 44 ? k_cols_half<LOGN, kStream, kStream, true, false, false, RG, RGC, K::B, true, false, kHalfHL, HKW, (LOGN == 12 ? 4 : 0)>
+                       : variant == 45 ? k_cols_half<LOGN, kStream, kStream, true, false, false, RG, RGC, K::B, true, false, kHalfHL, HKW, (LOGN == 12 ? 8 : 0)>
                                       : k_cols_half<LOGN, kStream, kStream, true, false, false, RG, RGC, K::B, true, false, kHalfHL, HKW>;
       if (variant >= 12 && variant <= 14 && !seed)  // half-strip items (k_cols_half2): H in VGPRs
       {

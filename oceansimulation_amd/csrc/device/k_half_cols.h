@@ -93,13 +93,8 @@ __device__ __forceinline__ int half_group_offset(int y, int strip, int b = 0)
 // (16 B per thread each, after K::LDS1) and pairs [HL, HL + HK) in VGPRs from round 0 to round 2; only
 // the rest goes through the scratch. The scratch's HBM traffic (its lines are written back and, about
 // half of them, re-fetched: 1.30x algorithmic) costs 0.118 of 0.912 ms (halfbench_nohs).
-// LPF (whole grids, persistent grid): the next item's first LPF h0 chunks (m < LPF: rows m T .. of the
-// strip, 16 KiB each at N = 4096) are fetched straight into the LDS exchange area by
-// global_load_lds_dwordx4 once this item's last transform has left it, so they are in flight during the
-// round-2 stores and the item switch, and round 0 reads them from the LDS instead of waiting on HBM.
 template <int LOGN, int LA = 0, int SA = kStream, bool HS = false, bool SLAB = false, bool SEED = false, int RG = 1,
-          int RGC = 1, int CPI = ColFirstCfg<LOGN>::B, bool HP = false, bool PC = false, int HL = 0, int HK = 0,
-          int LPF = 0>
+          int RGC = 1, int CPI = ColFirstCfg<LOGN>::B, bool HP = false, bool PC = false, int HL = 0, int HK = 0>
 __global__ __launch_bounds__(FftShape<LOGN>::T * CPI, CPI < ColFirstCfg<LOGN>::B ? 4 : 1) void k_cols_half(FrameParams fp, const float4* __restrict__ h0,
                                                                      float4* __restrict__ gab, float4* __restrict__ gde,
                                                                      float2* __restrict__ gc,
@@ -124,27 +119,6 @@ __global__ __launch_bounds__(FftShape<LOGN>::T * CPI, CPI < ColFirstCfg<LOGN>::B
   const int nstrips = SLAB ? hsl.nstrips : STRIPS;
   const int total = fp.cascades * nstrips * HALVES;
   const float dim = (float)N;
-  static_assert(LPF == 0 || (!SLAB && !SEED && HALVES == 1 && LPF * WG * 16 <= K::LDS1), "LDS prefetch of whole-grid h0");
-  // LPF: h0 chunks of item `it` into the exchange area, lane-linear per wave (slot m WG + tid)
-  auto lds_prefetch = [&](int it) __attribute__((always_inline)) {
-    const int c_ = it / nstrips, s_ = it - c_ * nstrips;
-    const int xb_ = s_ == STRIPS - 1 ? 0 : N / (2 * B) + s_;
-    // buffer form: one descriptor (SGPRs) and one lane offset instead of a 64-bit address per load;
-    // the piece offset rides in the lane offset, as every production load does (device/memory.h)
-    const auto rsrc = srd(h0 + ((size_t)c_ * (N / B) + xb_) * N * B, kAllBytes);
-    const int lane_off = opaque((int)threadIdx.x) * 16;
-    const int wbase = __builtin_amdgcn_readfirstlane((int)threadIdx.x & ~63) * 16;
-#pragma unroll
-    for (int m = 0; m < LPF; m++)
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(
-          rsrc, (__attribute__((address_space(3))) void*)(static_cast<unsigned char*>(xch) + m * WG * 16 + wbase), 16,
-          lane_off + ((m + 8) & 15) * T * B * 16, 0, 0, LA);
-  };
-  if constexpr (LPF > 0)
-  {
-    if ((int)blockIdx.x < total)
-      lds_prefetch(blockIdx.x);
-  }
   for (int item = HALVES > 1 ? xcd_pair_slot(blockIdx.x, gridDim.x) : blockIdx.x; item < total; item += gridDim.x)
   {
     const int hh = HALVES > 1 ? item % HALVES : 0, si = HALVES > 1 ? item / HALVES : item;
@@ -233,10 +207,7 @@ __global__ __launch_bounds__(FftShape<LOGN>::T * CPI, CPI < ColFirstCfg<LOGN>::B
         float2 hprev = make_float2(0.0f, 0.0f);
 #pragma unroll
         for (int m = 0; m < 16; m++)  // fftShift on y folded into the load
-          a[m] = m < LPF ? reinterpret_cast<const float4*>(xch)[m * WG + threadIdx.x]
-                         : ld4s<LA>(src, voff, ((m + 8) & 15) * T * B * 16);
-        if constexpr (LPF > 0)
-          __syncthreads();  // every wave has its chunks before the transform's first exchange reuses the area
+          a[m] = ld4s<LA>(src, voff, ((m + 8) & 15) * T * B * 16);
 #pragma unroll
         for (int m = 0; m < 16; m++)
         {
@@ -295,12 +266,6 @@ __global__ __launch_bounds__(FftShape<LOGN>::T * CPI, CPI < ColFirstCfg<LOGN>::B
         }
       }
       fft_run<LOGN, CPI, true>(v, i, HALVES > 1 ? opaque((int)threadIdx.x) % CPI : b, xch, tw);
-      if constexpr (LPF > 0)
-      {
-        // the transform's last exchange ended with a barrier: the area is free for the next item's h0
-        if (round == 2 && item + (int)gridDim.x < total)
-          lds_prefetch(item + gridDim.x);
-      }
 #pragma unroll
       for (int m = 0; m < 16; m++)
       {

@@ -1,6 +1,10 @@
 // device/k_rows_xs.h — the row pass of N = 16384 (the four-step path's blocks, RowSrc): one row of both
 // images per 1024-thread workgroup with the x transform in four steps (XS, as k_rows_half<.., XS>),
-// and the next image's field loads in flight during the current image's transform (PF).
+// the next image's field loads in flight during the current image's transform (PF), and a streaming
+// T_in (round 4): each kept element's own and -u CPairs are formed and their re-halves written to the
+// LDS at once, only the im-halves wait in registers for the second half. 3.738 -> 3.680 ms per 16384^2
+// pass (tools/microbench/rm16bench, profiles/r04_rm16bench_xs2.log; the round-3 form is k_rows_xs_r3
+// in tools/microbench/ab_kernels.h; maps within 1e-7 of it, FMA contraction differs per kernel).
 #pragma once
 
 #include <hip/hip_runtime.h>
@@ -27,9 +31,9 @@ namespace oceanfft
 // L2): keeping it (16 VGPRs) beside the prefetch spills.
 template <int LOGN, int PF>
 __global__ __launch_bounds__(1024) void k_rows_xs(FrameParams fp, const float4* __restrict__ spec, float4* __restrict__ maps,
-                                                  float* __restrict__ jac, FoamParams foam,
-                                                  const float2* __restrict__ tw_glob, int rows, RowSrc rs,
-                                                  const float2* __restrict__ tw2_glob)
+                                                   float* __restrict__ jac, FoamParams foam,
+                                                   const float2* __restrict__ tw_glob, int rows, RowSrc rs,
+                                                   const float2* __restrict__ tw2_glob)
 {
   using S = FftShape<LOGN>;
   using X = XsCfg<LOGN>;
@@ -45,12 +49,8 @@ __global__ __launch_bounds__(1024) void k_rows_xs(FrameParams fp, const float4* 
 
   const int total = fp.cascades * rows;
   const float dim = (float)N;
-  // Source block of column u: u >> lcpr (cpr a power of two, launch_rm_rows), wave-uniform because
-  // cpr is a multiple of 64: computed on the scalar unit from the wave's first column, so a load's
-  // address costs one VALU mask instead of a division.
   const int lcpr = 31 - __builtin_clz(rs.cpr), cmask = rs.cpr - 1;
   const int wave0 = __builtin_amdgcn_readfirstlane((int)threadIdx.x & ~63);
-  // the 8 kept elements u = m T + tid of one image: (A, B) or (D, E)
   float4 fp4[8], nx4[8];
   auto issue = [&](int item, int img, float4* p4, int m0, int m1) __attribute__((always_inline)) {
     const int c = item / rows, yl = item - c * rows;
@@ -59,7 +59,7 @@ __global__ __launch_bounds__(1024) void k_rows_xs(FrameParams fp, const float4* 
 #pragma unroll
     for (int m = m0; m < m1; m++)
     {
-      const int src = (m * T + sopaque(wave0)) >> lcpr;  // source block (scalar, computed here: not hoisted)
+      const int src = (m * T + sopaque(wave0)) >> lcpr;
       const size_t sb = (size_t)src * rs.src_stride;
       p4[m] = ld4<kStream>(reinterpret_cast<const float4*>((img == 0 ? rs.ab : rs.de) + sb) + base,
                            ((m * T + i) & cmask) * 16);
@@ -72,7 +72,7 @@ __global__ __launch_bounds__(1024) void k_rows_xs(FrameParams fp, const float4* 
   {
     const int c = item / rows, yl = item - c * rows;
     const float dk = fp.c[c].dk;
-    const float sgy = (yl & 1) ? -1.0f : 1.0f;  // (-1)^q of the Nyquist-row term (rows start at an even q)
+    const float sgy = (yl & 1) ? -1.0f : 1.0f;
     const size_t base = ((size_t)c * rows + yl) * rs.lp;
 #pragma unroll
     for (int img = 0; img < 2; img++)
@@ -80,39 +80,12 @@ __global__ __launch_bounds__(1024) void k_rows_xs(FrameParams fp, const float4* 
       const int cimg = c * 2 + img;
       const int tid = opaque((int)threadIdx.x), i = tid;
       const float4* sp = spec + (size_t)cimg * N;
-      issue(item, img, fp4, PF, 8);  // the elements not prefetched
-      CPair v[16];  // own lanes in v[m], the -u lanes in v[m + 8] until the transposition
-#pragma unroll
-      for (int m = 0; m < 8; m++)
-      {
-        const int u = m * T + i;
-        const float kx = (float)u * dk;
-        const float4 s4 = ld4<0>(sp, (N / 2 - u) * 16);  // the -u column's Nyquist-row term (x = N/2 - u)
-        const int src = (m * T + sopaque(wave0)) >> lcpr;
-        const float2 cc = ld2<0>(reinterpret_cast<const float2*>(rs.c + (size_t)src * rs.src_stride) + base,
-                                 (u & cmask) * 8);  // C
-        if (img == 0)
-        {
-          const CPair p = raw_pair(fp4[m]);  // (A, B)
-          const float Ar = p.re.x, Ai = p.im.x, Br = p.re.y, Bi = p.im.y, Cr = cc.x, Ci = cc.y;
-          v[m] = CPair{f2v{(1.0f - kx) * Ar, -Bi - kx * Cr}, f2v{(1.0f - kx) * Ai, Br - kx * Ci}};
-          v[m + 8] = CPair{f2v{(1.0f + kx) * Ar + sgy * s4.x, -Bi + kx * Cr + sgy * s4.z},
-                           f2v{-(1.0f + kx) * Ai + sgy * s4.y, -Br - kx * Ci + sgy * s4.w}};
-        }
-        else
-        {
-          const CPair q = raw_pair(fp4[m]);  // (D, E)
-          const float Cr = cc.x, Ci = cc.y, Dr = q.re.x, Di = q.im.x, Er = q.re.y, Ei = q.im.y;
-          const float kx2 = kx * kx;
-          v[m] = CPair{f2v{-(Di - kx2 * Ci), -Er + kx * Di}, f2v{Dr - kx2 * Cr, -Ei - kx * Dr}};
-          v[m + 8] = CPair{f2v{-(Di + kx2 * Ci) + sgy * s4.x, -Er - kx * Di + sgy * s4.z},
-                           f2v{-Dr - kx2 * Cr + sgy * s4.y, Ei - kx * Dr + sgy * s4.w}};
-        }
-      }
+      issue(item, img, fp4, PF, 8);
+      auto pslot = [&](int n) { return (n & 15) * RS + (n >> 4); };
+      // thread 0: the Nyquist column (u = -N/2) takes the -u lane of u = 0 (T_in slot N/2)
+      CPair nyq{};
       if (i == 0)
       {
-        // thread 0: the Nyquist column u = -N/2 (block nyq_src, column cpr) replaces the unused -u
-        // lane of u = 0 (T_in puts v[8] at n = N/2)
         const size_t ns = (size_t)rs.nyq_src * rs.src_stride;
         const float kx = -(dim / 2.0f) * dk;
         const float2 cc = ld2<kStream>(reinterpret_cast<const float2*>(rs.c + ns) + base, rs.cpr * 8);
@@ -120,14 +93,49 @@ __global__ __launch_bounds__(1024) void k_rows_xs(FrameParams fp, const float4* 
                                       rs.cpr * 16);
         const CPair p = raw_pair(t);
         if (img == 0)
-          v[8] = CPair{f2v{(1.0f - kx) * p.re.x, -p.im.y - kx * cc.x}, f2v{(1.0f - kx) * p.im.x, p.re.y - kx * cc.y}};
+          nyq = CPair{f2v{(1.0f - kx) * p.re.x, -p.im.y - kx * cc.x}, f2v{(1.0f - kx) * p.im.x, p.re.y - kx * cc.y}};
         else
         {
           const float kx2 = kx * kx;
-          v[8] = CPair{f2v{-(p.im.x - kx2 * cc.y), -p.re.y + kx * p.im.x}, f2v{p.re.x - kx2 * cc.x, -p.im.y - kx * p.re.x}};
+          nyq = CPair{f2v{-(p.im.x - kx2 * cc.y), -p.re.y + kx * p.im.x}, f2v{p.re.x - kx2 * cc.x, -p.im.y - kx * p.re.x}};
         }
       }
-      // the next image's fields: this row's (D, E), or the next row's (A, B) and C
+      __syncthreads();  // the previous image's T_out reads are done: T_in's first half streams in now
+      float2 ho[8], hn[8];  // the im halves of the own and -u lanes, written after the first half
+#pragma unroll
+      for (int m = 0; m < 8; m++)
+      {
+        const int u = m * T + i;
+        const float kx = (float)u * dk;
+        const float4 s4 = ld4<0>(sp, (N / 2 - u) * 16);
+        const int src = (m * T + sopaque(wave0)) >> lcpr;
+        const float2 cc = ld2<0>(reinterpret_cast<const float2*>(rs.c + (size_t)src * rs.src_stride) + base,
+                                 (u & cmask) * 8);
+        CPair own, neg;
+        if (img == 0)
+        {
+          const CPair p = raw_pair(fp4[m]);
+          const float Ar = p.re.x, Ai = p.im.x, Br = p.re.y, Bi = p.im.y, Cr = cc.x, Ci = cc.y;
+          own = CPair{f2v{(1.0f - kx) * Ar, -Bi - kx * Cr}, f2v{(1.0f - kx) * Ai, Br - kx * Ci}};
+          neg = CPair{f2v{(1.0f + kx) * Ar + sgy * s4.x, -Bi + kx * Cr + sgy * s4.z},
+                      f2v{-(1.0f + kx) * Ai + sgy * s4.y, -Br - kx * Ci + sgy * s4.w}};
+        }
+        else
+        {
+          const CPair q = raw_pair(fp4[m]);
+          const float Cr = cc.x, Ci = cc.y, Dr = q.re.x, Di = q.im.x, Er = q.re.y, Ei = q.im.y;
+          const float kx2 = kx * kx;
+          own = CPair{f2v{-(Di - kx2 * Ci), -Er + kx * Di}, f2v{Dr - kx2 * Cr, -Ei - kx * Dr}};
+          neg = CPair{f2v{-(Di + kx2 * Ci) + sgy * s4.x, -Er - kx * Di + sgy * s4.z},
+                      f2v{-Dr - kx2 * Cr + sgy * s4.y, Ei - kx * Dr + sgy * s4.w}};
+        }
+        if (m == 0 && i == 0)
+          neg = nyq;
+        xs[pslot(i + m * T)] = half_of(own, 0);
+        xs[pslot(m == 0 && i == 0 ? N / 2 : N - i - m * T)] = half_of(neg, 0);
+        ho[m] = half_of(own, 1);
+        hn[m] = half_of(neg, 1);
+      }
       if constexpr (PF > 0)
       {
         if (img == 0)
@@ -135,36 +143,29 @@ __global__ __launch_bounds__(1024) void k_rows_xs(FrameParams fp, const float4* 
         else if (item + (int)gridDim.x < total)
           issue(item + gridDim.x, 0, nx4, 0, PF);
       }
-      // x index n = n1 + 16 n2, output k = k2 + 1024 k1: T_in gives wave n1 = w the inputs x(w + 16 n2)
-      // (own lanes at n, the -u lanes at N - n, thread 0's Nyquist column at N/2); the wave's
-      // 1024-point sub-transform; times W_N^(n1 k2); T_out gives thread k2 = tid the 16 values
-      // Z_n1(k2); the 16-point DFT over n1 leaves v[k1] = X(tid + T k1). LDS slot of n: (n mod 16) RS + n / 16.
       const int w = tid >> 6, l = tid & 63;
-      auto pslot = [&](int n) { return (n & 15) * RS + (n >> 4); };
-      __syncthreads();  // the previous image's T_out reads are done
+      CPair v[16];
+      __syncthreads();
 #pragma unroll
-      for (int h = 0; h < 2; h++)
+      for (int m = 0; m < 16; m++)
+        set_half(v[m], 0, xs[w * RS + l + 64 * m]);
+      __syncthreads();
+#pragma unroll
+      for (int m = 0; m < 8; m++)
       {
-        if (h)
-          __syncthreads();
-#pragma unroll
-        for (int m = 0; m < 8; m++)
-        {
-          xs[pslot(i + m * T)] = half_of(v[m], h);
-          xs[pslot(m == 0 && i == 0 ? N / 2 : N - i - m * T)] = half_of(v[m + 8], h);
-        }
-        __syncthreads();
-#pragma unroll
-        for (int m = 0; m < 16; m++)
-          set_half(v[m], h, xs[w * RS + l + 64 * m]);
+        xs[pslot(i + m * T)] = ho[m];
+        xs[pslot(m == 0 && i == 0 ? N / 2 : N - i - m * T)] = hn[m];
       }
-      // region w is the wave's alone until T_out's first barrier: its exchanges need no barriers
-      fft_run<L2, 0, true, true>(v, l, 0, l, 0, xs + w * RS, tw2);  // v[m] = Y_w(l + 64 m)
+      __syncthreads();
+#pragma unroll
+      for (int m = 0; m < 16; m++)
+        set_half(v[m], 1, xs[w * RS + l + 64 * m]);
+      fft_run<L2, 0, true, true>(v, l, 0, l, 0, xs + w * RS, tw2);
       const float2 base_w = twiddle<LOGN>(w * l, tw);
 #pragma unroll
       for (int m = 0; m < 16; m++)
         v[m] = cmul(v[m], base_w);
-      apply_stage_twiddles<LOGN>(v, 64 * w, tw);  // x W_N^(w (l + 64 m))
+      apply_stage_twiddles<LOGN>(v, 64 * w, tw);
 #pragma unroll
       for (int h = 0; h < 2; h++)
       {
@@ -185,8 +186,6 @@ __global__ __launch_bounds__(1024) void k_rows_xs(FrameParams fp, const float4* 
         st4<kStream>(dst + m * T, tid * 16, from_pair(v[m]));
       if (img == 1)
       {
-        // displacementMap (Dz, dDx/dx, dDz/dz, dDx/dz) = (re0, im0, re1, im1): Jacobian,
-        // spectrum.compute:246-259
         const float lam = foam.displacement[c];
         float* jb = jac + ((size_t)c * rows + yl) * N;
 #pragma unroll
@@ -197,7 +196,6 @@ __global__ __launch_bounds__(1024) void k_rows_xs(FrameParams fp, const float4* 
 #pragma unroll
       for (int m = 0; m < PF; m++)
         fp4[m] = nx4[m];
-
     }
   }
 }

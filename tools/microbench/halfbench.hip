@@ -190,42 +190,6 @@ int main(int argc, char** argv)
     std::printf("rows, row layout (round 1)              median %7.3f ms  bit-identical %s\n", tr[1][4], same ? "yes" : "NO");
     return 0;
   }
-  if (argc > 3 && std::strcmp(argv[3], "lpf") == 0 && logn == 12)
-  {
-    // pass 1 with the next item's first 4 / 8 h0 chunks fetched into the LDS during round 2 (variants
-    // 44 / 45, buffer_load ... lds) against production: same arithmetic, the fields must match
-    CHECK(c1());
-    CHECK(hipDeviceSynchronize());
-    auto pab = snap(gab, ht * sizeof(float4)), pde = snap(gcd, ht * sizeof(float4)), pc = snap(ge, ht * sizeof(float2));
-    const int vars[] = {44, 45};
-    std::vector<std::function<hipError_t()>> runs = {c1};
-    for (int v : vars)
-      runs.push_back([&, v] { return launch_half_columns_ab(logn, fp, h0, gab, gcd, ge, spec, tw, 0, cus, hs, cus, nullptr, v); });
-    for (size_t k = 1; k < runs.size(); k++)
-    {
-      CHECK(hipMemset(gab, 0, ht * sizeof(float4)));
-      CHECK(hipMemset(gcd, 0, ht * sizeof(float4)));
-      CHECK(hipMemset(ge, 0, ht * sizeof(float2)));
-      CHECK(runs[k]());
-      CHECK(hipDeviceSynchronize());
-      std::printf("cols variant %d vs production: gab, gde, gc\n", vars[k - 1]);
-      const bool same = (int)diff(snap(gab, ht * sizeof(float4)), pab) & (int)diff(snap(gcd, ht * sizeof(float4)), pde) &
-                        (int)diff(snap(ge, ht * sizeof(float2)), pc);
-      std::printf("  bit-identical: %s\n", same ? "yes" : "NO");
-    }
-    std::vector<std::vector<float>> t(runs.size());
-    for (int r = 0; r < 9; r++)
-      for (size_t k = 0; k < runs.size(); k++)
-        t[k].push_back(time_ms(runs[k], 10));
-    for (size_t k = 0; k < runs.size(); k++)
-    {
-      std::sort(t[k].begin(), t[k].end());
-      std::printf("cols %-12s median %7.3f ms  %7.1f GB/s at 28 B/pt\n",
-                  k == 0 ? "production" : ("variant " + std::to_string(vars[k - 1])).c_str(), t[k][4],
-                  28.04 * pts / t[k][4] / 1e6);
-    }
-    return 0;
-  }
   if (argc > 3 && std::strcmp(argv[3], "hp") == 0 && logn == 12)
   {
     // row pass: production (k_rows_half, mirror exchange + fft_run<12>) against k_rows_hp (T_in with

@@ -189,8 +189,7 @@ int main()
       {"k_rows_xp (64 x 256, permlane/DPP), PF 0", mkp(k_rows_xp<LOGN, 0>), {}},
       {"k_rows_xp PF 2", mkp(k_rows_xp<LOGN, 2>), {}},
       {"k_rows_xp PF 3", mkp(k_rows_xp<LOGN, 3>), {}},
-      {"k_rows_xs2 (streaming T_in) PF 2", mkn(k_rows_xs2<LOGN, 2>), {}},
-      {"k_rows_xs2 PF 4", mkn(k_rows_xs2<LOGN, 4>), {}},
+      {"k_rows_xs_r3 (round-3 production) PF 2", mkn(k_rows_xs_r3<LOGN, 2>), {}},
   };
   // XS vs the plain transform: same lanes, different rounding order (max |diff| vs max |value|)
   auto snapf = [&](const void* p, size_t n) {
@@ -231,8 +230,7 @@ int main()
   compare(7, 10, "k_rows_xp PF 0 vs k_rows_xs PF 2");
   compare(7, 11, "k_rows_xp PF 2 vs k_rows_xs PF 2");
   compare(10, 12, "k_rows_xp PF 3 vs PF 0");
-  compare(7, 13, "k_rows_xs2 PF 2 vs k_rows_xs PF 2");
-  compare(7, 14, "k_rows_xs2 PF 4 vs k_rows_xs PF 2");
+  compare(13, 7, "k_rows_xs PF 2 (streaming T_in) vs round 3");
   for (int r = 0; r < 5; r++)
     for (auto& v : vs)
       v.t.push_back(time_ms(v.run, 3));

@@ -47,9 +47,7 @@ __device__ __forceinline__ int hp_slot(int n1, int j) { return n1 * HpCfg::RS + 
 //         n1 = 4 w + s (four 256-point sub-transforms per wave).
 //   sub-transform as k_rows_xp: v[b] = Y_n1(p + 16 b), then x W_N^(n1 (p + 16 b)).
 //   T_out: thread k2 = tid receives Z_n1(k2), n1 < 16; DFT-16: v[k1] = X(tid + 256 k1).
-// ST: streaming T_in (as k_rows_xs): each element's own and -u CPairs are formed and their re-halves
-// written to the LDS at once, only the im-halves wait in registers for the second half.
-template <int RG, int RGC, bool RM = false, bool ST = false>
+template <int RG, int RGC, bool RM = false>
 __global__ __launch_bounds__(256, 4) void k_rows_hp(FrameParams fp, const float4* __restrict__ gab,
                                                  const float4* __restrict__ gde, const float2* __restrict__ gc,
                                                  const float4* __restrict__ spec, float4* __restrict__ maps,
@@ -85,45 +83,7 @@ __global__ __launch_bounds__(256, 4) void k_rows_hp(FrameParams fp, const float4
       const int cimg = c * 2 + img;
       const float4* sp = spec + (size_t)cimg * N;
       const int tid = opaque((int)threadIdx.x), i = tid;
-      // thread 0: the Nyquist column u = -N/2 (first column of the last strip; RM: block nyq_src, column
-      // cpr) replaces the unused -u lane of u = 0 (T_in slot N/2)
-      CPair nyq{};
-      if (i == 0)
-      {
-        const int off = RM ? rs.cpr : half_group_offset<LOGN, RG>(y, N / 2 / B);
-        const int offc = RM ? off : half_group_offset<LOGN, RGC>(y, N / 2 / B);
-        const size_t ns = RM ? (size_t)rs.nyq_src * rs.src_stride : 0;
-        const float4* fab = RM ? reinterpret_cast<const float4*>(rs.ab + ns) : gab;
-        const float4* fde = RM ? reinterpret_cast<const float4*>(rs.de + ns) : gde;
-        const float2* fc = RM ? reinterpret_cast<const float2*>(rs.c + ns) : gc;
-        const float kx = -(dim / 2.0f) * dk;
-        if (RM || img == 0)
-          cnyq = ld2<0>(fc + base, offc * 8);
-        const float2 cc = cnyq;
-        if (img == 0)
-        {
-          const CPair p = raw_pair(ld4<LA>(fab + base, off * 16));
-          nyq = CPair{f2v{(1.0f - kx) * p.re.x, -p.im.y - kx * cc.x}, f2v{(1.0f - kx) * p.im.x, p.re.y - kx * cc.y}};
-        }
-        else
-        {
-          const CPair q = raw_pair(ld4<LA>(fde + base, off * 16));
-          const float kx2 = kx * kx;
-          nyq = CPair{f2v{-(q.im.x - kx2 * cc.y), -q.re.y + kx * q.im.x}, f2v{q.re.x - kx2 * cc.x, -q.im.y - kx * q.re.x}};
-        }
-      }
-      // T_in slots: own lanes at n = i + m T, the -u lanes at N - n, thread 0's Nyquist column at N/2
-      const int w = tid >> 6, l = tid & 63, s = l & 3, p = l >> 2;
-      const int n1r = 4 * w + s;
-      const int rd = n1r * RS + (p ^ hp_swz(n1r));  // + 16 m: x(n1r + 16 (p + 16 m))
-      const int wo = hp_slot(i & 15, i >> 4);   // + 16 m
-      const int nm = N - i;
-      const int wm = hp_slot(nm & 15, nm >> 4);  // - 16 m
-      const int wm0 = i == 0 ? hp_slot(0, (N / 2) >> 4) : wm;
-      if constexpr (ST)
-        __syncthreads();  // the previous image's T_out reads are done: T_in's first half streams in
-      CPair v[16];  // !ST: own lanes in v[m], the -u lanes in v[m + 8] until T_in
-      float2 ho[ST ? 8 : 1], hn[ST ? 8 : 1];  // ST: the im-halves, written after the first half
+      CPair v[16];  // own lanes in v[m], the -u lanes in v[m + 8] until T_in
 #pragma unroll
       for (int m = 0; m < 8; m++)
       {
@@ -137,7 +97,6 @@ __global__ __launch_bounds__(256, 4) void k_rows_hp(FrameParams fp, const float4
         const float2* fc = RM ? reinterpret_cast<const float2*>(rs.c + (size_t)src * rs.src_stride) : gc;
         const float kx = (float)u * dk;
         const float4 s4 = ld4<0>(sp, (N / 2 - u) * 16);
-        CPair own, neg;
         if (img == 0)
         {
           const CPair p = raw_pair(ld4<LA>(fab + base, off * 16));
@@ -145,9 +104,9 @@ __global__ __launch_bounds__(256, 4) void k_rows_hp(FrameParams fp, const float4
           if constexpr (!RM)
             ckeep[m] = cc;
           const float Ar = p.re.x, Ai = p.im.x, Br = p.re.y, Bi = p.im.y, Cr = cc.x, Ci = cc.y;
-          own = CPair{f2v{(1.0f - kx) * Ar, -Bi - kx * Cr}, f2v{(1.0f - kx) * Ai, Br - kx * Ci}};
-          neg = CPair{f2v{(1.0f + kx) * Ar + sgy * s4.x, -Bi + kx * Cr + sgy * s4.z},
-                      f2v{-(1.0f + kx) * Ai + sgy * s4.y, -Br - kx * Ci + sgy * s4.w}};
+          v[m] = CPair{f2v{(1.0f - kx) * Ar, -Bi - kx * Cr}, f2v{(1.0f - kx) * Ai, Br - kx * Ci}};
+          v[m + 8] = CPair{f2v{(1.0f + kx) * Ar + sgy * s4.x, -Bi + kx * Cr + sgy * s4.z},
+                           f2v{-(1.0f + kx) * Ai + sgy * s4.y, -Br - kx * Ci + sgy * s4.w}};
         }
         else
         {
@@ -161,63 +120,61 @@ __global__ __launch_bounds__(256, 4) void k_rows_hp(FrameParams fp, const float4
             cc = ckeep[m];
           const float Cr = cc.x, Ci = cc.y, Dr = q.re.x, Di = q.im.x, Er = q.re.y, Ei = q.im.y;
           const float kx2 = kx * kx;
-          own = CPair{f2v{-(Di - kx2 * Ci), -Er + kx * Di}, f2v{Dr - kx2 * Cr, -Ei - kx * Dr}};
-          neg = CPair{f2v{-(Di + kx2 * Ci) + sgy * s4.x, -Er - kx * Di + sgy * s4.z},
-                      f2v{-Dr - kx2 * Cr + sgy * s4.y, Ei - kx * Dr + sgy * s4.w}};
+          v[m] = CPair{f2v{-(Di - kx2 * Ci), -Er + kx * Di}, f2v{Dr - kx2 * Cr, -Ei - kx * Dr}};
+          v[m + 8] = CPair{f2v{-(Di + kx2 * Ci) + sgy * s4.x, -Er - kx * Di + sgy * s4.z},
+                           f2v{-Dr - kx2 * Cr + sgy * s4.y, Ei - kx * Dr + sgy * s4.w}};
         }
-        if (m == 0 && i == 0)
-          neg = nyq;
-        if constexpr (ST)
+      }
+      if (i == 0)
+      {
+        // the Nyquist column u = -N/2 (first column of the last strip; RM: block nyq_src, column cpr)
+        // replaces the unused -u lane of u = 0
+        const int off = RM ? rs.cpr : half_group_offset<LOGN, RG>(y, N / 2 / B);
+        const int offc = RM ? off : half_group_offset<LOGN, RGC>(y, N / 2 / B);
+        const size_t ns = RM ? (size_t)rs.nyq_src * rs.src_stride : 0;
+        const float4* fab = RM ? reinterpret_cast<const float4*>(rs.ab + ns) : gab;
+        const float4* fde = RM ? reinterpret_cast<const float4*>(rs.de + ns) : gde;
+        const float2* fc = RM ? reinterpret_cast<const float2*>(rs.c + ns) : gc;
+        const float kx = -(dim / 2.0f) * dk;
+        if (RM || img == 0)
+          cnyq = ld2<0>(fc + base, offc * 8);
+        const float2 cc = cnyq;
+        if (img == 0)
         {
-          xs[wo + 16 * m] = half_of(own, 0);
-          xs[(m == 0 ? wm0 : wm) - 16 * m] = half_of(neg, 0);
-          ho[m] = half_of(own, 1);
-          hn[m] = half_of(neg, 1);
+          const CPair p = raw_pair(ld4<LA>(fab + base, off * 16));
+          v[8] = CPair{f2v{(1.0f - kx) * p.re.x, -p.im.y - kx * cc.x}, f2v{(1.0f - kx) * p.im.x, p.re.y - kx * cc.y}};
         }
         else
         {
-          v[m] = own;
-          v[m + 8] = neg;
+          const CPair q = raw_pair(ld4<LA>(fde + base, off * 16));
+          const float kx2 = kx * kx;
+          v[8] = CPair{f2v{-(q.im.x - kx2 * cc.y), -q.re.y + kx * q.im.x}, f2v{q.re.x - kx2 * cc.x, -q.im.y - kx * q.re.x}};
         }
       }
-      // ---- T_in
-      if constexpr (ST)
-      {
-        __syncthreads();
+      // ---- T_in (own lanes at n = i + m T, the -u lanes at N - n, thread 0's v[8] at N/2)
+      const int w = tid >> 6, l = tid & 63, s = l & 3, p = l >> 2;
+      const int n1r = 4 * w + s;
+      const int rd = n1r * RS + (p ^ hp_swz(n1r));  // + 16 m: x(n1r + 16 (p + 16 m))
+      const int wo = hp_slot(i & 15, i >> 4);   // + 16 m
+      const int nm = N - i;
+      const int wm = hp_slot(nm & 15, nm >> 4);  // - 16 m
+      const int wm0 = i == 0 ? hp_slot(0, (N / 2) >> 4) : wm;
+      __syncthreads();  // the previous image's T_out reads are done
 #pragma unroll
-        for (int m = 0; m < 16; m++)
-          set_half(v[m], 0, xs[rd + 16 * m]);
-        __syncthreads();
+      for (int h = 0; h < 2; h++)
+      {
+        if (h)
+          __syncthreads();
 #pragma unroll
         for (int m = 0; m < 8; m++)
         {
-          xs[wo + 16 * m] = ho[m];
-          xs[(m == 0 ? wm0 : wm) - 16 * m] = hn[m];
+          xs[wo + 16 * m] = half_of(v[m], h);
+          xs[(m == 0 ? wm0 : wm) - 16 * m] = half_of(v[m + 8], h);
         }
         __syncthreads();
 #pragma unroll
         for (int m = 0; m < 16; m++)
-          set_half(v[m], 1, xs[rd + 16 * m]);
-      }
-      else
-      {
-        __syncthreads();  // the previous image's T_out reads are done
-#pragma unroll
-        for (int h = 0; h < 2; h++)
-        {
-          if (h)
-            __syncthreads();
-#pragma unroll
-          for (int m = 0; m < 8; m++)
-          {
-            xs[wo + 16 * m] = half_of(v[m], h);
-            xs[(m == 0 ? wm0 : wm) - 16 * m] = half_of(v[m + 8], h);
-          }
-          __syncthreads();
-#pragma unroll
-          for (int m = 0; m < 16; m++)
-            set_half(v[m], h, xs[rd + 16 * m]);
-        }
+          set_half(v[m], h, xs[rd + 16 * m]);
       }
       // ---- the 256-point sub-transform of n1r in the wave's registers
       idft16(v);

@@ -230,30 +230,16 @@ int main(int argc, char** argv)
     }
     std::printf("k_rows_hp vs k_rows_half: maps max|diff| %.3g of max %.3g (%.2g), jacobian %.3g of %.3g (grid %d)\n", dm, am,
                 dm / am, dj, aj, hgrid);
-    auto hps = k_rows_hp<kHalfRG, kHalfRGC, false, true>;  // streaming T_in
-    CHECK(hipFuncSetAttribute((const void*)hps, hipFuncAttributeMaxDynamicSharedMemorySize, HpCfg::LDS));
-    auto rhs = [&] {
-      hipLaunchKernelGGL(hps, dim3(hgrid), dim3(256), HpCfg::LDS, 0, fp, gab, gcd, ge, spec, maps, jac, foam, tw, 0,
-                         RowSrc{});
-      return hipGetLastError();
-    };
-    CHECK(hipMemset(maps, 0, mb));
-    CHECK(rhs());
-    CHECK(hipDeviceSynchronize());
-    std::printf("k_rows_hp streaming T_in vs k_rows_hp: %s\n",
-                snap(maps, mb) == hm && snap(jac, jb) == hj ? "bit-identical" : "DIFFER");
-    std::vector<std::vector<float>> tr(3);
+    std::vector<std::vector<float>> tr(2);
     for (int r = 0; r < 9; r++)
     {
       tr[0].push_back(time_ms(r1, 10));
       tr[1].push_back(time_ms(rhp, 10));
-      tr[2].push_back(time_ms(rhs, 10));
     }
-    for (int k = 0; k < 3; k++)
+    for (int k = 0; k < 2; k++)
       std::sort(tr[k].begin(), tr[k].end());
     std::printf("rows, k_rows_half (round 3)     median %7.3f ms  %7.1f GB/s at 56 B/pt\n", tr[0][4], 56.04 * pts / tr[0][4] / 1e6);
     std::printf("rows, k_rows_hp (permlane/DPP) median %7.3f ms  %7.1f GB/s at 56 B/pt\n", tr[1][4], 56.04 * pts / tr[1][4] / 1e6);
-    std::printf("rows, k_rows_hp streaming T_in median %7.3f ms  %7.1f GB/s at 56 B/pt\n", tr[2][4], 56.04 * pts / tr[2][4] / 1e6);
     return 0;
   }
   if (argc > 3 && std::strcmp(argv[3], "rg") == 0 && logn == 12)

@@ -397,3 +397,27 @@ def test_rccl_all_to_all_large_pieces_world1(ocean):
     del a, b
     torch.cuda.empty_cache()
     comm.close()
+
+
+def test_debug_copy_exact_and_refuses_bad_arguments(ocean):
+    """ocean_debug_copy (the paced exchange traffic of bench.py's 8-rank projection) copies exactly on
+    any workgroup count, including a ragged last grid stride, and refuses unaligned or non-multiple-of-16
+    sizes and workgroup counts outside [1, 65536]."""
+    import torch
+
+    from oceansimulation_amd import capi
+    from oceansimulation_amd.waves import debug_copy
+
+    n = (37 << 20) + 48
+    a = torch.randint(0, 255, (n,), dtype=torch.uint8, device="cuda")
+    for wgs in (1, 7, 96, 4096):
+        b = torch.zeros_like(a)
+        debug_copy(b.data_ptr(), a.data_ptr(), n, wgs)
+        torch.cuda.synchronize()
+        assert torch.equal(a, b), wgs
+    with pytest.raises(capi.OceanError):
+        debug_copy(b.data_ptr(), a.data_ptr(), n - 8, 4)
+    with pytest.raises(capi.OceanError):
+        debug_copy(b.data_ptr() + 8, a.data_ptr(), 1024, 4)
+    with pytest.raises(capi.OceanError):
+        debug_copy(b.data_ptr(), a.data_ptr(), 1024, 0)

@@ -11,6 +11,7 @@
 #include "device/evolve.h"
 #include "device/fft.h"
 #include "device/grid.h"
+#include "device/lane_xchg.h"
 #include "device/memory.h"
 #include "device/spectrum.h"
 
@@ -63,6 +64,44 @@ __device__ __forceinline__ int half_group_offset(int y, int strip, int b = 0)
   return RG == 1 ? (strip * N + y) * FB + b : (((y / RG) * FS + strip) * RG + (y % RG)) * FB + b;
 }
 
+// HX: the y transform of a 4096-point column (B = 4 columns per 1024-thread workgroup) with one LDS
+// exchange instead of fft_run's two. Thread t = 64 w + 4 a + b holds x(n) of column b at n = a + 16 w +
+// 256 m in v[m] (the production load order); with k = k0 + 16 k1 + 256 k2,
+//   W^(nk) = W_16^(m k0) . W_N^((a + 16 w) k0) . W_16^(w k1) . W_256^(a k1) . W_16^(a k2):
+// a DFT-16 over m in registers, twiddle, an LDS transposition of (register k0, wave w) — slot
+// (k0 16 + w) 64 + lane, 64 consecutive 8-B slots per access, conflict-free — a DFT-16 over w, twiddle,
+// the in-wave transposition register bits 0..3 <-> lane bits 2..5 (lane_xchg.h: v_permlane16/32_swap +
+// DPP) and a DFT-16 over a. On exit v[m] = X(w + 16 a + 256 m): rows i2 + m T with i2 = w + 16 a. Two
+// split halves of 128 KiB, 4 barriers per round against fft_run's 8.
+// HX 2's storage row of row y (and its inverse): y = k0 + 16 k1 + 256 k2 -> 256 k0 + 16 k2 + k1.
+__host__ __device__ constexpr int hx_store_row(int y) { return ((y & 15) << 8) | ((y >> 8) << 4) | ((y >> 4) & 15); }
+__host__ __device__ constexpr int hx_row_of_store(int s) { return (s >> 8) | ((s & 15) << 4) | (((s >> 4) & 15) << 8); }
+
+__device__ __forceinline__ void fft_cols_hx(CPair* v, int t, void* lds, const float2* __restrict__ tw)
+{
+  constexpr int LOGN = 12;
+  float2* xs = reinterpret_cast<float2*>(lds);
+  const int w = t >> 6, lane = t & 63, a = (t >> 2) & 15;
+  idft16(v);
+  apply_stage_twiddles<LOGN>(v, a + 16 * w, tw);  // x W_N^((a + 16 w) k0)
+#pragma unroll
+  for (int h = 0; h < 2; h++)
+  {
+    __syncthreads();  // the previous reads of the region are done
+#pragma unroll
+    for (int k0 = 0; k0 < 16; k0++)
+      xs[(k0 * 16 + w) * 64 + lane] = half_of(v[k0], h);
+    __syncthreads();
+#pragma unroll
+    for (int ww = 0; ww < 16; ww++)  // this wave is now k0 = w
+      set_half(v[ww], h, xs[(w * 16 + ww) * 64 + lane]);
+  }
+  idft16(v);                                      // v[k1]
+  apply_stage_twiddles<LOGN>(v, 16 * a, tw);      // x W_256^(a k1)
+  transpose_reg_lanes_2_5(v);                     // v[a'], lane bits 2..5 = k1
+  idft16(v);                                      // v[k2] = X(w + 16 a + 256 k2)
+}
+
 // Pass 1: per strip of B columns (u >= 0, or the Nyquist strip), three y-iFFT rounds of CPairs:
 // (A, B), (D, E), (C, 0), stored as gab, gde (float4) and gc (float2): pass 2 reads (A, B) + C for
 // image 0 and C + (D, E) for image 1. H is re-evolved per round from h0: keeping the 16 H (32 VGPRs)
@@ -93,8 +132,13 @@ __device__ __forceinline__ int half_group_offset(int y, int strip, int b = 0)
 // (16 B per thread each, after K::LDS1) and pairs [HL, HL + HK) in VGPRs from round 0 to round 2; only
 // the rest goes through the scratch. The scratch's HBM traffic (its lines are written back and, about
 // half of them, re-fetched: 1.30x algorithmic) costs 0.118 of 0.912 ms (halfbench_nohs).
+// HX (N = 4096, whole strips): the transform is fft_cols_hx; 1: the thread stores rows i2 + m T; 2
+// (whole grids, RG > 1): the fields hold row y = k0 + 16 k1 + 256 k2 at storage row hx_store_row(y) =
+// 256 k0 + 16 k2 + k1, so each store instruction writes 16 consecutive storage rows (whole lines);
+// the row pass reads storage rows (k_rows_hp YP).
 template <int LOGN, int LA = 0, int SA = kStream, bool HS = false, bool SLAB = false, bool SEED = false, int RG = 1,
-          int RGC = 1, int CPI = ColFirstCfg<LOGN>::B, bool HP = false, bool PC = false, int HL = 0, int HK = 0>
+          int RGC = 1, int CPI = ColFirstCfg<LOGN>::B, bool HP = false, bool PC = false, int HL = 0, int HK = 0,
+          int HX = 0>
 __global__ __launch_bounds__(FftShape<LOGN>::T * CPI, CPI < ColFirstCfg<LOGN>::B ? 4 : 1) void k_cols_half(FrameParams fp, const float4* __restrict__ h0,
                                                                      float4* __restrict__ gab, float4* __restrict__ gde,
                                                                      float2* __restrict__ gc,
@@ -110,6 +154,9 @@ __global__ __launch_bounds__(FftShape<LOGN>::T * CPI, CPI < ColFirstCfg<LOGN>::B
   static_assert(SLAB ? HC::SLAB_SUPPORTED : HC::SUPPORTED, "half-spectrum path: one strip per item (B = 4 unless SLAB)");
   static_assert(CPI * HALVES == B && HALVES <= 2 && (HALVES == 1 || (!SLAB && !SEED)), "whole or half strips");
   static_assert((HL == 0 && HK == 0) || (HS && HP && !PC && HL + HK <= 8), "H pairs outside the scratch");
+  static_assert(!HX || (LOGN == 12 && CPI == 4 && B == 4 && !PC), "HX: 4096-point columns, whole 4-column strips");
+  static_assert(HX != 2 || (!SLAB && RG > 1 && RGC > 1), "HX 2: whole-grid row-group layouts");
+  constexpr int MSTEP = HX == 2 ? 16 : T;  // storage rows between v[m] and v[m + 1]
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   float2* tw = reinterpret_cast<float2*>(smem);
   void* xch = smem + ((S::TW_ENTRIES * 8 + 15) / 16) * 16;
@@ -265,13 +312,22 @@ __global__ __launch_bounds__(FftShape<LOGN>::T * CPI, CPI < ColFirstCfg<LOGN>::B
 #endif
         }
       }
-      fft_run<LOGN, CPI, true>(v, i, HALVES > 1 ? opaque((int)threadIdx.x) % CPI : b, xch, tw);
+      int io = i;  // the thread's output rows io + m T
+      if constexpr (HX)
+      {
+        const int t = opaque((int)threadIdx.x);
+        fft_cols_hx(v, t, xch, tw);
+        io = HX == 2 ? 256 * (t >> 6) + ((t >> 2) & 15) : (t >> 6) + 16 * ((t >> 2) & 15);
+      }
+      else
+        fft_run<LOGN, CPI, true>(v, i, HALVES > 1 ? opaque((int)threadIdx.x) % CPI : b, xch, tw);
+      const int vo = (io * B + b) * 16;
 #pragma unroll
       for (int m = 0; m < 16; m++)
       {
         if constexpr (SLAB)
         {
-          // row y = m T + i lies in block q = m T / w (w is a multiple of T), at yl = m T % w + i
+          // row y = m T + io lies in block q = m T / w (w is a multiple of T), at yl = m T % w + io
           const size_t part = (size_t)fp.cascades * hsl.S * hsl.w * B;  // elements per part
           const int q = (m * T) / hsl.w, yl0 = (m * T) % hsl.w;
           const size_t el = (((size_t)c * hsl.S + s) * hsl.w + yl0) * B;
@@ -279,29 +335,29 @@ __global__ __launch_bounds__(FftShape<LOGN>::T * CPI, CPI < ColFirstCfg<LOGN>::B
           // The block base is built at its store (sopaque): hoisted, the 16 descriptors spilled SGPRs.
           unsigned char* blk = send + sopaque((size_t)q * (part * 40 + (size_t)fp.cascades * 2 * N * 16));
           if (round == 0)
-            st4<SA>(blk + el * 16, voff, pair_raw(v[m]));
+            st4<SA>(blk + el * 16, vo, pair_raw(v[m]));
           else if (round == 1)
-            st4<SA>(blk + part * 16 + el * 16, voff, pair_raw(v[m]));
+            st4<SA>(blk + part * 16 + el * 16, vo, pair_raw(v[m]));
           else
-            st2<SA>(blk + part * 32 + el * 8, (i * B + b) * 8, make_float2(v[m].re.x, v[m].im.x));
+            st2<SA>(blk + part * 32 + el * 8, (io * B + b) * 8, make_float2(v[m].re.x, v[m].im.x));
         }
         else if constexpr (RG == 1 && RGC == 1)
         {
           if (round == 0)
-            st4s<SA>(gab + gbase, voff, m * T * B * 16, pair_raw(v[m]));
+            st4s<SA>(gab + gbase, vo, m * T * B * 16, pair_raw(v[m]));
           else if (round == 1)
-            st4s<SA>(gde + gbase, voff, m * T * B * 16, pair_raw(v[m]));
+            st4s<SA>(gde + gbase, vo, m * T * B * 16, pair_raw(v[m]));
           else
-            st2s<SA>(gc + gbase, (i * B + b) * 8, m * T * B * 8, make_float2(v[m].re.x, v[m].im.x));
+            st2s<SA>(gc + gbase, (io * B + b) * 8, m * T * B * 8, make_float2(v[m].re.x, v[m].im.x));
         }
         else if (round == 0)  // one descriptor per field; the row group of m T in soffset
-          st4s<SA>(gab + gbase, half_group_offset<LOGN, RG>(i, 0, b) * 16, half_group_offset<LOGN, RG>(m * T, 0) * 16,
+          st4s<SA>(gab + gbase, half_group_offset<LOGN, RG>(io, 0, b) * 16, half_group_offset<LOGN, RG>(m * MSTEP, 0) * 16,
                    pair_raw(v[m]));
         else if (round == 1)
-          st4s<SA>(gde + gbase, half_group_offset<LOGN, RG>(i, 0, b) * 16, half_group_offset<LOGN, RG>(m * T, 0) * 16,
+          st4s<SA>(gde + gbase, half_group_offset<LOGN, RG>(io, 0, b) * 16, half_group_offset<LOGN, RG>(m * MSTEP, 0) * 16,
                    pair_raw(v[m]));
         else
-          st2s<SA>(gc + cgbase, half_group_offset<LOGN, RGC>(i, 0, b) * 8, half_group_offset<LOGN, RGC>(m * T, 0) * 8,
+          st2s<SA>(gc + cgbase, half_group_offset<LOGN, RGC>(io, 0, b) * 8, half_group_offset<LOGN, RGC>(m * MSTEP, 0) * 8,
                    make_float2(v[m].re.x, v[m].im.x));
       }
     };

@@ -262,7 +262,7 @@ def test_parse_rocprof_refuses_above_peak(tmp_path, monkeypatch):
 
 
 def test_xp_hp_index_model():
-    """tools/xp_model.py plays k_rows_xp's (16384) and k_rows_hp's (4096) LDS slots, in-wave
+    """tools/xp_model.py plays k_rows_xp's (16384), k_rows_hp's and k_cols_half HX's (4096) LDS slots, in-wave
     register <-> lane bit transpositions, twiddles and output layout on the host: both must be the
     unnormalised inverse DFT (the T_in write slots must also cover every x index exactly once)."""
     import importlib.util
@@ -273,3 +273,4 @@ def test_xp_hp_index_model():
     assert m.model_xp() < 1e-12
     assert m.model_hp() < 1e-12
     assert m.hp_bank_multiplicity() == 1  # k_rows_hp's four LDS access shapes are conflict-free
+    assert m.model_hx() < 1e-12  # k_cols_half HX (measured, not kept) and its storage-row bijection

@@ -1,6 +1,6 @@
 // halfbench.hip — interleaved A/B timing of half-spectrum frame-pass variants (8 cascades x 4096^2),
 // with a bit-identity check of every variant's output against the baseline variant.
-// Build: see Makefile target `microbench`. Usage: halfbench [logn] [cascades] [quick|mall|rows|overlap|rowabl|hpair]
+// Build: see Makefile target `microbench`. Usage: halfbench [logn] [cascades] [quick|mall|rows|overlap|rowabl|hpair|hp|hx]
 #include "all_kernels.h"
 
 #include <algorithm>
@@ -240,6 +240,89 @@ int main(int argc, char** argv)
       std::sort(tr[k].begin(), tr[k].end());
     std::printf("rows, k_rows_half (round 3)     median %7.3f ms  %7.1f GB/s at 56 B/pt\n", tr[0][4], 56.04 * pts / tr[0][4] / 1e6);
     std::printf("rows, k_rows_hp (permlane/DPP) median %7.3f ms  %7.1f GB/s at 56 B/pt\n", tr[1][4], 56.04 * pts / tr[1][4] / 1e6);
+    return 0;
+  }
+  if (argc > 3 && std::strcmp(argv[3], "hx") == 0 && logn == 12)
+  {
+    // pass 1: production (fft_run<12>: two split LDS exchanges, 8 barriers per round) against HX (one
+    // LDS exchange + the in-wave transposition of lane_xchg.h, 4 barriers). HX 1 stores rows w + 16 a +
+    // 256 m (half lines per store instruction), HX 2 stores them in storage-row order (whole lines;
+    // the row pass k_rows_hp YP reads storage rows). Different radix order, so the maps agree to
+    // rounding, not bit for bit. Frames with k_rows_hp.
+    using K = ColFirstCfg<12>;
+    using S = FftShape<12>;
+    const int clds = ((S::TW_ENTRIES * 8 + 15) / 16) * 16 + K::LDS1 + kHalfHL * K::WG1 * 16;
+    auto cols = [&](auto kern) {
+      return std::function<hipError_t()>([=] {
+        hipError_t e = launch_half_nyquist(fp, n, K::B, h0, spec, nullptr, 1, 0, nullptr, 0, cus);
+        if (e != hipSuccess)
+          return e;
+        int grid = persistent_grid(kern, K::WG1, clds, fp.cascades * HalfCfg<12>::STRIPS, cus);
+        grid = grid > cus ? cus : grid;
+        hipLaunchKernelGGL(kern, dim3(grid), dim3(K::WG1), clds, 0, fp, h0, gab, gcd, ge, tw, hs, HalfSlab{},
+                           (unsigned char*)nullptr, 1, nullptr);
+        return hipGetLastError();
+      });
+    };
+    auto rows = [&](auto kern) {
+      return std::function<hipError_t()>([=] {
+        const int grid = persistent_grid(kern, 256, HpCfg::LDS, fp.cascades * n, cus);
+        hipLaunchKernelGGL(kern, dim3(grid), dim3(256), HpCfg::LDS, 0, fp, gab, gcd, ge, spec, maps, jac, foam, tw, 0,
+                           RowSrc{});
+        return hipGetLastError();
+      });
+    };
+    auto rp = rows(k_rows_hp<kHalfRG, kHalfRGC>), ry = rows(k_rows_hp<kHalfRG, kHalfRGC, false, true>);
+    std::vector<std::function<hipError_t()>> vc = {
+        cols(k_cols_half<12, kStream, kStream, true, false, false, kHalfRG, kHalfRGC, 4, true, false, kHalfHL, kHalfHK>),
+        cols(k_cols_half<12, kStream, kStream, true, false, false, kHalfRG, kHalfRGC, 4, true, false, kHalfHL, kHalfHK, 1>),
+        cols(k_cols_half<12, kStream, kStream, true, false, false, kHalfRG, kHalfRGC, 4, true, false, kHalfHL, kHalfHK, 2>),
+        cols(k_cols_half<12, kStream, kStream, true, false, false, kHalfRG, kHalfRGC, 4, true, false, kHalfHL, 2, 2>)};
+    std::vector<std::function<hipError_t()>> vr = {rp, rp, ry, ry};
+    const char* nm[] = {"production (fft_run, HK 4)", "HX 1 (row order), HK 4", "HX 2 (storage order), HK 4",
+                        "HX 2 (storage order), HK 2"};
+    const int NV = 4;
+    auto rel = [](const std::vector<unsigned char>& a, const std::vector<unsigned char>& b) {
+      const float* x = reinterpret_cast<const float*>(a.data());
+      const float* y = reinterpret_cast<const float*>(b.data());
+      double d = 0, m = 0;
+      for (size_t k = 0; k < a.size() / 4; k++)
+      {
+        d = std::max(d, (double)std::fabs(x[k] - y[k]));
+        m = std::max(m, (double)std::fabs(x[k]));
+      }
+      return d / (m > 0 ? m : 1);
+    };
+    CHECK(vc[0]());
+    CHECK(vr[0]());
+    CHECK(hipDeviceSynchronize());
+    auto pm = snap(maps, mb), pj = snap(jac, jb);
+    for (int k = 1; k < NV; k++)
+    {
+      CHECK(hipMemset(maps, 0, mb));
+      CHECK(hipMemset(jac, 0, jb));
+      CHECK(vc[k]());
+      CHECK(vr[k]());
+      CHECK(hipDeviceSynchronize());
+      std::printf("%s vs production: maps %.2g jacobian %.2g (max |diff| / max)\n", nm[k], rel(snap(maps, mb), pm),
+                  rel(snap(jac, jb), pj));
+    }
+    std::vector<std::vector<float>> t(NV), tr(NV), tf(NV);
+    for (int r = 0; r < 9; r++)
+      for (int k = 0; k < NV; k++)
+      {
+        t[k].push_back(time_ms(vc[k], 10));
+        tr[k].push_back(time_ms(vr[k], 10));
+        tf[k].push_back(time_ms([&] { CHECK(vc[k]()); return vr[k](); }, 10));
+      }
+    for (int k = 0; k < NV; k++)
+    {
+      std::sort(t[k].begin(), t[k].end());
+      std::sort(tr[k].begin(), tr[k].end());
+      std::sort(tf[k].begin(), tf[k].end());
+      std::printf("cols %-28s median %7.3f ms  %7.1f GB/s at 28 B/pt   rows %7.3f ms   frame %7.3f ms\n", nm[k], t[k][4],
+                  28.0 * pts / t[k][4] / 1e6, tr[k][4], tf[k][4]);
+    }
     return 0;
   }
   if (argc > 3 && std::strcmp(argv[3], "rg") == 0 && logn == 12)

@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
-"""Host model of the index arithmetic of k_rows_xp (N = 16384, 64 x 256 split) and k_rows_hp (N = 4096,
-16 x 256 split): the LDS slots of T_in / T_out, the in-wave register <-> lane bit transpositions of
+"""Host model of the index arithmetic of k_rows_xp (N = 16384, 64 x 256 split), k_rows_hp (N = 4096,
+16 x 256 split) and k_cols_half HX (N = 4096, 16 x 16 x 16): the LDS slots of T_in / T_out, the in-wave register <-> lane bit transpositions of
 device/lane_xchg.h (element (R = r, L = l) -> (R = l, L = r)), the twiddles and the output layout,
 played on numpy arrays [thread][register] and checked against N * ifft (the unnormalised inverse
 transform, sign +). It validates the kernels' indexing on the CPU; the hardware semantics of the
@@ -153,6 +153,36 @@ def model_hp(seed=2):
     return np.max(np.abs(X - ref)) / np.max(np.abs(ref))
 
 
+def model_hx(seed=3):
+    """k_cols_half HX (fft_cols_hx): one 4096-point column, threads (w, a) with x(a + 16 w + 256 m) in
+    v[m]; DFT over m, x W_N^((a + 16 w) k0), LDS transposition (register k0 <-> wave w), DFT over w,
+    x W_256^(a k1), register <-> lane-bits-2..5 transposition (k1 <-> a), DFT over a: thread (w, a)
+    then holds X(w + 16 a + 256 m). Also checks HX 2's storage-row permutation is a bijection."""
+    N = 4096
+    rng = np.random.default_rng(seed)
+    x = rng.standard_normal(N) + 1j * rng.standard_normal(N)
+    w, a, m = np.meshgrid(np.arange(16), np.arange(16), np.arange(16), indexing="ij")
+    v = x[a + 16 * w + 256 * m]              # v[w, a, m]
+    v = idft(v, 2)
+    v = v * W((a + 16 * w) * m, N)           # m now indexes k0
+    v = np.transpose(v, (2, 1, 0))           # wave k0, lane a, register w
+    v = idft(v, 2)                           # register k1
+    v = v * W(16 * a * m, N)
+    v = np.transpose(v, (0, 2, 1))           # lane k1, register a
+    v = idft(v, 2)                           # register k2
+    X = np.zeros(N, complex)
+    X[w + 16 * a + 256 * m] = v
+    ref = np.fft.ifft(x) * N
+    store = lambda y: ((y & 15) << 8) | ((y >> 8) << 4) | ((y >> 4) & 15)  # noqa: E731
+    back = lambda s: (s >> 8) | ((s & 15) << 4) | (((s >> 4) & 15) << 8)  # noqa: E731
+    y = np.arange(N)
+    assert np.array_equal(back(store(y)), y) and len(set(store(y).tolist())) == N
+    # a store instruction (wave k0, register k2) covers 16 consecutive storage rows
+    assert all(sorted(store(k0 + 16 * np.arange(16) + 256 * k2)) == list(range(256 * k0 + 16 * k2, 256 * k0 + 16 * k2 + 16))
+               for k0 in range(16) for k2 in range(16))
+    return np.max(np.abs(X - ref)) / np.max(np.abs(ref))
+
+
 def hp_bank_multiplicity():
     """Worst bank multiplicity of k_rows_hp's four LDS access shapes (MI355X_MICROARCH.md §LDS:
     ds_write_b64 in 16-lane groups, bank of 8-B slot mod 16; ds_read_b64 in 32-lane groups, mod 32):
@@ -173,3 +203,4 @@ if __name__ == "__main__":
     print(f"k_rows_hp LDS bank multiplicity (1 = conflict-free): {hp_bank_multiplicity()}")
     print(f"k_rows_xp model (16384): max |X - N ifft(x)| / max = {model_xp():.2e}")
     print(f"k_rows_hp model (4096):  max |X - N ifft(x)| / max = {model_hp():.2e}")
+    print(f"k_cols_half HX model:    max |X - N ifft(x)| / max = {model_hx():.2e}")

@@ -1,6 +1,6 @@
 // halfbench.hip — interleaved A/B timing of half-spectrum frame-pass variants (8 cascades x 4096^2),
 // with a bit-identity check of every variant's output against the baseline variant.
-// Build: see Makefile target `microbench`. Usage: halfbench [logn] [cascades] [quick|mall|rows|overlap|rowabl|hpair|hp|hx]
+// Build: see Makefile target `microbench`. Usage: halfbench [logn] [cascades] [quick|mall|rows|overlap|rowabl|hpair|hp|hx|xgrid]
 #include "all_kernels.h"
 
 #include <algorithm>
@@ -809,6 +809,102 @@ int main(int argc, char** argv)
     std::printf("C=%d frame, both passes on one stream     median %7.3f ms (%d frames)\n", C, ts[3], F);
     std::printf("C=%d frame, pass 1 of f+1 beside pass 2 of f median %7.3f ms  bit-identical %s\n", C, tp[3],
                 same ? "yes" : "NO");
+    return 0;
+  }
+  if (argc > 3 && std::strcmp(argv[3], "xgrid") == 0)
+  {
+    // frame overlap with the production launchers (k_cols_half, k_rows_hp): frame f+1's column pass on
+    // stream A beside frame f's row pass on stream B, the column pass's persistent grid limited to
+    // `ccus` workgroups (1 per CU) so frame f's row pass keeps the other CUs. Against serial frames.
+    float4 *gab2, *gcd2, *spec2;
+    float2* ge2;
+    CHECK(hipMalloc(&gab2, ht * sizeof(float4)));
+    CHECK(hipMalloc(&gcd2, ht * sizeof(float4)));
+    CHECK(hipMalloc(&ge2, ht * sizeof(float2)));
+    CHECK(hipMalloc(&spec2, (size_t)C * 2 * n * sizeof(float4)));
+    float4* sab[2] = {gab, gab2};
+    float4* sde[2] = {gcd, gcd2};
+    float2* sc[2] = {ge, ge2};
+    float4* ssp[2] = {spec, spec2};
+    hipStream_t sa, sb;
+    CHECK(hipStreamCreateWithFlags(&sa, hipStreamNonBlocking));
+    CHECK(hipStreamCreateWithFlags(&sb, hipStreamNonBlocking));
+    hipEvent_t evc[2], evr[2], e0;
+    for (int k = 0; k < 2; k++)
+    {
+      CHECK(hipEventCreateWithFlags(&evc[k], hipEventDisableTiming));
+      CHECK(hipEventCreateWithFlags(&evr[k], hipEventDisableTiming));
+      CHECK(hipEventRecord(evr[k], 0));
+    }
+    CHECK(hipEventCreateWithFlags(&e0, hipEventDisableTiming));
+    const int F = 20;
+    auto pc = [&](int s, hipStream_t st, int ccus) {
+      return launch_half_columns(logn, fp, h0, sab[s], sde[s], sc[s], ssp[s], tw, st, ccus, hs, cus, nullptr);
+    };
+    auto pr = [&](int s, hipStream_t st, int rcus) {
+      return launch_half_rows(logn, fp, sab[s], sde[s], sc[s], ssp[s], maps, jac, foam, tw, st, rcus);
+    };
+    auto serial = [&] {
+      for (int f = 0; f < F; f++)
+      {
+        CHECK(pc(0, 0, cus));
+        CHECK(pr(0, 0, cus));
+      }
+      return hipSuccess;
+    };
+    auto piped = [&](int ccus, int rcus) {
+      CHECK(hipEventRecord(e0, 0));
+      CHECK(hipStreamWaitEvent(sa, e0, 0));
+      CHECK(hipStreamWaitEvent(sb, e0, 0));
+      for (int f = 0; f < F; f++)
+      {
+        const int s = f & 1;
+        CHECK(hipStreamWaitEvent(sa, evr[s], 0));
+        CHECK(pc(s, sa, ccus));
+        CHECK(hipEventRecord(evc[s], sa));
+        CHECK(hipStreamWaitEvent(sb, evc[s], 0));
+        CHECK(pr(s, sb, rcus));
+        CHECK(hipEventRecord(evr[s], sb));
+      }
+      CHECK(hipStreamWaitEvent(0, evr[(F - 1) & 1], 0));
+      return hipSuccess;
+    };
+    CHECK(serial());
+    CHECK(hipDeviceSynchronize());
+    auto bm = snap(maps, mb), bj = snap(jac, jb);
+    // bal: the fewest workgroups that keep the full grid's number of item rounds (ceil(items / 256))
+    const int items = C * HalfCfg<12>::STRIPS, rounds = (items + cus - 1) / cus, bal = (items + rounds - 1) / rounds;
+    const int cc[] = {cus, bal, 224, 192, 128};
+    const int NC = 5;
+    bool same[NC];
+    for (int k = 0; k < NC; k++)
+    {
+      CHECK(hipMemset(maps, 0, mb));
+      CHECK(piped(cc[k], cus));
+      CHECK(hipDeviceSynchronize());
+      std::printf("pipelined (column grid %d) vs serial frames:\n", cc[k]);
+      same[k] = (int)diff(snap(maps, mb), bm) & (int)diff(snap(jac, jb), bj);
+    }
+    std::vector<float> ts;
+    std::vector<std::vector<float>> tp(NC), tcol(NC);
+    for (int r = 0; r < 7; r++)
+    {
+      ts.push_back(time_ms(serial, 1) / F);
+      for (int k = 0; k < NC; k++)
+      {
+        tp[k].push_back(time_ms([&] { return piped(cc[k], cus); }, 1) / F);
+        tcol[k].push_back(time_ms([&] { return pc(0, 0, cc[k]); }, 10));
+      }
+    }
+    std::sort(ts.begin(), ts.end());
+    std::printf("C=%d frame, serial                                  median %7.3f ms (%d frames)\n", C, ts[3], F);
+    for (int k = 0; k < NC; k++)
+    {
+      std::sort(tp[k].begin(), tp[k].end());
+      std::sort(tcol[k].begin(), tcol[k].end());
+      std::printf("C=%d frame, overlapped, column grid %3d             median %7.3f ms  (column pass alone %7.3f ms)  bit-identical %s\n",
+                  C, cc[k], tp[k][3], tcol[k][3], same[k] ? "yes" : "NO");
+    }
     return 0;
   }
   if (argc > 3 && std::strcmp(argv[3], "overlap") == 0)

@@ -90,7 +90,8 @@ def parse(argv=None):
                          "line is printed without the unfinished legs and every rank exits")
     ap.add_argument("--frame-overlap", choices=("auto", "on", "off"), default="auto",
                     help="ocean_generator_set_frame_overlap (frame f+1's column pass beside frame f's row pass): "
-                         "auto = on at <= 2 cascades per GPU on the half-spectrum path (8 x 4096^2: slower)")
+                         "auto = on at <= 2 cascades per GPU on the half-spectrum path below 4096 (4096: the "
+                         "half-strip column pass runs faster serial)")
     ap.add_argument("--full-spectrum", action="store_true",
                     help="time the full-spectrum frame path instead of the default half-spectrum one")
     ap.add_argument("--slab-n", type=int, default=16384, help="side of the single slab-decomposed grid")
@@ -409,26 +410,29 @@ def weak_leg(ocean, fft, args, rank: int, world: int, dt: float) -> dict:
             "ms_per_step": 1000.0 * el / args.steps, "points_per_s": float(n) * n * C * world * args.steps / el}
 
 
-def use_frame_overlap(args, cascades: int, path: str) -> bool:
+def use_frame_overlap(args, cascades: int, path: str, n: int) -> bool:
     """The headline's frame-overlap mode: on at <= 2 cascades per GPU (the 4- and 8-GPU strong-scaling
-    shares) on the blocked half-spectrum path, where the passes' launch tails dominate."""
+    shares) on the blocked half-spectrum path below 4096, where the passes' launch tails dominate. At
+    4096 those shares run pass 1 on half strips (launch_common.h half_fields_fb), whose serial frame
+    is the faster one: 0.318 against 0.346 ms overlapped at one cascade, 0.599 against 0.656 at two
+    (profiles/r04_halfbench_xgrid_fb2_{1,2}.log)."""
     if args.frame_overlap != "auto":
         return args.frame_overlap == "on" and path == "half"
-    return path == "half" and cascades <= 2
+    return path == "half" and cascades <= 2 and n < 4096
 
 
 def one_cascade_leg(ocean, fft, args, dt: float) -> dict:
     """The P = 8 point of the strong-scaling headline on one GPU: ONE 4096^2 cascade per frame (what
     each of 8 GPUs runs when the 8 cascades are split 1 per GPU; src/Waves.cpp:20-39 runs one generator
     per cascade). Launch tails weigh more than in the 8-cascade batch; the headline runs this share
-    with frame overlap (use_frame_overlap), the serial frame is reported beside it."""
+    with frame overlap where use_frame_overlap chooses it (below 4096), the serial frame beside it."""
     n = args.n
     gen = ocean.Generator(fft, 1)
     ocean.apply_settings(gen.GetOceanSettings(0), **cascade_settings(0, 0))
     for _ in range(max(args.warmup, 2)):
         gen.CalculateOcean(dt)
     steps = max(args.steps, 20)
-    overlap = use_frame_overlap(args, 1, frame_path(n, args.full_spectrum))
+    overlap = use_frame_overlap(args, 1, frame_path(n, args.full_spectrum), n)
     # serial and overlapped frames interleaved (3 runs each, median), so clock drift hits both alike
     runs = {False: [], True: []}
     for _ in range(3):
@@ -1031,7 +1035,7 @@ def main(argv=None):
         gen.GenerateSpectrum()
     ms, cnt = gen.kernel_times()
     h0_ms = ms[0] / reps  # all cascades, per regeneration
-    overlap = use_frame_overlap(args, C, path)
+    overlap = use_frame_overlap(args, C, path, n)
     if overlap:
         gen.set_frame_overlap(True)
     for _ in range(args.warmup):

@@ -120,7 +120,8 @@ __device__ __forceinline__ void fft_cols_hx(CPair* v, int t, void* lds, const fl
 // RG / RGC (whole grids): rows per group of the gab/gde and the gc layout (half_group_offset).
 // CPI: columns per item (B = the whole strip; B / 2: half strips, T * CPI threads, two workgroups
 // per CU so one's loads and stores overlap the other's transform; the strip's two halves are items
-// 2p, 2p + 1 on one XCD, whose loads share h0 lines and whose half-line stores meet in L2).
+// 2p, 2p + 1 on one XCD, whose loads share h0 lines). Production at <= 2 cascades with FB = 2
+// (half_fields_fb); on the 4-column layout the halves' stores are half lines (slower).
 // HP: the H scratch holds pairs (H(m), H(m + 1)) per thread in 16-B entries ([m / 2][thread]): 8
 // stores and 16 loads of 16 B per item instead of 16 and 32 of 8 B.
 // PC (packed C round, needs HS + HP and whole strips of B >= 2): round 2's CPair (C, 0) wastes its
@@ -136,9 +137,12 @@ __device__ __forceinline__ void fft_cols_hx(CPair* v, int t, void* lds, const fl
 // (whole grids, RG > 1): the fields hold row y = k0 + 16 k1 + 256 k2 at storage row hx_store_row(y) =
 // 256 k0 + 16 k2 + k1, so each store instruction writes 16 consecutive storage rows (whole lines);
 // the row pass reads storage rows (k_rows_hp YP).
+// FB (half strips, whole grids): the fields are FB = CPI columns wide (half_group_offset<.., FB>), so a
+// half-strip item's stores are whole lines when RG * FB * 16 B = 128 B (gab, gde) and RGC * FB * 8 B
+// = 128 B (gc); the row pass reads the same layout (k_rows_hp FB).
 template <int LOGN, int LA = 0, int SA = kStream, bool HS = false, bool SLAB = false, bool SEED = false, int RG = 1,
           int RGC = 1, int CPI = ColFirstCfg<LOGN>::B, bool HP = false, bool PC = false, int HL = 0, int HK = 0,
-          int HX = 0>
+          int HX = 0, int FB = 4>
 __global__ __launch_bounds__(FftShape<LOGN>::T * CPI, CPI < ColFirstCfg<LOGN>::B ? 4 : 1) void k_cols_half(FrameParams fp, const float4* __restrict__ h0,
                                                                      float4* __restrict__ gab, float4* __restrict__ gde,
                                                                      float2* __restrict__ gc,
@@ -152,15 +156,17 @@ __global__ __launch_bounds__(FftShape<LOGN>::T * CPI, CPI < ColFirstCfg<LOGN>::B
   using HC = HalfCfg<LOGN>;
   constexpr int N = S::N, T = S::T, B = K::B, STRIPS = HC::STRIPS, WG = T * CPI, HALVES = B / CPI;
   static_assert(SLAB ? HC::SLAB_SUPPORTED : HC::SUPPORTED, "half-spectrum path: one strip per item (B = 4 unless SLAB)");
-  static_assert(CPI * HALVES == B && HALVES <= 2 && (HALVES == 1 || (!SLAB && !SEED)), "whole or half strips");
+  static_assert(CPI * HALVES == B && HALVES <= 2 && (HALVES == 1 || !SLAB), "whole or half strips");
   static_assert((HL == 0 && HK == 0) || (HS && HP && !PC && HL + HK <= 8), "H pairs outside the scratch");
   static_assert(!HX || (LOGN == 12 && CPI == 4 && B == 4 && !PC), "HX: 4096-point columns, whole 4-column strips");
   static_assert(HX != 2 || (!SLAB && RG > 1 && RGC > 1), "HX 2: whole-grid row-group layouts");
   constexpr int MSTEP = HX == 2 ? 16 : T;  // storage rows between v[m] and v[m + 1]
+  static_assert(FB == 4 || (FB == CPI && HALVES == 2 && !SLAB && RG > 1 && RGC > 1 && !HX), "FB: half-strip fields");
+  constexpr int XB = CPI * S::PADDED * 8;  // the exchange's bytes (K::LDS1 for whole strips)
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   float2* tw = reinterpret_cast<float2*>(smem);
   void* xch = smem + ((S::TW_ENTRIES * 8 + 15) / 16) * 16;
-  float4* hlds = reinterpret_cast<float4*>(static_cast<unsigned char*>(xch) + K::LDS1);  // HL pairs [p][thread]
+  float4* hlds = reinterpret_cast<float4*>(static_cast<unsigned char*>(xch) + XB);  // HL pairs [p][thread]
   load_twiddles<LOGN>(tw, tw_glob);
 
   const int nstrips = SLAB ? hsl.nstrips : STRIPS;
@@ -179,10 +185,12 @@ __global__ __launch_bounds__(FftShape<LOGN>::T * CPI, CPI < ColFirstCfg<LOGN>::B
     const float4* src = (!SLAB || h0_full) ? h0 + ((size_t)c * (N / B) + xb) * N * B
                                            : h0 + ((size_t)c * nstrips + s) * N * B;
     // the strip's first texel in the cascade's fields (whole grids); + half_group_offset(m T, 0) per m
+    const int fs = FB == 4 ? s : 2 * s + hh;  // field strip
     const size_t gbase = RG == 1 ? ((size_t)c * STRIPS + s) * N * B
-                                 : (size_t)c * STRIPS * N * B + half_group_offset<LOGN, RG>(0, s);
+                                 : (size_t)c * STRIPS * N * B + half_group_offset<LOGN, RG, FB>(0, fs);
     const size_t cgbase = RGC == 1 ? ((size_t)c * STRIPS + s) * N * B
-                                   : (size_t)c * STRIPS * N * B + half_group_offset<LOGN, RGC>(0, s);
+                                   : (size_t)c * STRIPS * N * B + half_group_offset<LOGN, RGC, FB>(0, fs);
+    const int bf = FB == 4 ? b : b - hh * CPI;  // column within the field strip
     const int x = xb * B + b;
     float4 hk[HK > 0 ? HK : 1];  // HK: H pairs kept in VGPRs across the rounds
     // one field round: (A, B), (D, E) or (C, 0) of the 16 texels, y-iFFT, store
@@ -351,13 +359,13 @@ __global__ __launch_bounds__(FftShape<LOGN>::T * CPI, CPI < ColFirstCfg<LOGN>::B
             st2s<SA>(gc + gbase, (io * B + b) * 8, m * T * B * 8, make_float2(v[m].re.x, v[m].im.x));
         }
         else if (round == 0)  // one descriptor per field; the row group of m T in soffset
-          st4s<SA>(gab + gbase, half_group_offset<LOGN, RG>(io, 0, b) * 16, half_group_offset<LOGN, RG>(m * MSTEP, 0) * 16,
+          st4s<SA>(gab + gbase, half_group_offset<LOGN, RG, FB>(io, 0, bf) * 16, half_group_offset<LOGN, RG, FB>(m * MSTEP, 0) * 16,
                    pair_raw(v[m]));
         else if (round == 1)
-          st4s<SA>(gde + gbase, half_group_offset<LOGN, RG>(io, 0, b) * 16, half_group_offset<LOGN, RG>(m * MSTEP, 0) * 16,
+          st4s<SA>(gde + gbase, half_group_offset<LOGN, RG, FB>(io, 0, bf) * 16, half_group_offset<LOGN, RG, FB>(m * MSTEP, 0) * 16,
                    pair_raw(v[m]));
         else
-          st2s<SA>(gc + cgbase, half_group_offset<LOGN, RGC>(io, 0, b) * 8, half_group_offset<LOGN, RGC>(m * MSTEP, 0) * 8,
+          st2s<SA>(gc + cgbase, half_group_offset<LOGN, RGC, FB>(io, 0, bf) * 8, half_group_offset<LOGN, RGC, FB>(m * MSTEP, 0) * 8,
                    make_float2(v[m].re.x, v[m].im.x));
       }
     };

@@ -48,8 +48,9 @@ __device__ __forceinline__ int hp_slot(int n1, int j) { return n1 * HpCfg::RS + 
 //   sub-transform as k_rows_xp: v[b] = Y_n1(p + 16 b), then x W_N^(n1 (p + 16 b)).
 //   T_out: thread k2 = tid receives Z_n1(k2), n1 < 16; DFT-16: v[k1] = X(tid + 256 k1).
 // YP: the fields hold row y at storage row hx_store_row(y) (k_cols_half HX 2); items run over storage
-// rows, so the 4 rows of a gc line stay on one XCD.
-template <int RG, int RGC, bool RM = false, bool YP = false>
+// rows, so the 4 rows of a gc line stay on one XCD. FB: field strips of FB columns (k_cols_half FB);
+// GRP: consecutive rows per XCD group (the rows of a gc line).
+template <int RG, int RGC, bool RM = false, bool YP = false, int FB = 4, int GRP = 4>
 __global__ __launch_bounds__(256, 4) void k_rows_hp(FrameParams fp, const float4* __restrict__ gab,
                                                  const float4* __restrict__ gde, const float2* __restrict__ gc,
                                                  const float4* __restrict__ spec, float4* __restrict__ maps,
@@ -73,7 +74,7 @@ __global__ __launch_bounds__(256, 4) void k_rows_hp(FrameParams fp, const float4
   constexpr int LA = RM ? kStream : 0;
   const int lcpr = RM ? 31 - __builtin_clz(rs.cpr) : 0, cmask = RM ? rs.cpr - 1 : 0;
   const int wave0 = __builtin_amdgcn_readfirstlane((int)threadIdx.x & ~63);
-  for (int item = RM ? (int)blockIdx.x : xcd_group_slot<4>(blockIdx.x, gridDim.x); item < total; item += gridDim.x)
+  for (int item = RM ? (int)blockIdx.x : xcd_group_slot<GRP>(blockIdx.x, gridDim.x); item < total; item += gridDim.x)
   {
     const int c = item / nrows, yf = item - c * nrows;  // RM: yf is the local row (slabs start at an even row)
     const int y = YP ? hx_row_of_store(yf) : yf;       // the output row; yf addresses the fields
@@ -94,8 +95,8 @@ __global__ __launch_bounds__(256, 4) void k_rows_hp(FrameParams fp, const float4
         const int u = m * T + i;
         // RM: source block of column u (wave-uniform, a scalar shift) and the element in its row
         const int src = RM ? (m * T + sopaque(wave0)) >> lcpr : 0;
-        const int off = RM ? (u & cmask) : half_group_offset<LOGN, RG>(yf, u / B, u % B);
-        const int offc = RM ? off : half_group_offset<LOGN, RGC>(yf, u / B, u % B);
+        const int off = RM ? (u & cmask) : half_group_offset<LOGN, RG, FB>(yf, u / FB, u % FB);
+        const int offc = RM ? off : half_group_offset<LOGN, RGC, FB>(yf, u / FB, u % FB);
         const float4* fab = RM ? reinterpret_cast<const float4*>(rs.ab + (size_t)src * rs.src_stride) : gab;
         const float4* fde = RM ? reinterpret_cast<const float4*>(rs.de + (size_t)src * rs.src_stride) : gde;
         const float2* fc = RM ? reinterpret_cast<const float2*>(rs.c + (size_t)src * rs.src_stride) : gc;
@@ -133,8 +134,8 @@ __global__ __launch_bounds__(256, 4) void k_rows_hp(FrameParams fp, const float4
       {
         // the Nyquist column u = -N/2 (first column of the last strip; RM: block nyq_src, column cpr)
         // replaces the unused -u lane of u = 0
-        const int off = RM ? rs.cpr : half_group_offset<LOGN, RG>(yf, N / 2 / B);
-        const int offc = RM ? off : half_group_offset<LOGN, RGC>(yf, N / 2 / B);
+        const int off = RM ? rs.cpr : half_group_offset<LOGN, RG, FB>(yf, N / 2 / FB);
+        const int offc = RM ? off : half_group_offset<LOGN, RGC, FB>(yf, N / 2 / FB);
         const size_t ns = RM ? (size_t)rs.nyq_src * rs.src_stride : 0;
         const float4* fab = RM ? reinterpret_cast<const float4*>(rs.ab + ns) : gab;
         const float4* fde = RM ? reinterpret_cast<const float4*>(rs.de + ns) : gde;

@@ -66,6 +66,15 @@ inline bool g_force_persistent = false;  // tools/microbench A/B only
 // (profiles/r04_halfbench_hp.log). Both paths switch together, so slabs stay bit-identical to whole grids.
 inline int half_rows_variant = 1;
 
+// Whole-grid half-spectrum fields at N = 4096 with <= 2 cascades per launch (the 4- and 8-GPU shares of
+// the headline): pass 1 on half strips, two 512-thread workgroups per CU, into field strips FB = 2
+// columns wide (whole-line stores: gab / gde row groups of 4, gc of 8), the row pass on that layout.
+// Same per-column arithmetic as the 4-column strips, so the maps are bit-identical to them; at one
+// cascade the frame takes 0.319 against 0.339 ms, at two 0.597 against 0.609, at three and more it
+// loses (profiles/r04_halfbench_fb2h_{1,2,3,4,8}.log). Both launchers take the layout from here.
+inline int half_fields_fb(int logn, int cascades) { return logn == 12 && cascades <= 2 ? 2 : 4; }
+constexpr int kHalfRG2 = 4, kHalfRGC2 = 8;  // the FB = 2 layout's row groups
+
 inline bool one_shot_grids(int cus)
 {
   const int d = device_cu_count();

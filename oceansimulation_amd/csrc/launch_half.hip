@@ -57,6 +57,28 @@ hipError_t launch_half_columns(int logn, const FrameParams& fp, const float4* h0
       // evaluates h0 in round 0 and keeps kHalfHKSeed pairs in VGPRs.
       constexpr int RG = kHalfRG, RGC = kHalfRGC;
       constexpr int HKW = LOGN == 12 ? kHalfHK : 2;
+      if constexpr (LOGN == 12)
+      {
+        if (half_fields_fb(LOGN, fp.cascades) == 2)
+        {
+          // half strips (FB = 2): 512-thread workgroups, two per CU (a 68-KiB exchange each)
+          constexpr int WGH = S::T * 2;
+          auto kern = seed ? k_cols_half<LOGN, 0, kStream, true, false, true, kHalfRG2, kHalfRGC2, 2, true, false, kHalfHL,
+                                         kHalfHKSeed, 0, 2>
+                           : k_cols_half<LOGN, kStream, kStream, true, false, false, kHalfRG2, kHalfRGC2, 2, true, false,
+                                         kHalfHL, kHalfHK, 0, 2>;
+          const int lds = ((S::TW_ENTRIES * 8 + 15) / 16) * 16 + 2 * S::PADDED * 8 + kHalfHL * WGH * 16;
+          int grid = persistent_grid(kern, WGH, lds, fp.cascades * HalfCfg<LOGN>::STRIPS * 2, cus);
+          const int slices = hs_blocks * (1024 / WGH);
+          if (grid > slices)
+            grid = slices;
+          if (grid < 1)
+            return hipErrorInvalidValue;
+          hipLaunchKernelGGL(kern, dim3(grid), dim3(WGH), lds, stream, fp, h0, gab, gcd, ge, tw, hs, HalfSlab{},
+                             (unsigned char*)nullptr, 1, seed);
+          return hipGetLastError();
+        }
+      }
       auto kern = seed ? k_cols_half<LOGN, 0, kStream, true, false, true, RG, RGC, K::B, true, false, kHalfHL, kHalfHKSeed>
                        : k_cols_half<LOGN, kStream, kStream, true, false, false, RG, RGC, K::B, true, false, kHalfHL, HKW>;
       const int lds = ((S::TW_ENTRIES * 8 + 15) / 16) * 16 + K::LDS1 + kHalfHL * K::WG1 * 16;
@@ -96,7 +118,8 @@ hipError_t launch_half_rows(int logn, const FrameParams& fp, const float4* gab, 
       {
         if (half_rows_variant == 1)
         {
-          auto kern = k_rows_hp<RG, RGC>;
+          auto kern = half_fields_fb(LOGN, fp.cascades) == 2 ? k_rows_hp<kHalfRG2, kHalfRGC2, false, false, 2, kHalfRGC2>
+                                                             : k_rows_hp<RG, RGC>;
           const int grid = persistent_grid(kern, 256, HpCfg::LDS, fp.cascades * S::N, cus);
           hipLaunchKernelGGL(kern, dim3(grid), dim3(256), HpCfg::LDS, stream, fp, gab, gcd, ge, rcorr, maps, jac, foam, tw, 0,
                              RowSrc{});

@@ -411,6 +411,32 @@ def test_batched_cascades_equal_individual(ocean):
         assert np.array_equal(one.jacobian_map_host(0), batch.jacobian_map_host(c))
 
 
+def test_half_strip_shape_bit_exact_across_cascade_counts(ocean):
+    """At 4096 the column pass runs on half strips (FB = 2 fields, two 512-thread workgroups per CU)
+    when a launch holds <= 2 cascades and on whole strips above (launch_common.h half_fields_fb). A
+    cascade's maps and Jacobian are bit-identical in 1-, 2- and 3-cascade generators, for plain
+    frames and for the fused re-seed frames of the reference app's loop (src/Generator.cpp:45-83,
+    src/Waves.cpp:91-94)."""
+    n = 4096
+    planes = [5.0, 251.0, 4093.0]
+    fft = ocean.FFTCalculator(n)
+    gens = {k: ocean.Generator(fft, k) for k in (1, 2, 3)}
+    for k, g in gens.items():
+        g.set_h0_memo(False)
+        for c in range(k):
+            ocean.apply_settings(g.GetOceanSettings(c), planeSize=planes[c], seed=(12342 + 4097 * c, 8934))
+    for dt, upd in ((0.5, False), (1.0 / 60.0, True), (1.0 / 60.0, False)):
+        for g in gens.values():
+            g.CalculateOcean(dt, update_ocean=upd)
+        for k in (1, 2):
+            for c in range(k):
+                for get in ("height_map_host", "displacement_map_host", "jacobian_map_host"):
+                    assert np.array_equal(getattr(gens[k], get)(c), getattr(gens[3], get)(c)), (dt, upd, k, c, get)
+    for g in gens.values():
+        g.close()
+    fft.close()
+
+
 def test_update_spectrum_semantics(ocean, oracle):
     """h0 is regenerated on the first call and when update_ocean is set (src/Generator.cpp:55-59)."""
     n = 128

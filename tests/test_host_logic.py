@@ -65,11 +65,12 @@ def test_frame_overlap_mode_choice():
     cascades per GPU on the blocked half path; --frame-overlap on/off overrides, never on other paths."""
     b = _bench()
     auto = b.parse([])
-    assert [b.use_frame_overlap(auto, c, "half") for c in (8, 4, 2, 1)] == [False, False, True, True]
-    assert not b.use_frame_overlap(auto, 1, "full") and not b.use_frame_overlap(auto, 1, "four-step")
-    assert b.use_frame_overlap(b.parse(["--frame-overlap", "on"]), 8, "half")
-    assert not b.use_frame_overlap(b.parse(["--frame-overlap", "on"]), 8, "full")
-    assert not b.use_frame_overlap(b.parse(["--frame-overlap", "off"]), 1, "half")
+    assert [b.use_frame_overlap(auto, c, "half", 2048) for c in (8, 4, 2, 1)] == [False, False, True, True]
+    assert not any(b.use_frame_overlap(auto, c, "half", 4096) for c in (8, 4, 2, 1))  # half strips: serial
+    assert not b.use_frame_overlap(auto, 1, "full", 2048) and not b.use_frame_overlap(auto, 1, "four-step", 8192)
+    assert b.use_frame_overlap(b.parse(["--frame-overlap", "on"]), 8, "half", 4096)
+    assert not b.use_frame_overlap(b.parse(["--frame-overlap", "on"]), 8, "full", 4096)
+    assert not b.use_frame_overlap(b.parse(["--frame-overlap", "off"]), 1, "half", 1024)
 
 
 def test_lane_err_metric():

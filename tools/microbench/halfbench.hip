@@ -1,6 +1,6 @@
 // halfbench.hip — interleaved A/B timing of half-spectrum frame-pass variants (8 cascades x 4096^2),
 // with a bit-identity check of every variant's output against the baseline variant.
-// Build: see Makefile target `microbench`. Usage: halfbench [logn] [cascades] [quick|mall|rows|overlap|rowabl|hpair|hp|hx|xgrid]
+// Build: see Makefile target `microbench`. Usage: halfbench [logn] [cascades] [quick|mall|rows|overlap|rowabl|hpair|hp|hx|xgrid|fb2h]
 #include "all_kernels.h"
 
 #include <algorithm>
@@ -809,6 +809,92 @@ int main(int argc, char** argv)
     std::printf("C=%d frame, both passes on one stream     median %7.3f ms (%d frames)\n", C, ts[3], F);
     std::printf("C=%d frame, pass 1 of f+1 beside pass 2 of f median %7.3f ms  bit-identical %s\n", C, tp[3],
                 same ? "yes" : "NO");
+    return 0;
+  }
+  if (argc > 3 && std::strcmp(argv[3], "fb2h") == 0 && logn == 12)
+  {
+    // pass 1 on half strips at two 512-thread workgroups per CU (k_cols_half CPI = 2, 128 VGPRs, a
+    // 68-KiB exchange each) with fields FB = 2 columns wide (whole-line stores: gab / gde RG = 4, gc
+    // RGC = 8 or 4), the row pass k_rows_hp on that layout; against production (whole strips, one
+    // 1024-thread workgroup per CU). Same per-column arithmetic; the maps are compared to rounding.
+    using K = ColFirstCfg<12>;
+    using S = FftShape<12>;
+    const int tw0 = ((S::TW_ENTRIES * 8 + 15) / 16) * 16;
+    auto cols = [&](auto kern, int wg, int lds) {
+      return std::function<hipError_t()>([=] {
+        hipError_t e = launch_half_nyquist(fp, n, K::B, h0, spec, nullptr, 1, 0, nullptr, 0, cus);
+        if (e != hipSuccess)
+          return e;
+        const int items = fp.cascades * HalfCfg<12>::STRIPS * (K::WG1 / wg);
+        int grid = persistent_grid(kern, wg, lds, items, cus);
+        const int slices = cus * (1024 / wg);  // hs: cus slices of 16 x 1024 entries
+        grid = grid > slices ? slices : grid;
+        hipLaunchKernelGGL(kern, dim3(grid), dim3(wg), lds, 0, fp, h0, gab, gcd, ge, tw, hs, HalfSlab{},
+                           (unsigned char*)nullptr, 1, nullptr);
+        return hipGetLastError();
+      });
+    };
+    auto rows = [&](auto kern) {
+      return std::function<hipError_t()>([=] {
+        const int grid = persistent_grid(kern, 256, HpCfg::LDS, fp.cascades * n, cus);
+        hipLaunchKernelGGL(kern, dim3(grid), dim3(256), HpCfg::LDS, 0, fp, gab, gcd, ge, spec, maps, jac, foam, tw, 0,
+                           RowSrc{});
+        return hipGetLastError();
+      });
+    };
+    const int lds4 = tw0 + K::LDS1 + kHalfHL * 1024 * 16, lds2 = tw0 + 2 * S::PADDED * 8 + kHalfHL * 512 * 16;
+    std::vector<std::function<hipError_t()>> vc = {
+        cols(k_cols_half<12, kStream, kStream, true, false, false, kHalfRG, kHalfRGC, 4, true, false, kHalfHL, kHalfHK>, 1024, lds4),
+        cols(k_cols_half<12, kStream, kStream, true, false, false, 4, 8, 2, true, false, kHalfHL, 4, 0, 2>, 512, lds2),
+        cols(k_cols_half<12, kStream, kStream, true, false, false, 4, 8, 2, true, false, kHalfHL, 2, 0, 2>, 512, lds2),
+        cols(k_cols_half<12, kStream, kStream, true, false, false, 4, 4, 2, true, false, kHalfHL, 4, 0, 2>, 512, lds2)};
+    std::vector<std::function<hipError_t()>> vr = {rows(k_rows_hp<kHalfRG, kHalfRGC>),
+                                                   rows(k_rows_hp<4, 8, false, false, 2, 8>),
+                                                   rows(k_rows_hp<4, 8, false, false, 2, 8>),
+                                                   rows(k_rows_hp<4, 4, false, false, 2, 4>)};
+    const char* nm[] = {"production (whole strips)", "half strips FB 2, RGC 8, HK 4", "half strips FB 2, RGC 8, HK 2",
+                        "half strips FB 2, RGC 4, HK 4"};
+    const int NV = 4;
+    auto rel = [](const std::vector<unsigned char>& a, const std::vector<unsigned char>& b) {
+      const float* x = reinterpret_cast<const float*>(a.data());
+      const float* y = reinterpret_cast<const float*>(b.data());
+      double d = 0, m = 0;
+      for (size_t k = 0; k < a.size() / 4; k++)
+      {
+        d = std::max(d, (double)std::fabs(x[k] - y[k]));
+        m = std::max(m, (double)std::fabs(x[k]));
+      }
+      return d / (m > 0 ? m : 1);
+    };
+    CHECK(vc[0]());
+    CHECK(vr[0]());
+    CHECK(hipDeviceSynchronize());
+    auto pm = snap(maps, mb), pj = snap(jac, jb);
+    for (int k = 1; k < NV; k++)
+    {
+      CHECK(hipMemset(maps, 0, mb));
+      CHECK(hipMemset(jac, 0, jb));
+      CHECK(vc[k]());
+      CHECK(vr[k]());
+      CHECK(hipDeviceSynchronize());
+      std::printf("%s vs production: maps %.2g jacobian %.2g (max |diff| / max)\n", nm[k], rel(snap(maps, mb), pm),
+                  rel(snap(jac, jb), pj));
+    }
+    std::vector<std::vector<float>> t(NV), tr(NV), tf(NV);
+    for (int r = 0; r < 9; r++)
+      for (int k = 0; k < NV; k++)
+      {
+        t[k].push_back(time_ms(vc[k], 10));
+        tr[k].push_back(time_ms(vr[k], 10));
+        tf[k].push_back(time_ms([&] { CHECK(vc[k]()); return vr[k](); }, 10));
+      }
+    for (int k = 0; k < NV; k++)
+    {
+      std::sort(t[k].begin(), t[k].end());
+      std::sort(tr[k].begin(), tr[k].end());
+      std::sort(tf[k].begin(), tf[k].end());
+      std::printf("%-32s cols %7.3f ms  rows %7.3f ms  frame %7.3f ms\n", nm[k], t[k][4], tr[k][4], tf[k][4]);
+    }
     return 0;
   }
   if (argc > 3 && std::strcmp(argv[3], "xgrid") == 0)

@@ -847,14 +847,18 @@ int main(int argc, char** argv)
         cols(k_cols_half<12, kStream, kStream, true, false, false, kHalfRG, kHalfRGC, 4, true, false, kHalfHL, kHalfHK>, 1024, lds4),
         cols(k_cols_half<12, kStream, kStream, true, false, false, 4, 8, 2, true, false, kHalfHL, 4, 0, 2>, 512, lds2),
         cols(k_cols_half<12, kStream, kStream, true, false, false, 4, 8, 2, true, false, kHalfHL, 2, 0, 2>, 512, lds2),
-        cols(k_cols_half<12, kStream, kStream, true, false, false, 4, 4, 2, true, false, kHalfHL, 4, 0, 2>, 512, lds2)};
+        cols(k_cols_half<12, kStream, kStream, true, false, false, 4, 4, 2, true, false, kHalfHL, 4, 0, 2>, 512, lds2),
+        cols(k_cols_half<12, kStream, kStream, true, false, false, 4, 8, 2, true, false, kHalfHL, 4, 0, 2>, 512, lds2),
+        cols(k_cols_half<12, kStream, kStream, true, false, false, 4, 8, 2, true, false, kHalfHL, 4, 0, 2>, 512, lds2)};
     std::vector<std::function<hipError_t()>> vr = {rows(k_rows_hp<kHalfRG, kHalfRGC>),
                                                    rows(k_rows_hp<4, 8, false, false, 2, 8>),
                                                    rows(k_rows_hp<4, 8, false, false, 2, 8>),
-                                                   rows(k_rows_hp<4, 4, false, false, 2, 4>)};
+                                                   rows(k_rows_hp<4, 4, false, false, 2, 4>),
+                                                   rows(k_rows_hp<4, 8, false, false, 2, 4>),
+                                                   rows(k_rows_hp<4, 8, false, false, 2, 16>)};
     const char* nm[] = {"production (whole strips)", "half strips FB 2, RGC 8, HK 4", "half strips FB 2, RGC 8, HK 2",
-                        "half strips FB 2, RGC 4, HK 4"};
-    const int NV = 4;
+                        "half strips FB 2, RGC 4, HK 4", "FB 2, RGC 8, rows GRP 4", "FB 2, RGC 8, rows GRP 16"};
+    const int NV = 6;
     auto rel = [](const std::vector<unsigned char>& a, const std::vector<unsigned char>& b) {
       const float* x = reinterpret_cast<const float*>(a.data());
       const float* y = reinterpret_cast<const float*>(b.data());

@@ -36,6 +36,7 @@ extern "C" {
 #define OCEAN_ERR_HIP 2       /* HIP runtime error (message in ocean_last_error) */
 #define OCEAN_ERR_NO_DEVICE 3 /* no GPU visible */
 #define OCEAN_ERR_OOM 4       /* device allocation failed */
+/* OCEAN_ERR_TIMEOUT 5: see the one-sided slab exchange below */
 
 #define OCEAN_MAX_CASCADES 64
 
@@ -230,12 +231,68 @@ int ocean_generator_slab_frame(ocean_generator* gen, ocean_comm* comm, float tim
 int ocean_generator_slab_frame_pipelined(ocean_generator* gen, ocean_comm* comm, float timestep, int update_spectrum);
 int ocean_generator_slab_flush(ocean_generator* gen);
 
+/* ---- the one-sided slab exchange over peer-mapped memory (IPC, xGMI) -----------------------
+ * No send buffer and no copy kernel: the column pass's second step stores block q of its output
+ * straight into rank q's receive slot, through a mapping of rank q's device memory (hipIpc handles
+ * exchanged by the caller), and the row pass reads its own slot. Per frame each rank raises one
+ * flag word in every rank's flag array after its stores ("ready") and one after its row pass has
+ * read its slot ("freed"); the waits for them are one-wave kernels on the streams, bounded by a
+ * timeout (ocean_peers_set_timeout), so a missing peer never holds the GPU: the frame goes on, and
+ * ocean_peers_synchronize reports OCEAN_ERR_TIMEOUT. Four-step slabs only (N = 8192 / 16384, the
+ * default path there); the RCCL exchange above serves every slab path. SURVEY §8e, the reference's
+ * CalculateOcean (src/Generator.cpp:45-83) split over P ranks.
+ * Use: ocean_peers_create on every rank, ocean_peers_handle -> the caller gathers the P handles (in
+ * rank order, e.g. an all-gather) -> ocean_peers_connect; frames; ocean_peers_synchronize on every
+ * rank and a host barrier across ranks before ocean_peers_destroy (a peer may still signal). */
+#define OCEAN_ERR_TIMEOUT 5   /* a peer's frame signal did not arrive within the timeout */
+#define OCEAN_PEER_HANDLE_BYTES 256
+typedef struct ocean_peers ocean_peers;
+/* Two receive slots of ocean_generator_exchange_bytes(gen) and the flag words, in this process's
+ * device memory; gen must be a slab generator on the four-step path. */
+int ocean_peers_create(ocean_peers** out, ocean_generator* gen);
+int ocean_peers_destroy(ocean_peers* peers);
+/* This rank's handle (rank, ranks, slot size, the IPC handles of its slots and flags). */
+int ocean_peers_handle(const ocean_peers* peers, unsigned char handle[OCEAN_PEER_HANDLE_BYTES]);
+/* Map every other rank's slots and flags: handles = ranks * OCEAN_PEER_HANDLE_BYTES, in rank order
+ * (this rank's own entry is checked and used locally). */
+int ocean_peers_connect(ocean_peers* peers, const unsigned char* handles);
+/* The same for `ranks` ocean_peers of one process on one device (the single-GPU emulation of a P-rank
+ * grid, tests): each rank's peers are the others' buffers directly, no IPC. */
+int ocean_peers_connect_local(ocean_peers* const* all, int ranks);
+/* Wait timeout in milliseconds (default 20000). */
+int ocean_peers_set_timeout(ocean_peers* peers, int ms);
+/* CUs the put kernels (the Nyquist-row term and step 2) are sized for (0 = the plan's budget): with
+ * the stores bound by xGMI, fewer workgroups leave the other CUs to the row pass of the previous
+ * frame in the pipelined frame. */
+int ocean_peers_set_put_cus(ocean_peers* peers, int cus);
+/* The stream pipelined frames run their column pass and put on (null: the peers' own). The one-GPU
+ * emulation gives all P ranks one such stream, as one GPU has one path out over xGMI. */
+int ocean_peers_set_put_stream(ocean_peers* peers, void* hip_stream);
+/* Serial frame on the generator's stream: time += dt, h0 if needed, step 1, wait for the slot, put,
+ * signal; wait for every rank's blocks, row pass, signal. */
+int ocean_generator_slab_frame_put(ocean_generator* gen, ocean_peers* peers, float timestep, int update_spectrum);
+/* Pipelined: frame f's column pass and put on the peers' own stream, beside frame f - 1's row pass on
+ * the generator's stream (two slots); the maps lag by one frame until ocean_peers_flush. */
+int ocean_generator_slab_frame_put_pipelined(ocean_generator* gen, ocean_peers* peers, float timestep,
+                                             int update_spectrum);
+int ocean_peers_flush(ocean_peers* peers);
+/* The two halves of a serial frame, for callers (and the one-GPU emulation) that issue the column
+ * passes of all ranks before their row passes: columns + put + signal; wait + rows + signal. */
+int ocean_generator_slab_put_columns(ocean_generator* gen, ocean_peers* peers, float timestep, int update_spectrum);
+int ocean_generator_slab_put_rows(ocean_generator* gen, ocean_peers* peers);
+/* Wait for this rank's streams; OCEAN_ERR_TIMEOUT when any wait gave up (which, and at which frame,
+ * in ocean_last_error). */
+int ocean_peers_synchronize(ocean_peers* peers);
+
 /* ---- instrumentation (bench) ------------------------------------------------------------- */
 /* When enabled, each kernel launch of the generator is bracketed by HIP events on its stream. */
 int ocean_generator_set_profiling(ocean_generator* gen, int enable);
 /* Synchronises, then returns per-kernel totals since the last call and resets them.
  * Index 0 = spectrum (h0), 1 = column pass (evolve + y iFFT), 2 = row pass (x iFFT + foam). */
 int ocean_generator_kernel_times(ocean_generator* gen, double ms_total[3], int64_t launches[3]);
+/* The same with index 3 = the put of one-sided frames (the slot wait + the Nyquist-row term + step 2,
+ * which index 1 includes). */
+int ocean_generator_kernel_times4(ocean_generator* gen, double ms_total[4], int64_t launches[4]);
 
 /* ---- debug -------------------------------------------------------------------------------- */
 /* Device Hash (resources/spectrum.compute:109-117) of count (x, y) pairs in device memory:

@@ -16,8 +16,10 @@ OCEAN_ERR_INVALID = 1
 OCEAN_ERR_HIP = 2
 OCEAN_ERR_NO_DEVICE = 3
 OCEAN_ERR_OOM = 4
+OCEAN_ERR_TIMEOUT = 5
 OCEAN_MAX_CASCADES = 64
 OCEAN_COMM_ID_BYTES = 128
+OCEAN_PEER_HANDLE_BYTES = 256
 
 
 class OceanSettings(ctypes.Structure):
@@ -101,6 +103,21 @@ SIGNATURES = {
     "ocean_generator_slab_frame": (_i, [_vp, _vp, _f, _i]),
     "ocean_generator_slab_frame_pipelined": (_i, [_vp, _vp, _f, _i]),
     "ocean_generator_slab_flush": (_i, [_vp]),
+    "ocean_peers_create": (_i, [ctypes.POINTER(_vp), _vp]),
+    "ocean_peers_destroy": (_i, [_vp]),
+    "ocean_peers_handle": (_i, [_vp, _vp]),
+    "ocean_peers_connect": (_i, [_vp, _vp]),
+    "ocean_peers_connect_local": (_i, [ctypes.POINTER(_vp), _i]),
+    "ocean_peers_set_timeout": (_i, [_vp, _i]),
+    "ocean_peers_set_put_cus": (_i, [_vp, _i]),
+    "ocean_peers_set_put_stream": (_i, [_vp, _vp]),
+    "ocean_generator_kernel_times4": (_i, [_vp, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int64)]),
+    "ocean_generator_slab_frame_put": (_i, [_vp, _vp, _f, _i]),
+    "ocean_generator_slab_frame_put_pipelined": (_i, [_vp, _vp, _f, _i]),
+    "ocean_peers_flush": (_i, [_vp]),
+    "ocean_generator_slab_put_columns": (_i, [_vp, _vp, _f, _i]),
+    "ocean_generator_slab_put_rows": (_i, [_vp, _vp]),
+    "ocean_peers_synchronize": (_i, [_vp]),
 }
 
 _lib = None

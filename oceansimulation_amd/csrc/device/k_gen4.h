@@ -139,10 +139,14 @@ __global__ __launch_bounds__(256, MINW) void k_gen4_step1(FrameParams fp, Gen4Ge
 // otherwise two adjacent float2 columns of gc in the reference's (re0, im0, re1, im1) order,
 // transformed as the two lanes of one CPair. cols: columns to transform (< pitch).
 // CI: columns per workgroup (8: 128-B pieces, 512-thread workgroups, two per CU at N2 = 1024).
-template <int LOGN2, bool PAIRS, int CI = ColCfg<LOGN2>::C>
+// PUT (the one-sided exchange, ocean_peers): block q goes straight to dst[q], the address of this
+// rank's block in rank q's receive slot (a peer mapping over xGMI, or local memory for q == rank),
+// instead of send + q * blk_bytes; no send buffer exists. Each workgroup ends with a system-scope
+// release, so its stores have left this XCD's L2 before the kernel's completion is signalled.
+template <int LOGN2, bool PAIRS, int CI = ColCfg<LOGN2>::C, bool PUT = false>
 __global__ __launch_bounds__(FftShape<LOGN2>::T * CI, CI < ColCfg<LOGN2>::C ? 4 : 1) void k_gen4_step2(
     int cascades, int cols, int pitch, const float4* __restrict__ work, unsigned char* __restrict__ send,
-    size_t part_off, Gen4Geom g, const float2* __restrict__ tw_glob)
+    size_t part_off, Gen4Geom g, const float2* __restrict__ tw_glob, const uint64_t* __restrict__ dst)
 {
   using S = FftShape<LOGN2>;
   constexpr int N2 = S::N, T = S::T, C = CI, N = N2 * 16;
@@ -177,10 +181,14 @@ __global__ __launch_bounds__(FftShape<LOGN2>::T * CI, CI < ColCfg<LOGN2>::C ? 4 
     {
       const int q = (m * T) / kpb, k2b = m * T - q * kpb;
       // the block row base is built at its store (sopaque): hoisted, the 16 bases take 32 SGPRs
-      unsigned char* dst = send + sopaque(q * g.blk_bytes + part_off + ((size_t)c * g.w + k1 + 16 * k2b) * pitch * 16);
-      st4<kStream>(dst, soff, PAIRS ? pair_raw(v[m]) : from_pair(v[m]));
+      const size_t boff = part_off + ((size_t)c * g.w + k1 + 16 * k2b) * pitch * 16;
+      unsigned char* d = PUT ? reinterpret_cast<unsigned char*>(sopaque((size_t)dst[q] + boff))
+                             : send + sopaque(q * g.blk_bytes + boff);
+      st4<kStream>(d, soff, PAIRS ? pair_raw(v[m]) : from_pair(v[m]));
     }
   }
+  if constexpr (PUT)
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
 }
 
 // Strip-dealt half-spectrum fields -> row-major (HalfSlab blocks -> [c][yl][kp], kp = STRIPS * B):

@@ -127,7 +127,12 @@ hipError_t launch_half_rows(int logn, const FrameParams& fp, const float4* gab, 
         }
       }
       constexpr int RPW = LOGN == 12 ? 1 : 2, GRP = LOGN == 12 ? 4 : 2;
+      // the column pass chose the field layout by cascade count (half_fields_fb): the fallback reads
+      // the same one (FB = 2 with row groups 4 / 8 at 4096 and <= 2 cascades)
       auto kern = k_rows_half<LOGN, 0, kStream, 0, RPW, true, false, RG, RGC, 4, GRP>;
+      if constexpr (LOGN == 12)
+        if (half_fields_fb(LOGN, fp.cascades) == 2)
+          kern = k_rows_half<LOGN, 0, kStream, 0, RPW, true, false, kHalfRG2, kHalfRGC2, 2, GRP>;
       const int lds = ((S::TW_ENTRIES * 8 + 15) / 16) * 16 + lds_row_slots<LOGN>(RPW) * 8;
       const int grid = persistent_grid(kern, S::T * RPW, lds, fp.cascades * (S::N / RPW), cus);
       hipLaunchKernelGGL(kern, dim3(grid), dim3(S::T * RPW), lds, stream, fp, gab, gcd, ge, rcorr, maps, jac, foam, tw,

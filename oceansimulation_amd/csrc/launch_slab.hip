@@ -227,9 +227,10 @@ static size_t gen4_part_offset(int cascades, const Gen4Geom& g, int part)
 }
 
 hipError_t launch_gen4_columns(int logn, const FrameParams& fp, const Gen4Geom& g, const float4* h0, const float4* h0row,
-                               void* parts, void* send, const float2* tw, const float2* tw2, hipStream_t stream, int cus)
+                               void* parts, void* send, const float2* tw, const float2* tw2, hipStream_t stream, int cus,
+                               const Gen4Put* put)
 {
-  if (!tw2 || g.cols % kGen4Block != 0)
+  if (!tw2 || g.cols % kGen4Block != 0 || (put && !put->dst))
     return hipErrorInvalidValue;
   return with_logn(logn, [&](auto L) -> hipError_t {
     constexpr int LOGN = decltype(L)::value;
@@ -240,18 +241,34 @@ hipError_t launch_gen4_columns(int logn, const FrameParams& fp, const Gen4Geom& 
       constexpr int N = 1 << LOGN, N2 = N / 16, LOGN2 = LOGN - 4;
       const int C = fp.cascades;
       unsigned char* snd = static_cast<unsigned char*>(send);
-      // the Nyquist-row term, into every destination block (each frame's row pass reads its own)
-      float4* spec = reinterpret_cast<float4*>(snd + gen4_part_offset(C, g, 3));
-      hipError_t e = launch_half_nyquist(fp, N, kGen4Block, h0, spec, h0row, g.ranks, g.blk_bytes, nullptr, stream, cus);
-      if (e != hipSuccess)
-        return e;
       // step 1: h0 -> the rank's parts [c][N][lp]
       auto k1 = k_gen4_step1<LOGN>;
       const int ncols = g.cols + g.nyq;
       const int items = C * ((ncols + 63) / 64) * (N2 / 4);
       hipLaunchKernelGGL(k1, dim3(persistent_grid(k1, 256, 0, items, cus)), dim3(256), 0, stream, fp, g, h0,
                          (unsigned char*)parts, tw);
-      e = hipGetLastError();
+      hipError_t e = hipGetLastError();
+      if (e != hipSuccess)
+        return e;
+      // the one-sided exchange writes into the peers' receive slots: only once they are free
+      if (put && put->start)
+      {
+        e = hipEventRecord(put->start, stream);
+        if (e != hipSuccess)
+          return e;
+      }
+      if (put && put->wait)
+      {
+        e = launch_peer_wait(*put->wait, stream);
+        if (e != hipSuccess)
+          return e;
+      }
+      const int cus2 = put && put->cus > 0 ? put->cus : cus;
+      // the Nyquist-row term, into every destination block (each frame's row pass reads its own)
+      e = put ? launch_half_nyquist(fp, N, kGen4Block, h0, nullptr, h0row, g.ranks, 0, nullptr, stream, cus2, put->dst,
+                                    gen4_part_offset(C, g, 3))
+              : launch_half_nyquist(fp, N, kGen4Block, h0, reinterpret_cast<float4*>(snd + gen4_part_offset(C, g, 3)),
+                                    h0row, g.ranks, g.blk_bytes, nullptr, stream, cus);
       if (e != hipSuccess)
         return e;
       // step 2: parts -> destination blocks. 8 columns per workgroup at N2 = 1024 (512 threads, two per
@@ -264,15 +281,18 @@ hipError_t launch_gen4_columns(int logn, const FrameParams& fp, const Gen4Geom& 
       const float4* wde = wab + part;
       const float4* wc = wde + part;  // gc (float2 texels) viewed as pairs of columns
       const int lds2 = ((FftShape<LOGN2>::TW_ENTRIES * 8 + 15) / 16) * 16 + CI * FftShape<LOGN2>::PADDED * 8;
-      auto sp = k_gen4_step2<LOGN2, true, CI>;
-      auto sc = k_gen4_step2<LOGN2, false, CI>;
+      auto sp = put ? k_gen4_step2<LOGN2, true, CI, true> : k_gen4_step2<LOGN2, true, CI>;
+      auto sc = put ? k_gen4_step2<LOGN2, false, CI, true> : k_gen4_step2<LOGN2, false, CI>;
+      const uint64_t* dst = put ? put->dst : nullptr;
       const int pcols = (ncols + 1) / 2;
-      const int gp = persistent_grid(sp, WG2, lds2, C * 16 * ((ncols + CI - 1) / CI), cus);
-      const int gcg = persistent_grid(sc, WG2, lds2, C * 16 * ((pcols + CI - 1) / CI), cus);
-      hipLaunchKernelGGL(sp, dim3(gp), dim3(WG2), lds2, stream, C, ncols, g.lp, wab, snd, gen4_part_offset(C, g, 0), g, tw2);
-      hipLaunchKernelGGL(sp, dim3(gp), dim3(WG2), lds2, stream, C, ncols, g.lp, wde, snd, gen4_part_offset(C, g, 1), g, tw2);
+      const int gp = persistent_grid(sp, WG2, lds2, C * 16 * ((ncols + CI - 1) / CI), cus2);
+      const int gcg = persistent_grid(sc, WG2, lds2, C * 16 * ((pcols + CI - 1) / CI), cus2);
+      hipLaunchKernelGGL(sp, dim3(gp), dim3(WG2), lds2, stream, C, ncols, g.lp, wab, snd, gen4_part_offset(C, g, 0), g, tw2,
+                         dst);
+      hipLaunchKernelGGL(sp, dim3(gp), dim3(WG2), lds2, stream, C, ncols, g.lp, wde, snd, gen4_part_offset(C, g, 1), g, tw2,
+                         dst);
       hipLaunchKernelGGL(sc, dim3(gcg), dim3(WG2), lds2, stream, C, pcols, g.lp / 2, wc, snd, gen4_part_offset(C, g, 2), g,
-                         tw2);
+                         tw2, dst);
       return hipGetLastError();
     }
   });

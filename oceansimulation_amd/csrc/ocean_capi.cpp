@@ -139,6 +139,11 @@ struct ocean_generator
   FrameParams slot_frame[2]{};     // the column pass's per-cascade values of the frame in each slot
   FoamParams slot_foam[2]{};       // and the settings' displacement its row pass uses
   int64_t frames_issued = 0;
+  // the one-sided exchange bound to this generator (ocean_peers_create), and the event that orders its
+  // put stream after h0 writes on the generator's stream
+  ocean_peers* peers = nullptr;
+  hipEvent_t put_h0 = nullptr;
+  hipStream_t cols_stream = nullptr;  // the stream the last four-step column pass ran on
   // ocean_generator_set_frame_overlap (blocked half path): frame f's column pass on `side` into field
   // slot f % 2, beside frame f - 1's row pass on the generator's stream
   bool overlap = false;
@@ -152,9 +157,12 @@ struct ocean_generator
   bool profiling = false;
   std::vector<EventPair> pending;
   std::vector<hipEvent_t> pool;
-  double ms[3] = {0, 0, 0};
-  int64_t launches[3] = {0, 0, 0};
+  double ms[4] = {0, 0, 0, 0};         // per kind: 0 h0, 1 column pass, 2 row pass, 3 the put inside 1
+  int64_t launches[4] = {0, 0, 0, 0};
 };
+
+static void peers_detach(ocean_peers* p);  // the one-sided exchange section below
+static bool peers_pending(const ocean_peers* p);
 
 extern "C" {
 
@@ -622,6 +630,8 @@ int ocean_generator_destroy(ocean_generator* g)
   // communicator must outlive the generator, include/oceanfft.h). Drain it before the slots go.
   if (g->comm_stream)
     (void)hipStreamSynchronize(g->comm_stream);
+  if (g->peers)
+    peers_detach(g->peers);
   if (g->fft)
     (void)hipStreamSynchronize(g->fft->stream);
   for (auto& p : g->pending)
@@ -652,6 +662,8 @@ int ocean_generator_destroy(ocean_generator* g)
   }
   if (g->comm_stream)
     (void)hipStreamDestroy(g->comm_stream);
+  if (g->put_h0)
+    (void)hipEventDestroy(g->put_h0);
   if (g->side)
   {
     (void)hipStreamSynchronize(g->side);
@@ -780,7 +792,10 @@ static bool same_h0_inputs(const std::vector<ocean_settings>& a, const std::vect
   return true;
 }
 
-static int generator_columns(ocean_generator* g, float timestep, int update_spectrum, float4* out)
+// put (four-step slabs, the one-sided exchange): step 2 stores into the peers' receive slots, on
+// col_stream (null: the generator's stream), which first waits for the h0 writes issued so far.
+static int generator_columns(ocean_generator* g, float timestep, int update_spectrum, float4* out,
+                             const Gen4Put* put = nullptr, hipStream_t col_stream = nullptr)
 {
   ocean_fft* f = g->fft;
   for (auto& s : g->settings)
@@ -860,11 +875,46 @@ static int generator_columns(ocean_generator* g, float timestep, int update_spec
                   std::string("column pass buffers: ") + hipGetErrorString(e));
   }
   if (uses_gen4(g))
+  {
+    // the column pass's stream (the put stream of pipelined one-sided frames) runs after the last
+    // column pass on another stream (step 1 rewrites the parts its step 2 read) and after h0 writes
+    hipStream_t cs = col_stream ? col_stream : f->stream;
+    hipStream_t after = g->cols_stream && g->cols_stream != cs ? g->cols_stream
+                        : cs != f->stream && g->h0_dirty   ? f->stream
+                                                           : nullptr;
+    if (after)
+    {
+      if (!g->put_h0)
+        HIP_TRY(hipEventCreateWithFlags(&g->put_h0, hipEventDisableTiming), "column pass: event");
+      HIP_TRY(hipEventRecord(g->put_h0, after), "column pass: stream event");
+      HIP_TRY(hipStreamWaitEvent(cs, g->put_h0, 0), "column pass: stream order");
+      if (after == f->stream)
+        g->h0_dirty = false;
+    }
+    g->cols_stream = cs;
+    // profiling a put: kind 3 brackets the wait + put kernels inside the column pass (kind 1)
+    Gen4Put timed_put = put ? *put : Gen4Put{};
+    EventPair pp{3, nullptr, nullptr};
+    if (put && g->profiling)
+    {
+      pp.a = take_event(g);
+      pp.b = take_event(g);
+      timed_put.start = pp.a;
+    }
     HIP_TRY(timed(g, 1, [&] {
               return launch_gen4_columns(f->logn, fp, g->g4, g->h0, g->ranks > 1 ? g->h0row : nullptr, g->parts,
-                                         out ? (void*)out : (void*)g->xbuf, f->twiddles, f->tw2, f->stream, f->cus);
-            }),
+                                         out ? (void*)out : (void*)g->xbuf, f->twiddles, f->tw2, cs, f->cus,
+                                         put ? &timed_put : nullptr);
+            }, cs),
             "column pass (half spectrum, four-step)");
+    if (pp.a)
+    {
+      HIP_TRY(hipEventRecord(pp.b, cs), "column pass: put event");
+      g->pending.push_back(pp);
+    }
+  }
+  else if (put)
+    return fail(OCEAN_ERR_INVALID, "column pass: the one-sided exchange needs the four-step path (N = 8192 / 16384)");
   else if (g->hslab)
     HIP_TRY(timed(g, 1, [&] {
               return launch_half_slab_columns(f->logn, fp, g->hsl, g->ranks, g->h0, g->ranks == 1, g->h0row,
@@ -969,6 +1019,12 @@ int ocean_generator_set_half_spectrum(ocean_generator* g, int enable)
 {
   if (!g)
     return fail(OCEAN_ERR_INVALID, "ocean_generator_set_half_spectrum: null generator");
+  if (peers_pending(g->peers))
+  {
+    const int rc = ocean_peers_flush(g->peers);  // a pipelined one-sided frame in flight lands first
+    if (rc != OCEAN_OK)
+      return rc;
+  }
   if (g->pending_slot >= 0)
   {
     // a pipelined slab frame's column pass wrote its blocks in the current path's layout: its row
@@ -1073,6 +1129,12 @@ int ocean_generator_set_four_step(ocean_generator* g, int enable)
 {
   if (!g)
     return fail(OCEAN_ERR_INVALID, "ocean_generator_set_four_step: null generator");
+  if (peers_pending(g->peers))
+  {
+    const int rc = ocean_peers_flush(g->peers);  // a pipelined one-sided frame in flight lands first
+    if (rc != OCEAN_OK)
+      return rc;
+  }
   if (g->pending_slot >= 0)
   {
     const int rc = ocean_generator_slab_flush(g);  // as in ocean_generator_set_half_spectrum
@@ -1421,6 +1483,421 @@ int ocean_generator_slab_flush(ocean_generator* g)
   return slot_rows(g, s);
 }
 
+// ---------------------------------------------------------------------------------------------
+// The one-sided slab exchange (ocean_peers): the four-step column pass stores block q into rank q's
+// receive slot through a peer mapping, and per-frame flag words replace the all-to-all (SURVEY §8e;
+// DESIGN.md §6 "one-sided exchange").
+// ---------------------------------------------------------------------------------------------
+}  // extern "C"
+
+namespace
+{
+constexpr int kMaxRanks = 16;
+constexpr int kReadyWord = 0, kFreedWord = 16, kErrWord = 48, kFlagWords = 64;
+constexpr uint32_t kPeerMagic = 0x4f505231;  // "OPR1"
+
+struct PeerHandle
+{
+  uint32_t magic;
+  int32_t rank, ranks;
+  uint32_t flags_uncached;
+  uint64_t slot_bytes;
+  hipIpcMemHandle_t data, flags;
+};
+static_assert(sizeof(PeerHandle) <= OCEAN_PEER_HANDLE_BYTES, "peer handle size");
+}  // namespace
+
+struct ocean_peers
+{
+  ocean_generator* g = nullptr;
+  int rank = 0, ranks = 1;
+  size_t blk = 0, slot = 0;        // block bytes, slot bytes (ranks * blk = the exchange bytes)
+  unsigned char* data = nullptr;   // this rank's two receive slots
+  uint32_t* flags = nullptr;       // this rank's flag words: ready[16] | freed[16] | .. | err @ 48
+  bool flags_uncached = false;
+  unsigned char* peer_data[kMaxRanks] = {};
+  uint32_t* peer_flags[kMaxRanks] = {};
+  bool mapped[2 * kMaxRanks] = {};  // data / flags opened with hipIpcOpenMemHandle (closed on destroy)
+  bool connected = false;
+  uint64_t* table = nullptr;       // device: put destinations [2 slots][16], then the flag arrays [16]
+  hipStream_t put_stream = nullptr;  // the stream pipelined column passes + puts run on
+  hipStream_t own_stream = nullptr;  // the one ocean_peers_create made (put_stream unless replaced)
+  long long deadline = 0;          // wall-clock ticks
+  int timeout_ms = 20000;
+  int put_cus = 0;
+  int64_t frames = 0;              // frames whose column pass was issued
+  int64_t rows = 0;                // frames whose row pass was issued
+  FrameParams slot_frame[2]{};
+  FoamParams slot_foam[2]{};
+};
+
+namespace
+{
+int peers_deadline(ocean_peers* p)
+{
+  int khz = 0;
+  HIP_TRY(hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, p->g ? p->g->fft->device : 0),
+          "ocean_peers: wall clock rate");
+  p->deadline = (long long)(khz > 0 ? khz : 100000) * p->timeout_ms;
+  return OCEAN_OK;
+}
+
+int check_peers(const ocean_generator* g, const ocean_peers* p, const char* who)
+{
+  if (!g || !p || p->g != g)
+    return fail(OCEAN_ERR_INVALID, std::string(who) + ": null generator, or peers created for another generator");
+  if (!p->connected)
+    return fail(OCEAN_ERR_INVALID, std::string(who) + ": ocean_peers_connect has not run");
+  if (!uses_gen4(g) || hslab_xbuf_bytes(g) != p->slot)
+    return fail(OCEAN_ERR_INVALID, std::string(who) + ": the generator left the four-step path (or its exchange size "
+                                                      "changed) since ocean_peers_create");
+  return OCEAN_OK;
+}
+
+// the device table: dst[s][q] = rank q's slot s + this rank's block offset, then the flag arrays
+int peers_table(ocean_peers* p)
+{
+  uint64_t host[3 * kMaxRanks] = {};
+  for (int s = 0; s < 2; s++)
+    for (int q = 0; q < p->ranks; q++)
+      host[s * kMaxRanks + q] = (uint64_t)(uintptr_t)(p->peer_data[q] + s * p->slot + (size_t)p->rank * p->blk);
+  for (int q = 0; q < p->ranks; q++)
+    host[2 * kMaxRanks + q] = (uint64_t)(uintptr_t)p->peer_flags[q];
+  HIP_TRY(hipMemcpy(p->table, host, sizeof(host), hipMemcpyHostToDevice), "ocean_peers: destination table");
+  p->connected = true;
+  return OCEAN_OK;
+}
+
+PeerWait peer_wait(ocean_peers* p, int word0, int64_t target)
+{
+  return PeerWait{p->flags, word0, p->ranks, (uint32_t)target, p->deadline, p->flags + kErrWord};
+}
+
+uint32_t* const* flag_table(const ocean_peers* p)
+{
+  return reinterpret_cast<uint32_t* const*>(p->table + 2 * kMaxRanks);
+}
+
+// Column pass of frame f = p->frames into every rank's slot f % 2, on `stream` (the generator's or the
+// put stream): step 1, wait until every rank has finished reading that slot (frame f - 2's row pass),
+// the put, then this rank's "ready" word (f + 1) in every rank's flags.
+int put_columns(ocean_generator* g, ocean_peers* p, float timestep, int update_spectrum, hipStream_t stream)
+{
+  const int64_t f = p->frames;
+  const int s = (int)(f % 2);
+  const PeerWait w = peer_wait(p, kFreedWord, f - 1);
+  const Gen4Put put{p->table + s * kMaxRanks, f >= 2 ? &w : nullptr, p->put_cus};
+  int rc = generator_columns(g, timestep, update_spectrum, nullptr, &put, stream);
+  if (rc != OCEAN_OK)
+    return rc;
+  HIP_TRY(launch_peer_signal(flag_table(p), p->ranks, kReadyWord + p->rank, (uint32_t)(f + 1),
+                             stream ? stream : g->fft->stream),
+          "one-sided exchange: ready signal");
+  p->slot_frame[s] = g->frame;
+  p->slot_foam[s] = current_foam(g);
+  p->frames = f + 1;
+  return OCEAN_OK;
+}
+
+// Row pass of the oldest frame whose rows are not issued yet, on the generator's stream: wait for
+// every rank's blocks, rows, then this rank's "freed" word (f + 1) in every rank's flags.
+int put_rows(ocean_generator* g, ocean_peers* p)
+{
+  ocean_fft* f = g->fft;
+  const int64_t fr = p->rows;
+  if (fr >= p->frames)
+    return fail(OCEAN_ERR_INVALID, "ocean_generator_slab_put_rows: no column pass issued for this frame");
+  const int s = (int)(fr % 2);
+  HIP_TRY(launch_peer_wait(peer_wait(p, kReadyWord, fr + 1), f->stream), "one-sided exchange: ready wait");
+  const FrameParams newest = g->frame;
+  g->frame = p->slot_frame[s];
+  const int rc = generator_rows(g, reinterpret_cast<const float4*>(p->data + s * p->slot), &p->slot_foam[s]);
+  g->frame = newest;
+  if (rc != OCEAN_OK)
+    return rc;
+  HIP_TRY(launch_peer_signal(flag_table(p), p->ranks, kFreedWord + p->rank, (uint32_t)(fr + 1), f->stream),
+          "one-sided exchange: freed signal");
+  p->rows = fr + 1;
+  return OCEAN_OK;
+}
+
+void peers_release(ocean_peers* p)
+{
+  if (p->put_stream)
+    (void)hipStreamSynchronize(p->put_stream);
+  if (p->g && p->g->fft)
+    (void)hipStreamSynchronize(p->g->fft->stream);
+  for (int q = 0; q < kMaxRanks; q++)
+  {
+    if (p->mapped[q] && p->peer_data[q])
+      (void)hipIpcCloseMemHandle(p->peer_data[q]);
+    if (p->mapped[kMaxRanks + q] && p->peer_flags[q])
+      (void)hipIpcCloseMemHandle(p->peer_flags[q]);
+    p->mapped[q] = p->mapped[kMaxRanks + q] = false;
+  }
+}
+}  // namespace
+
+// a column pass whose row pass is not issued yet (a pipelined frame in flight)
+static bool peers_pending(const ocean_peers* p) { return p && p->rows < p->frames; }
+
+// called by ocean_generator_destroy: a generator destroyed before its peers leaves them unusable
+static void peers_detach(ocean_peers* p)
+{
+  if (!p)
+    return;
+  if (p->put_stream)
+    (void)hipStreamSynchronize(p->put_stream);
+  p->g = nullptr;
+  p->connected = false;
+}
+
+extern "C" {
+
+int ocean_peers_create(ocean_peers** out, ocean_generator* g)
+{
+  if (!out || !g)
+    return fail(OCEAN_ERR_INVALID, "ocean_peers_create: null argument");
+  *out = nullptr;
+  if (!g->slab || !uses_gen4(g))
+    return fail(OCEAN_ERR_INVALID, "ocean_peers_create: a slab generator on the four-step path (N = 8192 / 16384)");
+  if (g->peers)
+    return fail(OCEAN_ERR_INVALID, "ocean_peers_create: the generator already has peers");
+  hipError_t e = hslab_buffers(g);
+  if (e != hipSuccess)
+    return hip_fail(e, "ocean_peers_create: generator buffers");
+  auto* p = new ocean_peers();
+  p->g = g;
+  p->rank = g->rank;
+  p->ranks = g->ranks;
+  p->slot = hslab_xbuf_bytes(g);
+  p->blk = p->slot / g->ranks;
+  e = hipMalloc(&p->data, 2 * p->slot);
+  // the flag words in uncached memory: polled by one wave, written by the peers over xGMI
+  if (e == hipSuccess)
+  {
+    if (hipExtMallocWithFlags((void**)&p->flags, kFlagWords * sizeof(uint32_t), hipDeviceMallocUncached) == hipSuccess)
+      p->flags_uncached = true;
+    else
+    {
+      (void)hipGetLastError();
+      e = hipMalloc(&p->flags, kFlagWords * sizeof(uint32_t));
+    }
+  }
+  if (e == hipSuccess)
+    e = hipMalloc(&p->table, 3 * kMaxRanks * sizeof(uint64_t));
+  if (e == hipSuccess)
+    e = hipMemset(p->flags, 0, kFlagWords * sizeof(uint32_t));
+  if (e == hipSuccess)
+    e = hipStreamCreateWithFlags(&p->own_stream, hipStreamNonBlocking);
+  p->put_stream = p->own_stream;
+  if (e == hipSuccess)
+    e = hipDeviceSynchronize();
+  int rc = e == hipSuccess ? peers_deadline(p) : OCEAN_OK;
+  if (e != hipSuccess || rc != OCEAN_OK)
+  {
+    const int code = e == hipErrorOutOfMemory ? OCEAN_ERR_OOM : OCEAN_ERR_HIP;
+    p->g = nullptr;
+    ocean_peers_destroy(p);
+    return rc != OCEAN_OK ? rc : fail(code, std::string("ocean_peers_create: ") + hipGetErrorString(e));
+  }
+  p->peer_data[p->rank] = p->data;
+  p->peer_flags[p->rank] = p->flags;
+  g->peers = p;
+  *out = p;
+  return OCEAN_OK;
+}
+
+int ocean_peers_destroy(ocean_peers* p)
+{
+  if (!p)
+    return OCEAN_OK;
+  peers_release(p);
+  if (p->g)
+    p->g->peers = nullptr;
+  if (p->own_stream)
+    (void)hipStreamDestroy(p->own_stream);
+  for (void* q : {(void*)p->data, (void*)p->flags, (void*)p->table})
+    if (q)
+      (void)hipFree(q);
+  delete p;
+  return OCEAN_OK;
+}
+
+int ocean_peers_handle(const ocean_peers* p, unsigned char handle[OCEAN_PEER_HANDLE_BYTES])
+{
+  if (!p || !handle)
+    return fail(OCEAN_ERR_INVALID, "ocean_peers_handle: null argument");
+  PeerHandle h{};
+  h.magic = kPeerMagic;
+  h.rank = p->rank;
+  h.ranks = p->ranks;
+  h.flags_uncached = p->flags_uncached ? 1 : 0;
+  h.slot_bytes = p->slot;
+  HIP_TRY(hipIpcGetMemHandle(&h.data, p->data), "ocean_peers_handle: hipIpcGetMemHandle (slots)");
+  HIP_TRY(hipIpcGetMemHandle(&h.flags, p->flags), "ocean_peers_handle: hipIpcGetMemHandle (flags)");
+  std::memset(handle, 0, OCEAN_PEER_HANDLE_BYTES);
+  std::memcpy(handle, &h, sizeof(h));
+  return OCEAN_OK;
+}
+
+int ocean_peers_connect(ocean_peers* p, const unsigned char* handles)
+{
+  if (!p || !handles || !p->g)
+    return fail(OCEAN_ERR_INVALID, "ocean_peers_connect: null argument or detached peers");
+  if (p->connected)
+    return fail(OCEAN_ERR_INVALID, "ocean_peers_connect: already connected");
+  for (int q = 0; q < p->ranks; q++)
+  {
+    PeerHandle h;
+    std::memcpy(&h, handles + (size_t)q * OCEAN_PEER_HANDLE_BYTES, sizeof(h));
+    if (h.magic != kPeerMagic || h.rank != q || h.ranks != p->ranks || h.slot_bytes != p->slot)
+      return fail(OCEAN_ERR_INVALID, "ocean_peers_connect: handle " + std::to_string(q) + " is not rank " +
+                                         std::to_string(q) + " of " + std::to_string(p->ranks) +
+                                         " with this grid's slot size");
+    if (q == p->rank)
+      continue;
+    void* d = nullptr;
+    void* fl = nullptr;
+    hipError_t e = hipIpcOpenMemHandle(&d, h.data, hipIpcMemLazyEnablePeerAccess);
+    if (e == hipSuccess)
+    {
+      p->peer_data[q] = static_cast<unsigned char*>(d);
+      p->mapped[q] = true;
+      e = hipIpcOpenMemHandle(&fl, h.flags, hipIpcMemLazyEnablePeerAccess);
+    }
+    if (e == hipSuccess)
+    {
+      p->peer_flags[q] = static_cast<uint32_t*>(fl);
+      p->mapped[kMaxRanks + q] = true;
+    }
+    if (e != hipSuccess)
+    {
+      peers_release(p);
+      return hip_fail(e, ("ocean_peers_connect: hipIpcOpenMemHandle of rank " + std::to_string(q)).c_str());
+    }
+  }
+  return peers_table(p);
+}
+
+int ocean_peers_connect_local(ocean_peers* const* all, int ranks)
+{
+  if (!all || ranks < 1 || ranks > kMaxRanks)
+    return fail(OCEAN_ERR_INVALID, "ocean_peers_connect_local: null array or ranks outside [1, 16]");
+  for (int q = 0; q < ranks; q++)
+    if (!all[q] || !all[q]->g || all[q]->rank != q || all[q]->ranks != ranks || all[q]->slot != all[0]->slot ||
+        all[q]->connected)
+      return fail(OCEAN_ERR_INVALID, "ocean_peers_connect_local: entry " + std::to_string(q) +
+                                         " is not an unconnected rank " + std::to_string(q) + " of " +
+                                         std::to_string(ranks) + " of one grid");
+  for (int r = 0; r < ranks; r++)
+  {
+    for (int q = 0; q < ranks; q++)
+    {
+      all[r]->peer_data[q] = all[q]->data;
+      all[r]->peer_flags[q] = all[q]->flags;
+    }
+    const int rc = peers_table(all[r]);
+    if (rc != OCEAN_OK)
+      return rc;
+  }
+  return OCEAN_OK;
+}
+
+int ocean_peers_set_timeout(ocean_peers* p, int ms)
+{
+  if (!p || ms < 1)
+    return fail(OCEAN_ERR_INVALID, "ocean_peers_set_timeout: null peers or ms < 1");
+  p->timeout_ms = ms;
+  return peers_deadline(p);
+}
+
+int ocean_peers_set_put_cus(ocean_peers* p, int cus)
+{
+  if (!p || !p->g || cus < 0 || cus > p->g->fft->device_cus)
+    return fail(OCEAN_ERR_INVALID, "ocean_peers_set_put_cus: null peers or CUs outside [0, device CUs]");
+  p->put_cus = cus;
+  return OCEAN_OK;
+}
+
+int ocean_peers_set_put_stream(ocean_peers* p, void* hip_stream)
+{
+  if (!p || !p->g)
+    return fail(OCEAN_ERR_INVALID, "ocean_peers_set_put_stream: null or detached peers");
+  if (p->rows < p->frames)
+    return fail(OCEAN_ERR_INVALID, "ocean_peers_set_put_stream: a pipelined frame is in flight (flush first)");
+  hipStream_t next = hip_stream ? (hipStream_t)hip_stream : p->own_stream;
+  if (next != p->put_stream)
+    HIP_TRY(hipStreamSynchronize(p->put_stream), "ocean_peers_set_put_stream");
+  p->put_stream = next;
+  return OCEAN_OK;
+}
+
+int ocean_generator_slab_put_columns(ocean_generator* g, ocean_peers* p, float timestep, int update_spectrum)
+{
+  int rc = check_peers(g, p, "ocean_generator_slab_put_columns");
+  if (rc == OCEAN_OK && g->pending_slot >= 0)
+    rc = ocean_generator_slab_flush(g);  // an RCCL pipelined frame in flight lands first
+  return rc != OCEAN_OK ? rc : put_columns(g, p, timestep, update_spectrum, nullptr);
+}
+
+int ocean_generator_slab_put_rows(ocean_generator* g, ocean_peers* p)
+{
+  const int rc = check_peers(g, p, "ocean_generator_slab_put_rows");
+  return rc != OCEAN_OK ? rc : put_rows(g, p);
+}
+
+int ocean_generator_slab_frame_put(ocean_generator* g, ocean_peers* p, float timestep, int update_spectrum)
+{
+  int rc = check_peers(g, p, "ocean_generator_slab_frame_put");
+  if (rc == OCEAN_OK && g->pending_slot >= 0)
+    rc = ocean_generator_slab_flush(g);
+  while (rc == OCEAN_OK && p->rows < p->frames)  // a pipelined frame in flight lands first
+    rc = put_rows(g, p);
+  if (rc == OCEAN_OK)
+    rc = put_columns(g, p, timestep, update_spectrum, nullptr);
+  return rc != OCEAN_OK ? rc : put_rows(g, p);
+}
+
+int ocean_generator_slab_frame_put_pipelined(ocean_generator* g, ocean_peers* p, float timestep, int update_spectrum)
+{
+  int rc = check_peers(g, p, "ocean_generator_slab_frame_put_pipelined");
+  if (rc == OCEAN_OK && g->pending_slot >= 0)
+    rc = ocean_generator_slab_flush(g);
+  if (rc == OCEAN_OK)
+    rc = put_columns(g, p, timestep, update_spectrum, p->put_stream);
+  while (rc == OCEAN_OK && p->rows < p->frames - 1)  // frame f - 1's row pass beside frame f's columns
+    rc = put_rows(g, p);
+  return rc;
+}
+
+int ocean_peers_flush(ocean_peers* p)
+{
+  if (!p || !p->g)
+    return fail(OCEAN_ERR_INVALID, "ocean_peers_flush: null or detached peers");
+  int rc = OCEAN_OK;
+  while (rc == OCEAN_OK && p->rows < p->frames)
+    rc = put_rows(p->g, p);
+  return rc;
+}
+
+int ocean_peers_synchronize(ocean_peers* p)
+{
+  if (!p)
+    return fail(OCEAN_ERR_INVALID, "ocean_peers_synchronize: null peers");
+  HIP_TRY(hipStreamSynchronize(p->put_stream), "ocean_peers_synchronize: put stream");
+  if (p->g)
+    HIP_TRY(hipStreamSynchronize(p->g->fft->stream), "ocean_peers_synchronize: generator stream");
+  uint32_t err = 0;
+  HIP_TRY(hipMemcpy(&err, p->flags + kErrWord, sizeof(err), hipMemcpyDeviceToHost), "ocean_peers_synchronize: status");
+  if (err != 0)
+    return fail(OCEAN_ERR_TIMEOUT, std::string("one-sided exchange: a wait for the peers' ") +
+                                       (err - 1 == kReadyWord ? "blocks (ready)" : "slot release (freed)") +
+                                       " timed out after " + std::to_string(p->timeout_ms) +
+                                       " ms; the frames since then are invalid");
+  return OCEAN_OK;
+}
+
 int ocean_slab_layout(size_t texture_size, int rank, int ranks, int half, int64_t out[6])
 {
   int logn = 0;
@@ -1583,7 +2060,7 @@ int ocean_generator_set_profiling(ocean_generator* g, int enable)
   return OCEAN_OK;
 }
 
-int ocean_generator_kernel_times(ocean_generator* g, double ms_total[3], int64_t launches[3])
+int ocean_generator_kernel_times4(ocean_generator* g, double ms_total[4], int64_t launches[4])
 {
   if (!g)
     return fail(OCEAN_ERR_INVALID, "ocean_generator_kernel_times: null generator");
@@ -1591,6 +2068,7 @@ int ocean_generator_kernel_times(ocean_generator* g, double ms_total[3], int64_t
   for (auto& p : g->pending)
   {
     float ms = 0.0f;
+    HIP_TRY(hipEventSynchronize(p.b), "hipEventSynchronize");  // pairs on the put stream too
     HIP_TRY(hipEventElapsedTime(&ms, p.a, p.b), "hipEventElapsedTime");
     g->ms[p.kind] += ms;
     g->launches[p.kind] += 1;
@@ -1598,7 +2076,7 @@ int ocean_generator_kernel_times(ocean_generator* g, double ms_total[3], int64_t
     g->pool.push_back(p.b);
   }
   g->pending.clear();
-  for (int k = 0; k < 3; k++)
+  for (int k = 0; k < 4; k++)
   {
     if (ms_total)
       ms_total[k] = g->ms[k];
@@ -1608,6 +2086,21 @@ int ocean_generator_kernel_times(ocean_generator* g, double ms_total[3], int64_t
     g->launches[k] = 0;
   }
   return OCEAN_OK;
+}
+
+int ocean_generator_kernel_times(ocean_generator* g, double ms_total[3], int64_t launches[3])
+{
+  double m[4];
+  int64_t l[4];
+  const int rc = ocean_generator_kernel_times4(g, m, l);
+  for (int k = 0; rc == OCEAN_OK && k < 3; k++)
+  {
+    if (ms_total)
+      ms_total[k] = m[k];
+    if (launches)
+      launches[k] = l[k];
+  }
+  return rc;
 }
 
 int ocean_debug_copy(void* dst, const void* src, size_t bytes, int workgroups, void* hip_stream)

@@ -160,9 +160,26 @@ hipError_t launch_half_rows(int logn, const FrameParams& fp, const float4* gab, 
                             hipStream_t stream, int cus);
 // The Nyquist-row term of the half-spectrum paths (k_half_nyquist): spec[c][2][N] from row y = 0 of
 // h0 (h0row [c][N] when given, else the whole grid's h0 blocked blk columns wide; seed: evaluated in
-// place), written `copies` times copy_stride bytes apart (one copy per exchange block).
+// place), written `copies` times copy_stride bytes apart (one copy per exchange block), or with dst
+// (the one-sided exchange) copy k at dst[k] + dst_off.
 hipError_t launch_half_nyquist(const FrameParams& fp, int n, int blk, const float4* h0, float4* spec, const float4* h0row,
-                               int copies, size_t copy_stride, const void* seed, hipStream_t stream, int cus);
+                               int copies, size_t copy_stride, const void* seed, hipStream_t stream, int cus,
+                               const uint64_t* dst = nullptr, size_t dst_off = 0);
+// One-sided slab exchange (ocean_peers): the frame signals. A wait polls flags[word0 .. word0 + ranks)
+// of this rank until each reaches `target`, giving up after deadline_ticks of the device wall clock
+// (err[0] then records word0 + 1, and later waits return at once).
+struct PeerWait
+{
+  const uint32_t* flags;
+  int word0;
+  int ranks;
+  uint32_t target;
+  long long deadline_ticks;
+  uint32_t* err;
+};
+hipError_t launch_peer_wait(const PeerWait& w, hipStream_t stream);
+// Stores `value` into word `word` of every rank's flags (flags[q]: device array of ranks pointers).
+hipError_t launch_peer_signal(uint32_t* const* flags, int ranks, int word, uint32_t value, hipStream_t stream);
 // Strip-dealt half-spectrum path (HalfSlab): N = 1024 .. 16384. Columns: the Nyquist-row term (from
 // h0 when h0_full, i.e. the whole grid's blocked h0, else from h0row = row 0 of every column) into
 // every destination block of `send`, and pass 1 of the rank's strips into the blocks (ranks *
@@ -182,15 +199,26 @@ hipError_t launch_half_slab_rows(int logn, const FrameParams& fp, const HalfSlab
 hipError_t launch_rows_ifft_rows(int logn, int rows, float4* data, const float2* tw, hipStream_t stream, int cus);
 // The four-step column pass (Gen4Geom; N = 8192 / 16384, whole grids and slabs of P <= 16). h0: the
 // whole grid's image blocked gen4_h0_block() columns wide (whole_h0), or the rank's columns
-// (gen4_geom's h0_* offsets). Columns: the Nyquist-row term into every block of `send`, step 1 into
-// `parts` (gen4_parts_bytes), step 2 into the destination blocks of `send` (ranks * blk_bytes).
+// (gen4_geom's h0_* offsets). Columns: step 1 into `parts` (gen4_parts_bytes), then the Nyquist-row
+// term into every block of `send` and step 2 into the destination blocks of `send` (ranks *
+// blk_bytes). One-sided exchange (put != null): no send buffer; block q (term included) goes to
+// put->dst[q], a device table of ranks addresses (this rank's block in rank q's receive slot), after
+// put->wait (the peers have released the slots), on put->cus CUs (0: cus).
 // Rows: the row pass over the w rows of the received blocks. tw2: the N/16-point twiddle table.
 bool gen4_supported(int logn);
 int gen4_h0_block();
 Gen4Geom gen4_geom(int logn, int cascades, int rank, int ranks, bool whole_h0);
 size_t gen4_parts_bytes(int logn, int cascades, const Gen4Geom& g);
+struct Gen4Put
+{
+  const uint64_t* dst;
+  const PeerWait* wait;     // null: no wait
+  int cus;
+  hipEvent_t start = nullptr;  // profiling: recorded before the wait and the put kernels
+};
 hipError_t launch_gen4_columns(int logn, const FrameParams& fp, const Gen4Geom& g, const float4* h0, const float4* h0row,
-                               void* parts, void* send, const float2* tw, const float2* tw2, hipStream_t stream, int cus);
+                               void* parts, void* send, const float2* tw, const float2* tw2, hipStream_t stream, int cus,
+                               const Gen4Put* put = nullptr);
 hipError_t launch_gen4_rows(int logn, const FrameParams& fp, const Gen4Geom& g, const void* recv, float4* maps, float* jac,
                             const FoamParams& foam, const float2* tw, const float2* tw2, hipStream_t stream, int cus);
 // The N/16-point twiddle table that the four-step paths (gen4, the standalone EncodeIFFT at 8192 /

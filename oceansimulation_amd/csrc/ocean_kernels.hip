@@ -127,10 +127,13 @@ __global__ void k_hash(const uint32_t* __restrict__ xy, int count, uint32_t* __r
 // exchange buffer, so each frame's row pass reads the term of its own frame (the pipeline keeps two
 // frames in flight).
 // seed (the fused re-seed frame, h0 not materialised): the two row-0 texels are evaluated here.
+// dst (the one-sided exchange): copy k goes to dst[k] + dst_off, this rank's block in rank k's
+// receive slot, instead of spec + k * copy_stride.
 __global__ __launch_bounds__(256) void k_half_nyquist(FrameParams fp, int n, int blk, const float4* __restrict__ h0,
                                                       float4* __restrict__ spec, const float4* __restrict__ h0row,
                                                       int copies, size_t copy_stride,
-                                                      const SpectrumConsts* __restrict__ seed)
+                                                      const SpectrumConsts* __restrict__ seed,
+                                                      const uint64_t* __restrict__ dst, size_t dst_off)
 {
   const int total = fp.cascades * n;
   const float dim = (float)n;
@@ -170,11 +173,76 @@ __global__ __launch_bounds__(256) void k_half_nyquist(FrameParams fp, int n, int
     }
     for (int k = 0; k < copies; k++)
     {
-      float4* sp = reinterpret_cast<float4*>(reinterpret_cast<unsigned char*>(spec) + k * copy_stride);
+      float4* sp = reinterpret_cast<float4*>(dst ? reinterpret_cast<unsigned char*>(dst[k]) + dst_off
+                                                 : reinterpret_cast<unsigned char*>(spec) + k * copy_stride);
       sp[((size_t)c * 2 + 0) * n + x] = s01;
       sp[((size_t)c * 2 + 1) * n + x] = s23;
     }
   }
+  if (dst)  // the one-sided exchange: this workgroup's stores leave the L2 before completion is signalled
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+}
+
+// ------------------------------------------------------------------------------------------------
+// Frame signals of the one-sided slab exchange (ocean_peers, include/oceanfft.h). Every rank owns a
+// small array of 32-bit flag words in uncached device memory; word `ready + q` counts the frames
+// whose blocks rank q has stored into this rank's receive slots, word `freed + q` the frames whose
+// receive slot rank q's row pass has finished reading. Peers write them through their IPC mappings
+// (xGMI), this rank's own words locally. Values are frame numbers + 1, so they only grow.
+// ------------------------------------------------------------------------------------------------
+// k_peer_signal: one wave; lane q < ranks stores `value` into word `word` of rank q's flags, after a
+// system-scope release (the stores of the kernels before it in the stream are complete: the stream
+// orders them, and the put kernels end with their own system-scope release).
+__global__ __launch_bounds__(64) void k_peer_signal(uint32_t* const* __restrict__ flags, int ranks, int word,
+                                                    uint32_t value)
+{
+  const int q = threadIdx.x;
+  if (q < ranks)
+    __hip_atomic_store(flags[q] + word, value, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// k_peer_wait: one wave; lane q < ranks polls word `word0 + q` of this rank's flags until it reaches
+// `target` (as a wrapping difference). Every lane exits: on success, or when the wall clock passes
+// `deadline_ticks` after the start, in which case err[0] records the word range that timed out
+// (word0 + 1) and the frame goes on with whatever the slots hold; err is sticky, so the waits of
+// later frames return at once and the host reports the failure (ocean_peers_synchronize). A wait can
+// never hold the GPU past its deadline.
+__global__ __launch_bounds__(64) void k_peer_wait(const uint32_t* __restrict__ flags, int word0, int ranks,
+                                                  uint32_t target, long long deadline_ticks, uint32_t* __restrict__ err)
+{
+  const int q = threadIdx.x;
+  if (__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0)
+    return;
+  const long long t0 = wall_clock64();
+  bool ok = q >= ranks;
+  for (;;)
+  {
+    if (!ok)
+      ok = (int)(__hip_atomic_load(flags + word0 + q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) - target) >= 0;
+    if (__all(ok))
+      break;
+    if (wall_clock64() - t0 > deadline_ticks)
+    {
+      if (q == 0)
+        __hip_atomic_store(err, (uint32_t)(word0 + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      break;
+    }
+    __builtin_amdgcn_s_sleep(4);
+  }
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+}
+
+hipError_t launch_peer_signal(uint32_t* const* flags, int ranks, int word, uint32_t value, hipStream_t stream)
+{
+  hipLaunchKernelGGL(k_peer_signal, dim3(1), dim3(64), 0, stream, flags, ranks, word, value);
+  return hipGetLastError();
+}
+
+hipError_t launch_peer_wait(const PeerWait& w, hipStream_t stream)
+{
+  hipLaunchKernelGGL(k_peer_wait, dim3(1), dim3(64), 0, stream, w.flags, w.word0, w.ranks, w.target, w.deadline_ticks,
+                     w.err);
+  return hipGetLastError();
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -372,13 +440,14 @@ hipError_t launch_generate_spectrum_row(const OceanSettings& s, int n, float4* r
 
 
 hipError_t launch_half_nyquist(const FrameParams& fp, int n, int blk, const float4* h0, float4* spec, const float4* h0row,
-                               int copies, size_t copy_stride, const void* seed, hipStream_t stream, int cus)
+                               int copies, size_t copy_stride, const void* seed, hipStream_t stream, int cus,
+                               const uint64_t* dst, size_t dst_off)
 {
   long blocks = ((long)fp.cascades * n + 255) / 256;
   if (blocks > (long)cus * 4)
     blocks = (long)cus * 4;
   hipLaunchKernelGGL(k_half_nyquist, dim3((unsigned)blocks), dim3(256), 0, stream, fp, n, blk, h0, spec, h0row, copies,
-                     copy_stride, static_cast<const SpectrumConsts*>(seed));
+                     copy_stride, static_cast<const SpectrumConsts*>(seed), dst, dst_off);
   return hipGetLastError();
 }
 

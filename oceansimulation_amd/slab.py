@@ -10,7 +10,11 @@ Frames are independent until their exchange (the column pass depends only on h0 
 pass (two buffer slots, the exchange on its own stream); steady state is max(exchange, passes)
 instead of their sum. Maps then lag the last issued frame by one until `flush()`.
 
-Three exchanges are provided:
+Four exchanges are provided:
+  * `PeerExchange` + `SlabGenerator.frame_put` / `frame_put_pipelined`: the one-sided exchange of
+    the C ABI (ocean_peers, four-step slabs): the column pass stores each destination block straight
+    into the owning rank's receive slot through an IPC mapping of its memory, and one flag word per
+    rank and frame replaces the collective — no send buffer, no copy kernel;
   * `RcclComm` + `SlabGenerator.frame` / `frame_pipelined`: the library's own all-to-all, grouped
     ncclSend / ncclRecv over RCCL inside the C ABI (ocean_generator_slab_frame[_pipelined]), one
     process per GPU — used by bench.py;
@@ -97,6 +101,25 @@ class SlabGenerator:
     def flush(self) -> None:
         check(lib().ocean_generator_slab_flush(self._h), "ocean_generator_slab_flush")
 
+    def frame_put(self, peers: "PeerExchange", timestep: float, update_ocean: bool = False) -> None:
+        """One frame over the one-sided exchange (ocean_generator_slab_frame_put)."""
+        check(lib().ocean_generator_slab_frame_put(self._h, peers.handle, ctypes.c_float(timestep),
+                                                   1 if update_ocean else 0), "ocean_generator_slab_frame_put")
+
+    def frame_put_pipelined(self, peers: "PeerExchange", timestep: float, update_ocean: bool = False) -> None:
+        """Frame f's column pass and put on the peers' stream beside frame f - 1's row pass; the maps lag
+        by one frame until peers.flush()."""
+        check(lib().ocean_generator_slab_frame_put_pipelined(self._h, peers.handle, ctypes.c_float(timestep),
+                                                             1 if update_ocean else 0),
+              "ocean_generator_slab_frame_put_pipelined")
+
+    def put_columns(self, peers: "PeerExchange", timestep: float, update_ocean: bool = False) -> None:
+        check(lib().ocean_generator_slab_put_columns(self._h, peers.handle, ctypes.c_float(timestep),
+                                                     1 if update_ocean else 0), "ocean_generator_slab_put_columns")
+
+    def put_rows(self, peers: "PeerExchange") -> None:
+        check(lib().ocean_generator_slab_put_rows(self._h, peers.handle), "ocean_generator_slab_put_rows")
+
     def height_map_host(self) -> np.ndarray:
         self.fft.synchronize()
         return hip.to_host(int(lib().ocean_generator_height_map(self._h, 0)), (self.rows, self.n, 4))
@@ -116,6 +139,13 @@ class SlabGenerator:
         ms = (ctypes.c_double * 3)()
         cnt = (ctypes.c_int64 * 3)()
         check(lib().ocean_generator_kernel_times(self._h, ms, cnt), "ocean_generator_kernel_times")
+        return list(ms), list(cnt)
+
+    def kernel_times4(self):
+        """kernel_times with index 3 = the put of one-sided frames (inside index 1)."""
+        ms = (ctypes.c_double * 4)()
+        cnt = (ctypes.c_int64 * 4)()
+        check(lib().ocean_generator_kernel_times4(self._h, ms, cnt), "ocean_generator_kernel_times4")
         return list(ms), list(cnt)
 
     def close(self) -> None:
@@ -165,6 +195,89 @@ class RcclComm:
             self.close()
         except Exception:
             pass
+
+
+class PeerExchange:
+    """The one-sided slab exchange of one rank (ocean_peers): two receive slots and the flag words in
+    this process's device memory. connect(gather) hands this rank's handle to `gather(bytes) -> list of
+    bytes in rank order` (e.g. a torch.distributed all_gather_object) and maps the others'; or
+    connect_local(...) for P ranks of one process (the one-GPU emulation). Before close(), every rank
+    must have synchronized and passed a host barrier: a peer may still signal into this rank's flags."""
+
+    def __init__(self, gen: SlabGenerator):
+        h = ctypes.c_void_p()
+        check(lib().ocean_peers_create(ctypes.byref(h), gen.handle), "ocean_peers_create")
+        self._h = h
+        self.gen = gen
+
+    @property
+    def handle(self):
+        return self._h
+
+    def exported(self) -> bytes:
+        from .capi import OCEAN_PEER_HANDLE_BYTES
+
+        buf = (ctypes.c_ubyte * OCEAN_PEER_HANDLE_BYTES)()
+        check(lib().ocean_peers_handle(self._h, buf), "ocean_peers_handle")
+        return bytes(buf)
+
+    def connect(self, gather) -> None:
+        handles = b"".join(gather(self.exported()))
+        buf = (ctypes.c_ubyte * len(handles)).from_buffer_copy(handles)
+        check(lib().ocean_peers_connect(self._h, buf), "ocean_peers_connect")
+
+    @staticmethod
+    def connect_local(peers) -> None:
+        arr = (ctypes.c_void_p * len(peers))(*[p.handle.value for p in peers])
+        check(lib().ocean_peers_connect_local(arr, len(peers)), "ocean_peers_connect_local")
+
+    def set_timeout(self, ms: int) -> None:
+        check(lib().ocean_peers_set_timeout(self._h, int(ms)), "ocean_peers_set_timeout")
+
+    def set_put_cus(self, cus: int) -> None:
+        check(lib().ocean_peers_set_put_cus(self._h, int(cus)), "ocean_peers_set_put_cus")
+
+    def set_put_stream(self, stream: int | None) -> None:
+        check(lib().ocean_peers_set_put_stream(self._h, ctypes.c_void_p(stream or 0)), "ocean_peers_set_put_stream")
+
+    def flush(self) -> None:
+        check(lib().ocean_peers_flush(self._h), "ocean_peers_flush")
+
+    def synchronize(self) -> None:
+        """Wait for this rank's streams; raises OceanError (OCEAN_ERR_TIMEOUT) when a wait gave up."""
+        check(lib().ocean_peers_synchronize(self._h), "ocean_peers_synchronize")
+
+    def close(self) -> None:
+        if self._h:
+            lib().ocean_peers_destroy(self._h)
+            self._h = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def torch_gather_bytes(blob: bytes):
+    """All-gather one bytes object per rank over the default torch.distributed group (rank order)."""
+    import torch.distributed as dist
+
+    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+        return [blob]
+    out = [None] * dist.get_world_size()
+    dist.all_gather_object(out, blob)
+    return out
+
+
+def emulate_put_frame(slabs, peers, timestep: float, update_ocean: bool = False) -> None:
+    """One frame of a P-rank slab grid inside one process over the one-sided exchange (peers joined
+    by PeerExchange.connect_local): every rank's column pass stores into the others' slots, then every
+    rank's row pass reads its own."""
+    for g, p in zip(slabs, peers):
+        g.put_columns(p, timestep, update_ocean)
+    for g, p in zip(slabs, peers):
+        g.put_rows(p)
 
 
 def torch_share_id(uid: bytes) -> bytes:

@@ -1,0 +1,162 @@
+"""The one-sided slab exchange (ocean_peers, include/oceanfft.h): the four-step column pass stores each
+destination block straight into the owning rank's receive slot, and per-frame flag words replace the
+all-to-all (the reference's CalculateOcean, src/Generator.cpp:45-83, split over ranks).
+
+- P ranks in one process (ocean_peers_connect_local: the peers are the other ranks' buffers): serial
+  frames, frames issued column-passes-first, and pipelined frames against the whole-grid generator,
+  bit for bit on the device.
+- Two ranks as two processes on GPU 0 (IPC handles over gloo, tests/peer_rank.py): the
+  cross-process path itself, each rank checking its row slab against a whole grid.
+- A rank whose peer never signals: the bounded wait gives up, and ocean_peers_synchronize reports
+  OCEAN_ERR_TIMEOUT instead of hanging.
+"""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.fixture(scope="module")
+def ocean():
+    import oceansimulation_amd as o
+    from oceansimulation_amd import capi
+
+    assert capi.lib().ocean_device_count() > 0, "no GPU visible to liboceanfft.so"
+    return o
+
+
+def _dev_equal(ptr_a: int, ptr_b: int, nbytes: int) -> bool:
+    import torch
+
+    from oceansimulation_amd import hip
+
+    a = torch.empty(nbytes, dtype=torch.uint8, device="cuda")
+    b = torch.empty_like(a)
+    hip.copy_d2d(a.data_ptr(), ptr_a, nbytes)
+    hip.copy_d2d(b.data_ptr(), ptr_b, nbytes)
+    return bool(torch.equal(a, b))
+
+
+def _same(L, slabs, whole, n):
+    from oceansimulation_amd import hip
+
+    hip.synchronize()
+    P = len(slabs)
+    w = n // P
+    for r, g in enumerate(slabs):
+        for get, tex in ((L.ocean_generator_height_map, 16), (L.ocean_generator_displacement_map, 16),
+                         (L.ocean_generator_jacobian_map, 4)):
+            if not _dev_equal(int(get(g.handle, 0)), int(get(whole.handle, 0)) + r * w * n * tex, w * n * tex):
+                return f"rank {r} {get.__name__}"
+    return None
+
+
+@pytest.mark.parametrize("n,P", [(8192, 1), (8192, 2), (8192, 8), (16384, 8)])
+def test_put_exchange_in_one_process_bit_exact(ocean, n, P):
+    """P slab ranks over one grid, joined locally: frames issued as every rank's column pass + put
+    then every rank's row pass, then pipelined frames (rank r's frame f column pass on its put stream
+    beside its frame f - 1 row pass), equal the whole grid bit for bit after every check."""
+    from oceansimulation_amd import capi
+    from oceansimulation_amd.slab import PeerExchange, SlabGenerator, emulate_put_frame
+
+    L = capi.lib()
+    fft = ocean.FFTCalculator(n)
+    whole = ocean.Generator(fft, 1)
+    ocean.apply_settings(whole.GetOceanSettings(0), planeSize=777.0)
+    slabs = [SlabGenerator(fft, r, P) for r in range(P)]
+    for g in slabs:
+        ocean.apply_settings(g.GetOceanSettings(), planeSize=777.0)
+    peers = [PeerExchange(g) for g in slabs]
+    for p in peers:
+        p.set_timeout(10000)
+    PeerExchange.connect_local(peers)
+    for k, dt in enumerate((0.5, 1.0 / 60.0, 2.0)):
+        emulate_put_frame(slabs, peers, dt, update_ocean=(k == 0))
+        whole.CalculateOcean(dt)
+        assert _same(L, slabs, whole, n) is None, (n, P, "serial", k, _same(L, slabs, whole, n))
+    steps = [0.25, 1.0 / 30.0, 0.125]
+    for dt in steps:
+        for g, p in zip(slabs, peers):
+            g.frame_put_pipelined(p, dt)
+    for p in peers:
+        p.flush()
+    for dt in steps:
+        whole.CalculateOcean(dt)
+    assert _same(L, slabs, whole, n) is None, (n, P, "pipelined")
+    for p in peers:
+        p.synchronize()
+        p.close()
+    for g in slabs:
+        g.close()
+    whole.close()
+    fft.close()
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+@pytest.mark.timeout(300)
+def test_put_exchange_two_processes_bit_exact(ocean):
+    """Two slab ranks of one 8192^2 grid as two processes on GPU 0: the receive slots and flag words
+    are mapped across the processes with hipIpcOpenMemHandle (the mapping the 8-GPU node uses over
+    xGMI), serial and pipelined frames, each rank's row slab bit-exact against a whole grid."""
+    port = _free_port()
+    env = dict(os.environ, PYTHONUNBUFFERED="1")
+    procs = [subprocess.Popen([sys.executable, os.path.join(ROOT, "tests", "peer_rank.py"), str(r), "2", str(port),
+                               "8192"], stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, env=env)
+             for r in range(2)]
+    results = []
+    for p in procs:
+        try:
+            out, err = p.communicate(timeout=240)
+        except subprocess.TimeoutExpired:
+            for q in procs:
+                q.kill()
+            raise
+        lines = [ln for ln in out.splitlines() if ln.startswith("{")]
+        assert p.returncode == 0 and lines, (p.returncode, out[-2000:], err[-4000:])
+        results.append(json.loads(lines[-1]))
+    assert all(r["ok"] for r in results), results
+
+
+def test_put_wait_times_out_without_peer(ocean):
+    """Rank 0 of two issues its frame alone: its row pass waits for rank 1's blocks, which never come.
+    The wait gives up after the timeout (every wave exits), the stream drains, and
+    ocean_peers_synchronize reports OCEAN_ERR_TIMEOUT."""
+    import time
+
+    from oceansimulation_amd import capi
+    from oceansimulation_amd.capi import OceanError
+    from oceansimulation_amd.slab import PeerExchange, SlabGenerator
+
+    n = 8192
+    fft = ocean.FFTCalculator(n)
+    slabs = [SlabGenerator(fft, r, 2) for r in range(2)]
+    peers = [PeerExchange(g) for g in slabs]
+    PeerExchange.connect_local(peers)
+    peers[0].set_timeout(300)
+    t0 = time.perf_counter()
+    slabs[0].put_columns(peers[0], 0.5, True)
+    slabs[0].put_rows(peers[0])
+    with pytest.raises(OceanError) as exc:
+        peers[0].synchronize()
+    assert exc.value.code == capi.OCEAN_ERR_TIMEOUT
+    assert "ready" in str(exc.value)
+    assert time.perf_counter() - t0 < 30.0
+    for p in peers:
+        p.close()
+    for g in slabs:
+        g.close()
+    fft.close()

@@ -107,9 +107,9 @@ int main()
     const int gpn = C * 16 * ((KP + ci - 1) / ci), gcn = C * 16 * (((KP + 1) / 2 + ci - 1) / ci);
     const int wg = FftShape<LOGN2>::T * ci;
     return [=] {
-      hipLaunchKernelGGL(kp, dim3(gpn), dim3(wg), lds, 0, C, KP, PITCH, wab, blk, (size_t)0, g, tw2);
-      hipLaunchKernelGGL(kp, dim3(gpn), dim3(wg), lds, 0, C, KP, PITCH, wab + part, blk, 16 * rt, g, tw2);
-      hipLaunchKernelGGL(kc, dim3(gcn), dim3(wg), lds, 0, C, (KP + 1) / 2, PITCH / 2, wab + 2 * part, blk, 32 * rt, g, tw2);
+      hipLaunchKernelGGL(kp, dim3(gpn), dim3(wg), lds, 0, C, KP, PITCH, wab, blk, (size_t)0, g, tw2, (const uint64_t*)nullptr);
+      hipLaunchKernelGGL(kp, dim3(gpn), dim3(wg), lds, 0, C, KP, PITCH, wab + part, blk, 16 * rt, g, tw2, (const uint64_t*)nullptr);
+      hipLaunchKernelGGL(kc, dim3(gcn), dim3(wg), lds, 0, C, (KP + 1) / 2, PITCH / 2, wab + 2 * part, blk, 32 * rt, g, tw2, (const uint64_t*)nullptr);
     };
   };
   float4* rab = reinterpret_cast<float4*>(blk);

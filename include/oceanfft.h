@@ -265,14 +265,15 @@ int ocean_peers_set_timeout(ocean_peers* peers, int ms);
  * the stores bound by xGMI, fewer workgroups leave the other CUs to the row pass of the previous
  * frame in the pipelined frame. */
 int ocean_peers_set_put_cus(ocean_peers* peers, int cus);
-/* The stream pipelined frames run their column pass and put on (null: the peers' own). The one-GPU
- * emulation gives all P ranks one such stream, as one GPU has one path out over xGMI. */
-int ocean_peers_set_put_stream(ocean_peers* peers, void* hip_stream);
+/* The streams pipelined frames run step 1 of the column pass and the put on (null: the peers' own).
+ * The one-GPU emulation gives all P ranks one pair, as one GPU has one path out over xGMI. */
+int ocean_peers_set_streams(ocean_peers* peers, void* column_stream, void* put_stream);
 /* Serial frame on the generator's stream: time += dt, h0 if needed, step 1, wait for the slot, put,
  * signal; wait for every rank's blocks, row pass, signal. */
 int ocean_generator_slab_frame_put(ocean_generator* gen, ocean_peers* peers, float timestep, int update_spectrum);
-/* Pipelined: frame f's column pass and put on the peers' own stream, beside frame f - 1's row pass on
- * the generator's stream (two slots); the maps lag by one frame until ocean_peers_flush. */
+/* Pipelined: frame f's step 1 on the peers' column stream (into one of two parts slots), its put on
+ * their put stream, beside frame f + 1's step 1 and frame f - 1's row pass on the generator's stream
+ * (two receive slots); the maps lag by one frame until ocean_peers_flush. */
 int ocean_generator_slab_frame_put_pipelined(ocean_generator* gen, ocean_peers* peers, float timestep,
                                              int update_spectrum);
 int ocean_peers_flush(ocean_peers* peers);
@@ -290,8 +291,8 @@ int ocean_generator_set_profiling(ocean_generator* gen, int enable);
 /* Synchronises, then returns per-kernel totals since the last call and resets them.
  * Index 0 = spectrum (h0), 1 = column pass (evolve + y iFFT), 2 = row pass (x iFFT + foam). */
 int ocean_generator_kernel_times(ocean_generator* gen, double ms_total[3], int64_t launches[3]);
-/* The same with index 3 = the put of one-sided frames (the slot wait + the Nyquist-row term + step 2,
- * which index 1 includes). */
+/* The same with index 3 = the put of one-sided frames (the slot wait + the Nyquist-row term + step 2).
+ * Index 1 includes it in serial frames; in pipelined ones index 1 is step 1 alone (its own stream). */
 int ocean_generator_kernel_times4(ocean_generator* gen, double ms_total[4], int64_t launches[4]);
 
 /* ---- debug -------------------------------------------------------------------------------- */

@@ -141,8 +141,8 @@ __global__ __launch_bounds__(256, MINW) void k_gen4_step1(FrameParams fp, Gen4Ge
 // CI: columns per workgroup (8: 128-B pieces, 512-thread workgroups, two per CU at N2 = 1024).
 // PUT (the one-sided exchange, ocean_peers): block q goes straight to dst[q], the address of this
 // rank's block in rank q's receive slot (a peer mapping over xGMI, or local memory for q == rank),
-// instead of send + q * blk_bytes; no send buffer exists. Each workgroup ends with a system-scope
-// release, so its stores have left this XCD's L2 before the kernel's completion is signalled.
+// instead of send + q * blk_bytes; no send buffer exists. (The ready signal after the kernel writes
+// back every XCD's L2 before it raises the peers' flags: k_peer_signal_release.)
 template <int LOGN2, bool PAIRS, int CI = ColCfg<LOGN2>::C, bool PUT = false>
 __global__ __launch_bounds__(FftShape<LOGN2>::T * CI, CI < ColCfg<LOGN2>::C ? 4 : 1) void k_gen4_step2(
     int cascades, int cols, int pitch, const float4* __restrict__ work, unsigned char* __restrict__ send,
@@ -187,8 +187,6 @@ __global__ __launch_bounds__(FftShape<LOGN2>::T * CI, CI < ColCfg<LOGN2>::C ? 4 
       st4<kStream>(d, soff, PAIRS ? pair_raw(v[m]) : from_pair(v[m]));
     }
   }
-  if constexpr (PUT)
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
 }
 
 // Strip-dealt half-spectrum fields -> row-major (HalfSlab blocks -> [c][yl][kp], kp = STRIPS * B):

@@ -250,6 +250,18 @@ hipError_t launch_gen4_columns(int logn, const FrameParams& fp, const Gen4Geom& 
       hipError_t e = hipGetLastError();
       if (e != hipSuccess)
         return e;
+      // the put on its own stream (pipelined one-sided frames): after step 1
+      if (put && put->stream && put->stream != stream)
+      {
+        if (!put->handoff)
+          return hipErrorInvalidValue;
+        e = hipEventRecord(put->handoff, stream);
+        if (e == hipSuccess)
+          e = hipStreamWaitEvent(put->stream, put->handoff, 0);
+        if (e != hipSuccess)
+          return e;
+        stream = put->stream;
+      }
       // the one-sided exchange writes into the peers' receive slots: only once they are free
       if (put && put->start)
       {

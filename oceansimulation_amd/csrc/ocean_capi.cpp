@@ -902,14 +902,14 @@ static int generator_columns(ocean_generator* g, float timestep, int update_spec
       timed_put.start = pp.a;
     }
     HIP_TRY(timed(g, 1, [&] {
-              return launch_gen4_columns(f->logn, fp, g->g4, g->h0, g->ranks > 1 ? g->h0row : nullptr, g->parts,
-                                         out ? (void*)out : (void*)g->xbuf, f->twiddles, f->tw2, cs, f->cus,
-                                         put ? &timed_put : nullptr);
+              return launch_gen4_columns(f->logn, fp, g->g4, g->h0, g->ranks > 1 ? g->h0row : nullptr,
+                                         put && put->parts ? put->parts : g->parts, out ? (void*)out : (void*)g->xbuf,
+                                         f->twiddles, f->tw2, cs, f->cus, put ? &timed_put : nullptr);
             }, cs),
             "column pass (half spectrum, four-step)");
     if (pp.a)
     {
-      HIP_TRY(hipEventRecord(pp.b, cs), "column pass: put event");
+      HIP_TRY(hipEventRecord(pp.b, put && put->stream ? put->stream : cs), "column pass: put event");
       g->pending.push_back(pp);
     }
   }
@@ -1493,7 +1493,7 @@ int ocean_generator_slab_flush(ocean_generator* g)
 namespace
 {
 constexpr int kMaxRanks = 16;
-constexpr int kReadyWord = 0, kFreedWord = 16, kErrWord = 48, kFlagWords = 64;
+constexpr int kReadyWord = 0, kFreedWord = 16, kReleaseCounter = 40, kErrWord = 48, kFlagWords = 64;
 constexpr uint32_t kPeerMagic = 0x4f505231;  // "OPR1"
 
 struct PeerHandle
@@ -1513,15 +1513,20 @@ struct ocean_peers
   int rank = 0, ranks = 1;
   size_t blk = 0, slot = 0;        // block bytes, slot bytes (ranks * blk = the exchange bytes)
   unsigned char* data = nullptr;   // this rank's two receive slots
-  uint32_t* flags = nullptr;       // this rank's flag words: ready[16] | freed[16] | .. | err @ 48
+  uint32_t* flags = nullptr;       // this rank's flag words: ready[16] | freed[16] | .. | release counter @ 40 | err @ 48
   bool flags_uncached = false;
   unsigned char* peer_data[kMaxRanks] = {};
   uint32_t* peer_flags[kMaxRanks] = {};
   bool mapped[2 * kMaxRanks] = {};  // data / flags opened with hipIpcOpenMemHandle (closed on destroy)
   bool connected = false;
   uint64_t* table = nullptr;       // device: put destinations [2 slots][16], then the flag arrays [16]
-  hipStream_t put_stream = nullptr;  // the stream pipelined column passes + puts run on
-  hipStream_t own_stream = nullptr;  // the one ocean_peers_create made (put_stream unless replaced)
+  // pipelined frames: step 1 on s1_stream into parts slot f % 2, the put on put_stream, the row pass
+  // on the generator's stream (ocean_peers_set_streams can replace the first two)
+  hipStream_t s1_stream = nullptr, put_stream = nullptr;
+  hipStream_t own_s1 = nullptr, own_put = nullptr;
+  unsigned char* parts2 = nullptr;   // step 1's second parts slot
+  hipEvent_t s1_done[2] = {nullptr, nullptr}, put_done[2] = {nullptr, nullptr};
+  bool put_done_valid[2] = {false, false};
   long long deadline = 0;          // wall-clock ticks
   int timeout_ms = 20000;
   int put_cus = 0;
@@ -1578,21 +1583,49 @@ uint32_t* const* flag_table(const ocean_peers* p)
   return reinterpret_cast<uint32_t* const*>(p->table + 2 * kMaxRanks);
 }
 
-// Column pass of frame f = p->frames into every rank's slot f % 2, on `stream` (the generator's or the
-// put stream): step 1, wait until every rank has finished reading that slot (frame f - 2's row pass),
-// the put, then this rank's "ready" word (f + 1) in every rank's flags.
-int put_columns(ocean_generator* g, ocean_peers* p, float timestep, int update_spectrum, hipStream_t stream)
+// Column pass of frame f = p->frames into every rank's slot f % 2, then this rank's "ready" word (f + 1)
+// in every rank's flags. The put waits until every rank has finished reading that slot (frame f - 2's
+// row pass). Serial: all on the generator's stream. Pipelined: step 1 on s1_stream into parts slot f % 2
+// (after the put of frame f - 2 read that slot), the put on put_stream after step 1, so step 1 of frame
+// f + 1 and the row pass of frame f - 1 run beside the put of frame f.
+int put_columns(ocean_generator* g, ocean_peers* p, float timestep, int update_spectrum, bool pipelined)
 {
+  ocean_fft* fs = g->fft;
   const int64_t f = p->frames;
   const int s = (int)(f % 2);
   const PeerWait w = peer_wait(p, kFreedWord, f - 1);
-  const Gen4Put put{p->table + s * kMaxRanks, f >= 2 ? &w : nullptr, p->put_cus};
-  int rc = generator_columns(g, timestep, update_spectrum, nullptr, &put, stream);
+  Gen4Put put{p->table + s * kMaxRanks, f >= 2 ? &w : nullptr, p->put_cus};
+  hipStream_t cs = nullptr;
+  if (pipelined)
+  {
+    if (!p->parts2)
+      HIP_TRY(hipMalloc(&p->parts2, gen4_parts_bytes(fs->logn, g->cascades, g->g4)), "one-sided exchange: parts slot");
+    cs = p->s1_stream;
+    put.parts = s ? p->parts2 : g->parts;
+    put.stream = p->put_stream;
+    put.handoff = p->s1_done[s];
+    if (p->put_done_valid[s])
+      HIP_TRY(hipStreamWaitEvent(cs, p->put_done[s], 0), "one-sided exchange: parts slot reuse");
+  }
+  else
+    for (int k = 0; k < 2; k++)  // a serial frame after pipelined ones: its step 1 rewrites parts slot 0
+      if (p->put_done_valid[k])
+      {
+        HIP_TRY(hipStreamWaitEvent(fs->stream, p->put_done[k], 0), "one-sided exchange: stream order");
+        p->put_done_valid[k] = false;
+      }
+  int rc = generator_columns(g, timestep, update_spectrum, nullptr, &put, cs);
   if (rc != OCEAN_OK)
     return rc;
-  HIP_TRY(launch_peer_signal(flag_table(p), p->ranks, kReadyWord + p->rank, (uint32_t)(f + 1),
-                             stream ? stream : g->fft->stream),
+  hipStream_t ps = pipelined ? p->put_stream : fs->stream;
+  HIP_TRY(launch_peer_signal_release(flag_table(p), p->ranks, kReadyWord + p->rank, (uint32_t)(f + 1),
+                                     p->flags + kReleaseCounter, ps),
           "one-sided exchange: ready signal");
+  if (pipelined)
+  {
+    HIP_TRY(hipEventRecord(p->put_done[s], ps), "one-sided exchange: events");
+    p->put_done_valid[s] = true;
+  }
   p->slot_frame[s] = g->frame;
   p->slot_foam[s] = current_foam(g);
   p->frames = f + 1;
@@ -1623,8 +1656,9 @@ int put_rows(ocean_generator* g, ocean_peers* p)
 
 void peers_release(ocean_peers* p)
 {
-  if (p->put_stream)
-    (void)hipStreamSynchronize(p->put_stream);
+  for (hipStream_t st : {p->s1_stream, p->put_stream})
+    if (st)
+      (void)hipStreamSynchronize(st);
   if (p->g && p->g->fft)
     (void)hipStreamSynchronize(p->g->fft->stream);
   for (int q = 0; q < kMaxRanks; q++)
@@ -1646,8 +1680,9 @@ static void peers_detach(ocean_peers* p)
 {
   if (!p)
     return;
-  if (p->put_stream)
-    (void)hipStreamSynchronize(p->put_stream);
+  for (hipStream_t st : {p->s1_stream, p->put_stream})
+    if (st)
+      (void)hipStreamSynchronize(st);
   p->g = nullptr;
   p->connected = false;
 }
@@ -1689,8 +1724,17 @@ int ocean_peers_create(ocean_peers** out, ocean_generator* g)
   if (e == hipSuccess)
     e = hipMemset(p->flags, 0, kFlagWords * sizeof(uint32_t));
   if (e == hipSuccess)
-    e = hipStreamCreateWithFlags(&p->own_stream, hipStreamNonBlocking);
-  p->put_stream = p->own_stream;
+    e = hipStreamCreateWithFlags(&p->own_s1, hipStreamNonBlocking);
+  if (e == hipSuccess)
+    e = hipStreamCreateWithFlags(&p->own_put, hipStreamNonBlocking);
+  for (int k = 0; k < 2 && e == hipSuccess; k++)
+  {
+    e = hipEventCreateWithFlags(&p->s1_done[k], hipEventDisableTiming);
+    if (e == hipSuccess)
+      e = hipEventCreateWithFlags(&p->put_done[k], hipEventDisableTiming);
+  }
+  p->s1_stream = p->own_s1;
+  p->put_stream = p->own_put;
   if (e == hipSuccess)
     e = hipDeviceSynchronize();
   int rc = e == hipSuccess ? peers_deadline(p) : OCEAN_OK;
@@ -1715,9 +1759,14 @@ int ocean_peers_destroy(ocean_peers* p)
   peers_release(p);
   if (p->g)
     p->g->peers = nullptr;
-  if (p->own_stream)
-    (void)hipStreamDestroy(p->own_stream);
-  for (void* q : {(void*)p->data, (void*)p->flags, (void*)p->table})
+  for (hipStream_t st : {p->own_s1, p->own_put})
+    if (st)
+      (void)hipStreamDestroy(st);
+  for (int k = 0; k < 2; k++)
+    for (hipEvent_t ev : {p->s1_done[k], p->put_done[k]})
+      if (ev)
+        (void)hipEventDestroy(ev);
+  for (void* q : {(void*)p->data, (void*)p->flags, (void*)p->table, (void*)p->parts2})
     if (q)
       (void)hipFree(q);
   delete p;
@@ -1820,16 +1869,17 @@ int ocean_peers_set_put_cus(ocean_peers* p, int cus)
   return OCEAN_OK;
 }
 
-int ocean_peers_set_put_stream(ocean_peers* p, void* hip_stream)
+int ocean_peers_set_streams(ocean_peers* p, void* column_stream, void* put_stream)
 {
   if (!p || !p->g)
-    return fail(OCEAN_ERR_INVALID, "ocean_peers_set_put_stream: null or detached peers");
+    return fail(OCEAN_ERR_INVALID, "ocean_peers_set_streams: null or detached peers");
   if (p->rows < p->frames)
-    return fail(OCEAN_ERR_INVALID, "ocean_peers_set_put_stream: a pipelined frame is in flight (flush first)");
-  hipStream_t next = hip_stream ? (hipStream_t)hip_stream : p->own_stream;
-  if (next != p->put_stream)
-    HIP_TRY(hipStreamSynchronize(p->put_stream), "ocean_peers_set_put_stream");
-  p->put_stream = next;
+    return fail(OCEAN_ERR_INVALID, "ocean_peers_set_streams: a pipelined frame is in flight (flush first)");
+  for (hipStream_t st : {p->s1_stream, p->put_stream})
+    HIP_TRY(hipStreamSynchronize(st), "ocean_peers_set_streams");
+  p->s1_stream = column_stream ? (hipStream_t)column_stream : p->own_s1;
+  p->put_stream = put_stream ? (hipStream_t)put_stream : p->own_put;
+  p->put_done_valid[0] = p->put_done_valid[1] = false;  // both old streams are drained
   return OCEAN_OK;
 }
 
@@ -1838,7 +1888,7 @@ int ocean_generator_slab_put_columns(ocean_generator* g, ocean_peers* p, float t
   int rc = check_peers(g, p, "ocean_generator_slab_put_columns");
   if (rc == OCEAN_OK && g->pending_slot >= 0)
     rc = ocean_generator_slab_flush(g);  // an RCCL pipelined frame in flight lands first
-  return rc != OCEAN_OK ? rc : put_columns(g, p, timestep, update_spectrum, nullptr);
+  return rc != OCEAN_OK ? rc : put_columns(g, p, timestep, update_spectrum, false);
 }
 
 int ocean_generator_slab_put_rows(ocean_generator* g, ocean_peers* p)
@@ -1855,7 +1905,7 @@ int ocean_generator_slab_frame_put(ocean_generator* g, ocean_peers* p, float tim
   while (rc == OCEAN_OK && p->rows < p->frames)  // a pipelined frame in flight lands first
     rc = put_rows(g, p);
   if (rc == OCEAN_OK)
-    rc = put_columns(g, p, timestep, update_spectrum, nullptr);
+    rc = put_columns(g, p, timestep, update_spectrum, false);
   return rc != OCEAN_OK ? rc : put_rows(g, p);
 }
 
@@ -1865,7 +1915,7 @@ int ocean_generator_slab_frame_put_pipelined(ocean_generator* g, ocean_peers* p,
   if (rc == OCEAN_OK && g->pending_slot >= 0)
     rc = ocean_generator_slab_flush(g);
   if (rc == OCEAN_OK)
-    rc = put_columns(g, p, timestep, update_spectrum, p->put_stream);
+    rc = put_columns(g, p, timestep, update_spectrum, true);
   while (rc == OCEAN_OK && p->rows < p->frames - 1)  // frame f - 1's row pass beside frame f's columns
     rc = put_rows(g, p);
   return rc;
@@ -1885,6 +1935,7 @@ int ocean_peers_synchronize(ocean_peers* p)
 {
   if (!p)
     return fail(OCEAN_ERR_INVALID, "ocean_peers_synchronize: null peers");
+  HIP_TRY(hipStreamSynchronize(p->s1_stream), "ocean_peers_synchronize: column stream");
   HIP_TRY(hipStreamSynchronize(p->put_stream), "ocean_peers_synchronize: put stream");
   if (p->g)
     HIP_TRY(hipStreamSynchronize(p->g->fft->stream), "ocean_peers_synchronize: generator stream");

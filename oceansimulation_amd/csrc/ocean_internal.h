@@ -180,6 +180,9 @@ struct PeerWait
 hipError_t launch_peer_wait(const PeerWait& w, hipStream_t stream);
 // Stores `value` into word `word` of every rank's flags (flags[q]: device array of ranks pointers).
 hipError_t launch_peer_signal(uint32_t* const* flags, int ranks, int word, uint32_t value, hipStream_t stream);
+// The same after writing back every XCD's L2 (the puts' stores); counter: a word of this rank's flags.
+hipError_t launch_peer_signal_release(uint32_t* const* flags, int ranks, int word, uint32_t value, uint32_t* counter,
+                                      hipStream_t stream);
 // Strip-dealt half-spectrum path (HalfSlab): N = 1024 .. 16384. Columns: the Nyquist-row term (from
 // h0 when h0_full, i.e. the whole grid's blocked h0, else from h0row = row 0 of every column) into
 // every destination block of `send`, and pass 1 of the rank's strips into the blocks (ranks *
@@ -212,9 +215,12 @@ size_t gen4_parts_bytes(int logn, int cascades, const Gen4Geom& g);
 struct Gen4Put
 {
   const uint64_t* dst;
-  const PeerWait* wait;     // null: no wait
+  const PeerWait* wait;          // null: no wait
   int cus;
-  hipEvent_t start = nullptr;  // profiling: recorded before the wait and the put kernels
+  hipEvent_t start = nullptr;    // profiling: recorded before the wait and the put kernels
+  hipStream_t stream = nullptr;  // the put kernels' stream (null: step 1's), after `handoff`
+  hipEvent_t handoff = nullptr;  // recorded on step 1's stream after step 1 when `stream` is set
+  void* parts = nullptr;         // the caller's parts slot (null: the generator's)
 };
 hipError_t launch_gen4_columns(int logn, const FrameParams& fp, const Gen4Geom& g, const float4* h0, const float4* h0row,
                                void* parts, void* send, const float2* tw, const float2* tw2, hipStream_t stream, int cus,

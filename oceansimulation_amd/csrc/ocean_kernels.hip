@@ -179,8 +179,6 @@ __global__ __launch_bounds__(256) void k_half_nyquist(FrameParams fp, int n, int
       sp[((size_t)c * 2 + 1) * n + x] = s23;
     }
   }
-  if (dst)  // the one-sided exchange: this workgroup's stores leave the L2 before completion is signalled
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -190,14 +188,34 @@ __global__ __launch_bounds__(256) void k_half_nyquist(FrameParams fp, int n, int
 // receive slot rank q's row pass has finished reading. Peers write them through their IPC mappings
 // (xGMI), this rank's own words locally. Values are frame numbers + 1, so they only grow.
 // ------------------------------------------------------------------------------------------------
-// k_peer_signal: one wave; lane q < ranks stores `value` into word `word` of rank q's flags, after a
-// system-scope release (the stores of the kernels before it in the stream are complete: the stream
-// orders them, and the put kernels end with their own system-scope release).
+// k_peer_signal: one wave; lane q < ranks stores `value` into word `word` of rank q's flags with a
+// system-scope release (the "freed" signal: the row pass before it in the stream only read).
 __global__ __launch_bounds__(64) void k_peer_signal(uint32_t* const* __restrict__ flags, int ranks, int word,
                                                     uint32_t value)
 {
   const int q = threadIdx.x;
   if (q < ranks)
+    __hip_atomic_store(flags[q] + word, value, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// k_peer_signal_release: the "ready" signal after the puts. The put kernels' stores to the peers may
+// still sit in the XCD L2s (each XCD has its own); kPeerReleaseBlocks workgroups, dealt over all 8
+// XCDs, each write back their XCD's L2 (a system-scope release fence), then count themselves in on
+// `counter` (this rank's flag memory); the last one in raises the flags, as k_peer_signal does.
+// The counter only grows: the last workgroup of a launch is the one that sees a multiple of the
+// block count minus one, so no reset is needed between frames.
+constexpr int kPeerReleaseBlocks = 64;
+
+__global__ __launch_bounds__(64) void k_peer_signal_release(uint32_t* const* __restrict__ flags, int ranks, int word,
+                                                            uint32_t value, uint32_t* __restrict__ counter)
+{
+  if (threadIdx.x != 0)
+    return;
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+  const uint32_t n = __hip_atomic_fetch_add(counter, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_SYSTEM);
+  if ((n + 1) % kPeerReleaseBlocks != 0)
+    return;
+  for (int q = 0; q < ranks; q++)
     __hip_atomic_store(flags[q] + word, value, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
@@ -235,6 +253,14 @@ __global__ __launch_bounds__(64) void k_peer_wait(const uint32_t* __restrict__ f
 hipError_t launch_peer_signal(uint32_t* const* flags, int ranks, int word, uint32_t value, hipStream_t stream)
 {
   hipLaunchKernelGGL(k_peer_signal, dim3(1), dim3(64), 0, stream, flags, ranks, word, value);
+  return hipGetLastError();
+}
+
+hipError_t launch_peer_signal_release(uint32_t* const* flags, int ranks, int word, uint32_t value, uint32_t* counter,
+                                      hipStream_t stream)
+{
+  hipLaunchKernelGGL(k_peer_signal_release, dim3(kPeerReleaseBlocks), dim3(64), 0, stream, flags, ranks, word, value,
+                     counter);
   return hipGetLastError();
 }
 

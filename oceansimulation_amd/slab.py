@@ -237,8 +237,10 @@ class PeerExchange:
     def set_put_cus(self, cus: int) -> None:
         check(lib().ocean_peers_set_put_cus(self._h, int(cus)), "ocean_peers_set_put_cus")
 
-    def set_put_stream(self, stream: int | None) -> None:
-        check(lib().ocean_peers_set_put_stream(self._h, ctypes.c_void_p(stream or 0)), "ocean_peers_set_put_stream")
+    def set_streams(self, column_stream: int | None, put_stream: int | None) -> None:
+        """Streams of pipelined frames' step 1 and put (None: the peers' own)."""
+        check(lib().ocean_peers_set_streams(self._h, ctypes.c_void_p(column_stream or 0), ctypes.c_void_p(put_stream or 0)),
+              "ocean_peers_set_streams")
 
     def flush(self) -> None:
         check(lib().ocean_peers_flush(self._h), "ocean_peers_flush")

@@ -101,12 +101,12 @@ def parse(argv=None):
                          "(28: a P = 8 rank's 2048 rows of 16384 run in 9 rounds of one-row workgroups on 228 CUs, "
                          "10 on 224)")
     ap.add_argument("--no-put", action="store_true", help="skip the one-sided (ocean_peers) slab exchange legs")
-    ap.add_argument("--slab-put-cus", type=int, default=64,
-                    help="CUs the put kernels of the second pipelined one-sided variant are sized for")
+    ap.add_argument("--slab-put-cus-per-xcd", type=int, default=8,
+                    help="CUs of every XCD the put stream of the masked pipelined one-sided variant runs on")
     ap.add_argument("--put-timeout-ms", type=int, default=10000,
                     help="one-sided exchange: how long a frame signal wait may take before the frame is given up")
     ap.add_argument("--slab-mask-layouts", default="",
-                    help="comma-separated reserved-CU layouts (top, xcd, stride) for extra CU-masked 8-rank projections")
+                    help="reserved-CU layouts (per_xcd) for extra CU-masked 8-rank RCCL projections")
     ap.add_argument("--shared-gpu", action="store_true",
                     help="rehearsal: every rank on GPU 0 with gloo collectives and host-staged exchanges "
                          "(exercises the N > 1 paths on a one-GPU machine; not a measurement)")
@@ -125,6 +125,7 @@ def parse(argv=None):
 ARGV_ENV = "OCEAN_BENCH_ARGV"  # launch_ranks -> its ranks: the original argument list (JSON)
 LEGS_TIMEOUT_RC = 3  # exit status when the optional legs overran their deadline (headline still printed)
 VERIFY_FAILED_RC = 4  # exit status when a leg's maps did not match its bit-exact check (line still printed)
+EXCHANGE_ABORT_RC = 5  # exit status when the RCCL slab exchange failed on a rank (line still printed)
 
 
 def _free_port() -> int:
@@ -468,7 +469,10 @@ def one_cascade_leg(ocean, fft, args, dt: float) -> dict:
             runs[mode].append(timed_frames(gen, steps, dt, 1))
     gen.set_frame_overlap(False)
     el_serial = sorted(runs[False])[1]
-    el = sorted(runs[True])[1] if overlap else el_serial
+    el_overlap = sorted(runs[True])[1] if overlap else None
+    # the share's figure is the faster mode (at 4096 with <= 2 cascades the half-strip column pass is
+    # faster serial, so a forced --frame-overlap on must not report the slower number)
+    el = min(el_serial, el_overlap) if overlap else el_serial
     gen.set_profiling(True)
     gen.kernel_times()
     for _ in range(steps):
@@ -479,8 +483,9 @@ def one_cascade_leg(ocean, fft, args, dt: float) -> dict:
     frame_ms = 1000.0 * el / steps
     passes_ms = ms[1] / max(cnt[1], 1) + ms[2] / max(cnt[2], 1)
     return {"what": f"1 cascade of {n}^2 per frame (the per-GPU share at 8 GPUs)",
-            "one_cascade_ms": frame_ms, "frame_overlap": overlap,
+            "one_cascade_ms": frame_ms, "frame_overlap": overlap and el_overlap <= el_serial,
             "one_cascade_serial_ms": 1000.0 * el_serial / steps, "one_cascade_passes_ms": passes_ms,
+            **({"one_cascade_overlapped_ms": 1000.0 * el_overlap / steps} if overlap else {}),
             "points_per_s": float(n) * n / (frame_ms * 1e-3),
             "frac_hbm_peak": b * n * n / (frame_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
             "frame_hbm_bytes_per_point": b}
@@ -759,10 +764,11 @@ def slab_grid(args, rank: int, world: int, local: int) -> dict:
     if comm is not None and not all_ranks_ok(first_error is None):
         # The library's exchange failed on some rank. The frame is enqueued asynchronously, so a rank
         # whose own call succeeded may hold sends its failed peer never matches: no rank falls back to
-        # torch alone (the all-reduce above makes every rank take the same branch), and the leg ends
-        # here with the error rather than waiting in RCCL.
-        raise RuntimeError("slab leg: the library's RCCL exchange failed on a rank: " +
-                           (first_error or "(on another rank)"))
+        # torch alone (the all-reduce above makes every rank take the same branch), and the rank ends
+        # without touching the generator or the communicator again (their destructors would wait in
+        # RCCL): main prints the line and leaves with os._exit.
+        raise ExchangeAbort("slab leg: the library's RCCL exchange failed on a rank: " +
+                            (first_error or "(on another rank)"))
     frame(1.0 / 60.0)
     g.set_profiling(True)
     g.kernel_times()
@@ -867,7 +873,7 @@ def slab_grid(args, rank: int, world: int, local: int) -> dict:
         out["put"] = put_leg(args, ocean, fft, g, whole, rank, world, all_ranks_ok)
         verified["put"] = out["put"].get("verified", False)
         if verified["put"]:
-            for k in ("serial_ms_per_frame", "pipelined_ms_per_frame", "pipelined_put64_ms_per_frame"):
+            for k in ("serial_ms_per_frame", "pipelined_ms_per_frame", "pipelined_masked_ms_per_frame"):
                 if k in out["put"]:
                     legs["put_" + k.replace("_ms_per_frame", "")] = out["put"][k]
     whole.close()
@@ -883,6 +889,10 @@ def slab_grid(args, rank: int, world: int, local: int) -> dict:
         comm.close()
     fft.close()
     return out
+
+
+class ExchangeAbort(RuntimeError):
+    """The RCCL slab exchange failed: RCCL work may be pending, so the rank must not run destructors."""
 
 
 def guarded_timed(run_steps, world: int):
@@ -906,8 +916,8 @@ def put_leg(args, ocean, fft, g, whole, rank: int, world: int, all_ranks_ok) -> 
     """The slab frame over the one-sided exchange (ocean_peers): the column pass stores each destination
     block into the owning rank's receive slot through an IPC mapping of its memory (over xGMI between
     GPUs; on the --shared-gpu rehearsal between processes on one GPU), one flag word per rank and frame.
-    Serial frames, pipelined frames (put on all CUs, and on --slab-put-cus CUs), then this rank's rows
-    against the whole grid. Every rank takes the same branch at every collective."""
+    Serial frames, pipelined frames (unmasked streams, and the put on --slab-put-cus-per-xcd CUs of
+    every XCD: ocean_peers_set_put_cu_mask), then this rank's rows against the whole grid. Every rank takes the same branch at every collective."""
     from oceansimulation_amd.slab import PeerExchange, torch_gather_bytes
 
     dt, per = 1.0 / 60.0, args.slab_steps
@@ -944,9 +954,10 @@ def put_leg(args, ocean, fft, g, whole, rank: int, world: int, all_ranks_ok) -> 
     el, e = guarded_timed(lambda: [g.frame_put(peers, dt) for _ in range(per)], world)
     errors += [e] if e else []
     res["serial_ms_per_frame"] = 1000.0 * el / per
-    for label, cus in (("", 0), ("_put64", args.slab_put_cus)):
+    for label, per_xcd in (("", 0), ("_masked", args.slab_put_cus_per_xcd)):
         try:
-            peers.set_put_cus(cus)
+            peers.set_put_cu_mask(per_xcd)
+            peers.set_put_cus(8 * per_xcd)
         except Exception as e:
             errors.append(f"{type(e).__name__}: {e}")
 
@@ -957,7 +968,7 @@ def put_leg(args, ocean, fft, g, whole, rank: int, world: int, all_ranks_ok) -> 
         el, e = guarded_timed(steps, world)
         errors += [e] if e else []
         res[f"pipelined{label}_ms_per_frame"] = 1000.0 * el / per
-    res["put_cus_variant"] = args.slab_put_cus
+    res["put_cus_per_xcd_variant"] = args.slab_put_cus_per_xcd
     try:
         peers.synchronize()
         res["verified"] = verify_slab_rows(ocean, fft, g, whole, rank, world)
@@ -982,18 +993,16 @@ XGMI_ONE_WAY_GBS = XGMI_LINKS * XGMI_LINK_GBS_BIDIR / 2.0  # 537.6 GB/s per rank
 
 
 def reserved_cu_set(layout: str, dev_cus: int, reserve: int):
-    """The logical CU indices (hipExtStreamCreateWithCUMask bits) left to the exchange: "top" = the last
-    `reserve`; "xcd" = the same number at the top of every 32-CU block (one block per XCD if the logical
-    numbering is XCD-major); "stride" = every (dev_cus / reserve)-th CU (one per XCD per step if the
-    numbering interleaves the XCDs)."""
-    if layout == "top":
-        return list(range(dev_cus - reserve, dev_cus))
-    if layout == "xcd":
-        blocks = max(1, dev_cus // 32)
-        per = max(1, reserve // blocks)
-        return [b * 32 + 32 - 1 - k for b in range(blocks) for k in range(per)]
-    step = max(1, dev_cus // reserve)
-    return list(range(step - 1, dev_cus, step))[:reserve]
+    """The logical CU indices (hipExtStreamCreateWithCUMask bits) left to the exchange. Bit c is CU c / 8
+    of XCD c % 8, and an XCD whose bits are all clear runs on all its CUs (tools/xcdmask/xcdprobe,
+    profiles/r05_xcdprobe.log): "per_xcd" = reserve / 8 CUs of every XCD, the only kind of set that
+    keeps both streams off each other's CUs. (Round 4's "top", "xcd" and "stride" sets named whole XCDs
+    or single CUs of a few; the XCDs they left without bits ran on all CUs, so they did not separate
+    the streams.)"""
+    per = max(1, reserve // 8)
+    if layout != "per_xcd":
+        raise ValueError(f"reserved CU layout {layout!r}: only per_xcd splits every XCD")
+    return [c for c in range(dev_cus) if c // 8 >= dev_cus // 8 - per]
 
 
 def p8_rank_projection(args, one_gpu_frame_ms: float, ranks: int = 8, masked: str = "") -> dict:
@@ -1195,10 +1204,16 @@ def p8_rank_projection(args, one_gpu_frame_ms: float, ranks: int = 8, masked: st
     return out
 
 
-def _put_emulation(args, ranks: int, mask_cus: int = 0, calibrate: bool = True) -> dict:
-    """One emulation of p8_put_projection: the 8 ranks joined locally; mask_cus > 0 puts the put stream
-    on that many CUs (hipExtStreamCreateWithCUMask, the "stride" set: the same number on every XCD) and
-    the step-1 and row-pass streams on the others, the put kernels sized for them."""
+def put_cu_set(per_xcd: int, dev_cus: int):
+    """Logical CUs of a put stream with `per_xcd` CUs of every XCD (bit c = CU c / 8 of XCD c % 8), as
+    ocean_peers_set_put_cu_mask builds it."""
+    return [c for c in range(dev_cus) if c // 8 < per_xcd]
+
+
+def _put_emulation(args, ranks: int, calibrate: bool = True, per_xcd: int = 0, put_cus: int = 0) -> dict:
+    """One emulation of p8_put_projection: the 8 ranks joined locally; per_xcd > 0 puts the put stream
+    on that many CUs of every XCD (hipExtStreamCreateWithCUMask, as ocean_peers_set_put_cu_mask) and
+    the step-1 and row-pass streams on the others, the put kernels sized for put_cus CUs (0: its own)."""
     import torch
 
     import oceansimulation_amd as ocean
@@ -1207,22 +1222,24 @@ def _put_emulation(args, ranks: int, mask_cus: int = 0, calibrate: bool = True) 
 
     n, dt, steps = args.slab_n, 1.0 / 60.0, args.slab_steps
     raw = []
-    if mask_cus:
+    mask_cus = 0
+    if per_xcd:
         dev_cus = torch.cuda.get_device_properties(torch.cuda.current_device()).multi_processor_count
-        res = set(reserved_cu_set("stride", dev_cus, mask_cus))
+        res = set(put_cu_set(per_xcd, dev_cus))
+        mask_cus = len(res)
         rest = [c for c in range(dev_cus) if c not in res]
         raw = [stream_with_cu_mask(rest, dev_cus), stream_with_cu_mask(rest, dev_cus),
-               stream_with_cu_mask(sorted(res), dev_cus)]
-        comp, s1, put = (torch.cuda.ExternalStream(h) for h in raw)
+               stream_with_cu_mask(sorted(res), dev_cus), stream_with_cu_mask(rest, dev_cus)]
+        comp, s1, put, rows_st = (torch.cuda.ExternalStream(h) for h in raw)
     else:
-        comp, s1, put = torch.cuda.Stream(), torch.cuda.Stream(), torch.cuda.Stream()
+        comp, s1, put, rows_st = (torch.cuda.Stream() for _ in range(4))
     fft = ocean.FFTCalculator(n, stream=comp.cuda_stream)
     slabs = [SlabGenerator(fft, r, ranks) for r in range(ranks)]
     peers = [PeerExchange(g) for g in slabs]
     try:
         PeerExchange.connect_local(peers)
         for p in peers:
-            p.set_streams(s1.cuda_stream, put.cuda_stream)
+            p.set_streams(s1.cuda_stream, put.cuda_stream, rows_st.cuda_stream)
         emulate_put_frame(slabs, peers, dt, update_ocean=True)
         emulate_put_frame(slabs, peers, dt)
 
@@ -1244,7 +1261,7 @@ def _put_emulation(args, ranks: int, mask_cus: int = 0, calibrate: bool = True) 
                 puts.append(ms[3] / max(cnt[3], 1))
             return cols, rows, puts
 
-        def pipelined(put_cus):
+        def pipelined(put_cus, profile=False):
             for p in peers:
                 p.set_put_cus(put_cus)
 
@@ -1256,6 +1273,19 @@ def _put_emulation(args, ranks: int, mask_cus: int = 0, calibrate: bool = True) 
                     p.flush()
             frames(2)
             torch.cuda.synchronize()
+            if profile:  # a separate run: the pipelined frame's kernels under contention
+                for g in slabs:
+                    g.set_profiling(True)
+                    g.kernel_times4()
+                frames(steps)
+                torch.cuda.synchronize()
+                tot = [0.0] * 4
+                for g in slabs:
+                    ms, cnt = g.kernel_times4()
+                    g.set_profiling(False)
+                    for i in range(4):
+                        tot[i] += ms[i] / max(cnt[i], 1) / ranks
+                return {"step1_ms": tot[1], "put_ms": tot[3], "row_pass_ms": tot[2]}
             t0 = time.perf_counter()
             frames(steps)
             torch.cuda.synchronize()
@@ -1283,7 +1313,8 @@ def _put_emulation(args, ranks: int, mask_cus: int = 0, calibrate: bool = True) 
             out["pipelined_paced_rank_frame_ms"] = pipelined(pace[0])
             out["exchange_bytes_per_rank"] = xbytes * (ranks - 1) // ranks
         else:
-            out["pipelined_rank_frame_ms"] = pipelined(mask_cus)
+            out["pipelined_rank_frame_ms"] = pipelined(put_cus or mask_cus)
+            out["kernels_in_pipelined_frame"] = pipelined(put_cus or mask_cus, profile=True)
         for p in peers:
             p.synchronize()
         return out
@@ -1312,9 +1343,12 @@ def p8_put_projection(args, one_gpu_frame_ms: float, ranks: int = 8) -> dict:
       pipelined: frame f's puts beside frame f + 1's step 1 and frame f - 1's row passes;
       paced: the put kernels on the most CUs (ocean_peers_set_put_cus) whose put still takes at least
       exchange_ms_at_rate alone (its stores then leave no faster than xGMI would carry them);
-      cu_masked: the paced put on its own CUs (a CU-masked put stream, the "stride" set), step 1 and
-      the row passes on the others, so the put's workgroups never wait behind theirs.
-    Bound on the 8-GPU frame: max(the best paced pipelined rank frame, exchange at the xGMI rate)."""
+      cu_masked (the design, ocean_peers_set_put_cu_mask(K)): the put stream CU-masked to K CUs of every
+      XCD, step 1 and the row passes on the others, so the put's workgroups never wait behind theirs.
+    Bound on the 8-GPU frame: max(the best masked pipelined rank frame, exchange at the xGMI rate): the emulated
+    put stores faster than xGMI would carry them, so that frame is what the passes need beside the put's
+    local traffic, and on the node the put takes exchange_ms_at_rate on its own XCDs. The put paced by
+    its workgroup count instead (a latency-bound put) is reported as projected_speedup_latency_bound_put."""
     out = {
         "what": f"{ranks} slab ranks of the single {args.slab_n}x{args.slab_n} grid emulated on one GPU over the "
                 "one-sided exchange: each rank's column pass stores its destination blocks into the other ranks' "
@@ -1329,26 +1363,45 @@ def p8_put_projection(args, one_gpu_frame_ms: float, ranks: int = 8) -> dict:
     rate_ms = out["exchange_bytes_per_rank"] / (XGMI_ONE_WAY_GBS * 1e9) * 1e3
     out["exchange_ms_at_rate"] = rate_ms
     out["passes_only_speedup_vs_1gpu"] = one_gpu_frame_ms / out["passes_ms"]
-    variants = {"paced": out["pipelined_paced_rank_frame_ms"]}
+    # the design: the put stream CU-masked to K CUs of every XCD (ocean_peers_set_put_cu_mask(K)), step 1
+    # and the row passes on the others. Its put stores faster than xGMI would carry them, so the frame
+    # measured here is what the passes need beside the put's local traffic; on the node the put then
+    # takes exchange_ms_at_rate on its own CUs, and the frame is the larger of the two
     masked = {}
-    for k in sorted({out["paced_put_cus"], out["paced_put_cus"] + 8, 32}):
+    for k in (4, 8, 12):
         try:
-            masked[k] = _put_emulation(args, ranks, mask_cus=k, calibrate=False)["pipelined_rank_frame_ms"]
-            variants[f"cu_masked_{k}"] = masked[k]
+            masked[f"put_{k}_per_xcd"] = _put_emulation(args, ranks, calibrate=False, per_xcd=k)
+        except Exception as e:  # reported; the bound then rests on the others
+            masked[f"put_{k}_per_xcd"] = {"error": f"{type(e).__name__}: {e}"}
+    out["cu_masked"] = masked
+    # sensitivity: the put instead paced by its workgroup count (the fewest CUs that keep it slower
+    # than xGMI): a latency-bound put, slowed further by the passes' traffic
+    paced = {"cu_paced": out["pipelined_paced_rank_frame_ms"]}
+    for k in (8,):
+        try:
+            paced[f"put_{k}_per_xcd_cu_paced"] = _put_emulation(args, ranks, calibrate=False, per_xcd=k,
+                                                               put_cus=out["paced_put_cus"])["pipelined_rank_frame_ms"]
         except Exception as e:  # reported, never fatal
-            masked[k] = f"{type(e).__name__}: {e}"
-    out["cu_masked_pipelined_rank_frame_ms"] = masked
-    best = min(variants, key=variants.get)
-    bound = max(variants[best], rate_ms)
-    out["best_variant"] = best
+            paced[f"put_{k}_per_xcd_cu_paced"] = f"{type(e).__name__}: {e}"
+    out["cu_paced_pipelined_rank_frame_ms"] = paced
+    numeric = [v for v in paced.values() if isinstance(v, float)]
+    if numeric:
+        out["projected_speedup_latency_bound_put"] = one_gpu_frame_ms / max(min(numeric), rate_ms)
+    frames = {k: v["pipelined_rank_frame_ms"] for k, v in masked.items() if "pipelined_rank_frame_ms" in v}
+    best = min(frames, key=frames.get) if frames else None
+    frame = frames[best] if best else min(numeric)
+    out["best_mask"] = best
+    bound = max(frame, rate_ms)
     out["frame_bound_ms"] = bound
-    out["bounding_term"] = (f"pipelined passes ({best}) with the put paced to the xGMI rate"
-                            if variants[best] >= rate_ms else "exchange at the xGMI rate")
+    out["bounding_term"] = ("exchange at the xGMI rate (the passes beside the put take less)" if rate_ms >= frame
+                            else "the pipelined passes beside the put")
     out["projected_speedup_vs_1gpu"] = one_gpu_frame_ms / bound
-    out["projected_speedup_note"] = ("one-GPU frame / max(one rank's pipelined frame emulated with its put on the "
-                                     "CUs that pace it to the xGMI rate, its exchange bytes at the one-way xGMI "
-                                     "rate); the local HBM traffic is the passes' own (the peers' stores land in "
-                                     "this rank's slots instead of a send buffer being copied)")
+    out["projected_speedup_note"] = ("one-GPU frame / max(one rank's pipelined frame emulated with the put on its "
+                                     "own K CUs of every XCD (step 1 and rows on the others), the rank's exchange bytes at the "
+                                     "one-way xGMI rate); the local HBM traffic is the passes' own (the peers' "
+                                     "stores land in this rank's slots instead of a send buffer being copied). "
+                                     "projected_speedup_latency_bound_put: the put paced by its workgroup count "
+                                     "instead (pessimistic)")
     return out
 
 
@@ -1577,6 +1630,15 @@ def main(argv=None):
                         sl[f"p8_rank_projection_cu_masked_{lay}"] = p8_rank_projection(args, one, masked=lay)
                     except Exception as e:  # reported, never fatal
                         sl[f"p8_rank_projection_cu_masked_{lay}"] = {"error": f"{type(e).__name__}: {e}"}
+        except ExchangeAbort as e:
+            # sends may be pending in RCCL: print the line and leave without any destructor
+            out["slab"] = dict(out.get("slab", {}), error=f"{type(e).__name__}: {e}")
+            watchdog.finish()
+            if rank == 0:
+                print(json.dumps(out), flush=True)
+            sys.stdout.flush()
+            sys.stderr.flush()
+            os._exit(EXCHANGE_ABORT_RC)
         except Exception as e:  # reported, never fatal to the headline measurement
             out["slab"] = dict(out.get("slab", {}), error=f"{type(e).__name__}: {e}")
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

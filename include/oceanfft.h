@@ -167,7 +167,10 @@ int ocean_generator_set_h0_memo(ocean_generator* gen, int enable);
  * the generator's stream whenever the library writes h0 (seeding, re-seeds) and after the h0 pointer
  * is handed out (ocean_generator_initial_spectrum); other work the caller enqueues on that stream
  * between frames is not waited for, so it must not write the generator's buffers. Costs 20 B of
- * device memory per point. Pays at 1-2 cascades per generator (8 x 4096^2: slower, leave it off).
+ * device memory per point. Pays at 1-2 cascades per generator below 4096 (8 x 4096^2: slower, leave it
+ * off). At 4096 with 1-2 cascades the column pass runs on half strips (two workgroups per CU), which
+ * share CUs with the overlapped row pass: there the serial frame is faster (0.318 against 0.346 ms at
+ * one cascade, profiles/r04_halfbench_xgrid_fb2_1.log), so leave it off as well.
  * Default 0. No reference counterpart (the reference barriers after every dispatch). */
 int ocean_generator_set_frame_overlap(ocean_generator* gen, int enable);
 /* Algorithmic HBM bytes per height-field point of the column pass [0] and the row pass [1] of the
@@ -265,9 +268,15 @@ int ocean_peers_set_timeout(ocean_peers* peers, int ms);
  * the stores bound by xGMI, fewer workgroups leave the other CUs to the row pass of the previous
  * frame in the pipelined frame. */
 int ocean_peers_set_put_cus(ocean_peers* peers, int cus);
-/* The streams pipelined frames run step 1 of the column pass and the put on (null: the peers' own).
- * The one-GPU emulation gives all P ranks one pair, as one GPU has one path out over xGMI. */
-int ocean_peers_set_streams(ocean_peers* peers, void* column_stream, void* put_stream);
+/* The streams pipelined frames run step 1 of the column pass, the put and the row pass on (null: the
+ * peers' own; the generator's stream waits for each row pass, so the maps stay ordered on it). The
+ * one-GPU emulation gives all P ranks one set, as one GPU has one path out over xGMI. */
+int ocean_peers_set_streams(ocean_peers* peers, void* column_stream, void* put_stream, void* row_stream);
+/* Recreate the peers' own streams CU-masked: the put on `cus_per_xcd` CUs of every XCD, step 1 and the
+ * row pass on the others (0: unmasked, the default). An xGMI-bound put then holds only its own CUs
+ * while it waits on the links. (A CU mask splits every XCD alike: workgroups are dealt to all 8 XCDs
+ * whatever the mask, and an XCD left without mask bits runs on all its CUs.) */
+int ocean_peers_set_put_cu_mask(ocean_peers* peers, int cus_per_xcd);
 /* Serial frame on the generator's stream: time += dt, h0 if needed, step 1, wait for the slot, put,
  * signal; wait for every rank's blocks, row pass, signal. */
 int ocean_generator_slab_frame_put(ocean_generator* gen, ocean_peers* peers, float timestep, int update_spectrum);

@@ -49,6 +49,11 @@ __global__ __launch_bounds__(1024) void k_rows_xs(FrameParams fp, const float4* 
 
   const int total = fp.cascades * rows;
   const float dim = (float)N;
+  // Element u = m T + i of a row sits in source block u >> log2(cpr) (RowSrc: each block holds cpr
+  // columns of every row). A wave's 64 lanes cover 64 consecutive u inside one block (cpr is a
+  // multiple of 64), so the block index is wave-uniform: it is computed from the wave's first thread
+  // (readfirstlane, kept in SGPRs by sopaque) with a shift, and each load is one buffer descriptor for
+  // the wave plus a lane offset.
   const int lcpr = 31 - __builtin_clz(rs.cpr), cmask = rs.cpr - 1;
   const int wave0 = __builtin_amdgcn_readfirstlane((int)threadIdx.x & ~63);
   float4 fp4[8], nx4[8];
@@ -100,6 +105,13 @@ __global__ __launch_bounds__(1024) void k_rows_xs(FrameParams fp, const float4* 
           nyq = CPair{f2v{-(p.im.x - kx2 * cc.y), -p.re.y + kx * p.im.x}, f2v{p.re.x - kx2 * cc.x, -p.im.y - kx * p.re.x}};
         }
       }
+      // T_in: the lanes at u and at -u of the reference's 4 packed fields are rebuilt from the kept
+      // half (Hermitian symmetry + the Nyquist-row term (-1)^y spec) and scattered into
+      // the LDS in the first step's order: element n of the row goes to slot pslot(n) = (n % 16) * RS
+      // + n / 16, so sub-transform n1 = n % 16 reads its 1024 inputs from one contiguous region of RS
+      // slots (RS = 1 mod 16 keeps 16-lane writes on distinct banks). The LDS holds one half (re or
+      // im plane) of the CPairs at a time: the re-halves are written as each element is formed, the
+      // im-halves wait in ho / hn until the first half has been read back.
       __syncthreads();  // the previous image's T_out reads are done: T_in's first half streams in now
       float2 ho[8], hn[8];  // the im halves of the own and -u lanes, written after the first half
 #pragma unroll
@@ -143,6 +155,10 @@ __global__ __launch_bounds__(1024) void k_rows_xs(FrameParams fp, const float4* 
         else if (item + (int)gridDim.x < total)
           issue(item + gridDim.x, 0, nx4, 0, PF);
       }
+      // four-step x transform: wave w holds sub-transform n1 = w's 16 x 64 elements (the 1024-point
+      // transform of region w runs inside the wave's own LDS region, whose exchanges need no
+      // workgroup barrier), then the twiddles W_N^(n1 k2), then T_out: the region-major layout is
+      // transposed through the LDS so each thread holds the 16 points of one 16-point DFT
       const int w = tid >> 6, l = tid & 63;
       CPair v[16];
       __syncthreads();
@@ -186,6 +202,8 @@ __global__ __launch_bounds__(1024) void k_rows_xs(FrameParams fp, const float4* 
         st4<kStream>(dst + m * T, tid * 16, from_pair(v[m]));
       if (img == 1)
       {
+        // computeFoam (resources/spectrum.compute:246-259): J = (1 + l dDx/dx)(1 + l dDz/dz) - l^2 (dDx/dz)^2
+        // from the displacement map's .y, .z, .w, l = the cascade's displacement
         const float lam = foam.displacement[c];
         float* jb = jac + ((size_t)c * rows + yl) * N;
 #pragma unroll

@@ -969,16 +969,21 @@ static FoamParams current_foam(const ocean_generator* g)
 
 // Second half: the x direction of both EncodeIFFTs + computeFoam (src/Generator.cpp:71-80). `frame_foam`:
 // the displacement of a pipelined slab frame's own settings (null: the current settings).
-static int generator_rows(ocean_generator* g, const float4* in, const FoamParams* frame_foam = nullptr)
+// row_stream (four-step path only; null: the generator's stream): the pipelined one-sided frame's rows.
+static int generator_rows(ocean_generator* g, const float4* in, const FoamParams* frame_foam = nullptr,
+                          hipStream_t row_stream = nullptr)
 {
   ocean_fft* f = g->fft;
   const FoamParams foam = frame_foam ? *frame_foam : current_foam(g);
   if (uses_gen4(g))
+  {
+    hipStream_t rs = row_stream ? row_stream : f->stream;
     HIP_TRY(timed(g, 2, [&] {
               return launch_gen4_rows(f->logn, g->frame, g->g4, in ? (const void*)in : (const void*)g->xbuf, g->maps,
-                                      g->jac, foam, f->twiddles, f->tw2, f->stream, f->cus);
-            }),
+                                      g->jac, foam, f->twiddles, f->tw2, rs, f->cus);
+            }, rs),
             "row pass (half spectrum, four-step)");
+  }
   else if (g->hslab)
     HIP_TRY(timed(g, 2, [&] {
               return launch_half_slab_rows(f->logn, g->frame, g->hsl, in ? (const void*)in : (const void*)g->xbuf,
@@ -1522,8 +1527,10 @@ struct ocean_peers
   uint64_t* table = nullptr;       // device: put destinations [2 slots][16], then the flag arrays [16]
   // pipelined frames: step 1 on s1_stream into parts slot f % 2, the put on put_stream, the row pass
   // on the generator's stream (ocean_peers_set_streams can replace the first two)
-  hipStream_t s1_stream = nullptr, put_stream = nullptr;
-  hipStream_t own_s1 = nullptr, own_put = nullptr;
+  hipStream_t s1_stream = nullptr, put_stream = nullptr, row_stream = nullptr;
+  hipStream_t own_s1 = nullptr, own_put = nullptr, own_rows = nullptr;
+  int put_cus_per_xcd = 0;           // own streams CU-masked: the put on this many CUs of every XCD
+  hipEvent_t rows_done = nullptr;    // pipelined rows on row_stream -> the generator's stream
   unsigned char* parts2 = nullptr;   // step 1's second parts slot
   hipEvent_t s1_done[2] = {nullptr, nullptr}, put_done[2] = {nullptr, nullptr};
   bool put_done_valid[2] = {false, false};
@@ -1632,31 +1639,72 @@ int put_columns(ocean_generator* g, ocean_peers* p, float timestep, int update_s
   return OCEAN_OK;
 }
 
-// Row pass of the oldest frame whose rows are not issued yet, on the generator's stream: wait for
-// every rank's blocks, rows, then this rank's "freed" word (f + 1) in every rank's flags.
-int put_rows(ocean_generator* g, ocean_peers* p)
+// Row pass of the oldest frame whose rows are not issued yet: wait for every rank's blocks, rows, then
+// this rank's "freed" word (f + 1) in every rank's flags. Serial: on the generator's stream. Pipelined:
+// on the peers' row stream, which the generator's stream then waits for (the maps stay ordered on it).
+int put_rows(ocean_generator* g, ocean_peers* p, bool pipelined = false)
 {
   ocean_fft* f = g->fft;
   const int64_t fr = p->rows;
   if (fr >= p->frames)
     return fail(OCEAN_ERR_INVALID, "ocean_generator_slab_put_rows: no column pass issued for this frame");
   const int s = (int)(fr % 2);
-  HIP_TRY(launch_peer_wait(peer_wait(p, kReadyWord, fr + 1), f->stream), "one-sided exchange: ready wait");
+  hipStream_t rs = pipelined ? p->row_stream : f->stream;
+  HIP_TRY(launch_peer_wait(peer_wait(p, kReadyWord, fr + 1), rs), "one-sided exchange: ready wait");
   const FrameParams newest = g->frame;
   g->frame = p->slot_frame[s];
-  const int rc = generator_rows(g, reinterpret_cast<const float4*>(p->data + s * p->slot), &p->slot_foam[s]);
+  const int rc = generator_rows(g, reinterpret_cast<const float4*>(p->data + s * p->slot), &p->slot_foam[s], rs);
   g->frame = newest;
   if (rc != OCEAN_OK)
     return rc;
-  HIP_TRY(launch_peer_signal(flag_table(p), p->ranks, kFreedWord + p->rank, (uint32_t)(fr + 1), f->stream),
+  HIP_TRY(launch_peer_signal(flag_table(p), p->ranks, kFreedWord + p->rank, (uint32_t)(fr + 1), rs),
           "one-sided exchange: freed signal");
+  if (rs != f->stream)
+  {
+    HIP_TRY(hipEventRecord(p->rows_done, rs), "one-sided exchange: events");
+    HIP_TRY(hipStreamWaitEvent(f->stream, p->rows_done, 0), "one-sided exchange: stream order");
+  }
   p->rows = fr + 1;
+  return OCEAN_OK;
+}
+
+// (Re)create the peers' own streams; with put_cus_per_xcd > 0 CU-masked: the put stream on that many
+// CUs of every XCD, the step-1 and row streams on the others. A hipExtStreamCreateWithCUMask bit c is
+// CU c / 8 of XCD c % 8, and an XCD whose bits are all clear runs on all its CUs (workgroups are dealt
+// to every XCD whatever the mask; tools/xcdmask, profiles/r05_xcdprobe.log): a mask can only split
+// each XCD, so the put takes the same share of each.
+int peers_streams(ocean_peers* p)
+{
+  for (hipStream_t* st : {&p->own_s1, &p->own_put, &p->own_rows})
+    if (*st)
+    {
+      HIP_TRY(hipStreamSynchronize(*st), "ocean_peers: streams");
+      HIP_TRY(hipStreamDestroy(*st), "ocean_peers: streams");
+      *st = nullptr;
+    }
+  const int cus = p->g->fft->device_cus;
+  if (p->put_cus_per_xcd > 0 && cus % 8 == 0 && p->put_cus_per_xcd < cus / 8)
+  {
+    std::vector<uint32_t> put((cus + 31) / 32, 0u), rest((cus + 31) / 32, 0u);
+    for (int c = 0; c < cus; c++)
+      (c / 8 < p->put_cus_per_xcd ? put : rest)[c / 32] |= 1u << (c % 32);
+    HIP_TRY(hipExtStreamCreateWithCUMask(&p->own_put, (uint32_t)put.size(), put.data()), "ocean_peers: put stream");
+    HIP_TRY(hipExtStreamCreateWithCUMask(&p->own_s1, (uint32_t)rest.size(), rest.data()), "ocean_peers: column stream");
+    HIP_TRY(hipExtStreamCreateWithCUMask(&p->own_rows, (uint32_t)rest.size(), rest.data()), "ocean_peers: row stream");
+  }
+  else
+    for (hipStream_t* st : {&p->own_s1, &p->own_put, &p->own_rows})
+      HIP_TRY(hipStreamCreateWithFlags(st, hipStreamNonBlocking), "ocean_peers: streams");
+  p->s1_stream = p->own_s1;
+  p->put_stream = p->own_put;
+  p->row_stream = p->own_rows;
+  p->put_done_valid[0] = p->put_done_valid[1] = false;
   return OCEAN_OK;
 }
 
 void peers_release(ocean_peers* p)
 {
-  for (hipStream_t st : {p->s1_stream, p->put_stream})
+  for (hipStream_t st : {p->s1_stream, p->put_stream, p->row_stream})
     if (st)
       (void)hipStreamSynchronize(st);
   if (p->g && p->g->fft)
@@ -1680,7 +1728,7 @@ static void peers_detach(ocean_peers* p)
 {
   if (!p)
     return;
-  for (hipStream_t st : {p->s1_stream, p->put_stream})
+  for (hipStream_t st : {p->s1_stream, p->put_stream, p->row_stream})
     if (st)
       (void)hipStreamSynchronize(st);
   p->g = nullptr;
@@ -1723,21 +1771,19 @@ int ocean_peers_create(ocean_peers** out, ocean_generator* g)
     e = hipMalloc(&p->table, 3 * kMaxRanks * sizeof(uint64_t));
   if (e == hipSuccess)
     e = hipMemset(p->flags, 0, kFlagWords * sizeof(uint32_t));
-  if (e == hipSuccess)
-    e = hipStreamCreateWithFlags(&p->own_s1, hipStreamNonBlocking);
-  if (e == hipSuccess)
-    e = hipStreamCreateWithFlags(&p->own_put, hipStreamNonBlocking);
   for (int k = 0; k < 2 && e == hipSuccess; k++)
   {
     e = hipEventCreateWithFlags(&p->s1_done[k], hipEventDisableTiming);
     if (e == hipSuccess)
       e = hipEventCreateWithFlags(&p->put_done[k], hipEventDisableTiming);
   }
-  p->s1_stream = p->own_s1;
-  p->put_stream = p->own_put;
+  if (e == hipSuccess)
+    e = hipEventCreateWithFlags(&p->rows_done, hipEventDisableTiming);
   if (e == hipSuccess)
     e = hipDeviceSynchronize();
   int rc = e == hipSuccess ? peers_deadline(p) : OCEAN_OK;
+  if (rc == OCEAN_OK && e == hipSuccess)
+    rc = peers_streams(p);
   if (e != hipSuccess || rc != OCEAN_OK)
   {
     const int code = e == hipErrorOutOfMemory ? OCEAN_ERR_OOM : OCEAN_ERR_HIP;
@@ -1759,13 +1805,15 @@ int ocean_peers_destroy(ocean_peers* p)
   peers_release(p);
   if (p->g)
     p->g->peers = nullptr;
-  for (hipStream_t st : {p->own_s1, p->own_put})
+  for (hipStream_t st : {p->own_s1, p->own_put, p->own_rows})
     if (st)
       (void)hipStreamDestroy(st);
   for (int k = 0; k < 2; k++)
     for (hipEvent_t ev : {p->s1_done[k], p->put_done[k]})
       if (ev)
         (void)hipEventDestroy(ev);
+  if (p->rows_done)
+    (void)hipEventDestroy(p->rows_done);
   for (void* q : {(void*)p->data, (void*)p->flags, (void*)p->table, (void*)p->parts2})
     if (q)
       (void)hipFree(q);
@@ -1869,18 +1917,32 @@ int ocean_peers_set_put_cus(ocean_peers* p, int cus)
   return OCEAN_OK;
 }
 
-int ocean_peers_set_streams(ocean_peers* p, void* column_stream, void* put_stream)
+int ocean_peers_set_streams(ocean_peers* p, void* column_stream, void* put_stream, void* row_stream)
 {
   if (!p || !p->g)
     return fail(OCEAN_ERR_INVALID, "ocean_peers_set_streams: null or detached peers");
   if (p->rows < p->frames)
     return fail(OCEAN_ERR_INVALID, "ocean_peers_set_streams: a pipelined frame is in flight (flush first)");
-  for (hipStream_t st : {p->s1_stream, p->put_stream})
+  for (hipStream_t st : {p->s1_stream, p->put_stream, p->row_stream})
     HIP_TRY(hipStreamSynchronize(st), "ocean_peers_set_streams");
   p->s1_stream = column_stream ? (hipStream_t)column_stream : p->own_s1;
   p->put_stream = put_stream ? (hipStream_t)put_stream : p->own_put;
-  p->put_done_valid[0] = p->put_done_valid[1] = false;  // both old streams are drained
+  p->row_stream = row_stream ? (hipStream_t)row_stream : p->own_rows;
+  p->put_done_valid[0] = p->put_done_valid[1] = false;  // the old streams are drained
   return OCEAN_OK;
+}
+
+int ocean_peers_set_put_cu_mask(ocean_peers* p, int cus_per_xcd)
+{
+  if (!p || !p->g || cus_per_xcd < 0 || cus_per_xcd >= p->g->fft->device_cus / 8)
+    return fail(OCEAN_ERR_INVALID, "ocean_peers_set_put_cu_mask: null peers or CUs per XCD outside [0, CUs / 8)");
+  if (p->rows < p->frames)
+    return fail(OCEAN_ERR_INVALID, "ocean_peers_set_put_cu_mask: a pipelined frame is in flight (flush first)");
+  const bool own = p->s1_stream == p->own_s1 && p->put_stream == p->own_put && p->row_stream == p->own_rows;
+  if (!own)
+    return fail(OCEAN_ERR_INVALID, "ocean_peers_set_put_cu_mask: the caller's streams are in use (ocean_peers_set_streams)");
+  p->put_cus_per_xcd = cus_per_xcd;
+  return peers_streams(p);
 }
 
 int ocean_generator_slab_put_columns(ocean_generator* g, ocean_peers* p, float timestep, int update_spectrum)
@@ -1917,7 +1979,7 @@ int ocean_generator_slab_frame_put_pipelined(ocean_generator* g, ocean_peers* p,
   if (rc == OCEAN_OK)
     rc = put_columns(g, p, timestep, update_spectrum, true);
   while (rc == OCEAN_OK && p->rows < p->frames - 1)  // frame f - 1's row pass beside frame f's columns
-    rc = put_rows(g, p);
+    rc = put_rows(g, p, true);
   return rc;
 }
 
@@ -1927,7 +1989,7 @@ int ocean_peers_flush(ocean_peers* p)
     return fail(OCEAN_ERR_INVALID, "ocean_peers_flush: null or detached peers");
   int rc = OCEAN_OK;
   while (rc == OCEAN_OK && p->rows < p->frames)
-    rc = put_rows(p->g, p);
+    rc = put_rows(p->g, p, true);
   return rc;
 }
 
@@ -1937,6 +1999,7 @@ int ocean_peers_synchronize(ocean_peers* p)
     return fail(OCEAN_ERR_INVALID, "ocean_peers_synchronize: null peers");
   HIP_TRY(hipStreamSynchronize(p->s1_stream), "ocean_peers_synchronize: column stream");
   HIP_TRY(hipStreamSynchronize(p->put_stream), "ocean_peers_synchronize: put stream");
+  HIP_TRY(hipStreamSynchronize(p->row_stream), "ocean_peers_synchronize: row stream");
   if (p->g)
     HIP_TRY(hipStreamSynchronize(p->g->fft->stream), "ocean_peers_synchronize: generator stream");
   uint32_t err = 0;

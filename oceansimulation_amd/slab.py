@@ -237,10 +237,15 @@ class PeerExchange:
     def set_put_cus(self, cus: int) -> None:
         check(lib().ocean_peers_set_put_cus(self._h, int(cus)), "ocean_peers_set_put_cus")
 
-    def set_streams(self, column_stream: int | None, put_stream: int | None) -> None:
-        """Streams of pipelined frames' step 1 and put (None: the peers' own)."""
-        check(lib().ocean_peers_set_streams(self._h, ctypes.c_void_p(column_stream or 0), ctypes.c_void_p(put_stream or 0)),
-              "ocean_peers_set_streams")
+    def set_streams(self, column_stream: int | None, put_stream: int | None, row_stream: int | None) -> None:
+        """Streams of pipelined frames' step 1, put and row pass (None: the peers' own)."""
+        check(lib().ocean_peers_set_streams(self._h, ctypes.c_void_p(column_stream or 0), ctypes.c_void_p(put_stream or 0),
+                                            ctypes.c_void_p(row_stream or 0)), "ocean_peers_set_streams")
+
+    def set_put_cu_mask(self, cus_per_xcd: int) -> None:
+        """CU-mask the peers' own streams: the put on `cus_per_xcd` CUs of every XCD, step 1 and rows on
+        the others (0: unmasked)."""
+        check(lib().ocean_peers_set_put_cu_mask(self._h, int(cus_per_xcd)), "ocean_peers_set_put_cu_mask")
 
     def flush(self) -> None:
         check(lib().ocean_peers_flush(self._h), "ocean_peers_flush")

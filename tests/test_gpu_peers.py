@@ -160,3 +160,36 @@ def test_put_wait_times_out_without_peer(ocean):
     for g in slabs:
         g.close()
     fft.close()
+
+
+def test_comm_wrap_checks_size_and_rank(ocean):
+    """ocean_comm_wrap takes the caller's ncclComm_t only when nranks / rank are the communicator's own
+    (ncclCommCount / ncclCommUserRank): a one-rank RCCL communicator made here (through the RCCL that
+    liboceanfft.so links, resolved via the library's own handle) is refused as rank 1 of 2 and taken as
+    rank 0 of 1."""
+    import ctypes
+
+    from oceansimulation_amd import capi
+
+    L = capi.lib()
+
+    class UniqueId(ctypes.Structure):
+        _fields_ = [("internal", ctypes.c_char * capi.OCEAN_COMM_ID_BYTES)]
+
+    get_id, init_rank, destroy = L.ncclGetUniqueId, L.ncclCommInitRank, L.ncclCommDestroy
+    get_id.argtypes, get_id.restype = [ctypes.POINTER(UniqueId)], ctypes.c_int
+    init_rank.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_int, UniqueId, ctypes.c_int]
+    init_rank.restype = ctypes.c_int
+    destroy.argtypes, destroy.restype = [ctypes.c_void_p], ctypes.c_int
+    uid = UniqueId()
+    assert get_id(ctypes.byref(uid)) == 0
+    nc = ctypes.c_void_p()
+    assert init_rank(ctypes.byref(nc), 1, uid, 0) == 0
+    wrapped = ctypes.c_void_p()
+    assert L.ocean_comm_wrap(ctypes.byref(wrapped), nc, 2, 1) == capi.OCEAN_ERR_INVALID
+    assert "rank 0 of 1" in L.ocean_last_error().decode()
+    assert not wrapped.value
+    assert L.ocean_comm_wrap(ctypes.byref(wrapped), nc, 1, 0) == capi.OCEAN_OK
+    assert wrapped.value
+    assert L.ocean_comm_destroy(wrapped) == capi.OCEAN_OK  # a wrapped communicator stays the caller's
+    assert destroy(nc) == 0

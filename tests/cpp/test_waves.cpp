@@ -5,8 +5,10 @@
 // 5/17/101 m, boundWavelength = 1, wavelength bounds; per frame CalculateOcean(dt, true) for
 // every generator (src/Waves.cpp:90-91: updateSpectrum is never cleared). Also checks
 // FFTCalculator::EncodeIFFT on a random image, and Waves::SlabGenerator at world size 1 (the RCCL
-// exchange with one rank, pipelined and not) against a whole-grid Waves::Generator, bit for bit.
-// Usage: test_waves [n] [frames] [slab n, 0 = skip]. Exit code 0 = all within tolerance.
+// exchange with one rank, pipelined and not) against a whole-grid Waves::Generator, bit for bit, and
+// two Waves::SlabGenerator ranks of one process over the one-sided exchange (Waves::SlabPeers joined
+// locally), serial and pipelined, against the whole grid, bit for bit.
+// Usage: test_waves [n] [frames] [slab n, 0 = skip] [put n, 0 = skip]. Exit code 0 = all within tolerance.
 #include <hip/hip_runtime_api.h>
 
 #include <cmath>
@@ -79,11 +81,66 @@ static int slab_world1(Vision::RenderDevice& device, int n, int frames)
   return failures;
 }
 
+// Two ranks of one n x n grid in this process over the one-sided exchange: PutColumns of both ranks,
+// then PutRows of both (serial frames), then pipelined frames + Flush, each rank's row slab against the
+// whole grid bit for bit.
+static int slab_put_two_ranks(Vision::RenderDevice& device, int n, int frames)
+{
+  int failures = 0;
+  Waves::FFTCalculator fft(&device, n);
+  Waves::Generator whole(&device, &fft);
+  Waves::SlabGenerator r0(&device, &fft, 0, 2), r1(&device, &fft, 1, 2);
+  Waves::SlabPeers p0(r0), p1(r1);
+  Waves::SlabPeers::ConnectLocal({&p0, &p1});
+  const float dt = 1.0f / 60.0f;
+  auto check_rows = [&](const char* what) {
+    p0.Synchronize();
+    p1.Synchronize();
+    const size_t half = (size_t)n * n / 2;
+    std::vector<float> w(half * 2 * 4), s(half * 4);
+    const Vision::ID ids[3][3] = {{whole.GetHeightMap(), r0.GetHeightMap(), r1.GetHeightMap()},
+                                  {whole.GetDisplacementMap(), r0.GetDisplacementMap(), r1.GetDisplacementMap()},
+                                  {whole.GetJacobianMap(), r0.GetJacobianMap(), r1.GetJacobianMap()}};
+    for (int m = 0; m < 3; m++)
+    {
+      const size_t ch = m == 2 ? 1 : 4;
+      device.GetTexture2DDataRaw(ids[m][0], w.data());
+      for (int r = 0; r < 2; r++)
+      {
+        device.GetTexture2DDataRaw(ids[m][1 + r], s.data());
+        const bool ok = std::memcmp(s.data(), w.data() + r * half * ch, half * ch * sizeof(float)) == 0;
+        std::printf("one-sided n=%d %s map %d rank %d: %s\n", n, what, m, r, ok ? "bit-exact" : "DIFFERS");
+        failures += !ok;
+      }
+    }
+  };
+  for (int f = 0; f < frames; f++)
+  {
+    whole.CalculateOcean(dt, f == 0);
+    r0.PutColumns(p0, dt, f == 0);
+    r1.PutColumns(p1, dt, f == 0);
+    r0.PutRows(p0);
+    r1.PutRows(p1);
+  }
+  check_rows("serial");
+  for (int f = 0; f < frames; f++)
+  {
+    whole.CalculateOcean(dt);
+    r0.CalculateOceanPutPipelined(p0, dt);
+    r1.CalculateOceanPutPipelined(p1, dt);
+  }
+  p0.Flush();
+  p1.Flush();
+  check_rows("pipelined");
+  return failures;
+}
+
 int main(int argc, char** argv)
 {
   const int n = argc > 1 ? std::atoi(argv[1]) : 256;
   const int frames = argc > 2 ? std::atoi(argv[2]) : 3;
   const int slab_n = argc > 3 ? std::atoi(argv[3]) : 1024;
+  const int put_n = argc > 4 ? std::atoi(argv[4]) : 8192;
   int failures = 0;
 
   Vision::RenderDevice device;  // default stream
@@ -176,6 +233,8 @@ int main(int argc, char** argv)
     delete g;
   if (slab_n > 0)
     failures += slab_world1(device, slab_n, frames);
+  if (put_n > 0)
+    failures += slab_put_two_ranks(device, put_n, frames);
   std::printf("%s (%d failures)\n", failures ? "FAIL" : "PASS", failures);
   return failures ? 1 : 0;
 }

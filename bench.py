@@ -289,7 +289,7 @@ def measured_traffic(kernel: str, n: int, cascades: int):
         rec = prof.get("kernels", {}).get(kernel)
         if (prof.get("device_source_sha256") == sha and prof.get("n") == n and prof.get("cascades") == cascades
                 and rec and rec.get("hbm_traffic_bytes")):
-            return {"hbm_traffic_bytes": rec["hbm_traffic_bytes"],
+            return {"hbm_traffic_bytes": rec["hbm_traffic_bytes"], "avg_ms": rec.get("avg_ms"),
                     "source": f"{os.path.relpath(path, ROOT)} (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, same "
                               f"workload, same device code sha256 {sha[:12]})"}
     return None
@@ -1558,6 +1558,7 @@ def main(argv=None):
         out["roofline"] = {
             "bound": "hbm",
             "kernel": dom_name,
+            "frac_source": "this run: HIP events around every launch of the timed loop, on the box running bench.py",
             "achieved": achieved,
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",
@@ -1571,6 +1572,14 @@ def main(argv=None):
             out["roofline"]["traffic_bytes_per_launch"] = pmc["hbm_traffic_bytes"]
             out["roofline"]["algorithmic_bytes_per_launch"] = dom["bytes"]
             out["roofline"]["traffic_source"] = pmc["source"]
+            if pmc.get("avg_ms"):
+                # the same kernel's duration in the committed rocprofv3 summary (another box, profiled run):
+                # the fraction that summary gives, beside this run's
+                out["roofline"]["committed_profile"] = {
+                    "avg_ms": pmc["avg_ms"],
+                    "frac": dom["bytes"] / (pmc["avg_ms"] * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                    "source": pmc["source"].split(" ")[0] + " (rocprofv3 --kernel-trace --stats, the profiling box)",
+                }
         else:
             out["roofline"]["traffic_note"] = ("no committed PMC summary of this device code "
                                                f"(sha256 {device_source_sha256()[:12]}); tools/profile_gpu.sh")

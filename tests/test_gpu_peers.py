@@ -90,6 +90,17 @@ def test_put_exchange_in_one_process_bit_exact(ocean, n, P):
     for dt in steps:
         whole.CalculateOcean(dt)
     assert _same(L, slabs, whole, n) is None, (n, P, "pipelined")
+    # the peers' own streams CU-masked (the put on 8 CUs of every XCD, step 1 and rows on the rest)
+    for p in peers:
+        p.set_put_cu_mask(8)
+    for dt in steps:
+        for g, p in zip(slabs, peers):
+            g.frame_put_pipelined(p, dt)
+    for p in peers:
+        p.flush()
+    for dt in steps:
+        whole.CalculateOcean(dt)
+    assert _same(L, slabs, whole, n) is None, (n, P, "pipelined, CU-masked put")
     for p in peers:
         p.synchronize()
         p.close()

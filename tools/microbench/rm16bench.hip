@@ -159,6 +159,14 @@ int main()
       hipLaunchKernelGGL(kern, dim3(C * N), dim3(S::T), XsCfg<LOGN>::LDS, 0, fp, spec, maps, jac, foam, tw, N, rs, tw2);
     };
   };
+  auto mkg = [&](auto kern, int grid) {  // k_rows_xs on a persistent grid: PF prefetches the next row too
+    CHECK(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, XsCfg<LOGN>::LDS));
+    return [=] {
+      hipLaunchKernelGGL(kern, dim3(grid), dim3(S::T), XsCfg<LOGN>::LDS, 0, fp, spec, maps, jac, foam, tw, N, rs, tw2);
+    };
+  };
+  int cus = 0;
+  CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0));
   auto mkp = [&](auto kern) {  // k_rows_xp (spec, maps, jac, foam, tw, rows, rs)
     CHECK(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, XpCfg<LOGN>::LDS));
     return [=] {
@@ -190,6 +198,9 @@ int main()
       {"k_rows_xp PF 2", mkp(k_rows_xp<LOGN, 2>), {}},
       {"k_rows_xp PF 3", mkp(k_rows_xp<LOGN, 3>), {}},
       {"k_rows_xs_r3 (round-3 production) PF 2", mkn(k_rows_xs_r3<LOGN, 2>), {}},
+      {"k_rows_xs PF 2, persistent grid (CUs)", mkg(k_rows_xs<LOGN, 2>, cus), {}},
+      {"k_rows_xs PF 3, persistent grid (CUs)", mkg(k_rows_xs<LOGN, 3>, cus), {}},
+      {"k_rows_xs PF 0, persistent grid (CUs)", mkg(k_rows_xs<LOGN, 0>, cus), {}},
   };
   // XS vs the plain transform: same lanes, different rounding order (max |diff| vs max |value|)
   auto snapf = [&](const void* p, size_t n) {
@@ -231,6 +242,7 @@ int main()
   compare(7, 11, "k_rows_xp PF 2 vs k_rows_xs PF 2");
   compare(10, 12, "k_rows_xp PF 3 vs PF 0");
   compare(13, 7, "k_rows_xs PF 2 (streaming T_in) vs round 3");
+  compare(7, 14, "k_rows_xs PF 2: persistent vs one-shot grid");
   for (int r = 0; r < 5; r++)
     for (auto& v : vs)
       v.t.push_back(time_ms(v.run, 3));

@@ -110,3 +110,47 @@ def test_world2_alltoall_matches_emulated_block_moves():
         p.join(timeout=30)
         assert p.exitcode == 0
     assert all(ok for _, ok in res)
+
+
+def _gather_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    import sys
+
+    import torch.distributed as dist
+
+    dist.init_process_group("gloo")
+    sys.path.insert(0, ROOT)
+    from oceansimulation_amd.slab import torch_gather_bytes
+
+    spec = importlib.util.spec_from_file_location("bench", os.path.join(ROOT, "bench.py"))
+    b = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(b)
+    # what put_leg hands ocean_peers_connect: every rank's 256-byte handle, in rank order
+    blob = bytes([rank]) * 256
+    got = torch_gather_bytes(blob)
+    # the verdicts every multi-rank leg agrees on before it branches (MIN over ranks)
+    agree_all = b.ranks_agree(True, world)
+    agree_one_fails = b.ranks_agree(rank != 1, world)
+    dist.destroy_process_group()
+    q.put((rank, [g[:1] for g in got], [len(g) for g in got], agree_all, agree_one_fails))
+
+
+@pytest.mark.timeout(120)
+def test_world2_peer_handles_gather_in_rank_order_and_verdicts_agree():
+    """The one-sided exchange's handle exchange (slab.torch_gather_bytes, an all_gather_object) gives
+    every rank all handles in rank order, and bench.ranks_agree makes every rank take the branch of the
+    most pessimistic one (a rank whose connect or check failed stops all of them)."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_gather_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=100) for _ in procs]
+    for p in procs:
+        p.join(timeout=30)
+        assert p.exitcode == 0
+    for rank, heads, lens, agree_all, agree_one_fails in res:
+        assert heads == [bytes([0]), bytes([1])] and lens == [256, 256]
+        assert agree_all is True and agree_one_fails is False

@@ -275,3 +275,24 @@ def test_xp_hp_index_model():
     assert m.model_hp() < 1e-12
     assert m.hp_bank_multiplicity() == 1  # k_rows_hp's four LDS access shapes are conflict-free
     assert m.model_hx() < 1e-12  # k_cols_half HX (measured, not kept) and its storage-row bijection
+
+
+def test_cu_mask_sets_split_every_xcd():
+    """A hipExtStreamCreateWithCUMask bit c is CU c / 8 of XCD c % 8, and an XCD without bits runs on
+    all its CUs (profiles/r05_xcdprobe.log): the put stream's set and the RCCL projection's reserved set
+    must give every XCD the same number of CUs, and the rest must be the complement."""
+    b = _bench()
+    dev = 256
+    for k in (4, 8, 12):
+        put = b.put_cu_set(k, dev)
+        assert len(put) == 8 * k
+        per_xcd = [sum(1 for c in put if c % 8 == x) for x in range(8)]
+        assert per_xcd == [k] * 8
+        rest = [c for c in range(dev) if c not in set(put)]
+        assert [sum(1 for c in rest if c % 8 == x) for x in range(8)] == [dev // 8 - k] * 8
+    res = b.reserved_cu_set("per_xcd", dev, 32)
+    assert [sum(1 for c in res if c % 8 == x) for x in range(8)] == [4] * 8
+    import pytest
+
+    with pytest.raises(ValueError):
+        b.reserved_cu_set("stride", dev, 32)

@@ -241,8 +241,9 @@ int ocean_generator_slab_flush(ocean_generator* gen);
  * flag word in every rank's flag array after its stores ("ready") and one after its row pass has
  * read its slot ("freed"); the waits for them are one-wave kernels on the streams, bounded by a
  * timeout (ocean_peers_set_timeout), so a missing peer never holds the GPU: the frame goes on, and
- * ocean_peers_synchronize reports OCEAN_ERR_TIMEOUT. Four-step slabs only (N = 8192 / 16384, the
- * default path there); the RCCL exchange above serves every slab path. SURVEY §8e, the reference's
+ * ocean_peers_synchronize reports OCEAN_ERR_TIMEOUT. Every half-spectrum slab path (N >= 1024): on the
+ * four-step slabs (N = 8192 / 16384) step 2 puts, on the strip-dealt ones the column pass itself; the
+ * RCCL exchange above also serves the full-spectrum slabs below 1024. SURVEY §8e, the reference's
  * CalculateOcean (src/Generator.cpp:45-83) split over P ranks.
  * Use: ocean_peers_create on every rank, ocean_peers_handle -> the caller gathers the P handles (in
  * rank order, e.g. an all-gather) -> ocean_peers_connect; frames; ocean_peers_synchronize on every
@@ -251,7 +252,8 @@ int ocean_generator_slab_flush(ocean_generator* gen);
 #define OCEAN_PEER_HANDLE_BYTES 256
 typedef struct ocean_peers ocean_peers;
 /* Two receive slots of ocean_generator_exchange_bytes(gen) and the flag words, in this process's
- * device memory; gen must be a slab generator on the four-step path. */
+ * device memory; gen must be a slab generator on a half-spectrum path (N >= 1024). A later path switch
+ * that changes the exchange size makes the peers refuse frames. */
 int ocean_peers_create(ocean_peers** out, ocean_generator* gen);
 int ocean_peers_destroy(ocean_peers* peers);
 /* This rank's handle (rank, ranks, slot size, the IPC handles of its slots and flags). */

@@ -140,9 +140,12 @@ __device__ __forceinline__ void fft_cols_hx(CPair* v, int t, void* lds, const fl
 // FB (half strips, whole grids): the fields are FB = CPI columns wide (half_group_offset<.., FB>), so a
 // half-strip item's stores are whole lines when RG * FB * 16 B = 128 B (gab, gde) and RGC * FB * 8 B
 // = 128 B (gc); the row pass reads the same layout (k_rows_hp FB).
+// PUT (SLAB only; the one-sided exchange, ocean_peers): `send` is then the device table of the ranks'
+// destinations, ((const uint64_t*)send)[q] = this rank's block in rank q's receive slot, and block q
+// is stored there instead of at send + q * block bytes.
 template <int LOGN, int LA = 0, int SA = kStream, bool HS = false, bool SLAB = false, bool SEED = false, int RG = 1,
           int RGC = 1, int CPI = ColFirstCfg<LOGN>::B, bool HP = false, bool PC = false, int HL = 0, int HK = 0,
-          int HX = 0, int FB = 4>
+          int HX = 0, int FB = 4, bool PUT = false>
 __global__ __launch_bounds__(FftShape<LOGN>::T * CPI, CPI < ColFirstCfg<LOGN>::B ? 4 : 1) void k_cols_half(FrameParams fp, const float4* __restrict__ h0,
                                                                      float4* __restrict__ gab, float4* __restrict__ gde,
                                                                      float2* __restrict__ gc,
@@ -162,6 +165,7 @@ __global__ __launch_bounds__(FftShape<LOGN>::T * CPI, CPI < ColFirstCfg<LOGN>::B
   static_assert(HX != 2 || (!SLAB && RG > 1 && RGC > 1), "HX 2: whole-grid row-group layouts");
   constexpr int MSTEP = HX == 2 ? 16 : T;  // storage rows between v[m] and v[m + 1]
   static_assert(FB == 4 || (FB == CPI && HALVES == 2 && !SLAB && RG > 1 && RGC > 1 && !HX), "FB: half-strip fields");
+  static_assert(!PUT || (SLAB && !PC), "PUT: the strip-dealt slab stores");
   constexpr int XB = CPI * S::PADDED * 8;  // the exchange's bytes (K::LDS1 for whole strips)
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   float2* tw = reinterpret_cast<float2*>(smem);
@@ -341,7 +345,9 @@ __global__ __launch_bounds__(FftShape<LOGN>::T * CPI, CPI < ColFirstCfg<LOGN>::B
           const size_t el = (((size_t)c * hsl.S + s) * hsl.w + yl0) * B;
           // block = the three parts, then the Nyquist-row term [c][2][N] (half_slab_block_bytes).
           // The block base is built at its store (sopaque): hoisted, the 16 descriptors spilled SGPRs.
-          unsigned char* blk = send + sopaque((size_t)q * (part * 40 + (size_t)fp.cascades * 2 * N * 16));
+          unsigned char* blk =
+              PUT ? reinterpret_cast<unsigned char*>(sopaque((size_t)reinterpret_cast<const uint64_t*>(send)[q]))
+                  : send + sopaque((size_t)q * (part * 40 + (size_t)fp.cascades * 2 * N * 16));
           if (round == 0)
             st4<SA>(blk + el * 16, vo, pair_raw(v[m]));
           else if (round == 1)

@@ -43,8 +43,10 @@ size_t half_slab_row_texels(int logn, int cascades, int w)
 
 hipError_t launch_half_slab_columns(int logn, const FrameParams& fp, const HalfSlab& hsl, int ranks, const float4* h0,
                                     bool h0_full, const float4* h0row, void* send, const float2* tw,
-                                    hipStream_t stream, int cus, float2* hs, int hs_blocks)
+                                    hipStream_t stream, int cus, float2* hs, int hs_blocks, const Gen4Put* put)
 {
+  if (put && (!put->dst || (put->stream && put->stream != stream)))
+    return hipErrorInvalidValue;
   return with_logn(logn, [&](auto L) -> hipError_t {
     constexpr int LOGN = decltype(L)::value;
     if constexpr (!HalfCfg<LOGN>::SLAB_SUPPORTED)
@@ -57,21 +59,35 @@ hipError_t launch_half_slab_columns(int logn, const FrameParams& fp, const HalfS
       if (hsl.w % S::T != 0 || !hs)
         return hipErrorInvalidValue;
       const size_t blk = half_slab_block_bytes(LOGN, fp.cascades, hsl);
-      float4* spec = reinterpret_cast<float4*>((unsigned char*)send + half_slab_spec_offset(LOGN, fp.cascades, hsl));
-      hipError_t e = launch_half_nyquist(fp, n, K::B, h0, spec, h0_full ? nullptr : h0row, ranks, blk, nullptr, stream, cus);
+      hipError_t e = hipSuccess;
+      // the one-sided exchange stores into the peers' receive slots: only once they are free
+      if (put && put->start)
+        e = hipEventRecord(put->start, stream);
+      if (e == hipSuccess && put && put->wait)
+        e = launch_peer_wait(*put->wait, stream);
+      if (e != hipSuccess)
+        return e;
+      const int cus2 = put && put->cus > 0 ? put->cus : cus;
+      const size_t spec_off = half_slab_spec_offset(LOGN, fp.cascades, hsl);
+      e = put ? launch_half_nyquist(fp, n, K::B, h0, nullptr, h0_full ? nullptr : h0row, ranks, 0, nullptr, stream, cus2,
+                                    put->dst, spec_off)
+              : launch_half_nyquist(fp, n, K::B, h0, reinterpret_cast<float4*>((unsigned char*)send + spec_off),
+                                    h0_full ? nullptr : h0row, ranks, blk, nullptr, stream, cus);
       if (e != hipSuccess || hsl.nstrips < 1)  // a rank past the last strip only builds the Nyquist-row term
         return e;
       // slab items keep fewer pairs in VGPRs: with four, the SLAB store addressing spills 8-16 B (at
       // N = 8192 already with two; one fits)
       constexpr int HKS = LOGN == 13 ? 1 : kHalfHK - 1;
-      auto kern = k_cols_half<LOGN, kStream, kStream, true, true, false, 1, 1, K::B, true, false, kHalfHL, HKS>;
+      auto kern = put ? k_cols_half<LOGN, kStream, kStream, true, true, false, 1, 1, K::B, true, false, kHalfHL, HKS, 0, 4, true>
+                      : k_cols_half<LOGN, kStream, kStream, true, true, false, 1, 1, K::B, true, false, kHalfHL, HKS>;
       const int lds = ((S::TW_ENTRIES * 8 + 15) / 16) * 16 + K::LDS1 + kHalfHL * K::WG1 * 16;
-      int grid = persistent_grid(kern, K::WG1, lds, fp.cascades * hsl.nstrips, cus);
+      int grid = persistent_grid(kern, K::WG1, lds, fp.cascades * hsl.nstrips, cus2);
       if (grid > hs_blocks)
         grid = hs_blocks;
+      unsigned char* target = put ? reinterpret_cast<unsigned char*>(const_cast<uint64_t*>(put->dst))
+                                  : static_cast<unsigned char*>(send);
       hipLaunchKernelGGL(kern, dim3(grid), dim3(K::WG1), lds, stream, fp, h0, (float4*)nullptr, (float4*)nullptr,
-                         (float2*)nullptr, tw, hs, hsl, (unsigned char*)send, h0_full ? 1 : 0,
-                         (const SpectrumConsts*)nullptr);
+                         (float2*)nullptr, tw, hs, hsl, target, h0_full ? 1 : 0, (const SpectrumConsts*)nullptr);
       return hipGetLastError();
     }
   });

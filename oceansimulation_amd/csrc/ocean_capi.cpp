@@ -874,10 +874,11 @@ static int generator_columns(ocean_generator* g, float timestep, int update_spec
       return fail(e == hipErrorOutOfMemory ? OCEAN_ERR_OOM : OCEAN_ERR_HIP,
                   std::string("column pass buffers: ") + hipGetErrorString(e));
   }
-  if (uses_gen4(g))
+  if (uses_gen4(g) || g->hslab)
   {
-    // the column pass's stream (the put stream of pipelined one-sided frames) runs after the last
-    // column pass on another stream (step 1 rewrites the parts its step 2 read) and after h0 writes
+    // the column pass's stream (the put or step-1 stream of pipelined one-sided frames) runs after the
+    // last column pass on another stream (step 1 rewrites the parts its step 2 read; the strip-dealt
+    // pass reuses its H scratch) and after h0 writes
     hipStream_t cs = col_stream ? col_stream : f->stream;
     hipStream_t after = g->cols_stream && g->cols_stream != cs ? g->cols_stream
                         : cs != f->stream && g->h0_dirty   ? f->stream
@@ -901,12 +902,20 @@ static int generator_columns(ocean_generator* g, float timestep, int update_spec
       pp.b = take_event(g);
       timed_put.start = pp.a;
     }
-    HIP_TRY(timed(g, 1, [&] {
-              return launch_gen4_columns(f->logn, fp, g->g4, g->h0, g->ranks > 1 ? g->h0row : nullptr,
-                                         put && put->parts ? put->parts : g->parts, out ? (void*)out : (void*)g->xbuf,
-                                         f->twiddles, f->tw2, cs, f->cus, put ? &timed_put : nullptr);
-            }, cs),
-            "column pass (half spectrum, four-step)");
+    if (uses_gen4(g))
+      HIP_TRY(timed(g, 1, [&] {
+                return launch_gen4_columns(f->logn, fp, g->g4, g->h0, g->ranks > 1 ? g->h0row : nullptr,
+                                           put && put->parts ? put->parts : g->parts, out ? (void*)out : (void*)g->xbuf,
+                                           f->twiddles, f->tw2, cs, f->cus, put ? &timed_put : nullptr);
+              }, cs),
+              "column pass (half spectrum, four-step)");
+    else
+      HIP_TRY(timed(g, 1, [&] {
+                return launch_half_slab_columns(f->logn, fp, g->hsl, g->ranks, g->h0, g->ranks == 1, g->h0row,
+                                                out ? (void*)out : (void*)g->xbuf, f->twiddles, cs, f->cus, g->hs,
+                                                f->device_cus, put ? &timed_put : nullptr);
+              }, cs),
+              "column pass (half spectrum, strip-dealt)");
     if (pp.a)
     {
       HIP_TRY(hipEventRecord(pp.b, put && put->stream ? put->stream : cs), "column pass: put event");
@@ -914,14 +923,7 @@ static int generator_columns(ocean_generator* g, float timestep, int update_spec
     }
   }
   else if (put)
-    return fail(OCEAN_ERR_INVALID, "column pass: the one-sided exchange needs the four-step path (N = 8192 / 16384)");
-  else if (g->hslab)
-    HIP_TRY(timed(g, 1, [&] {
-              return launch_half_slab_columns(f->logn, fp, g->hsl, g->ranks, g->h0, g->ranks == 1, g->h0row,
-                                              out ? (void*)out : (void*)g->xbuf, f->twiddles, f->stream, f->cus,
-                                              g->hs, f->device_cus);
-            }),
-            "column pass (half spectrum, strip-dealt)");
+    return fail(OCEAN_ERR_INVALID, "column pass: the one-sided exchange needs a half-spectrum slab path (N >= 1024)");
   else if (g->half && g->overlap)
   {
     // frame overlap: this column pass on the side stream into field slot oslot, after the row pass
@@ -1560,9 +1562,9 @@ int check_peers(const ocean_generator* g, const ocean_peers* p, const char* who)
     return fail(OCEAN_ERR_INVALID, std::string(who) + ": null generator, or peers created for another generator");
   if (!p->connected)
     return fail(OCEAN_ERR_INVALID, std::string(who) + ": ocean_peers_connect has not run");
-  if (!uses_gen4(g) || hslab_xbuf_bytes(g) != p->slot)
-    return fail(OCEAN_ERR_INVALID, std::string(who) + ": the generator left the four-step path (or its exchange size "
-                                                      "changed) since ocean_peers_create");
+  if (!g->hslab || hslab_xbuf_bytes(g) != p->slot)
+    return fail(OCEAN_ERR_INVALID, std::string(who) + ": the generator left the half-spectrum slab path (or its "
+                                                      "exchange size changed) since ocean_peers_create");
   return OCEAN_OK;
 }
 
@@ -1603,7 +1605,7 @@ int put_columns(ocean_generator* g, ocean_peers* p, float timestep, int update_s
   const PeerWait w = peer_wait(p, kFreedWord, f - 1);
   Gen4Put put{p->table + s * kMaxRanks, f >= 2 ? &w : nullptr, p->put_cus};
   hipStream_t cs = nullptr;
-  if (pipelined)
+  if (pipelined && uses_gen4(g))
   {
     if (!p->parts2)
       HIP_TRY(hipMalloc(&p->parts2, gen4_parts_bytes(fs->logn, g->cascades, g->g4)), "one-sided exchange: parts slot");
@@ -1614,6 +1616,8 @@ int put_columns(ocean_generator* g, ocean_peers* p, float timestep, int update_s
     if (p->put_done_valid[s])
       HIP_TRY(hipStreamWaitEvent(cs, p->put_done[s], 0), "one-sided exchange: parts slot reuse");
   }
+  else if (pipelined)
+    cs = p->put_stream;  // the strip-dealt pass stores its blocks itself: all of it on the put stream
   else
     for (int k = 0; k < 2; k++)  // a serial frame after pipelined ones: its step 1 rewrites parts slot 0
       if (p->put_done_valid[k])
@@ -1742,8 +1746,8 @@ int ocean_peers_create(ocean_peers** out, ocean_generator* g)
   if (!out || !g)
     return fail(OCEAN_ERR_INVALID, "ocean_peers_create: null argument");
   *out = nullptr;
-  if (!g->slab || !uses_gen4(g))
-    return fail(OCEAN_ERR_INVALID, "ocean_peers_create: a slab generator on the four-step path (N = 8192 / 16384)");
+  if (!g->slab || !g->hslab)
+    return fail(OCEAN_ERR_INVALID, "ocean_peers_create: a slab generator on a half-spectrum path (N >= 1024)");
   if (g->peers)
     return fail(OCEAN_ERR_INVALID, "ocean_peers_create: the generator already has peers");
   hipError_t e = hslab_buffers(g);

@@ -193,9 +193,12 @@ int half_strips(int logn);
 size_t half_slab_block_bytes(int logn, int cascades, const HalfSlab& h);
 size_t half_slab_row_texels(int logn, int cascades, int w);
 hipError_t launch_generate_spectrum_row(const OceanSettings& s, int n, float4* row, hipStream_t stream);
+struct Gen4Put;
+// put (the one-sided exchange): blocks and the Nyquist-row term go to put->dst[q] after put->wait;
+// the whole pass runs on `stream` (put->stream must be null or equal).
 hipError_t launch_half_slab_columns(int logn, const FrameParams& fp, const HalfSlab& hsl, int ranks, const float4* h0,
                                     bool h0_full, const float4* h0row, void* send, const float2* tw,
-                                    hipStream_t stream, int cus, float2* hs, int hs_blocks);
+                                    hipStream_t stream, int cus, float2* hs, int hs_blocks, const Gen4Put* put = nullptr);
 hipError_t launch_half_slab_rows(int logn, const FrameParams& fp, const HalfSlab& hsl, const void* recv, float4* rm_ab,
                                  float4* rm_de, float2* rm_c, float4* maps, float* jac, const FoamParams& foam,
                                  const float2* tw, const float2* tw2, hipStream_t stream, int cus);

@@ -58,11 +58,14 @@ def _same(L, slabs, whole, n):
     return None
 
 
-@pytest.mark.parametrize("n,P", [(8192, 1), (8192, 2), (8192, 8), (16384, 8)])
-def test_put_exchange_in_one_process_bit_exact(ocean, n, P):
+@pytest.mark.parametrize("n,P,four_step", [(8192, 1, True), (8192, 2, True), (8192, 8, True), (16384, 8, True),
+                                           (1024, 4, True), (4096, 8, True), (8192, 4, False)])
+def test_put_exchange_in_one_process_bit_exact(ocean, n, P, four_step):
     """P slab ranks over one grid, joined locally: frames issued as every rank's column pass + put
     then every rank's row pass, then pipelined frames (rank r's frame f column pass on its put stream
-    beside its frame f - 1 row pass), equal the whole grid bit for bit after every check."""
+    beside its frame f - 1 row pass), equal the whole grid bit for bit after every check. 8192 / 16384:
+    the four-step slabs (step 2 puts); 1024 / 4096 and 8192 with the four-step pass off: the strip-dealt
+    slabs (the column pass puts its strips' blocks itself)."""
     from oceansimulation_amd import capi
     from oceansimulation_amd.slab import PeerExchange, SlabGenerator, emulate_put_frame
 
@@ -73,6 +76,10 @@ def test_put_exchange_in_one_process_bit_exact(ocean, n, P):
     slabs = [SlabGenerator(fft, r, P) for r in range(P)]
     for g in slabs:
         ocean.apply_settings(g.GetOceanSettings(), planeSize=777.0)
+    if not four_step:
+        whole.set_four_step(False)
+        for g in slabs:
+            g.set_four_step(False)
     peers = [PeerExchange(g) for g in slabs]
     for p in peers:
         p.set_timeout(10000)
@@ -119,14 +126,16 @@ def _free_port():
 
 
 @pytest.mark.timeout(300)
-def test_put_exchange_two_processes_bit_exact(ocean):
-    """Two slab ranks of one 8192^2 grid as two processes on GPU 0: the receive slots and flag words
-    are mapped across the processes with hipIpcOpenMemHandle (the mapping the 8-GPU node uses over
-    xGMI), serial and pipelined frames, each rank's row slab bit-exact against a whole grid."""
+@pytest.mark.parametrize("n", [8192, 1024])
+def test_put_exchange_two_processes_bit_exact(ocean, n):
+    """Two slab ranks of one grid as two processes on GPU 0 (8192: four-step slabs; 1024: strip-dealt):
+    the receive slots and flag words are mapped across the processes with hipIpcOpenMemHandle (the
+    mapping the 8-GPU node uses over xGMI), serial and pipelined frames, each rank's row slab bit-exact
+    against a whole grid."""
     port = _free_port()
     env = dict(os.environ, PYTHONUNBUFFERED="1")
     procs = [subprocess.Popen([sys.executable, os.path.join(ROOT, "tests", "peer_rank.py"), str(r), "2", str(port),
-                               "8192"], stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, env=env)
+                               str(n)], stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, env=env)
              for r in range(2)]
     results = []
     for p in procs:

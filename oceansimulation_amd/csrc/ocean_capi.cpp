@@ -971,7 +971,7 @@ static FoamParams current_foam(const ocean_generator* g)
 
 // Second half: the x direction of both EncodeIFFTs + computeFoam (src/Generator.cpp:71-80). `frame_foam`:
 // the displacement of a pipelined slab frame's own settings (null: the current settings).
-// row_stream (four-step path only; null: the generator's stream): the pipelined one-sided frame's rows.
+// row_stream (half-spectrum slab paths; null: the generator's stream): the pipelined one-sided frame's rows.
 static int generator_rows(ocean_generator* g, const float4* in, const FoamParams* frame_foam = nullptr,
                           hipStream_t row_stream = nullptr)
 {
@@ -987,12 +987,17 @@ static int generator_rows(ocean_generator* g, const float4* in, const FoamParams
             "row pass (half spectrum, four-step)");
   }
   else if (g->hslab)
+  {
+    hipStream_t rs = row_stream ? row_stream : f->stream;
     HIP_TRY(timed(g, 2, [&] {
               return launch_half_slab_rows(f->logn, g->frame, g->hsl, in ? (const void*)in : (const void*)g->xbuf,
                                            g->rm_ab, g->rm_de, g->rm_c, g->maps, g->jac, foam, f->twiddles,
-                                           f->tw2, f->stream, f->cus);
-            }),
+                                           f->tw2, rs, f->cus);
+            }, rs),
             "row pass (half spectrum, strip-dealt)");
+  }
+  else if (row_stream)
+    return fail(OCEAN_ERR_INVALID, "row pass: a row stream needs a half-spectrum slab path");
   else if (g->half && g->overlap)
   {
     const int s = g->oslot;

@@ -85,6 +85,9 @@ def parse(argv=None):
     ap.add_argument("--headline-only", action="store_true",
                     help="the headline loop alone (every optional leg off): what tools/profile_gpu.sh profiles, "
                          "so each kernel's launches all cover the headline workload")
+    ap.add_argument("--no-verify", action="store_true",
+                    help="skip the headline's bit-exact check against one-cascade generators (implied by "
+                         "--headline-only, whose rocprofv3 traces must hold the headline's launches only)")
     ap.add_argument("--legs-timeout", type=float, default=300.0,
                     help="seconds allowed for the optional legs after the headline measurement; past it the "
                          "line is printed without the unfinished legs and every rank exits")
@@ -119,6 +122,7 @@ def parse(argv=None):
     args = ap.parse_args(argv)
     if args.headline_only:
         args.no_reseed = args.no_ifft = args.no_slab = args.no_surface = args.no_cpu_baseline = True
+        args.no_verify = True
     return args
 
 
@@ -1468,11 +1472,14 @@ def main(argv=None):
     el_max = max_over_ranks(el, world)
     ms, cnt = gen.kernel_times()
     # the headline checks its own maps (before the re-seed legs change how h0 is evaluated)
-    try:
-        headline_check = verify_cascades(ocean, fft, gen, mine)
-    except Exception as e:  # reported as a failed check
-        headline_check = {"verified": False, "error": f"{type(e).__name__}: {e}"}
-    headline_check["verified"] = ranks_agree(headline_check["verified"], world)
+    if args.no_verify:
+        headline_check = {"verified": None, "skipped": "--no-verify / --headline-only (profiling runs)"}
+    else:
+        try:
+            headline_check = verify_cascades(ocean, fft, gen, mine)
+        except Exception as e:  # reported as a failed check
+            headline_check = {"verified": False, "error": f"{type(e).__name__}: {e}"}
+        headline_check["verified"] = ranks_agree(headline_check["verified"], world)
 
     # The reference application's own loop re-seeds h0 on every frame (src/Waves.cpp:91-94, where
     # `updateSpectrum = false` is commented out): CalculateOcean(dt, true). Timed as its own leg.
@@ -1655,7 +1662,7 @@ def main(argv=None):
     if not watchdog.finish():
         return LEGS_TIMEOUT_RC  # the watchdog printed the line and is ending the process
     # a leg whose maps did not match its check fails the run (after the line is printed)
-    mismatch = not out["verified"]["verified"] or \
+    mismatch = out["verified"]["verified"] is False or \
         (isinstance(out.get("slab"), dict) and out["slab"].get("verified_all") is False) or \
         (isinstance(out.get("weak_scaling"), dict) and out["weak_scaling"].get("verified", {}).get("verified") is False)
     if rank == 0:

@@ -4,6 +4,7 @@
 #   KERNEL_REGEX  kernels to count (default: the frame passes)
 #   BENCH_ARGS    bench.py arguments
 #   PREFIX        output prefix (default pmc_sq)
+#   CMD           program + arguments to profile instead of bench.py (e.g. a microbench binary)
 # Output: gpurun_out/<prefix>_<k>/ (csv); summarise with tools/sq_summary.py.
 set -u
 cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
@@ -19,7 +20,7 @@ mkdir -p gpurun_out
 k=0
 for s in "${SETS[@]}"; do
   timeout -s KILL 150 rocprofv3 --pmc $s --kernel-include-regex "$KRE" -d gpurun_out/${P}_$k -o sq \
-    --output-format csv -- python3 bench.py $ARGS > gpurun_out/${P}_$k.log 2>&1 || { echo "pass $k failed rc=$?"; tail -5 gpurun_out/${P}_$k.log; exit 1; }
+    --output-format csv -- ${CMD:-python3 bench.py $ARGS} > gpurun_out/${P}_$k.log 2>&1 || { echo "pass $k failed rc=$?"; tail -5 gpurun_out/${P}_$k.log; exit 1; }
   echo "pass $k ok"
   k=$((k + 1))
 done

@@ -90,9 +90,13 @@ __device__ __forceinline__ void sincos_phase(float x, float* s, float* c)
 __device__ __forceinline__ float2 evolve(float4 a, float k, const CascadeFrame& f)
 {
 #pragma clang fp contract(off)  // rounds identically wherever it is inlined (rolled or unrolled loops)
+#ifdef OCEAN_ABLATE_EVOLVE  // timing ablation (tools/microbench): no dispersion / sin / cos, wrong results
+  float ws = k * f.time, wc = k;
+#else
   float phase = dispersion_evolve(k, f.g, f.h) * f.time;
   float ws, wc;
   sincos_phase(phase, &ws, &wc);
+#endif
   float ampx = a.x * wc - a.y * ws;
   float ampy = a.x * ws + a.y * wc;
   float ws2 = -ws;

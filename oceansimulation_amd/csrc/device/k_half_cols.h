@@ -143,9 +143,13 @@ __device__ __forceinline__ void fft_cols_hx(CPair* v, int t, void* lds, const fl
 // PUT (SLAB only; the one-sided exchange, ocean_peers): `send` is then the device table of the ranks'
 // destinations, ((const uint64_t*)send)[q] = this rank's block in rank q's receive slot, and block q
 // is stored there instead of at send + q * block bytes.
+// HB (half strips, whole grids): h0's strip width. HB = CPI = 2: h0 is blocked in 2-column strips, so a
+// half-strip item reads its own contiguous strip instead of the 32-B halves of 64-B row pieces that
+// its partner item reads the other halves of (launch_half_columns at <= 2 cascades: 0.122 -> 0.114 ms
+// per 4096^2 cascade, 0.935 -> 0.792 ms per 8, halfbench fb2h).
 template <int LOGN, int LA = 0, int SA = kStream, bool HS = false, bool SLAB = false, bool SEED = false, int RG = 1,
           int RGC = 1, int CPI = ColFirstCfg<LOGN>::B, bool HP = false, bool PC = false, int HL = 0, int HK = 0,
-          int HX = 0, int FB = 4, bool PUT = false>
+          int HX = 0, int FB = 4, bool PUT = false, int HB = ColFirstCfg<LOGN>::B>
 __global__ __launch_bounds__(FftShape<LOGN>::T * CPI, CPI < ColFirstCfg<LOGN>::B ? 4 : 1) void k_cols_half(FrameParams fp, const float4* __restrict__ h0,
                                                                      float4* __restrict__ gab, float4* __restrict__ gde,
                                                                      float2* __restrict__ gc,
@@ -166,6 +170,7 @@ __global__ __launch_bounds__(FftShape<LOGN>::T * CPI, CPI < ColFirstCfg<LOGN>::B
   constexpr int MSTEP = HX == 2 ? 16 : T;  // storage rows between v[m] and v[m + 1]
   static_assert(FB == 4 || (FB == CPI && HALVES == 2 && !SLAB && RG > 1 && RGC > 1 && !HX), "FB: half-strip fields");
   static_assert(!PUT || (SLAB && !PC), "PUT: the strip-dealt slab stores");
+  static_assert(HB == B || (HB == CPI && HALVES == 2 && !SLAB), "HB: half strips over 2-column h0 strips");
   constexpr int XB = CPI * S::PADDED * 8;  // the exchange's bytes (K::LDS1 for whole strips)
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   float2* tw = reinterpret_cast<float2*>(smem);
@@ -186,8 +191,9 @@ __global__ __launch_bounds__(FftShape<LOGN>::T * CPI, CPI < ColFirstCfg<LOGN>::B
     const int b = opaque((int)threadIdx.x) % CPI + hh * CPI;  // column within the strip
     const int xb = sg == STRIPS - 1 ? 0 : N / (2 * B) + sg;
     const CascadeFrame f = fp.c[c];
-    const float4* src = (!SLAB || h0_full) ? h0 + ((size_t)c * (N / B) + xb) * N * B
-                                           : h0 + ((size_t)c * nstrips + s) * N * B;
+    const float4* src = HB != B                  ? h0 + ((size_t)c * (N / HB) + xb * (B / HB) + hh) * N * HB
+                        : (!SLAB || h0_full) ? h0 + ((size_t)c * (N / B) + xb) * N * B
+                                             : h0 + ((size_t)c * nstrips + s) * N * B;
     // the strip's first texel in the cascade's fields (whole grids); + half_group_offset(m T, 0) per m
     const int fs = FB == 4 ? s : 2 * s + hh;  // field strip
     const size_t gbase = RG == 1 ? ((size_t)c * STRIPS + s) * N * B
@@ -264,9 +270,16 @@ __global__ __launch_bounds__(FftShape<LOGN>::T * CPI, CPI < ColFirstCfg<LOGN>::B
         const int hoff = opaque((int)threadIdx.x) * 8;
         float4 a[16];
         float2 hprev = make_float2(0.0f, 0.0f);
+#ifdef OCEAN_ABLATE_H0LOAD  // timing ablation (tools/microbench): every item reads cascade 0's strip 0 (L2-resident)
+        const float4* srcl = h0;
+#else
+        const float4* srcl = src;
+#endif
+        // HB = 2: the half strip's own 2-column h0 strip (contiguous 32-B row pieces)
+        const int loff = HB == B ? voff : (i * HB + (b - hh * CPI)) * 16;
 #pragma unroll
         for (int m = 0; m < 16; m++)  // fftShift on y folded into the load
-          a[m] = ld4s<LA>(src, voff, ((m + 8) & 15) * T * B * 16);
+          a[m] = ld4s<LA>(srcl, loff, ((m + 8) & 15) * T * HB * 16);
 #pragma unroll
         for (int m = 0; m < 16; m++)
         {
@@ -337,6 +350,11 @@ __global__ __launch_bounds__(FftShape<LOGN>::T * CPI, CPI < ColFirstCfg<LOGN>::B
 #pragma unroll
       for (int m = 0; m < 16; m++)
       {
+#ifdef OCEAN_ABLATE_FSTORE  // timing ablation (tools/microbench): the field stores skipped, values kept live
+        asm volatile("" ::"v"(v[m].re), "v"(v[m].im));
+        if (m >= 0)
+          continue;
+#endif
         if constexpr (SLAB)
         {
           // row y = m T + io lies in block q = m T / w (w is a multiple of T), at yl = m T % w + io

@@ -75,6 +75,7 @@ inline int half_rows_variant = 1;
 inline int half_fields_fb(int logn, int cascades) { return logn == 12 && cascades <= 2 ? 2 : 4; }
 constexpr int kHalfRG2 = 4, kHalfRGC2 = 8;  // the FB = 2 layout's row groups
 
+
 inline bool one_shot_grids(int cus)
 {
   const int d = device_cu_count();

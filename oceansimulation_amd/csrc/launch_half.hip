@@ -20,6 +20,8 @@ namespace oceanfft
 
 bool half_spectrum_supported(int logn) { return logn >= 10 && logn <= 12; }
 
+int half_h0_block(int logn, int cascades) { return half_fields_fb(logn, cascades) == 2 ? 2 : spectrum_block(logn); }
+
 size_t half_field_texels(int logn)
 {
   const size_t n = (size_t)1 << logn;
@@ -33,7 +35,7 @@ size_t half_hs_bytes(int logn, int blocks)
 
 hipError_t launch_half_columns(int logn, const FrameParams& fp, const float4* h0, float4* gab, float4* gcd, float2* ge,
                                float4* spec, const float2* tw, hipStream_t stream, int cus, float2* hs, int hs_blocks,
-                               const void* seed_consts)
+                               const void* seed_consts, int h0_blk)
 {
   if (!hs)  // the H scratch (half_hs_bytes): H evolved once per item instead of once per field round
     return hipErrorInvalidValue;
@@ -46,8 +48,11 @@ hipError_t launch_half_columns(int logn, const FrameParams& fp, const float4* h0
     {
       using K = ColFirstCfg<LOGN>;
       using S = FftShape<LOGN>;
+      const int hb = h0_blk > 0 ? h0_blk : K::B;
+      if (hb != K::B && (hb != 2 || half_fields_fb(LOGN, fp.cascades) != 2))
+        return hipErrorInvalidValue;  // 2-column h0 strips are read by the half-strip pass only
       // the Nyquist-row term: one row spectrum per image
-      hipError_t e = launch_half_nyquist(fp, S::N, K::B, h0, spec, nullptr, 1, 0, seed, stream, cus);
+      hipError_t e = launch_half_nyquist(fp, S::N, hb, h0, spec, nullptr, 1, 0, seed, stream, cus);
       if (e != hipSuccess)
         return e;
       // Field layout: row groups (kHalfRG, kHalfRGC). The H scratch in 16-B pairs (HP), one pair per
@@ -62,11 +67,15 @@ hipError_t launch_half_columns(int logn, const FrameParams& fp, const float4* h0
         if (half_fields_fb(LOGN, fp.cascades) == 2)
         {
           // half strips (FB = 2): 512-thread workgroups, two per CU (a 68-KiB exchange each)
+          // h0 in 2-column strips (hb = 2, half_h0_block): each item streams its own strip
           constexpr int WGH = S::T * 2;
           auto kern = seed ? k_cols_half<LOGN, 0, kStream, true, false, true, kHalfRG2, kHalfRGC2, 2, true, false, kHalfHL,
                                          kHalfHKSeed, 0, 2>
                            : k_cols_half<LOGN, kStream, kStream, true, false, false, kHalfRG2, kHalfRGC2, 2, true, false,
                                          kHalfHL, kHalfHK, 0, 2>;
+          if (!seed && hb == 2)
+            kern = k_cols_half<LOGN, kStream, kStream, true, false, false, kHalfRG2, kHalfRGC2, 2, true, false, kHalfHL,
+                               kHalfHK, 0, 2, false, 2>;
           const int lds = ((S::TW_ENTRIES * 8 + 15) / 16) * 16 + 2 * S::PADDED * 8 + kHalfHL * WGH * 16;
           int grid = persistent_grid(kern, WGH, lds, fp.cascades * HalfCfg<LOGN>::STRIPS * 2, cus);
           const int slices = hs_blocks * (1024 / WGH);

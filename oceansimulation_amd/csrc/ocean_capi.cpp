@@ -457,10 +457,15 @@ static bool uses_gen4(const ocean_generator* g)
   return g->four_step && g->hslab && gen4_supported(g->fft->logn);
 }
 
-// strip width of the h0 image the current frame path reads
+// strip width of the h0 image the current frame path reads (the whole-grid half path at <= 2
+// cascades of 4096: 2-column strips, one per half-strip item, launch_common.h half_h0_block)
 static int h0_block(const ocean_generator* g)
 {
-  return uses_gen4(g) ? gen4_h0_block() : spectrum_block(g->fft->logn);
+  if (uses_gen4(g))
+    return gen4_h0_block();
+  if (g->half && g->ranks == 1)
+    return half_h0_block(g->fft->logn, g->cascades);
+  return spectrum_block(g->fft->logn);
 }
 
 // h0 texels per cascade: the whole grid (ranks == 1), or the largest of a slab's layouts (its column
@@ -940,7 +945,7 @@ static int generator_columns(ocean_generator* g, float timestep, int update_spec
     HIP_TRY(timed(g, 1, [&] {
               return launch_half_columns(f->logn, fp, g->h0, s ? g->gab2 : g->gab, s ? g->gcd2 : g->gcd,
                                          s ? g->ge2 : g->ge, s ? g->spec2 : g->spec, f->twiddles, g->side, f->cus,
-                                         g->hs, f->device_cus, seed);
+                                         g->hs, f->device_cus, seed, g->h0_block);
             }, g->side),
             "column pass (half spectrum, overlapped)");
     HIP_TRY(hipEventRecord(g->ocols[s], g->side), "overlap: column event");
@@ -948,7 +953,7 @@ static int generator_columns(ocean_generator* g, float timestep, int update_spec
   else if (g->half)
     HIP_TRY(timed(g, 1, [&] {
               return launch_half_columns(f->logn, fp, g->h0, g->gab, g->gcd, g->ge, g->spec, f->twiddles, f->stream,
-                                         f->cus, g->hs, f->device_cus, seed);
+                                         f->cus, g->hs, f->device_cus, seed, g->h0_block);
             }),
             "column pass (half spectrum)");
   else

@@ -149,9 +149,14 @@ size_t half_field_texels(int logn);
 size_t half_hs_bytes(int logn, int blocks);  // also the strip-dealt path's
 // seed_consts (optional, device array of one seed_consts_bytes() record per cascade, needs hs): the
 // fused re-seed frame — pass 1 evaluates h0 itself and neither reads nor writes the h0 image.
+// h0's strip width for the whole-grid half path: the half-strip pass (4096, <= 2 cascades) reads
+// 2-column h0 strips (k_cols_half HB), the whole-strip pass the 4-column ones (spectrum_block)
+int half_h0_block(int logn, int cascades);
+// h0_blk: the strip width h0 is blocked in (0: spectrum_block; 2 only where the pass runs on half
+// strips, launch_common.h half_h0_block)
 hipError_t launch_half_columns(int logn, const FrameParams& fp, const float4* h0, float4* gab, float4* gcd, float2* ge,
                                float4* spec, const float2* tw, hipStream_t stream, int cus, float2* hs, int hs_blocks,
-                               const void* seed_consts = nullptr);
+                               const void* seed_consts = nullptr, int h0_blk = 0);
 // generateSpectrum's settings-only constants (host, the oracle's fp32 expressions), as a device record
 size_t seed_consts_bytes();
 void seed_consts(const OceanSettings& s, int n, void* out);

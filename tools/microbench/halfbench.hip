@@ -678,6 +678,17 @@ int main(int argc, char** argv)
     std::printf("re-seed cols, production              median %7.3f ms  bit-identical %s\n", t[1][4], same ? "yes" : "NO");
     return 0;
   }
+  if (argc > 3 && std::strcmp(argv[3], "abl") == 0)
+  {
+    // the production pass 1 alone (built with -DOCEAN_ABLATE_H0LOAD / -DOCEAN_ABLATE_FSTORE: timing
+    // ablations, wrong fields); median of 9 x 10 launches
+    std::vector<float> t;
+    for (int r = 0; r < 9; r++)
+      t.push_back(time_ms(c1, 10));
+    std::sort(t.begin(), t.end());
+    std::printf("cols production pass 1 median %7.3f ms (min %7.3f)\n", t[4], t[0]);
+    return 0;
+  }
   if (argc > 3 && std::strcmp(argv[3], "hkeep") == 0)
   {
     // pass 1 with some H pairs outside the scratch (variants 25..31: HL pairs in LDS, HK in VGPRs)

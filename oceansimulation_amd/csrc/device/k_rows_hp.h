@@ -50,7 +50,12 @@ __device__ __forceinline__ int hp_slot(int n1, int j) { return n1 * HpCfg::RS + 
 // YP: the fields hold row y at storage row hx_store_row(y) (k_cols_half HX 2); items run over storage
 // rows, so the 4 rows of a gc line stay on one XCD. FB: field strips of FB columns (k_cols_half FB);
 // GRP: consecutive rows per XCD group (the rows of a gc line).
-template <int RG, int RGC, bool RM = false, bool YP = false, int FB = 4, int GRP = 4>
+// EARLY (round 5, as k_rows_xs EARLY): a wave retires its memory instructions in issue order, so loads
+// issued after an image's 16 map stores wait for those stores. 1: image 1's (D, E) loads are issued
+// before image 0's stores (32 VGPRs from the end of image 0's transform to image 1's T_in); 2: and
+// the next row's (A, B) and C before image 1's stores (the first row's in a prologue; persistent
+// grids); whole grids only.
+template <int RG, int RGC, bool RM = false, bool YP = false, int FB = 4, int GRP = 4, int EARLY = 0>
 __global__ __launch_bounds__(256, 4) void k_rows_hp(FrameParams fp, const float4* __restrict__ gab,
                                                  const float4* __restrict__ gde, const float2* __restrict__ gc,
                                                  const float4* __restrict__ spec, float4* __restrict__ maps,
@@ -74,7 +79,27 @@ __global__ __launch_bounds__(256, 4) void k_rows_hp(FrameParams fp, const float4
   constexpr int LA = RM ? kStream : 0;
   const int lcpr = RM ? 31 - __builtin_clz(rs.cpr) : 0, cmask = RM ? rs.cpr - 1 : 0;
   const int wave0 = __builtin_amdgcn_readfirstlane((int)threadIdx.x & ~63);
-  for (int item = RM ? (int)blockIdx.x : xcd_group_slot<GRP>(blockIdx.x, gridDim.x); item < total; item += gridDim.x)
+  static_assert(!EARLY || !RM, "EARLY: whole-grid layouts");
+  float4 fpre[EARLY > 0 ? 8 : 1];  // EARLY: the next image's field texels, issued before the stores
+  float2 cpre[EARLY >= 2 ? 8 : 1];  // EARLY 2: the next row's C
+  // the field texels of image img of row item (whole grids), into f (and C into cdst)
+  auto issue = [&](int item, int img, float4* f, float2* cdst) __attribute__((always_inline)) {
+    const int c = item / nrows, yf = item - c * nrows;
+    const size_t base = (size_t)c * STRIPS * N * B;
+    const int i = opaque((int)threadIdx.x);
+#pragma unroll
+    for (int m = 0; m < 8; m++)
+    {
+      const int u = m * T + i;
+      f[m] = ld4<LA>((img == 0 ? gab : gde) + base, half_group_offset<LOGN, RG, FB>(yf, u / FB, u % FB) * 16);
+      if (cdst)
+        cdst[m] = ld2<0>(gc + base, half_group_offset<LOGN, RGC, FB>(yf, u / FB, u % FB) * 8);
+    }
+  };
+  const int item0 = RM ? (int)blockIdx.x : xcd_group_slot<GRP>(blockIdx.x, gridDim.x);
+  if (EARLY >= 2 && item0 < total)
+    issue(item0, 0, fpre, cpre);
+  for (int item = item0; item < total; item += gridDim.x)
   {
     const int c = item / nrows, yf = item - c * nrows;  // RM: yf is the local row (slabs start at an even row)
     const int y = YP ? hx_row_of_store(yf) : yf;       // the output row; yf addresses the fields
@@ -104,8 +129,8 @@ __global__ __launch_bounds__(256, 4) void k_rows_hp(FrameParams fp, const float4
         const float4 s4 = ld4<0>(sp, (N / 2 - u) * 16);
         if (img == 0)
         {
-          const CPair p = raw_pair(ld4<LA>(fab + base, off * 16));
-          const float2 cc = ld2<0>(fc + base, offc * 8);
+          const CPair p = raw_pair(EARLY >= 2 ? fpre[m] : ld4<LA>(fab + base, off * 16));
+          const float2 cc = EARLY >= 2 ? cpre[m] : ld2<0>(fc + base, offc * 8);
           if constexpr (!RM)
             ckeep[m] = cc;
           const float Ar = p.re.x, Ai = p.im.x, Br = p.re.y, Bi = p.im.y, Cr = cc.x, Ci = cc.y;
@@ -115,7 +140,7 @@ __global__ __launch_bounds__(256, 4) void k_rows_hp(FrameParams fp, const float4
         }
         else
         {
-          const CPair q = raw_pair(ld4<LA>(fde + base, off * 16));
+          const CPair q = raw_pair(EARLY > 0 ? fpre[m] : ld4<LA>(fde + base, off * 16));
           // RM: C again (its second read, a few microseconds after the first, comes from L2): keeping
           // it beside the source-block addressing spills
           float2 cc;
@@ -206,6 +231,18 @@ __global__ __launch_bounds__(256, 4) void k_rows_hp(FrameParams fp, const float4
           set_half(v[n1], h, xs[n1 * RS + (tid ^ hp_swz(n1))]);
       }
       idft16(v);  // v[k1] = X(tid + T k1)
+      if constexpr (EARLY > 0)
+      {
+        if (img == 0)
+          issue(item, 1, fpre, nullptr);
+        else if constexpr (EARLY >= 2)
+        {
+          // unconditional (the last row re-reads its own image 0) so that the consumed registers are
+          // not kept as the loop's other incoming value
+          const int nx = item + (int)gridDim.x < total ? item + (int)gridDim.x : item;
+          issue(nx, 0, fpre, cpre);
+        }
+      }
       float4* dst = maps + ((size_t)cimg * nrows + y) * N;
 #pragma unroll
       for (int m = 0; m < 16; m++)

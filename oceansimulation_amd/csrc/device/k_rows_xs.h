@@ -29,7 +29,17 @@ namespace oceanfft
 // phases. Registers: the 16 CPairs (64 VGPRs) and the prefetch (32); C (8 B per kept texel) is
 // loaded where each image uses it (the second read of a row's C, ~20 us after the first, is served by
 // L2): keeping it (16 VGPRs) beside the prefetch spills.
-template <int LOGN, int PF>
+// EARLY (round 5): the next image's loads are issued before the current image's map stores instead
+// of after them. A wave's vmcnt retires its memory instructions in issue order, so a load issued after
+// 16 stores cannot be consumed before those stores are acknowledged: issued first, the next image's
+// fields return while the current image's 256 KiB of stores drain. EARLY 1: image 1's 8 - PF field
+// loads not already prefetched; 2: and its 8 C loads (held in 16 VGPRs until image 1's T_in); 3 (PF 0,
+// persistent grids): also the next row's image-0 fields and C before image 1's stores, the first
+// row's in a prologue. rm16bench (profiles/r05_rm16bench_early.log, one box): PF 2 (round 4) 3.586 ms,
+// EARLY 1 3.467 (PF 2) / 3.596 (PF 0), EARLY 2 3.336 / 3.330, maps bit-identical. Measured and not kept:
+// also image 1's spec texels or its Nyquist texel before the stores (50-110 VGPRs spilled, 4.3-4.9
+// ms); without image 1's spec loads at all (a timing ablation) EARLY 2 gains only 1 % more.
+template <int LOGN, int PF, int EARLY = 0>
 __global__ __launch_bounds__(1024) void k_rows_xs(FrameParams fp, const float4* __restrict__ spec, float4* __restrict__ maps,
                                                    float* __restrict__ jac, FoamParams foam,
                                                    const float2* __restrict__ tw_glob, int rows, RowSrc rs,
@@ -56,7 +66,20 @@ __global__ __launch_bounds__(1024) void k_rows_xs(FrameParams fp, const float4* 
   // the wave plus a lane offset.
   const int lcpr = 31 - __builtin_clz(rs.cpr), cmask = rs.cpr - 1;
   const int wave0 = __builtin_amdgcn_readfirstlane((int)threadIdx.x & ~63);
+  static_assert(EARLY < 3 || PF == 0, "EARLY 3 carries the fields itself");
   float4 fp4[8], nx4[8];
+  float2 ccn[EARLY >= 2 ? 8 : 1];  // EARLY 2+: the next image's C, loaded before the current image's stores
+  auto issue_c = [&](int item, float2* cp) __attribute__((always_inline)) {
+    const int c = item / rows, yl = item - c * rows;
+    const size_t base = ((size_t)c * rows + yl) * rs.lp;
+    const int i = opaque((int)threadIdx.x);
+#pragma unroll
+    for (int m = 0; m < 8; m++)
+    {
+      const int src = (m * T + sopaque(wave0)) >> lcpr;
+      cp[m] = ld2<0>(reinterpret_cast<const float2*>(rs.c + (size_t)src * rs.src_stride) + base, ((m * T + i) & cmask) * 8);
+    }
+  };
   auto issue = [&](int item, int img, float4* p4, int m0, int m1) __attribute__((always_inline)) {
     const int c = item / rows, yl = item - c * rows;
     const size_t base = ((size_t)c * rows + yl) * rs.lp;
@@ -73,6 +96,11 @@ __global__ __launch_bounds__(1024) void k_rows_xs(FrameParams fp, const float4* 
   int item = blockIdx.x;
   if (PF > 0 && item < total)
     issue(item, 0, fp4, 0, PF);
+  if (EARLY >= 3 && item < total)
+  {
+    issue(item, 0, fp4, 0, 8);
+    issue_c(item, ccn);
+  }
   for (; item < total; item += gridDim.x)
   {
     const int c = item / rows, yl = item - c * rows;
@@ -85,7 +113,8 @@ __global__ __launch_bounds__(1024) void k_rows_xs(FrameParams fp, const float4* 
       const int cimg = c * 2 + img;
       const int tid = opaque((int)threadIdx.x), i = tid;
       const float4* sp = spec + (size_t)cimg * N;
-      issue(item, img, fp4, PF, 8);
+      if (!(EARLY && img == 1) && EARLY < 3)  // EARLY: issued before the previous image's stores
+        issue(item, img, fp4, PF, 8);
       auto pslot = [&](int n) { return (n & 15) * RS + (n >> 4); };
       // thread 0: the Nyquist column (u = -N/2) takes the -u lane of u = 0 (T_in slot N/2)
       CPair nyq{};
@@ -121,8 +150,10 @@ __global__ __launch_bounds__(1024) void k_rows_xs(FrameParams fp, const float4* 
         const float kx = (float)u * dk;
         const float4 s4 = ld4<0>(sp, (N / 2 - u) * 16);
         const int src = (m * T + sopaque(wave0)) >> lcpr;
-        const float2 cc = ld2<0>(reinterpret_cast<const float2*>(rs.c + (size_t)src * rs.src_stride) + base,
-                                 (u & cmask) * 8);
+        const float2 cc = (EARLY >= 2 && img == 1) || EARLY >= 3
+                              ? ccn[m]
+                              : ld2<0>(reinterpret_cast<const float2*>(rs.c + (size_t)src * rs.src_stride) + base,
+                                       (u & cmask) * 8);
         CPair own, neg;
         if (img == 0)
         {
@@ -196,6 +227,23 @@ __global__ __launch_bounds__(1024) void k_rows_xs(FrameParams fp, const float4* 
           set_half(v[n1], h, xs[n1 * RS + tid]);
       }
       idft16(v);
+      if constexpr (EARLY > 0)
+      {
+        if (img == 0)
+        {
+          issue(item, 1, fp4, EARLY >= 3 ? 0 : PF, 8);  // fp4 is free: image 0's fields were consumed by T_in
+          if constexpr (EARLY >= 2)
+            issue_c(item, ccn);
+        }
+        else if constexpr (EARLY >= 3)
+        {
+          // unconditional (the last row re-reads its own image 0: a conditional load would keep the
+          // consumed fp4 / ccn live through image 1's transform as the loop's other incoming value)
+          const int nx = item + (int)gridDim.x < total ? item + (int)gridDim.x : item;
+          issue(nx, 0, fp4, 0, 8);
+          issue_c(nx, ccn);
+        }
+      }
       float4* dst = maps + ((size_t)cimg * rows + yl) * N;
 #pragma unroll
       for (int m = 0; m < 16; m++)

@@ -90,7 +90,7 @@ struct LaunchCacheEntry
 };
 
 template <typename K>
-int persistent_grid(K kernel, int wg, int lds, int items, int cus)
+int blocks_per_cu(K kernel, int wg, int lds)
 {
   static std::mutex mu;
   static std::vector<LaunchCacheEntry> cache;
@@ -109,12 +109,30 @@ int persistent_grid(K kernel, int wg, int lds, int items, int cus)
       cache.push_back({(const void*)kernel, lds, per_cu});
     }
   }
-  if (one_shot_grids(cus))
-    return items < 1 ? 1 : items;
-  long g = (long)per_cu * cus;
+  return per_cu;
+}
+
+// Resident workgroups for `cus` CUs (at most `items`): the grid of a kernel that software-pipelines
+// across the items of one workgroup (k_rows_xs EARLY 3 issues the next row's loads before the current
+// row's stores), whatever one_shot_grids says.
+template <typename K>
+int resident_grid(K kernel, int wg, int lds, int items, int cus)
+{
+  long g = (long)blocks_per_cu(kernel, wg, lds) * cus;
   if (g > items)
     g = items;
   return g < 1 ? 1 : (int)g;
+}
+
+template <typename K>
+int persistent_grid(K kernel, int wg, int lds, int items, int cus)
+{
+  if (one_shot_grids(cus))
+  {
+    (void)blocks_per_cu(kernel, wg, lds);  // sets the LDS attribute once
+    return items < 1 ? 1 : items;
+  }
+  return resident_grid(kernel, wg, lds, items, cus);
 }
 
 }  // namespace oceanfft

@@ -678,6 +678,54 @@ int main(int argc, char** argv)
     std::printf("re-seed cols, production              median %7.3f ms  bit-identical %s\n", t[1][4], same ? "yes" : "NO");
     return 0;
   }
+  if (argc > 3 && std::strcmp(argv[3], "hpe") == 0 && logn == 12)
+  {
+    // k_rows_hp with the next image's / row's loads issued before the stores (EARLY 1, 2) against
+    // production on the production fields: maps bit-identical, medians of 9 x 10 launches
+    CHECK(c1());
+    CHECK(hipDeviceSynchronize());
+    auto rows = [&](auto kern) {
+      return std::function<hipError_t()>([=] {
+        const int grid = persistent_grid(kern, 256, HpCfg::LDS, fp.cascades * n, cus);
+        hipLaunchKernelGGL(kern, dim3(grid), dim3(256), HpCfg::LDS, 0, fp, gab, gcd, ge, spec, maps, jac, foam, tw, 0,
+                           RowSrc{});
+        return hipGetLastError();
+      });
+    };
+    std::vector<std::function<hipError_t()>> vr = {rows(k_rows_hp<kHalfRG, kHalfRGC>),
+                                                   rows(k_rows_hp<kHalfRG, kHalfRGC, false, false, 4, 4, 1>),
+                                                   rows(k_rows_hp<kHalfRG, kHalfRGC, false, false, 4, 4, 2>)};
+    const char* nm[] = {"k_rows_hp (production)", "k_rows_hp EARLY 1", "k_rows_hp EARLY 2"};
+    const int NV = 3;
+    CHECK(vr[0]());
+    CHECK(hipDeviceSynchronize());
+    auto pm = snap(maps, mb), pj = snap(jac, jb);
+    std::vector<int> same(NV, 1);
+    for (int k = 1; k < NV; k++)
+    {
+      CHECK(hipMemset(maps, 0, mb));
+      CHECK(hipMemset(jac, 0, jb));
+      CHECK(vr[k]());
+      CHECK(hipDeviceSynchronize());
+      std::printf("%s vs production: maps, jacobian\n", nm[k]);
+      same[k] = (int)diff(snap(maps, mb), pm) & (int)diff(snap(jac, jb), pj);
+    }
+    std::vector<std::vector<float>> t(NV), tf(NV);
+    for (int r = 0; r < 9; r++)
+      for (int k = 0; k < NV; k++)
+      {
+        t[k].push_back(time_ms(vr[k], 10));
+        tf[k].push_back(time_ms([&] { CHECK(c1()); return vr[k](); }, 10));
+      }
+    for (int k = 0; k < NV; k++)
+    {
+      std::sort(t[k].begin(), t[k].end());
+      std::sort(tf[k].begin(), tf[k].end());
+      std::printf("%-24s rows median %7.3f ms (%7.1f GB/s at 56 B/pt)  frame %7.3f ms  bit-identical %s\n", nm[k], t[k][4],
+                  56.04 * pts / t[k][4] / 1e6, tf[k][4], same[k] ? "yes" : "NO");
+    }
+    return 0;
+  }
   if (argc > 3 && std::strcmp(argv[3], "abl") == 0)
   {
     // the production pass 1 alone (built with -DOCEAN_ABLATE_H0LOAD / -DOCEAN_ABLATE_FSTORE: timing

@@ -201,6 +201,13 @@ int main()
       {"k_rows_xs PF 2, persistent grid (CUs)", mkg(k_rows_xs<LOGN, 2>, cus), {}},
       {"k_rows_xs PF 3, persistent grid (CUs)", mkg(k_rows_xs<LOGN, 3>, cus), {}},
       {"k_rows_xs PF 0, persistent grid (CUs)", mkg(k_rows_xs<LOGN, 0>, cus), {}},
+      {"k_rows_xs PF 2 EARLY 1", mkn(k_rows_xs<LOGN, 2, 1>), {}},
+      {"k_rows_xs PF 2 EARLY 2", mkn(k_rows_xs<LOGN, 2, 2>), {}},
+      {"k_rows_xs PF 0 EARLY 1", mkn(k_rows_xs<LOGN, 0, 1>), {}},
+      {"k_rows_xs PF 0 EARLY 2", mkn(k_rows_xs<LOGN, 0, 2>), {}},
+      {"k_rows_xs EARLY 3, persistent grid (CUs)", mkg(k_rows_xs<LOGN, 0, 3>, cus), {}},
+      {"k_rows_xs EARLY 3, one-shot grid", mkn(k_rows_xs<LOGN, 0, 3>), {}},
+      {"k_rows_xs PF 0 EARLY 2, persistent grid (CUs)", mkg(k_rows_xs<LOGN, 0, 2>, cus), {}},
   };
   // XS vs the plain transform: same lanes, different rounding order (max |diff| vs max |value|)
   auto snapf = [&](const void* p, size_t n) {
@@ -243,6 +250,13 @@ int main()
   compare(10, 12, "k_rows_xp PF 3 vs PF 0");
   compare(13, 7, "k_rows_xs PF 2 (streaming T_in) vs round 3");
   compare(7, 14, "k_rows_xs PF 2: persistent vs one-shot grid");
+  compare(7, 17, "k_rows_xs PF 2 EARLY 1 vs PF 2");
+  compare(7, 18, "k_rows_xs PF 2 EARLY 2 vs PF 2");
+  compare(7, 19, "k_rows_xs PF 0 EARLY 1 vs PF 2");
+  compare(7, 20, "k_rows_xs PF 0 EARLY 2 vs PF 2");
+  compare(7, 21, "k_rows_xs EARLY 3 persistent vs PF 2");
+  compare(7, 22, "k_rows_xs EARLY 3 one-shot vs PF 2");
+  compare(7, 23, "k_rows_xs PF 0 EARLY 2 persistent vs PF 2");
   for (int r = 0; r < 5; r++)
     for (auto& v : vs)
       v.t.push_back(time_ms(v.run, 3));

@@ -346,14 +346,16 @@ __global__ __launch_bounds__(256) void k_cols4_step1(int images, int x0, int wc,
 // Step 2, per (image, k1, strip of C slab columns): the N2-point inverse FFT along the work slab's
 // contiguous rows N2 k1 + n2 (n2 = i + m T), output X[k1 + 16 k2] to image row k1 + 16 k2 in the
 // reference layout. Loads and stores are C * 16 = 256-byte row pieces. tw_glob: the N2-point table.
-template <int LOGN2, bool WNT = true>
-__global__ __launch_bounds__(ColCfg<LOGN2>::WG) void k_cols4_step2(int images, int x0, int wc,
-                                                                 const float4* __restrict__ work, float4* __restrict__ img,
-                                                                 const float2* __restrict__ tw_glob)
+// CI: columns per workgroup (ColCfg's 16 = 1024 threads at N2 = 1024, production; 8 = 512 threads, two
+// per CU, as k_gen4_step2: 10.62 against 10.00 ms for 2 x 16384^2, tools/microbench/ifft4bench ci).
+template <int LOGN2, bool WNT = true, int CI = ColCfg<LOGN2>::C>
+__global__ __launch_bounds__(FftShape<LOGN2>::T * CI) void k_cols4_step2(int images, int x0, int wc,
+                                                                        const float4* __restrict__ work,
+                                                                        float4* __restrict__ img,
+                                                                        const float2* __restrict__ tw_glob)
 {
   using S = FftShape<LOGN2>;
-  using K = ColCfg<LOGN2>;
-  constexpr int N2 = S::N, T = S::T, C = K::C, LOGN = LOGN2 + 4, N = N2 * 16;
+  constexpr int N2 = S::N, T = S::T, C = CI, LOGN = LOGN2 + 4, N = N2 * 16;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   float2* tw = reinterpret_cast<float2*>(smem);
   void* xch = smem + ((S::TW_ENTRIES * 8 + 15) / 16) * 16;

@@ -143,13 +143,17 @@ __device__ __forceinline__ void fft_cols_hx(CPair* v, int t, void* lds, const fl
 // PUT (SLAB only; the one-sided exchange, ocean_peers): `send` is then the device table of the ranks'
 // destinations, ((const uint64_t*)send)[q] = this rank's block in rank q's receive slot, and block q
 // is stored there instead of at send + q * block bytes.
+// EARLY (round 5; a wave retires its memory instructions in issue order, so a load issued after the
+// round's field stores waits for them): bit 0, the scratch pairs of round r + 1 are loaded before
+// round r's stores (HS + HP); bits 1 / 2, the first 8 / all 16 h0 texels of the workgroup's next item
+// before round 2's stores (whole strips; the first item's in a prologue).
 // HB (half strips, whole grids): h0's strip width. HB = CPI = 2: h0 is blocked in 2-column strips, so a
 // half-strip item reads its own contiguous strip instead of the 32-B halves of 64-B row pieces that
 // its partner item reads the other halves of (launch_half_columns at <= 2 cascades: 0.122 -> 0.114 ms
 // per 4096^2 cascade, 0.935 -> 0.792 ms per 8, halfbench fb2h).
 template <int LOGN, int LA = 0, int SA = kStream, bool HS = false, bool SLAB = false, bool SEED = false, int RG = 1,
           int RGC = 1, int CPI = ColFirstCfg<LOGN>::B, bool HP = false, bool PC = false, int HL = 0, int HK = 0,
-          int HX = 0, int FB = 4, bool PUT = false, int HB = ColFirstCfg<LOGN>::B>
+          int HX = 0, int FB = 4, bool PUT = false, int HB = ColFirstCfg<LOGN>::B, int EARLY = 0>
 __global__ __launch_bounds__(FftShape<LOGN>::T * CPI, CPI < ColFirstCfg<LOGN>::B ? 4 : 1) void k_cols_half(FrameParams fp, const float4* __restrict__ h0,
                                                                      float4* __restrict__ gab, float4* __restrict__ gde,
                                                                      float2* __restrict__ gc,
@@ -181,6 +185,31 @@ __global__ __launch_bounds__(FftShape<LOGN>::T * CPI, CPI < ColFirstCfg<LOGN>::B
   const int nstrips = SLAB ? hsl.nstrips : STRIPS;
   const int total = fp.cascades * nstrips * HALVES;
   const float dim = (float)N;
+  constexpr int NPRE = 8 - HL - HK;  // scratch pairs per round (HP)
+  constexpr bool EPAIR = (EARLY & 1) && HS && HP && !PC && NPRE > 0;
+  constexpr int EH0 = (EARLY & 4) ? 16 : (EARLY & 2) ? 8 : 0;
+  static_assert(EH0 == 0 || (HALVES == 1 && HS && !SEED && !PC), "EARLY h0: whole strips");
+  float4 hpre[EPAIR ? NPRE : 1];  // EARLY 1: the next round's scratch pairs
+  float4 apre[EH0 > 0 ? EH0 : 1];  // EARLY 2 / 4: the next item's first h0 texels
+  // h0 of item `it` (whole strips): the strip's base and this thread's offset in it
+  auto h0_of = [&](int it, const float4*& sp, int& lo) __attribute__((always_inline)) {
+    const int c2 = it / nstrips, s2 = it - c2 * nstrips;
+    const int sg2 = SLAB ? hsl.strip0 + s2 : s2;
+    const int xb2 = sg2 == STRIPS - 1 ? 0 : N / (2 * B) + sg2;
+    sp = (!SLAB || h0_full) ? h0 + ((size_t)c2 * (N / B) + xb2) * N * B : h0 + ((size_t)c2 * nstrips + s2) * N * B;
+    const int t2 = opaque((int)threadIdx.x);
+    lo = (((t2 / CPI) % T) * B + t2 % CPI) * 16;
+  };
+  if constexpr (EH0 > 0)
+    if ((int)blockIdx.x < total)
+    {
+      const float4* sp;
+      int lo;
+      h0_of(blockIdx.x, sp, lo);
+#pragma unroll
+      for (int m = 0; m < EH0; m++)
+        apre[m] = ld4s<LA>(sp, lo, ((m + 8) & 15) * T * B * 16);
+    }
   for (int item = HALVES > 1 ? xcd_pair_slot(blockIdx.x, gridDim.x) : blockIdx.x; item < total; item += gridDim.x)
   {
     const int hh = HALVES > 1 ? item % HALVES : 0, si = HALVES > 1 ? item / HALVES : item;
@@ -279,7 +308,7 @@ __global__ __launch_bounds__(FftShape<LOGN>::T * CPI, CPI < ColFirstCfg<LOGN>::B
         const int loff = HB == B ? voff : (i * HB + (b - hh * CPI)) * 16;
 #pragma unroll
         for (int m = 0; m < 16; m++)  // fftShift on y folded into the load
-          a[m] = ld4s<LA>(srcl, loff, ((m + 8) & 15) * T * HB * 16);
+          a[m] = m < EH0 ? apre[m < EH0 ? m : 0] : ld4s<LA>(srcl, loff, ((m + 8) & 15) * T * HB * 16);
 #pragma unroll
         for (int m = 0; m < 16; m++)
         {
@@ -327,6 +356,7 @@ __global__ __launch_bounds__(FftShape<LOGN>::T * CPI, CPI < ColFirstCfg<LOGN>::B
               const int pi = m >> 1;
               const float4 p = pi < HL        ? hlds[pi * WG + threadIdx.x]
                                : pi < HL + HK ? hk[pi < HL + HK ? pi - HL : 0]
+                               : EPAIR        ? hpre[pi >= HL + HK ? pi - HL - HK : 0]
                                               : ld4s<kStream>(hsb, hoff * 2, pi * WG * 16);
               pack(m, make_float2(p.x, p.y), make_kvec(x, y, dim, f.dk));
               pack(m + 1, make_float2(p.z, p.w), make_kvec(x, y + T, dim, f.dk));
@@ -346,6 +376,25 @@ __global__ __launch_bounds__(FftShape<LOGN>::T * CPI, CPI < ColFirstCfg<LOGN>::B
       }
       else
         fft_run<LOGN, CPI, true>(v, i, HALVES > 1 ? opaque((int)threadIdx.x) % CPI : b, xch, tw);
+      if constexpr (EPAIR)
+        if (round < 2)  // the next round's scratch pairs, before this round's stores
+        {
+          const float2* hsb = hs + (size_t)blockIdx.x * 16 * WG;
+          const int hoff = opaque((int)threadIdx.x) * 8;
+#pragma unroll
+          for (int p = 0; p < NPRE; p++)
+            hpre[p] = ld4s<kStream>(hsb, hoff * 2, (HL + HK + p) * WG * 16);
+        }
+      if constexpr (EH0 > 0)
+        if (round == 2)  // the next item's first h0 texels, before this round's stores (unconditional:
+        {                // the last item re-reads its own, so the consumed registers are not kept live)
+          const float4* sp;
+          int lo;
+          h0_of(item + (int)gridDim.x < total ? item + (int)gridDim.x : item, sp, lo);
+#pragma unroll
+          for (int m = 0; m < EH0; m++)
+            apre[m] = ld4s<LA>(sp, lo, ((m + 8) & 15) * T * B * 16);
+        }
       const int vo = (io * B + b) * 16;
 #pragma unroll
       for (int m = 0; m < 16; m++)

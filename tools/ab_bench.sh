@@ -14,8 +14,14 @@ import json, sys
 line = [l for l in open(sys.argv[3]) if l.startswith("{")][-1]
 d = json.loads(line)
 k = d["kernels"]
+extra = ""
+il = d.get("ifft_only_large") or {}
+for n_, v_ in sorted(il.items()):
+    extra += f"  ifft {n_} {v_['ms_per_call']:.3f} ms"
+if "slab" in d:
+    extra += f"  16384 frame {d['slab']['ms_per_frame']:.3f} ms"
 print(f"{sys.argv[1]} run {sys.argv[2]}: frame {d['ms_per_step']:.4f} ms  cols {k['column_pass_k_cols_half']['avg_ms']:.4f}  "
-      f"rows {k['row_pass_k_rows_hp']['avg_ms']:.4f}  one cascade {d['strong_scaling']['one_cascade_ms']:.4f} ms", flush=True)
+      f"rows {k['row_pass_k_rows_hp']['avg_ms']:.4f}  one cascade {d['strong_scaling']['one_cascade_ms']:.4f} ms{extra}", flush=True)
 PY
   done
 done

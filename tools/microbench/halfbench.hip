@@ -678,6 +678,63 @@ int main(int argc, char** argv)
     std::printf("re-seed cols, production              median %7.3f ms  bit-identical %s\n", t[1][4], same ? "yes" : "NO");
     return 0;
   }
+  if (argc > 3 && std::strcmp(argv[3], "cole") == 0 && logn == 12)
+  {
+    // k_cols_half with loads issued before the round's stores (EARLY bits: 1 the next round's scratch
+    // pairs, 2 / 4 the next item's first 8 / 16 h0 texels) against production: fields bit-identical
+    using K = ColFirstCfg<12>;
+    using S = FftShape<12>;
+    const int lds4 = ((S::TW_ENTRIES * 8 + 15) / 16) * 16 + K::LDS1 + kHalfHL * 1024 * 16;
+    auto cols = [&](auto kern) {
+      return std::function<hipError_t()>([=] {
+        hipError_t e = launch_half_nyquist(fp, n, K::B, h0, spec, nullptr, 1, 0, nullptr, 0, cus);
+        if (e != hipSuccess)
+          return e;
+        int grid = persistent_grid(kern, 1024, lds4, fp.cascades * HalfCfg<12>::STRIPS, cus);
+        grid = grid > cus ? cus : grid;  // hs: cus slices of 16 x 1024 entries
+        hipLaunchKernelGGL(kern, dim3(grid), dim3(1024), lds4, 0, fp, h0, gab, gcd, ge, tw, hs, HalfSlab{},
+                           (unsigned char*)nullptr, 1, nullptr);
+        return hipGetLastError();
+      });
+    };
+#define KCH(E) k_cols_half<12, kStream, kStream, true, false, false, kHalfRG, kHalfRGC, 4, true, false, kHalfHL, kHalfHK, 0, 4, false, 4, E>
+    std::vector<std::function<hipError_t()>> vc = {cols(KCH(0)), cols(KCH(1)), cols(KCH(2)), cols(KCH(3)), cols(KCH(4)),
+                                                   cols(KCH(5))};
+#undef KCH
+    const char* nm[] = {"production", "EARLY 1 (scratch pairs)", "EARLY 2 (8 h0 texels)", "EARLY 3 (1 + 2)",
+                        "EARLY 4 (16 h0 texels)", "EARLY 5 (1 + 4)"};
+    const int NV = 6;
+    CHECK(vc[0]());
+    CHECK(hipDeviceSynchronize());
+    auto pab = snap(gab, ht * sizeof(float4)), pde = snap(gcd, ht * sizeof(float4)), pc = snap(ge, ht * sizeof(float2));
+    std::vector<int> same(NV, 1);
+    for (int k = 1; k < NV; k++)
+    {
+      CHECK(hipMemset(gab, 0, ht * sizeof(float4)));
+      CHECK(hipMemset(gcd, 0, ht * sizeof(float4)));
+      CHECK(hipMemset(ge, 0, ht * sizeof(float2)));
+      CHECK(vc[k]());
+      CHECK(hipDeviceSynchronize());
+      std::printf("%s vs production: gab, gde, gc\n", nm[k]);
+      same[k] = (int)diff(snap(gab, ht * sizeof(float4)), pab) & (int)diff(snap(gcd, ht * sizeof(float4)), pde) &
+                (int)diff(snap(ge, ht * sizeof(float2)), pc);
+    }
+    std::vector<std::vector<float>> t(NV), tf(NV);
+    for (int r = 0; r < 9; r++)
+      for (int k = 0; k < NV; k++)
+      {
+        t[k].push_back(time_ms(vc[k], 10));
+        tf[k].push_back(time_ms([&] { CHECK(vc[k]()); return r1(); }, 10));
+      }
+    for (int k = 0; k < NV; k++)
+    {
+      std::sort(t[k].begin(), t[k].end());
+      std::sort(tf[k].begin(), tf[k].end());
+      std::printf("cols %-26s median %7.3f ms   frame %7.3f ms  bit-identical %s\n", nm[k], t[k][4], tf[k][4],
+                  same[k] ? "yes" : "NO");
+    }
+    return 0;
+  }
   if (argc > 3 && std::strcmp(argv[3], "hpe") == 0 && logn == 12)
   {
     // k_rows_hp with the next image's / row's loads issued before the stores (EARLY 1, 2) against

@@ -120,12 +120,82 @@ static int mall_mode(int cus)
   return 0;
 }
 
+// "ci": 2 images of 16384^2, step 2 on 16 columns per 1024-thread workgroup (launch_ifft_fourstep,
+// production) against 8 per 512-thread workgroup (as k_gen4_step2), through a work slab of 2048 columns
+// and a whole-image work image; all bit-identical (the same per-column arithmetic). Round 5
+// (profiles/r05_ifft4bench_ci.log): 10.00 / 10.62 / 10.64 / 11.67 ms: neither is kept.
+static int ci_mode(int cus)
+{
+  constexpr int logn = 14, n = 1 << logn, imgs = 2;
+  const size_t tex = (size_t)n * n * imgs;
+  float4 *img, *work;
+  CHECK(hipMalloc(&img, tex * 16));
+  CHECK(hipMalloc(&work, ifft_fourstep_work_texels(logn, n) * 16));
+  hipLaunchKernelGGL(fill_img, dim3(4096), dim3(256), 0, 0, img, tex);
+  auto t1 = table(logn), t2 = table(logn - 4);
+  float2 *tw, *tw2;
+  CHECK(hipMalloc(&tw, t1.size() * 8));
+  CHECK(hipMalloc(&tw2, t2.size() * 8));
+  CHECK(hipMemcpy(tw, t1.data(), t1.size() * 8, hipMemcpyHostToDevice));
+  CHECK(hipMemcpy(tw2, t2.data(), t2.size() * 8, hipMemcpyHostToDevice));
+  std::vector<float4> base(tex), ref(tex), got(tex);
+  CHECK(hipDeviceSynchronize());
+  CHECK(hipMemcpy(base.data(), img, tex * 16, hipMemcpyDeviceToHost));
+  struct R { const char* name; int wc; bool ci8; std::vector<float> t; };
+  std::vector<R> rs = {{"CI 16, slab 2048", 2048, false, {}}, {"CI 8, slab 2048", 2048, true, {}},
+                       {"CI 16, whole image", n, false, {}}, {"CI 8, whole image", n, true, {}}};
+  // CI 8: rows, then per image and slab step 1 + k_cols4_step2<10, true, 8> (512-thread workgroups)
+  auto ci8 = [&](int wc) -> hipError_t {
+    hipError_t e = launch_rows_ifft(logn, imgs, img, tw, 0, cus);
+    if (e != hipSuccess)
+      return e;
+    using S2 = FftShape<logn - 4>;
+    constexpr int CI = 8, WG2 = S2::T * CI;
+    auto k1 = k_cols4_step1<logn>;
+    auto k2 = k_cols4_step2<logn - 4, true, CI>;
+    const int lds2 = ((S2::TW_ENTRIES * 8 + 15) / 16) * 16 + CI * S2::PADDED * 8;
+    for (int im = 0; im < imgs; im++)
+      for (int x0 = 0; x0 < n; x0 += wc)
+      {
+        float4* im0 = img + ((size_t)im << (2 * logn));
+        const int g1 = persistent_grid(k1, 256, 0, (wc / 64) * ((n / 16) / 4), cus);
+        hipLaunchKernelGGL(k1, dim3(g1), dim3(256), 0, 0, 1, x0, wc, im0, work, tw);
+        const int g2 = persistent_grid(k2, WG2, lds2, 16 * (wc / CI), cus);
+        hipLaunchKernelGGL(k2, dim3(g2), dim3(WG2), lds2, 0, 1, x0, wc, work, im0, tw2);
+      }
+    return hipGetLastError();
+  };
+  auto run = [&](const R& v) {
+    return v.ci8 ? ci8(v.wc) : launch_ifft_fourstep(logn, imgs, img, work, v.wc, tw, tw2, 0, cus);
+  };
+  for (size_t k = 0; k < rs.size(); k++)
+  {
+    CHECK(hipMemcpy(img, base.data(), tex * 16, hipMemcpyHostToDevice));
+    CHECK(run(rs[k]));
+    CHECK(hipDeviceSynchronize());
+    CHECK(hipMemcpy(k == 0 ? ref.data() : got.data(), img, tex * 16, hipMemcpyDeviceToHost));
+    if (k > 0)
+      std::printf("%s: %s\n", rs[k].name, std::memcmp(ref.data(), got.data(), tex * 16) == 0 ? "bit-identical" : "DIFFERS");
+  }
+  for (int r = 0; r < 5; r++)
+    for (auto& v : rs)
+      v.t.push_back(time_ms([&] { return run(v); }, 3));
+  for (auto& v : rs)
+  {
+    std::sort(v.t.begin(), v.t.end());
+    std::printf("2 x 16384^2 EncodeIFFT, %-20s median %7.3f ms\n", v.name, v.t[2]);
+  }
+  return 0;
+}
+
 int main(int argc, char** argv)
 {
   int cus = 0;
   CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0));
   if (argc > 1 && std::strcmp(argv[1], "mall") == 0)
     return mall_mode(cus);
+  if (argc > 1 && std::strcmp(argv[1], "ci") == 0)
+    return ci_mode(cus);
   for (int logn : {13, 14})
   {
     const int n = 1 << logn, imgs = logn == 13 ? (argc > 1 ? std::atoi(argv[1]) : 4) : 1;

@@ -38,7 +38,8 @@ namespace oceanfft
 // row's in a prologue. rm16bench (profiles/r05_rm16bench_early.log, one box): PF 2 (round 4) 3.586 ms,
 // EARLY 1 3.467 (PF 2) / 3.596 (PF 0), EARLY 2 3.336 / 3.330, maps bit-identical. Measured and not kept:
 // also image 1's spec texels or its Nyquist texel before the stores (50-110 VGPRs spilled, 4.3-4.9
-// ms); without image 1's spec loads at all (a timing ablation) EARLY 2 gains only 1 % more.
+// ms; the Nyquist texel beside EARLY 3 still spills 69, 4.27 ms, profiles/r05_rm16bench_early_nyq.log);
+// without image 1's spec loads at all (a timing ablation) EARLY 2 gains only 1 % more.
 template <int LOGN, int PF, int EARLY = 0>
 __global__ __launch_bounds__(1024) void k_rows_xs(FrameParams fp, const float4* __restrict__ spec, float4* __restrict__ maps,
                                                    float* __restrict__ jac, FoamParams foam,

@@ -1400,6 +1400,14 @@ def p8_put_projection(args, one_gpu_frame_ms: float, ranks: int = 8) -> dict:
     out["bounding_term"] = ("exchange at the xGMI rate (the passes beside the put take less)" if rate_ms >= frame
                             else "the pipelined passes beside the put")
     out["projected_speedup_vs_1gpu"] = one_gpu_frame_ms / bound
+    out["projected_frame_ms_8gpu"] = bound
+    # the SURVEY's own estimate (§8e) prices xGMI at 7 x 153.6 GB/s per GPU for the sends alone (the
+    # link figure read as one direction); reported beside the conservative one-way rate, never as it
+    survey_ms = out["exchange_bytes_per_rank"] / (XGMI_LINKS * XGMI_LINK_GBS_BIDIR * 1e9) * 1e3
+    out["projected_speedup_at_survey_xgmi_rate"] = {
+        "xgmi_GBps": XGMI_LINKS * XGMI_LINK_GBS_BIDIR, "exchange_ms": survey_ms,
+        "speedup": one_gpu_frame_ms / max(frame, survey_ms),
+        "bounding_term": "exchange" if survey_ms >= frame else "the pipelined passes beside the put"}
     out["projected_speedup_note"] = ("one-GPU frame / max(one rank's pipelined frame emulated with the put on its "
                                      "own K CUs of every XCD (step 1 and rows on the others), the rank's exchange bytes at the "
                                      "one-way xGMI rate); the local HBM traffic is the passes' own (the peers' "

@@ -1244,6 +1244,8 @@ def _put_emulation(args, ranks: int, calibrate: bool = True, per_xcd: int = 0, p
         PeerExchange.connect_local(peers)
         for p in peers:
             p.set_streams(s1.cuda_stream, put.cuda_stream, rows_st.cuda_stream)
+            if per_xcd:
+                p.set_row_cus(dev_cus - mask_cus)  # the masked row stream's CUs size its resident grid
         emulate_put_frame(slabs, peers, dt, update_ocean=True)
         emulate_put_frame(slabs, peers, dt)
 

@@ -274,6 +274,10 @@ int ocean_peers_set_put_cus(ocean_peers* peers, int cus);
  * peers' own; the generator's stream waits for each row pass, so the maps stay ordered on it). The
  * one-GPU emulation gives all P ranks one set, as one GPU has one path out over xGMI. */
 int ocean_peers_set_streams(ocean_peers* peers, void* column_stream, void* put_stream, void* row_stream);
+/* The CUs the caller's row stream may use when it is CU-masked (0 = all, the default; the peers' own
+ * masked streams know theirs): the 16384 row pass loops over rows on a resident grid, one workgroup per
+ * CU, so a grid sized for CUs the stream cannot use leaves whole workgroups waiting for a second turn. */
+int ocean_peers_set_row_cus(ocean_peers* peers, int cus);
 /* Recreate the peers' own streams CU-masked: the put on `cus_per_xcd` CUs of every XCD, step 1 and the
  * row pass on the others (0: unmasked, the default). An xGMI-bound put then holds only its own CUs
  * while it waits on the links. (A CU mask splits every XCD alike: workgroups are dealt to all 8 XCDs

@@ -111,6 +111,7 @@ SIGNATURES = {
     "ocean_peers_set_timeout": (_i, [_vp, _i]),
     "ocean_peers_set_put_cus": (_i, [_vp, _i]),
     "ocean_peers_set_streams": (_i, [_vp, _vp, _vp, _vp]),
+    "ocean_peers_set_row_cus": (_i, [_vp, _i]),
     "ocean_peers_set_put_cu_mask": (_i, [_vp, _i]),
     "ocean_generator_kernel_times4": (_i, [_vp, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int64)]),
     "ocean_generator_slab_frame_put": (_i, [_vp, _vp, _f, _i]),

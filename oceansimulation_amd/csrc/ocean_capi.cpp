@@ -977,17 +977,19 @@ static FoamParams current_foam(const ocean_generator* g)
 // Second half: the x direction of both EncodeIFFTs + computeFoam (src/Generator.cpp:71-80). `frame_foam`:
 // the displacement of a pipelined slab frame's own settings (null: the current settings).
 // row_stream (half-spectrum slab paths; null: the generator's stream): the pipelined one-sided frame's rows.
+// row_cus (> 0): the CUs the row stream may use (a CU-masked stream), which sizes resident grids.
 static int generator_rows(ocean_generator* g, const float4* in, const FoamParams* frame_foam = nullptr,
-                          hipStream_t row_stream = nullptr)
+                          hipStream_t row_stream = nullptr, int row_cus = 0)
 {
   ocean_fft* f = g->fft;
+  const int rcus = row_cus > 0 && row_cus < f->cus ? row_cus : f->cus;
   const FoamParams foam = frame_foam ? *frame_foam : current_foam(g);
   if (uses_gen4(g))
   {
     hipStream_t rs = row_stream ? row_stream : f->stream;
     HIP_TRY(timed(g, 2, [&] {
               return launch_gen4_rows(f->logn, g->frame, g->g4, in ? (const void*)in : (const void*)g->xbuf, g->maps,
-                                      g->jac, foam, f->twiddles, f->tw2, rs, f->cus);
+                                      g->jac, foam, f->twiddles, f->tw2, rs, rcus);
             }, rs),
             "row pass (half spectrum, four-step)");
   }
@@ -997,7 +999,7 @@ static int generator_rows(ocean_generator* g, const float4* in, const FoamParams
     HIP_TRY(timed(g, 2, [&] {
               return launch_half_slab_rows(f->logn, g->frame, g->hsl, in ? (const void*)in : (const void*)g->xbuf,
                                            g->rm_ab, g->rm_de, g->rm_c, g->maps, g->jac, foam, f->twiddles,
-                                           f->tw2, rs, f->cus);
+                                           f->tw2, rs, rcus);
             }, rs),
             "row pass (half spectrum, strip-dealt)");
   }
@@ -1542,6 +1544,8 @@ struct ocean_peers
   hipStream_t s1_stream = nullptr, put_stream = nullptr, row_stream = nullptr;
   hipStream_t own_s1 = nullptr, own_put = nullptr, own_rows = nullptr;
   int put_cus_per_xcd = 0;           // own streams CU-masked: the put on this many CUs of every XCD
+  int row_cus = 0;                   // the CUs the own row stream may use when masked (0: all)
+  int caller_row_cus = 0;            // ocean_peers_set_row_cus: the caller's row stream's CUs (0: all)
   hipEvent_t rows_done = nullptr;    // pipelined rows on row_stream -> the generator's stream
   unsigned char* parts2 = nullptr;   // step 1's second parts slot
   hipEvent_t s1_done[2] = {nullptr, nullptr}, put_done[2] = {nullptr, nullptr};
@@ -1667,7 +1671,8 @@ int put_rows(ocean_generator* g, ocean_peers* p, bool pipelined = false)
   HIP_TRY(launch_peer_wait(peer_wait(p, kReadyWord, fr + 1), rs), "one-sided exchange: ready wait");
   const FrameParams newest = g->frame;
   g->frame = p->slot_frame[s];
-  const int rc = generator_rows(g, reinterpret_cast<const float4*>(p->data + s * p->slot), &p->slot_foam[s], rs);
+  const int rc = generator_rows(g, reinterpret_cast<const float4*>(p->data + s * p->slot), &p->slot_foam[s], rs,
+                                rs == p->own_rows ? p->row_cus : p->caller_row_cus);
   g->frame = newest;
   if (rc != OCEAN_OK)
     return rc;
@@ -1705,10 +1710,14 @@ int peers_streams(ocean_peers* p)
     HIP_TRY(hipExtStreamCreateWithCUMask(&p->own_put, (uint32_t)put.size(), put.data()), "ocean_peers: put stream");
     HIP_TRY(hipExtStreamCreateWithCUMask(&p->own_s1, (uint32_t)rest.size(), rest.data()), "ocean_peers: column stream");
     HIP_TRY(hipExtStreamCreateWithCUMask(&p->own_rows, (uint32_t)rest.size(), rest.data()), "ocean_peers: row stream");
+    p->row_cus = cus - 8 * p->put_cus_per_xcd;  // resident row-pass grids sized to the masked stream
   }
   else
+  {
     for (hipStream_t* st : {&p->own_s1, &p->own_put, &p->own_rows})
       HIP_TRY(hipStreamCreateWithFlags(st, hipStreamNonBlocking), "ocean_peers: streams");
+    p->row_cus = 0;
+  }
   p->s1_stream = p->own_s1;
   p->put_stream = p->own_put;
   p->row_stream = p->own_rows;
@@ -1943,6 +1952,14 @@ int ocean_peers_set_streams(ocean_peers* p, void* column_stream, void* put_strea
   p->put_stream = put_stream ? (hipStream_t)put_stream : p->own_put;
   p->row_stream = row_stream ? (hipStream_t)row_stream : p->own_rows;
   p->put_done_valid[0] = p->put_done_valid[1] = false;  // the old streams are drained
+  return OCEAN_OK;
+}
+
+int ocean_peers_set_row_cus(ocean_peers* p, int cus)
+{
+  if (!p || !p->g || cus < 0)
+    return fail(OCEAN_ERR_INVALID, "ocean_peers_set_row_cus: null peers or negative CUs");
+  p->caller_row_cus = cus;
   return OCEAN_OK;
 }
 

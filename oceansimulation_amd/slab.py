@@ -242,6 +242,10 @@ class PeerExchange:
         check(lib().ocean_peers_set_streams(self._h, ctypes.c_void_p(column_stream or 0), ctypes.c_void_p(put_stream or 0),
                                             ctypes.c_void_p(row_stream or 0)), "ocean_peers_set_streams")
 
+    def set_row_cus(self, cus: int) -> None:
+        """The CUs the caller's (CU-masked) row stream may use: sizes the resident row-pass grid (0: all)."""
+        check(lib().ocean_peers_set_row_cus(self._h, int(cus)), "ocean_peers_set_row_cus")
+
     def set_put_cu_mask(self, cus_per_xcd: int) -> None:
         """CU-mask the peers' own streams: the put on `cus_per_xcd` CUs of every XCD, step 1 and rows on
         the others (0: unmasked)."""

@@ -678,6 +678,96 @@ int main(int argc, char** argv)
     std::printf("re-seed cols, production              median %7.3f ms  bit-identical %s\n", t[1][4], same ? "yes" : "NO");
     return 0;
   }
+  if (argc > 3 && std::strcmp(argv[3], "hs4") == 0 && logn == 12)
+  {
+    // half-strip pass 1 (two 512-thread workgroups per CU) reading 2-column h0 strips (HB 2) into the
+    // whole strips' 4-column fields (FB 4: each 128-B line written as two 64-B halves by the two items
+    // of a strip, on one XCD), so the production row pass reads them; against production and against
+    // the FB 2 fields (whole-line stores, k_rows_hp FB 2). Maps compared with production's.
+    using K = ColFirstCfg<12>;
+    using S = FftShape<12>;
+    float4* h0b2;
+    CHECK(hipMalloc(&h0b2, tex * C * sizeof(float4)));
+    for (int c = 0; c < C; c++)
+    {
+      OceanSettings s{};
+      s.seed[0] = 12342;
+      s.seed[1] = 8934;
+      s.U_10 = 40;
+      s.theta_0 = 25;
+      s.F = 800000;
+      s.g = 9.8f;
+      s.swell = 0.5f;
+      s.h = 100;
+      s.displacement = 0.4f;
+      s.planeSize = planes[c % 8];
+      s.scale = 1;
+      s.spread = 0.2f;
+      CHECK(launch_generate_spectrum(s, n, h0b2 + tex * c, 0, cus, 0, 0, 2));
+    }
+    const int tw0 = ((S::TW_ENTRIES * 8 + 15) / 16) * 16;
+    const int lds4 = tw0 + K::LDS1 + kHalfHL * 1024 * 16, lds2 = tw0 + 2 * S::PADDED * 8 + kHalfHL * 512 * 16;
+    auto cols = [&](auto kern, int wg, int lds, const float4* hsrc, int hb) {
+      return std::function<hipError_t()>([=] {
+        hipError_t e = launch_half_nyquist(fp, n, hb, hsrc, spec, nullptr, 1, 0, nullptr, 0, cus);
+        if (e != hipSuccess)
+          return e;
+        const int items = fp.cascades * HalfCfg<12>::STRIPS * (K::WG1 / wg);
+        int grid = persistent_grid(kern, wg, lds, items, cus);
+        const int slices = cus * (1024 / wg);
+        grid = grid > slices ? slices : grid;
+        hipLaunchKernelGGL(kern, dim3(grid), dim3(wg), lds, 0, fp, hsrc, gab, gcd, ge, tw, hs, HalfSlab{},
+                           (unsigned char*)nullptr, 1, nullptr);
+        return hipGetLastError();
+      });
+    };
+    auto rows = [&](auto kern) {
+      return std::function<hipError_t()>([=] {
+        const int grid = persistent_grid(kern, 256, HpCfg::LDS, fp.cascades * n, cus);
+        hipLaunchKernelGGL(kern, dim3(grid), dim3(256), HpCfg::LDS, 0, fp, gab, gcd, ge, spec, maps, jac, foam, tw, 0,
+                           RowSrc{});
+        return hipGetLastError();
+      });
+    };
+    std::vector<std::function<hipError_t()>> vc = {
+        cols(k_cols_half<12, kStream, kStream, true, false, false, kHalfRG, kHalfRGC, 4, true, false, kHalfHL, kHalfHK>, 1024, lds4, h0, 4),
+        cols(k_cols_half<12, kStream, kStream, true, false, false, kHalfRG, kHalfRGC, 2, true, false, kHalfHL, 4, 0, 4, false, 2>, 512, lds2, h0b2, 2),
+        cols(k_cols_half<12, kStream, kStream, true, false, false, kHalfRG2, kHalfRGC2, 2, true, false, kHalfHL, 4, 0, 2, false, 2>, 512, lds2, h0b2, 2)};
+    std::vector<std::function<hipError_t()>> vr = {rows(k_rows_hp<kHalfRG, kHalfRGC>), rows(k_rows_hp<kHalfRG, kHalfRGC>),
+                                                   rows(k_rows_hp<kHalfRG2, kHalfRGC2, false, false, 2, kHalfRGC2>)};
+    const char* nm[] = {"production (whole strips)", "half strips, h0 HB 2, fields FB 4", "half strips, h0 HB 2, fields FB 2"};
+    const int NV = 3;
+    CHECK(vc[0]());
+    CHECK(vr[0]());
+    CHECK(hipDeviceSynchronize());
+    auto pm = snap(maps, mb), pj = snap(jac, jb);
+    for (int k = 1; k < NV; k++)
+    {
+      CHECK(hipMemset(maps, 0, mb));
+      CHECK(hipMemset(jac, 0, jb));
+      CHECK(vc[k]());
+      CHECK(vr[k]());
+      CHECK(hipDeviceSynchronize());
+      std::printf("%s vs production: maps, jacobian\n", nm[k]);
+      (void)((int)diff(snap(maps, mb), pm) & (int)diff(snap(jac, jb), pj));
+    }
+    std::vector<std::vector<float>> t(NV), tr(NV), tf(NV);
+    for (int r = 0; r < 9; r++)
+      for (int k = 0; k < NV; k++)
+      {
+        t[k].push_back(time_ms(vc[k], 10));
+        tr[k].push_back(time_ms(vr[k], 10));
+        tf[k].push_back(time_ms([&] { CHECK(vc[k]()); return vr[k](); }, 10));
+      }
+    for (int k = 0; k < NV; k++)
+    {
+      std::sort(t[k].begin(), t[k].end());
+      std::sort(tr[k].begin(), tr[k].end());
+      std::sort(tf[k].begin(), tf[k].end());
+      std::printf("%-36s cols %7.3f ms  rows %7.3f ms  frame %7.3f ms\n", nm[k], t[k][4], tr[k][4], tf[k][4]);
+    }
+    return 0;
+  }
   if (argc > 3 && std::strcmp(argv[3], "cole") == 0 && logn == 12)
   {
     // k_cols_half with loads issued before the round's stores (EARLY bits: 1 the next round's scratch

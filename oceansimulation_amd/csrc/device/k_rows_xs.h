@@ -35,7 +35,10 @@ namespace oceanfft
 // fields return while the current image's 256 KiB of stores drain. EARLY 1: image 1's 8 - PF field
 // loads not already prefetched; 2: and its 8 C loads (held in 16 VGPRs until image 1's T_in); 3 (PF 0,
 // persistent grids): also the next row's image-0 fields and C before image 1's stores, the first
-// row's in a prologue. rm16bench (profiles/r05_rm16bench_early.log, one box): PF 2 (round 4) 3.586 ms,
+// row's in a prologue; 4 (production): as 3, with image 0's C kept in those 16 VGPRs for image 1
+// instead of re-read (no spills once nothing else is prefetched during the transform; the re-read
+// missed L2 often enough to make the pass read 1.087 x its bytes): 3.144 -> 3.076 ms, same box,
+// bit-identical (profiles/r05_rm16bench_keepc.log). rm16bench (profiles/r05_rm16bench_early.log, one box): PF 2 (round 4) 3.586 ms,
 // EARLY 1 3.467 (PF 2) / 3.596 (PF 0), EARLY 2 3.336 / 3.330, maps bit-identical. Measured and not kept:
 // also image 1's spec texels or its Nyquist texel before the stores (50-110 VGPRs spilled, 4.3-4.9
 // ms; the Nyquist texel beside EARLY 3 still spills 69, 4.27 ms, profiles/r05_rm16bench_early_nyq.log);
@@ -233,7 +236,7 @@ __global__ __launch_bounds__(1024) void k_rows_xs(FrameParams fp, const float4* 
         if (img == 0)
         {
           issue(item, 1, fp4, EARLY >= 3 ? 0 : PF, 8);  // fp4 is free: image 0's fields were consumed by T_in
-          if constexpr (EARLY >= 2)
+          if constexpr (EARLY >= 2 && EARLY != 4)  // EARLY 4: image 1 reuses image 0's C (kept in ccn)
             issue_c(item, ccn);
         }
         else if constexpr (EARLY >= 3)

@@ -99,9 +99,9 @@ hipError_t launch_half_slab_columns(int logn, const FrameParams& fp, const HalfS
 // appends for the sizes fourstep_table() names.
 // tools/microbench A/B at 16384: 0 = the plain transform, 1 = XS (k_rows_half), 2 = k_rows_xs, 3 =
 // k_rows_xs with 2 of the next image's 8 field loads in flight during the transform (PF; 4 spill), 4 =
-// k_rows_xs EARLY 3 on a resident grid: every image's loads issued before the previous image's stores
-// (round 5: 3.677 -> 3.158 ms per 16384^2 pass, same box, maps bit-identical,
-// profiles/r05_rm16bench_early.log).
+// k_rows_xs EARLY 4 on a resident grid: every image's loads issued before the previous image's stores,
+// and image 0's C kept for image 1 (round 5: 3.677 -> 3.158 (EARLY 3) -> 3.076 ms per 16384^2 pass,
+// maps bit-identical, profiles/r05_rm16bench_early.log, r05_rm16bench_keepc.log).
 // Measured and not kept: k_rows_xp (tools/microbench/k_rows_xp.h, the 64 x 256 split with the
 // sub-transforms' exchanges in the wave), 3.80-3.83 against 3.74 ms (profiles/r04_rm16bench_xp.log).
 inline int rm_rows_variant = 4;
@@ -135,7 +135,7 @@ hipError_t launch_rm_rows(const FrameParams& fp, const RowSrc& rs, const float4*
     {
       if (!tw2)
         return hipErrorInvalidValue;
-      auto kern = rm_rows_variant == 4 ? k_rows_xs<LOGN, 0, 3> : rm_rows_variant == 3 ? k_rows_xs<LOGN, 2> : k_rows_xs<LOGN, 0>;
+      auto kern = rm_rows_variant == 4 ? k_rows_xs<LOGN, 0, 4> : rm_rows_variant == 3 ? k_rows_xs<LOGN, 2> : k_rows_xs<LOGN, 0>;
       const int lds = XsCfg<LOGN>::LDS;
       const int grid = rm_rows_variant == 4 ? resident_grid(kern, S::T, lds, fp.cascades * rows, cus)
                                             : persistent_grid(kern, S::T, lds, fp.cascades * rows, cus);

@@ -208,6 +208,7 @@ int main()
       {"k_rows_xs EARLY 3, persistent grid (CUs)", mkg(k_rows_xs<LOGN, 0, 3>, cus), {}},
       {"k_rows_xs EARLY 3, one-shot grid", mkn(k_rows_xs<LOGN, 0, 3>), {}},
       {"k_rows_xs PF 0 EARLY 2, persistent grid (CUs)", mkg(k_rows_xs<LOGN, 0, 2>, cus), {}},
+      {"k_rows_xs EARLY 4 (C kept for image 1), persistent", mkg(k_rows_xs<LOGN, 0, 4>, cus), {}},
   };
   // XS vs the plain transform: same lanes, different rounding order (max |diff| vs max |value|)
   auto snapf = [&](const void* p, size_t n) {
@@ -257,6 +258,7 @@ int main()
   compare(7, 21, "k_rows_xs EARLY 3 persistent vs PF 2");
   compare(7, 22, "k_rows_xs EARLY 3 one-shot vs PF 2");
   compare(7, 23, "k_rows_xs PF 0 EARLY 2 persistent vs PF 2");
+  compare(7, 24, "k_rows_xs EARLY 4 persistent vs PF 2");
   for (int r = 0; r < 5; r++)
     for (auto& v : vs)
       v.t.push_back(time_ms(v.run, 3));

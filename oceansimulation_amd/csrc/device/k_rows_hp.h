@@ -55,8 +55,10 @@ __device__ __forceinline__ int hp_slot(int n1, int j) { return n1 * HpCfg::RS + 
 // before image 0's stores (32 VGPRs from the end of image 0's transform to image 1's T_in); 2: and
 // the next row's (A, B) and C before image 1's stores (the first row's in a prologue; persistent
 // grids); whole grids only.
-template <int RG, int RGC, bool RM = false, bool YP = false, int FB = 4, int GRP = 4, int EARLY = 0>
-__global__ __launch_bounds__(256, 4) void k_rows_hp(FrameParams fp, const float4* __restrict__ gab,
+// MINB: the workgroups per CU the launch bounds ask for (4: 128 VGPRs; 3: 168, room for EARLY 2's
+// prefetch without spills).
+template <int RG, int RGC, bool RM = false, bool YP = false, int FB = 4, int GRP = 4, int EARLY = 0, int MINB = 4>
+__global__ __launch_bounds__(256, MINB) void k_rows_hp(FrameParams fp, const float4* __restrict__ gab,
                                                  const float4* __restrict__ gde, const float2* __restrict__ gc,
                                                  const float4* __restrict__ spec, float4* __restrict__ maps,
                                                  float* __restrict__ jac, FoamParams foam,

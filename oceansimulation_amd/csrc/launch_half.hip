@@ -127,8 +127,11 @@ hipError_t launch_half_rows(int logn, const FrameParams& fp, const float4* gab, 
       {
         if (half_rows_variant == 1)
         {
+          // whole strips: three workgroups per CU with image 1's (D, E) loads issued before image 0's
+          // stores (EARLY 1, MINB 3): 1.362 / 1.366 -> 1.345 / 1.351 ms per 8 x 4096^2 on two boxes, maps
+          // bit-identical (halfbench hpe, profiles/r05_halfbench_hpe2_8.log, r05_halfbench_hpe3_8.log)
           auto kern = half_fields_fb(LOGN, fp.cascades) == 2 ? k_rows_hp<kHalfRG2, kHalfRGC2, false, false, 2, kHalfRGC2>
-                                                             : k_rows_hp<RG, RGC>;
+                                                             : k_rows_hp<RG, RGC, false, false, 4, 4, 1, 3>;
           const int grid = persistent_grid(kern, 256, HpCfg::LDS, fp.cascades * S::N, cus);
           hipLaunchKernelGGL(kern, dim3(grid), dim3(256), HpCfg::LDS, stream, fp, gab, gcd, ge, rcorr, maps, jac, foam, tw, 0,
                              RowSrc{});

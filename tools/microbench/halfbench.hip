@@ -841,9 +841,13 @@ int main(int argc, char** argv)
     };
     std::vector<std::function<hipError_t()>> vr = {rows(k_rows_hp<kHalfRG, kHalfRGC>),
                                                    rows(k_rows_hp<kHalfRG, kHalfRGC, false, false, 4, 4, 1>),
-                                                   rows(k_rows_hp<kHalfRG, kHalfRGC, false, false, 4, 4, 2>)};
-    const char* nm[] = {"k_rows_hp (production)", "k_rows_hp EARLY 1", "k_rows_hp EARLY 2"};
-    const int NV = 3;
+                                                   rows(k_rows_hp<kHalfRG, kHalfRGC, false, false, 4, 4, 2>),
+                                                   rows(k_rows_hp<kHalfRG, kHalfRGC, false, false, 4, 4, 0, 3>),
+                                                   rows(k_rows_hp<kHalfRG, kHalfRGC, false, false, 4, 4, 2, 3>),
+                                                   rows(k_rows_hp<kHalfRG, kHalfRGC, false, false, 4, 4, 1, 3>)};
+    const char* nm[] = {"k_rows_hp (production)", "k_rows_hp EARLY 1", "k_rows_hp EARLY 2", "3 WG/CU",
+                        "3 WG/CU EARLY 2", "3 WG/CU EARLY 1"};
+    const int NV = 6;
     CHECK(vr[0]());
     CHECK(hipDeviceSynchronize());
     auto pm = snap(maps, mb), pj = snap(jac, jb);

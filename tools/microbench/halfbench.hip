@@ -678,7 +678,7 @@ int main(int argc, char** argv)
     std::printf("re-seed cols, production              median %7.3f ms  bit-identical %s\n", t[1][4], same ? "yes" : "NO");
     return 0;
   }
-  if (argc > 3 && std::strcmp(argv[3], "hs4") == 0 && logn == 12)
+  if (argc > 3 && (std::strcmp(argv[3], "hs4") == 0 || std::strcmp(argv[3], "hpf") == 0) && logn == 12)
   {
     // half-strip pass 1 (two 512-thread workgroups per CU) reading 2-column h0 strips (HB 2) into the
     // whole strips' 4-column fields (FB 4: each 128-B line written as two 64-B halves by the two items
@@ -729,13 +729,21 @@ int main(int argc, char** argv)
         return hipGetLastError();
       });
     };
-    std::vector<std::function<hipError_t()>> vc = {
+    const bool hpf = std::strcmp(argv[3], "hpf") == 0;  // the FB 2 row pass variants instead
+    auto c2 = cols(k_cols_half<12, kStream, kStream, true, false, false, kHalfRG2, kHalfRGC2, 2, true, false, kHalfHL, 4, 0, 2, false, 2>, 512, lds2, h0b2, 2);
+    std::vector<std::function<hipError_t()>> vc = hpf ? std::vector<std::function<hipError_t()>>{c2, c2, c2} : std::vector<std::function<hipError_t()>>{
         cols(k_cols_half<12, kStream, kStream, true, false, false, kHalfRG, kHalfRGC, 4, true, false, kHalfHL, kHalfHK>, 1024, lds4, h0, 4),
         cols(k_cols_half<12, kStream, kStream, true, false, false, kHalfRG, kHalfRGC, 2, true, false, kHalfHL, 4, 0, 4, false, 2>, 512, lds2, h0b2, 2),
-        cols(k_cols_half<12, kStream, kStream, true, false, false, kHalfRG2, kHalfRGC2, 2, true, false, kHalfHL, 4, 0, 2, false, 2>, 512, lds2, h0b2, 2)};
-    std::vector<std::function<hipError_t()>> vr = {rows(k_rows_hp<kHalfRG, kHalfRGC>), rows(k_rows_hp<kHalfRG, kHalfRGC>),
-                                                   rows(k_rows_hp<kHalfRG2, kHalfRGC2, false, false, 2, kHalfRGC2>)};
-    const char* nm[] = {"production (whole strips)", "half strips, h0 HB 2, fields FB 4", "half strips, h0 HB 2, fields FB 2"};
+        c2};
+    std::vector<std::function<hipError_t()>> vr = hpf ? std::vector<std::function<hipError_t()>>{
+        rows(k_rows_hp<kHalfRG2, kHalfRGC2, false, false, 2, kHalfRGC2>),
+        rows(k_rows_hp<kHalfRG2, kHalfRGC2, false, false, 2, kHalfRGC2, 1, 3>),
+        rows(k_rows_hp<kHalfRG2, kHalfRGC2, false, false, 2, kHalfRGC2, 0, 3>)} : std::vector<std::function<hipError_t()>>{
+        rows(k_rows_hp<kHalfRG, kHalfRGC>), rows(k_rows_hp<kHalfRG, kHalfRGC>),
+        rows(k_rows_hp<kHalfRG2, kHalfRGC2, false, false, 2, kHalfRGC2>)};
+    const char* nm0[] = {"production (whole strips)", "half strips, h0 HB 2, fields FB 4", "half strips, h0 HB 2, fields FB 2"};
+    const char* nm1[] = {"FB 2 rows (production <= 2 casc.)", "FB 2 rows, 3 WG/CU EARLY 1", "FB 2 rows, 3 WG/CU"};
+    const char* const* nm = hpf ? nm1 : nm0;
     const int NV = 3;
     CHECK(vc[0]());
     CHECK(vr[0]());

@@ -716,6 +716,39 @@ def test_slab_pipeline_matches_whole_grid(ocean, n, ranks, budget):
         assert np.array_equal(got, want), "unsynchronised run"
 
 
+def test_16384_row_pass_resident_grid_under_cu_budget(ocean):
+    """The 16384 row pass loops over rows on a resident grid (k_rows_xs EARLY 4: each image's loads
+    issued before the previous image's stores, the next row's before this row's): with a CU budget of
+    100 (100 workgroups, ~164 rows each) the maps equal the full device's (256 workgroups) bit for bit."""
+    from oceansimulation_amd import capi
+
+    L = capi.lib()
+    n = 16384
+    outs = []
+    for budget in (0, 100):
+        fft = ocean.FFTCalculator(n)
+        fft.set_cu_budget(budget)
+        gen = ocean.Generator(fft, 1)
+        for dt in (0.5, 1.0 / 60.0):
+            gen.CalculateOcean(dt)
+        fft.synchronize()
+        outs.append((fft, gen))
+    from oceansimulation_amd import hip
+    import torch
+
+    for get, tex in ((L.ocean_generator_height_map, 16), (L.ocean_generator_displacement_map, 16),
+                     (L.ocean_generator_jacobian_map, 4)):
+        nb = n * n * tex
+        a = torch.empty(nb, dtype=torch.uint8, device="cuda")
+        b = torch.empty_like(a)
+        hip.copy_d2d(a.data_ptr(), int(get(outs[0][1].handle, 0)), nb)
+        hip.copy_d2d(b.data_ptr(), int(get(outs[1][1].handle, 0)), nb)
+        assert torch.equal(a, b), get.__name__
+    for fft, gen in outs:
+        gen.close()
+        fft.close()
+
+
 def test_cu_budget_validation(ocean):
     from oceansimulation_amd.capi import OceanError
 

@@ -108,6 +108,25 @@ def test_put_exchange_in_one_process_bit_exact(ocean, n, P, four_step):
     for dt in steps:
         whole.CalculateOcean(dt)
     assert _same(L, slabs, whole, n) is None, (n, P, "pipelined, CU-masked put")
+    if n == 16384:
+        # the caller's streams, the row stream declared to have 64 CUs (a resident row-pass grid of 64)
+        import torch
+
+        sts = [torch.cuda.Stream() for _ in range(3)]
+        for p in peers:
+            p.set_streams(*(st.cuda_stream for st in sts))
+            p.set_row_cus(64)
+        for dt in steps:
+            for g, p in zip(slabs, peers):
+                g.frame_put_pipelined(p, dt)
+        for p in peers:
+            p.flush()
+        for dt in steps:
+            whole.CalculateOcean(dt)
+        assert _same(L, slabs, whole, n) is None, (n, P, "pipelined, caller streams, 64 row CUs")
+        for p in peers:
+            p.synchronize()
+            p.set_streams(None, None, None)
     for p in peers:
         p.synchronize()
         p.close()

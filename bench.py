@@ -875,8 +875,9 @@ def slab_grid(args, rank: int, world: int, local: int) -> dict:
     # ---- the one-sided exchange (ocean_peers, four-step slabs) ----
     if n >= 8192 and not args.full_spectrum and not args.no_put and (world > 1 or args.slab_force_exchange):
         out["put"] = put_leg(args, ocean, fft, g, whole, rank, world, all_ranks_ok)
-        verified["put"] = out["put"].get("verified", False)
-        if verified["put"]:
+        if out["put"].get("verified", False) is not None:  # None: the leg was unavailable, see its error
+            verified["put"] = out["put"].get("verified", False)
+        if verified.get("put"):
             for k in ("serial_ms_per_frame", "pipelined_ms_per_frame", "pipelined_masked_ms_per_frame"):
                 if k in out["put"]:
                     legs["put_" + k.replace("_ms_per_frame", "")] = out["put"][k]
@@ -944,7 +945,10 @@ def put_leg(args, ocean, fft, g, whole, rank: int, world: int, all_ranks_ok) -> 
     elif err is None:
         err = "another rank could not create or export its peers"
     if not all_ranks_ok(err is None):
+        # the exchange could not be set up (no frame ran, nothing to compare): reported as unavailable,
+        # not as a failed check — a mismatch is a frame whose rows differ from the whole grid's
         res["error"] = err or "another rank could not connect"
+        res["verified"] = None
         barrier(world)
         if peers is not None:
             peers.close()

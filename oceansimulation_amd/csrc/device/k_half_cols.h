@@ -147,13 +147,16 @@ __device__ __forceinline__ void fft_cols_hx(CPair* v, int t, void* lds, const fl
 // round's field stores waits for them): bit 0, the scratch pairs of round r + 1 are loaded before
 // round r's stores (HS + HP); bits 1 / 2, the first 8 / all 16 h0 texels of the workgroup's next item
 // before round 2's stores (whole strips; the first item's in a prologue).
+// NYQ (whole grids): the Nyquist-row term (k_half_nyquist's spec, written to `send` as float4[C][2][N])
+// is computed by the workgroup of the last item slot, which has the fewest items, after them: one
+// launch per frame fewer (half_nyquist_texel, the same arithmetic as the kernel the slab paths use).
 // HB (half strips, whole grids): h0's strip width. HB = CPI = 2: h0 is blocked in 2-column strips, so a
 // half-strip item reads its own contiguous strip instead of the 32-B halves of 64-B row pieces that
 // its partner item reads the other halves of (launch_half_columns at <= 2 cascades: 0.122 -> 0.114 ms
 // per 4096^2 cascade, 0.935 -> 0.792 ms per 8, halfbench fb2h).
 template <int LOGN, int LA = 0, int SA = kStream, bool HS = false, bool SLAB = false, bool SEED = false, int RG = 1,
           int RGC = 1, int CPI = ColFirstCfg<LOGN>::B, bool HP = false, bool PC = false, int HL = 0, int HK = 0,
-          int HX = 0, int FB = 4, bool PUT = false, int HB = ColFirstCfg<LOGN>::B, int EARLY = 0>
+          int HX = 0, int FB = 4, bool PUT = false, int HB = ColFirstCfg<LOGN>::B, int EARLY = 0, bool NYQ = false>
 __global__ __launch_bounds__(FftShape<LOGN>::T * CPI, CPI < ColFirstCfg<LOGN>::B ? 4 : 1) void k_cols_half(FrameParams fp, const float4* __restrict__ h0,
                                                                      float4* __restrict__ gab, float4* __restrict__ gde,
                                                                      float2* __restrict__ gc,
@@ -175,6 +178,7 @@ __global__ __launch_bounds__(FftShape<LOGN>::T * CPI, CPI < ColFirstCfg<LOGN>::B
   static_assert(FB == 4 || (FB == CPI && HALVES == 2 && !SLAB && RG > 1 && RGC > 1 && !HX), "FB: half-strip fields");
   static_assert(!PUT || (SLAB && !PC), "PUT: the strip-dealt slab stores");
   static_assert(HB == B || (HB == CPI && HALVES == 2 && !SLAB), "HB: half strips over 2-column h0 strips");
+  static_assert(!NYQ || !SLAB, "NYQ: whole grids (send is the spec output)");
   constexpr int XB = CPI * S::PADDED * 8;  // the exchange's bytes (K::LDS1 for whole strips)
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   float2* tw = reinterpret_cast<float2*>(smem);
@@ -508,6 +512,10 @@ __global__ __launch_bounds__(FftShape<LOGN>::T * CPI, CPI < ColFirstCfg<LOGN>::B
         run_round(round);
     }
   }
+  if constexpr (NYQ)
+    if ((HALVES > 1 ? xcd_pair_slot(blockIdx.x, gridDim.x) : (int)blockIdx.x) == (int)gridDim.x - 1)
+      for (int idx = threadIdx.x; idx < fp.cascades * N; idx += WG)
+        half_nyquist_texel(fp, N, HB, h0, reinterpret_cast<float4*>(send), nullptr, 1, 0, seed, nullptr, 0, idx);
 }
 
 }  // namespace oceanfft

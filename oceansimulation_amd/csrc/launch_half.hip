@@ -51,10 +51,8 @@ hipError_t launch_half_columns(int logn, const FrameParams& fp, const float4* h0
       const int hb = h0_blk > 0 ? h0_blk : K::B;
       if (hb != K::B && (hb != 2 || half_fields_fb(LOGN, fp.cascades) != 2))
         return hipErrorInvalidValue;  // 2-column h0 strips are read by the half-strip pass only
-      // the Nyquist-row term: one row spectrum per image
-      hipError_t e = launch_half_nyquist(fp, S::N, hb, h0, spec, nullptr, 1, 0, seed, stream, cus);
-      if (e != hipSuccess)
-        return e;
+      // the Nyquist-row term (one row spectrum per image) is written by pass 1 itself (k_cols_half NYQ:
+      // its least-loaded workgroup, after its items), into `spec` passed as the kernel's `send`
       // Field layout: row groups (kHalfRG, kHalfRGC). The H scratch in 16-B pairs (HP), one pair per
       // thread in the LDS the exchange leaves free (kHalfHL) and kHalfHK pairs in VGPRs at 4096 (2
       // below: 128 VGPRs, so two (2048) or four (1024) workgroups share a CU). h0 is read once per
@@ -70,12 +68,12 @@ hipError_t launch_half_columns(int logn, const FrameParams& fp, const float4* h0
           // h0 in 2-column strips (hb = 2, half_h0_block): each item streams its own strip
           constexpr int WGH = S::T * 2;
           auto kern = seed ? k_cols_half<LOGN, 0, kStream, true, false, true, kHalfRG2, kHalfRGC2, 2, true, false, kHalfHL,
-                                         kHalfHKSeed, 0, 2>
+                                         kHalfHKSeed, 0, 2, false, K::B, 0, true>
                            : k_cols_half<LOGN, kStream, kStream, true, false, false, kHalfRG2, kHalfRGC2, 2, true, false,
-                                         kHalfHL, kHalfHK, 0, 2>;
+                                         kHalfHL, kHalfHK, 0, 2, false, K::B, 0, true>;
           if (!seed && hb == 2)
             kern = k_cols_half<LOGN, kStream, kStream, true, false, false, kHalfRG2, kHalfRGC2, 2, true, false, kHalfHL,
-                               kHalfHK, 0, 2, false, 2>;
+                               kHalfHK, 0, 2, false, 2, 0, true>;
           const int lds = ((S::TW_ENTRIES * 8 + 15) / 16) * 16 + 2 * S::PADDED * 8 + kHalfHL * WGH * 16;
           int grid = persistent_grid(kern, WGH, lds, fp.cascades * HalfCfg<LOGN>::STRIPS * 2, cus);
           const int slices = hs_blocks * (1024 / WGH);
@@ -84,12 +82,14 @@ hipError_t launch_half_columns(int logn, const FrameParams& fp, const float4* h0
           if (grid < 1)
             return hipErrorInvalidValue;
           hipLaunchKernelGGL(kern, dim3(grid), dim3(WGH), lds, stream, fp, h0, gab, gcd, ge, tw, hs, HalfSlab{},
-                             (unsigned char*)nullptr, 1, seed);
+                             reinterpret_cast<unsigned char*>(spec), 1, seed);
           return hipGetLastError();
         }
       }
-      auto kern = seed ? k_cols_half<LOGN, 0, kStream, true, false, true, RG, RGC, K::B, true, false, kHalfHL, kHalfHKSeed>
-                       : k_cols_half<LOGN, kStream, kStream, true, false, false, RG, RGC, K::B, true, false, kHalfHL, HKW>;
+      auto kern = seed ? k_cols_half<LOGN, 0, kStream, true, false, true, RG, RGC, K::B, true, false, kHalfHL, kHalfHKSeed,
+                                     0, 4, false, K::B, 0, true>
+                       : k_cols_half<LOGN, kStream, kStream, true, false, false, RG, RGC, K::B, true, false, kHalfHL, HKW, 0, 4,
+                                     false, K::B, 0, true>;
       const int lds = ((S::TW_ENTRIES * 8 + 15) / 16) * 16 + K::LDS1 + kHalfHL * K::WG1 * 16;
       int grid = persistent_grid(kern, K::WG1, lds, fp.cascades * HalfCfg<LOGN>::STRIPS, cus);
       // hs holds hs_blocks slices for 1024-thread workgroups (half_hs_bytes); a block uses 16 x WG1
@@ -100,7 +100,7 @@ hipError_t launch_half_columns(int logn, const FrameParams& fp, const float4* h0
       if (grid < 1)
         return hipErrorInvalidValue;
       hipLaunchKernelGGL(kern, dim3(grid), dim3(K::WG1), lds, stream, fp, h0, gab, gcd, ge, tw, hs, HalfSlab{},
-                         (unsigned char*)nullptr, 1, seed);  // gcd/ge: (D, E) / C
+                         reinterpret_cast<unsigned char*>(spec), 1, seed);  // gcd/ge: (D, E) / C; spec: NYQ
       return hipGetLastError();
     }
   });

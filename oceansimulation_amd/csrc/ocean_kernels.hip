@@ -136,49 +136,8 @@ __global__ __launch_bounds__(256) void k_half_nyquist(FrameParams fp, int n, int
                                                       const uint64_t* __restrict__ dst, size_t dst_off)
 {
   const int total = fp.cascades * n;
-  const float dim = (float)n;
   for (int idx = blockIdx.x * blockDim.x + threadIdx.x; idx < total; idx += gridDim.x * blockDim.x)
-  {
-    const int c = idx / n, x = idx - c * n;
-    float4 s01 = make_float4(0.0f, 0.0f, 0.0f, 0.0f), s23 = s01;
-    if (x > 0 && x < n / 2)
-    {
-      const CascadeFrame f = fp.c[c];
-      const int xp = n - x;  // u' = n/2 - x > 0 at column n/2 + u' = n - x; its mirror is x itself
-      const float4* hc = h0 + (size_t)c * n * n;
-      float4 ap, an;  // row y = 0 (v = -n/2)
-      if (seed)
-      {
-        ap = seed_texel(seed[c], xp, 0, dim);
-        an = seed_texel(seed[c], x, 0, dim);
-      }
-      else
-      {
-        ap = h0row ? h0row[(size_t)c * n + xp] : hc[(size_t)(xp / blk) * n * blk + (xp % blk)];
-        an = h0row ? h0row[(size_t)c * n + x] : hc[(size_t)(x / blk) * n * blk + (x % blk)];
-      }
-      const KVec qp = make_kvec(xp, 0, dim, f.dk), qn = make_kvec(x, 0, dim, f.dk);
-      const float2 hp = evolve(ap, qp.k, f), hn = evolve(an, qn.k, f);
-      const float2 dm = make_float2(hn.x - hp.x, hn.y + hp.y);  // Hn - conj(Hp)
-      const float2 dq = make_float2(hn.x + hp.x, hn.y - hp.y);  // Hn + conj(Hp)
-      const float kz = qn.kz, inv = qn.inv, dirz = qn.dirz, kx = qn.kx;
-      const float2 dA = dm;                                              // s = +1
-      const float2 dB = make_float2(kz * dq.x, kz * dq.y);               // s = -1
-      const float2 dC = make_float2(inv * dm.x, inv * dm.y);             // s = +1
-      const float2 dD = make_float2(dirz * dq.x, dirz * dq.y);           // s = -1
-      const float2 dE = make_float2(kz * dirz * dm.x, kz * dirz * dm.y); // s = +1
-      const float kx2 = kx * kx;
-      s01 = make_float4((1.0f - kx) * dA.x, (1.0f - kx) * dA.y, -dB.y - kx * dC.x, dB.x - kx * dC.y);
-      s23 = make_float4(-(dD.y - kx2 * dC.y), dD.x - kx2 * dC.x, -dE.x + kx * dD.y, -dE.y - kx * dD.x);
-    }
-    for (int k = 0; k < copies; k++)
-    {
-      float4* sp = reinterpret_cast<float4*>(dst ? reinterpret_cast<unsigned char*>(dst[k]) + dst_off
-                                                 : reinterpret_cast<unsigned char*>(spec) + k * copy_stride);
-      sp[((size_t)c * 2 + 0) * n + x] = s01;
-      sp[((size_t)c * 2 + 1) * n + x] = s23;
-    }
-  }
+    half_nyquist_texel(fp, n, blk, h0, spec, h0row, copies, copy_stride, seed, dst, dst_off, idx);
 }
 
 // ------------------------------------------------------------------------------------------------

@@ -1592,6 +1592,8 @@ def main(argv=None):
             out["roofline"]["traffic"] = pmc["hbm_traffic_bytes"] / (dom["avg_ms"] * 1e-3) / 1e9
             out["roofline"]["traffic_bytes_per_launch"] = pmc["hbm_traffic_bytes"]
             out["roofline"]["algorithmic_bytes_per_launch"] = dom["bytes"]
+            # box-independent: measured HBM bytes over algorithmic bytes (1.0 = no wasted re-reads)
+            out["roofline"]["traffic_over_algorithmic"] = pmc["hbm_traffic_bytes"] / dom["bytes"]
             out["roofline"]["traffic_source"] = pmc["source"]
             if pmc.get("avg_ms"):
                 # the same kernel's duration in the committed rocprofv3 summary (another box, profiled run):
@@ -1599,6 +1601,8 @@ def main(argv=None):
                 out["roofline"]["committed_profile"] = {
                     "avg_ms": pmc["avg_ms"],
                     "frac": dom["bytes"] / (pmc["avg_ms"] * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                    # the PMC bytes over the same box's duration (traffic above divides by this run's)
+                    "traffic_GBps": pmc["hbm_traffic_bytes"] / (pmc["avg_ms"] * 1e-3) / 1e9,
                     "source": pmc["source"].split(" ")[0] + " (rocprofv3 --kernel-trace --stats, the profiling box)",
                 }
         else:

@@ -297,8 +297,23 @@ int ocean_peers_flush(ocean_peers* peers);
 int ocean_generator_slab_put_columns(ocean_generator* gen, ocean_peers* peers, float timestep, int update_spectrum);
 int ocean_generator_slab_put_rows(ocean_generator* gen, ocean_peers* peers);
 /* Wait for this rank's streams; OCEAN_ERR_TIMEOUT when any wait gave up (which, and at which frame,
- * in ocean_last_error). */
+ * in ocean_last_error). After a timeout the device-side error word is cleared and the peers refuse every
+ * further frame with OCEAN_ERR_TIMEOUT (the ranks' flag counts no longer agree): destroy and recreate
+ * them. Pipelined row passes wait for the caller's work on the generator's stream before they rewrite
+ * the maps, and h0 re-seeds wait for the column pass still reading h0 on the peers' streams. */
 int ocean_peers_synchronize(ocean_peers* peers);
+
+/* Receive slot `slot` (0 or 1) of this rank: its device pointer and size (frame f's blocks land in
+ * slot f % 2). Debug only (tests/test_gpu_peers.py reads a slot into every XCD's L2 just before the
+ * peers' put rewrites it, to check that the row pass never reads a stale line). No reference counterpart. */
+int ocean_peers_debug_slot(const ocean_peers* peers, int slot, void** ptr, size_t* bytes);
+
+/* The whole-grid half-spectrum frame's layout pairing (N = 1024 .. 4096), host only: out = the field
+ * strip width, gab/gde row group, gc row group and h0 strip width the column pass WRITES / reads {0..3},
+ * the first three as the row pass (rows_variant 1 = k_rows_hp at 4096, 0 = k_rows_half) READS them
+ * {4..6}, and the h0 strip width the seeding writes {7}. Each launcher picks its kernel from the same
+ * descriptor it reports here (tests/test_capi_cpu.py checks the pairs over every shape). */
+int ocean_frame_plan(size_t texture_size, int cascades, int rows_variant, int32_t out[8]);
 
 /* ---- instrumentation (bench) ------------------------------------------------------------- */
 /* When enabled, each kernel launch of the generator is bracketed by HIP events on its stream. */

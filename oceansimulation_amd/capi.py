@@ -117,6 +117,8 @@ SIGNATURES = {
     "ocean_generator_slab_frame_put": (_i, [_vp, _vp, _f, _i]),
     "ocean_generator_slab_frame_put_pipelined": (_i, [_vp, _vp, _f, _i]),
     "ocean_peers_flush": (_i, [_vp]),
+    "ocean_frame_plan": (_i, [_sz, _i, _i, ctypes.POINTER(ctypes.c_int32)]),
+    "ocean_peers_debug_slot": (_i, [_vp, _i, ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(_sz)]),
     "ocean_generator_slab_put_columns": (_i, [_vp, _vp, _f, _i]),
     "ocean_generator_slab_put_rows": (_i, [_vp, _vp]),
     "ocean_peers_synchronize": (_i, [_vp]),

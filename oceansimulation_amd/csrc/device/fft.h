@@ -294,7 +294,10 @@ __device__ __forceinline__ void xsync()
 // Write the 16 stage outputs (padded indices wp(t), region reg_w), barrier, read back the next
 // stage's inputs for the thread's (possibly different) position i_r in region reg_r, barrier.
 // SPLIT: float4 data exchanged as two float2 lanes through a float2 buffer (half the LDS).
-template <int LOGN, int CI, bool SPLIT, bool WAVE = false, typename V, typename WP>
+// QUARTER (CPair only): the four floats re.x, re.y, im.x, im.y one at a time through a float buffer
+// (a quarter of the LDS, twice the split exchange's barriers), so a 1024-thread column workgroup
+// leaves room in the LDS for the H it keeps across its field rounds (k_cols_half QX).
+template <int LOGN, int CI, bool SPLIT, bool WAVE = false, bool QUARTER = false, typename V, typename WP>
 __device__ __forceinline__ void exchange(V* v, int reg_w, int i_r, int reg_r, void* lds_raw, WP wp)
 {
   using S = FftShape<LOGN>;
@@ -303,7 +306,35 @@ __device__ __forceinline__ void exchange(V* v, int reg_w, int i_r, int reg_r, vo
     touch(v[t]);
   return;
 #endif
-  if constexpr (!SPLIT)
+  if constexpr (QUARTER)
+  {
+    static_assert(sizeof(V) == 16 && SPLIT, "QUARTER exchange is for CPair data");
+    float* lds = reinterpret_cast<float*>(lds_raw);
+    auto get = [](const CPair& c, int q) { return q == 0 ? c.re.x : q == 1 ? c.re.y : q == 2 ? c.im.x : c.im.y; };
+    auto put = [](CPair& c, int q, float x) {
+      if (q == 0)
+        c.re.x = x;
+      else if (q == 1)
+        c.re.y = x;
+      else if (q == 2)
+        c.im.x = x;
+      else
+        c.im.y = x;
+    };
+#pragma unroll
+    for (int q = 0; q < 4; q++)
+    {
+#pragma unroll
+      for (int t = 0; t < 16; t++)
+        lds[lds_slot<CI, S::PADDED>(reg_w, wp(t))] = get(v[t], q);
+      xsync<WAVE>();
+#pragma unroll
+      for (int m = 0; m < 16; m++)
+        put(v[m], q, lds[lds_slot<CI, S::PADDED>(reg_r, read_pidx<LOGN>(i_r, m))]);
+      xsync<WAVE>();
+    }
+  }
+  else if constexpr (!SPLIT)
   {
     V* lds = reinterpret_cast<V*>(lds_raw);
 #pragma unroll
@@ -340,7 +371,7 @@ __device__ __forceinline__ void exchange(V* v, int reg_w, int i_r, int reg_r, vo
 // reg2. Any bijection (i, reg) -> (i2, reg2) over the workgroup is valid: it lets the global loads
 // and the global stores use different lane mappings for free. Transforms with a single stage
 // (N = 16) have no exchange and require i2 == i, reg2 == reg.
-template <int LOGN, int CI, bool SPLIT, bool WAVE = false, typename V>
+template <int LOGN, int CI, bool SPLIT, bool WAVE = false, bool QUARTER = false, typename V>
 __device__ __forceinline__ void fft_run(V* v, int i, int reg, int i2, int reg2, void* lds,
                                         const float2* __restrict__ tw)
 {
@@ -354,7 +385,7 @@ __device__ __forceinline__ void fft_run(V* v, int i, int reg, int i2, int reg2, 
     if constexpr (S::NSTAGE > 1)
     {
       const int base = 17 * i;  // pad16(16 i + t) = 17 i + t
-      exchange<LOGN, CI, SPLIT, WAVE>(v, reg, i2, reg2, lds, [&](int t) { return base + t; });
+      exchange<LOGN, CI, SPLIT, WAVE, QUARTER>(v, reg, i2, reg2, lds, [&](int t) { return base + t; });
     }
   }
   else
@@ -378,7 +409,7 @@ __device__ __forceinline__ void fft_run(V* v, int i, int reg, int i2, int reg2, 
         v[u + t * U] = w[t];
     }
     // output of butterfly b = i + u*T, element t -> y[b*R0 + t]; v index q = u + t*U
-    exchange<LOGN, CI, SPLIT, WAVE>(v, reg, i2, reg2, lds, [&](int q) {
+    exchange<LOGN, CI, SPLIT, WAVE, QUARTER>(v, reg, i2, reg2, lds, [&](int q) {
       int u = q % U, t = q / U;
       return pad16((i + u * T) * R0 + t);
     });
@@ -400,10 +431,10 @@ __device__ __forceinline__ void fft_run(V* v, int i, int reg, int i2, int reg2, 
       if (pp >= 16)
       {
         const int base = pad16(j), st = pp + pp / 16;
-        exchange<LOGN, CI, SPLIT, WAVE>(v, reg2, i2, reg2, lds, [&](int t) { return base + t * st; });
+        exchange<LOGN, CI, SPLIT, WAVE, QUARTER>(v, reg2, i2, reg2, lds, [&](int t) { return base + t * st; });
       }
       else
-        exchange<LOGN, CI, SPLIT, WAVE>(v, reg2, i2, reg2, lds, [&](int t) { return pad16(j + t * pp); });
+        exchange<LOGN, CI, SPLIT, WAVE, QUARTER>(v, reg2, i2, reg2, lds, [&](int t) { return pad16(j + t * pp); });
     }
     p *= 16;
   }

@@ -147,6 +147,10 @@ __device__ __forceinline__ void fft_cols_hx(CPair* v, int t, void* lds, const fl
 // round's field stores waits for them): bit 0, the scratch pairs of round r + 1 are loaded before
 // round r's stores (HS + HP); bits 1 / 2, the first 8 / all 16 h0 texels of the workgroup's next item
 // before round 2's stores (whole strips; the first item's in a prologue).
+// QX (round 6): the transform's LDS exchanges move one float at a time (fft.h QUARTER: 68 KiB instead of
+// 136 KiB at 4096, twice the barriers), so up to 5 of the thread's 8 H pairs fit in the LDS (HL) beside
+// HK in VGPRs: with HL + HK = 8 nothing goes through the scratch, and rounds 1 and 2 start on LDS reads
+// instead of scratch loads that a wave's vmcnt orders behind the previous round's field stores.
 // NYQ (whole grids): the Nyquist-row term (k_half_nyquist's spec, written to `send` as float4[C][2][N])
 // is computed by the workgroup of the last item slot, which has the fewest items, after them: one
 // launch per frame fewer (half_nyquist_texel, the same arithmetic as the kernel the slab paths use).
@@ -156,7 +160,8 @@ __device__ __forceinline__ void fft_cols_hx(CPair* v, int t, void* lds, const fl
 // per 4096^2 cascade, 0.935 -> 0.792 ms per 8, halfbench fb2h).
 template <int LOGN, int LA = 0, int SA = kStream, bool HS = false, bool SLAB = false, bool SEED = false, int RG = 1,
           int RGC = 1, int CPI = ColFirstCfg<LOGN>::B, bool HP = false, bool PC = false, int HL = 0, int HK = 0,
-          int HX = 0, int FB = 4, bool PUT = false, int HB = ColFirstCfg<LOGN>::B, int EARLY = 0, bool NYQ = false>
+          int HX = 0, int FB = 4, bool PUT = false, int HB = ColFirstCfg<LOGN>::B, int EARLY = 0, bool NYQ = false,
+          bool QX = false>
 __global__ __launch_bounds__(FftShape<LOGN>::T * CPI, CPI < ColFirstCfg<LOGN>::B ? 4 : 1) void k_cols_half(FrameParams fp, const float4* __restrict__ h0,
                                                                      float4* __restrict__ gab, float4* __restrict__ gde,
                                                                      float2* __restrict__ gc,
@@ -179,7 +184,8 @@ __global__ __launch_bounds__(FftShape<LOGN>::T * CPI, CPI < ColFirstCfg<LOGN>::B
   static_assert(!PUT || (SLAB && !PC), "PUT: the strip-dealt slab stores");
   static_assert(HB == B || (HB == CPI && HALVES == 2 && !SLAB), "HB: half strips over 2-column h0 strips");
   static_assert(!NYQ || !SLAB, "NYQ: whole grids (send is the spec output)");
-  constexpr int XB = CPI * S::PADDED * 8;  // the exchange's bytes (K::LDS1 for whole strips)
+  static_assert(!QX || (!HX && !PC), "QX: the fft_run transform");
+  constexpr int XB = CPI * S::PADDED * (QX ? 4 : 8);  // the exchange's bytes (K::LDS1 for whole strips; half with QX)
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   float2* tw = reinterpret_cast<float2*>(smem);
   void* xch = smem + ((S::TW_ENTRIES * 8 + 15) / 16) * 16;
@@ -379,7 +385,10 @@ __global__ __launch_bounds__(FftShape<LOGN>::T * CPI, CPI < ColFirstCfg<LOGN>::B
         io = HX == 2 ? 256 * (t >> 6) + ((t >> 2) & 15) : (t >> 6) + 16 * ((t >> 2) & 15);
       }
       else
-        fft_run<LOGN, CPI, true>(v, i, HALVES > 1 ? opaque((int)threadIdx.x) % CPI : b, xch, tw);
+      {
+        const int reg = HALVES > 1 ? opaque((int)threadIdx.x) % CPI : b;
+        fft_run<LOGN, CPI, true, false, QX>(v, i, reg, i, reg, xch, tw);
+      }
       if constexpr (EPAIR)
         if (round < 2)  // the next round's scratch pairs, before this round's stores
         {

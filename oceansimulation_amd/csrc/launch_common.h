@@ -75,6 +75,17 @@ inline int half_rows_variant = 1;
 inline int half_fields_fb(int logn, int cascades) { return logn == 12 && cascades <= 2 ? 2 : 4; }
 constexpr int kHalfRG2 = 4, kHalfRGC2 = 8;  // the FB = 2 layout's row groups
 
+// The whole-grid half-spectrum fields as one launcher writes / the other reads them: field strip width
+// FB, row groups of gab / gde (RG) and of gc (RGC), and the h0 strip width. launch_half_columns and
+// launch_half_rows each choose their kernel FROM their own descriptor (half_cols_layout /
+// half_rows_layout, launch_half.hip), and ocean_frame_plan reports both, so a CPU test can check every
+// (N, cascades, row-pass variant) pairs the layout the column pass writes with the one the row pass reads
+// (the round-4 fallback row pass read the FB = 4 layout the column pass no longer wrote at <= 2 cascades).
+struct HalfFieldLayout
+{
+  int fb, rg, rgc, h0_blk;
+};
+
 
 inline bool one_shot_grids(int cus)
 {

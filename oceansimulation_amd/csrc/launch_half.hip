@@ -7,6 +7,7 @@
 
 #include <cstdint>
 
+#include "oceanfft.h"
 #include "ocean_internal.h"
 #include "launch_common.h"
 #include "device/grid.h"
@@ -21,6 +22,26 @@ namespace oceanfft
 bool half_spectrum_supported(int logn) { return logn >= 10 && logn <= 12; }
 
 int half_h0_block(int logn, int cascades) { return half_fields_fb(logn, cascades) == 2 ? 2 : spectrum_block(logn); }
+
+// What launch_half_columns writes (and the h0 strips it reads): half strips into FB = 2 fields at 4096
+// with <= 2 cascades, else whole strips into the production row groups.
+HalfFieldLayout half_cols_layout(int logn, int cascades)
+{
+  if (half_fields_fb(logn, cascades) == 2)
+    return {2, kHalfRG2, kHalfRGC2, 2};
+  return {4, kHalfRG, kHalfRGC, spectrum_block(logn)};
+}
+
+// What launch_half_rows reads, per row-pass variant (1 = k_rows_hp at 4096, else k_rows_half).
+HalfFieldLayout half_rows_layout(int logn, int cascades, int variant)
+{
+  const int hb = spectrum_block(logn);  // not read by the row pass: reported as the whole-strip width
+  if (logn == 12 && variant == 1)
+    return half_fields_fb(logn, cascades) == 2 ? HalfFieldLayout{2, kHalfRG2, kHalfRGC2, 2} : HalfFieldLayout{4, kHalfRG, kHalfRGC, hb};
+  if (logn == 12 && half_fields_fb(logn, cascades) == 2)
+    return {2, kHalfRG2, kHalfRGC2, 2};
+  return {4, kHalfRG, kHalfRGC, hb};
+}
 
 size_t half_field_texels(int logn)
 {
@@ -60,10 +81,13 @@ hipError_t launch_half_columns(int logn, const FrameParams& fp, const float4* h0
       // evaluates h0 in round 0 and keeps kHalfHKSeed pairs in VGPRs.
       constexpr int RG = kHalfRG, RGC = kHalfRGC;
       constexpr int HKW = LOGN == 12 ? kHalfHK : 2;
+      const HalfFieldLayout lay = half_cols_layout(LOGN, fp.cascades);
       if constexpr (LOGN == 12)
       {
-        if (half_fields_fb(LOGN, fp.cascades) == 2)
+        if (lay.fb == 2)
         {
+          if (lay.rg != kHalfRG2 || lay.rgc != kHalfRGC2)
+            return hipErrorInvalidValue;  // the kernels below are instantiated for this layout only
           // half strips (FB = 2): 512-thread workgroups, two per CU (a 68-KiB exchange each)
           // h0 in 2-column strips (hb = 2, half_h0_block): each item streams its own strip
           constexpr int WGH = S::T * 2;
@@ -86,6 +110,8 @@ hipError_t launch_half_columns(int logn, const FrameParams& fp, const float4* h0
           return hipGetLastError();
         }
       }
+      if (lay.fb != 4 || lay.rg != RG || lay.rgc != RGC || lay.h0_blk != K::B)
+        return hipErrorInvalidValue;
       auto kern = seed ? k_cols_half<LOGN, 0, kStream, true, false, true, RG, RGC, K::B, true, false, kHalfHL, kHalfHKSeed,
                                      0, 4, false, K::B, 0, true>
                        : k_cols_half<LOGN, kStream, kStream, true, false, false, RG, RGC, K::B, true, false, kHalfHL, HKW, 0, 4,
@@ -123,6 +149,9 @@ hipError_t launch_half_rows(int logn, const FrameParams& fp, const float4* gab, 
       // workgroup, four per CU, the 4 rows of a gc line grouped on one XCD: 1.407 -> 1.377 ms per
       // 8 x 4096^2 against two-row workgroups (halfbench rowv 16), which stay below 4096.
       constexpr int RG = kHalfRG, RGC = kHalfRGC;
+      const HalfFieldLayout lay = half_rows_layout(LOGN, fp.cascades, half_rows_variant);
+      if (lay.fb == 2 ? (lay.rg != kHalfRG2 || lay.rgc != kHalfRGC2) : (lay.rg != RG || lay.rgc != RGC))
+        return hipErrorInvalidValue;  // the kernels below are instantiated for these two layouts only
       if constexpr (LOGN == 12)
       {
         if (half_rows_variant == 1)
@@ -130,7 +159,7 @@ hipError_t launch_half_rows(int logn, const FrameParams& fp, const float4* gab, 
           // whole strips: three workgroups per CU with image 1's (D, E) loads issued before image 0's
           // stores (EARLY 1, MINB 3): 1.362 / 1.366 -> 1.345 / 1.351 ms per 8 x 4096^2 on two boxes, maps
           // bit-identical (halfbench hpe, profiles/r05_halfbench_hpe2_8.log, r05_halfbench_hpe3_8.log)
-          auto kern = half_fields_fb(LOGN, fp.cascades) == 2 ? k_rows_hp<kHalfRG2, kHalfRGC2, false, false, 2, kHalfRGC2>
+          auto kern = lay.fb == 2 ? k_rows_hp<kHalfRG2, kHalfRGC2, false, false, 2, kHalfRGC2>
                                                              : k_rows_hp<RG, RGC, false, false, 4, 4, 1, 3>;
           const int grid = persistent_grid(kern, 256, HpCfg::LDS, fp.cascades * S::N, cus);
           hipLaunchKernelGGL(kern, dim3(grid), dim3(256), HpCfg::LDS, stream, fp, gab, gcd, ge, rcorr, maps, jac, foam, tw, 0,
@@ -143,7 +172,7 @@ hipError_t launch_half_rows(int logn, const FrameParams& fp, const float4* gab, 
       // the same one (FB = 2 with row groups 4 / 8 at 4096 and <= 2 cascades)
       auto kern = k_rows_half<LOGN, 0, kStream, 0, RPW, true, false, RG, RGC, 4, GRP>;
       if constexpr (LOGN == 12)
-        if (half_fields_fb(LOGN, fp.cascades) == 2)
+        if (lay.fb == 2)
           kern = k_rows_half<LOGN, 0, kStream, 0, RPW, true, false, kHalfRG2, kHalfRGC2, 2, GRP>;
       const int lds = ((S::TW_ENTRIES * 8 + 15) / 16) * 16 + lds_row_slots<LOGN>(RPW) * 8;
       const int grid = persistent_grid(kern, S::T * RPW, lds, fp.cascades * (S::N / RPW), cus);
@@ -155,3 +184,20 @@ hipError_t launch_half_rows(int logn, const FrameParams& fp, const float4* gab, 
 }
 
 }  // namespace oceanfft
+
+// The pairing table (include/oceanfft.h ocean_frame_plan): host only, no device needed.
+extern "C" int ocean_frame_plan(size_t texture_size, int cascades, int rows_variant, int32_t out[8])
+{
+  using namespace oceanfft;
+  int logn = 0;
+  while (logn < 15 && ((size_t)1 << logn) < texture_size)
+    logn++;
+  if (!out || ((size_t)1 << logn) != texture_size || !half_spectrum_supported(logn) || cascades < 1 ||
+      cascades > kMaxCascades || rows_variant < 0 || rows_variant > 1)
+    return OCEAN_ERR_INVALID;
+  const HalfFieldLayout c = half_cols_layout(logn, cascades), r = half_rows_layout(logn, cascades, rows_variant);
+  const int v[8] = {c.fb, c.rg, c.rgc, c.h0_blk, r.fb, r.rg, r.rgc, half_h0_block(logn, cascades)};
+  for (int k = 0; k < 8; k++)
+    out[k] = v[k];
+  return OCEAN_OK;
+}

@@ -143,7 +143,15 @@ struct ocean_generator
   // put stream after h0 writes on the generator's stream
   ocean_peers* peers = nullptr;
   hipEvent_t put_h0 = nullptr;
-  hipStream_t cols_stream = nullptr;  // the stream the last four-step column pass ran on
+  // Events, not stream handles: the peers' streams (and a caller's) may be destroyed or replaced
+  // between frames, and a recorded event stays valid (a stale `cols_stream`).
+  // cols_ev: the last strip-dealt / four-step column pass on its own stream (step 1 of a split put
+  // frame); the next column pass waits for it, on whatever stream (step 1 rewrites the parts; the
+  // strip-dealt pass reuses its H scratch); a no-op when both run on one stream.
+  // h0r_ev: the end of that pass's last h0 / h0row reader (the put stream's Nyquist-row kernel, which
+  // waited for step 1): every h0 / seed-constant write on the generator's stream waits for it.
+  hipEvent_t cols_ev = nullptr, h0r_ev = nullptr;
+  bool cols_ev_valid = false;
   // ocean_generator_set_frame_overlap (blocked half path): frame f's column pass on `side` into field
   // slot f % 2, beside frame f - 1's row pass on the generator's stream
   bool overlap = false;
@@ -669,6 +677,9 @@ int ocean_generator_destroy(ocean_generator* g)
     (void)hipStreamDestroy(g->comm_stream);
   if (g->put_h0)
     (void)hipEventDestroy(g->put_h0);
+  for (hipEvent_t ev : {g->cols_ev, g->h0r_ev})
+    if (ev)
+      (void)hipEventDestroy(ev);
   if (g->side)
   {
     (void)hipStreamSynchronize(g->side);
@@ -701,10 +712,24 @@ ocean_settings* ocean_generator_settings(ocean_generator* g, int c)
 }
 
 
+// h0, h0row and the fused re-seed constants are written on the generator's stream; a column pass that
+// ran on another stream (the one-sided exchange's step-1 / put streams) may still be reading them
+static int wait_h0_readers(ocean_generator* g)
+{
+  if (g->cols_ev_valid)
+    HIP_TRY(hipStreamWaitEvent(g->fft->stream, g->h0r_ev, 0), "h0 write: wait for the last column pass");
+  return OCEAN_OK;
+}
+
 // generateSpectrum with the given per-cascade settings (the current ones, or those a fused re-seed
 // frame evaluated h0 with, when that h0 image is materialised later)
 static int generate_spectrum_with(ocean_generator* g, const std::vector<ocean_settings>& settings)
 {
+  {
+    const int rc = wait_h0_readers(g);  // write-after-read on h0 (a pipelined put frame still in flight)
+    if (rc != OCEAN_OK)
+      return rc;
+  }
   g->h0_dirty = true;
   g->h0_stale = false;
   g->h0_block = h0_block(g);
@@ -833,6 +858,9 @@ static int generator_columns(ocean_generator* g, float timestep, int update_spec
         HIP_TRY(hipMalloc(&g->seedc, (size_t)kMaxCascades * seed_consts_bytes()), "seed constants");
       if (host != g->seedc_host)  // pageable source: staged before the call returns
       {
+        const int rc = wait_h0_readers(g);
+        if (rc != OCEAN_OK)
+          return rc;
         HIP_TRY(hipMemcpyAsync(g->seedc, host.data(), host.size(), hipMemcpyHostToDevice, f->stream), "seed constants");
         g->seedc_host.swap(host);
       }
@@ -885,19 +913,18 @@ static int generator_columns(ocean_generator* g, float timestep, int update_spec
     // last column pass on another stream (step 1 rewrites the parts its step 2 read; the strip-dealt
     // pass reuses its H scratch) and after h0 writes
     hipStream_t cs = col_stream ? col_stream : f->stream;
-    hipStream_t after = g->cols_stream && g->cols_stream != cs ? g->cols_stream
-                        : cs != f->stream && g->h0_dirty   ? f->stream
-                                                           : nullptr;
-    if (after)
+    // both orderings, independently: after the last column pass (whatever stream it ran on), and after
+    // the h0 writes on the generator's stream when this pass runs elsewhere
+    if (g->cols_ev_valid)
+      HIP_TRY(hipStreamWaitEvent(cs, g->cols_ev, 0), "column pass: after the last column pass");
+    if (cs != f->stream && g->h0_dirty)
     {
       if (!g->put_h0)
         HIP_TRY(hipEventCreateWithFlags(&g->put_h0, hipEventDisableTiming), "column pass: event");
-      HIP_TRY(hipEventRecord(g->put_h0, after), "column pass: stream event");
+      HIP_TRY(hipEventRecord(g->put_h0, f->stream), "column pass: stream event");
       HIP_TRY(hipStreamWaitEvent(cs, g->put_h0, 0), "column pass: stream order");
-      if (after == f->stream)
-        g->h0_dirty = false;
+      g->h0_dirty = false;  // only once the wait is enqueued
     }
-    g->cols_stream = cs;
     // profiling a put: kind 3 brackets the wait + put kernels inside the column pass (kind 1)
     Gen4Put timed_put = put ? *put : Gen4Put{};
     EventPair pp{3, nullptr, nullptr};
@@ -926,6 +953,13 @@ static int generator_columns(ocean_generator* g, float timestep, int update_spec
       HIP_TRY(hipEventRecord(pp.b, put && put->stream ? put->stream : cs), "column pass: put event");
       g->pending.push_back(pp);
     }
+    for (hipEvent_t* ev : {&g->cols_ev, &g->h0r_ev})
+      if (!*ev)
+        HIP_TRY(hipEventCreateWithFlags(ev, hipEventDisableTiming), "column pass: event");
+    HIP_TRY(hipEventRecord(g->cols_ev, cs), "column pass: end event");
+    // the h0 readers end on the put stream when step 2 runs there (it waited for step 1's handoff)
+    HIP_TRY(hipEventRecord(g->h0r_ev, put && put->stream ? put->stream : cs), "column pass: end event");
+    g->cols_ev_valid = true;
   }
   else if (put)
     return fail(OCEAN_ERR_INVALID, "column pass: the one-sided exchange needs a half-spectrum slab path (N >= 1024)");
@@ -1547,6 +1581,8 @@ struct ocean_peers
   int row_cus = 0;                   // the CUs the own row stream may use when masked (0: all)
   int caller_row_cus = 0;            // ocean_peers_set_row_cus: the caller's row stream's CUs (0: all)
   hipEvent_t rows_done = nullptr;    // pipelined rows on row_stream -> the generator's stream
+  hipEvent_t gen_ready = nullptr;    // the generator's stream -> pipelined rows (caller work on the maps)
+  bool failed = false;               // a wait timed out (ocean_peers_synchronize): frames are refused
   unsigned char* parts2 = nullptr;   // step 1's second parts slot
   hipEvent_t s1_done[2] = {nullptr, nullptr}, put_done[2] = {nullptr, nullptr};
   bool put_done_valid[2] = {false, false};
@@ -1576,6 +1612,10 @@ int check_peers(const ocean_generator* g, const ocean_peers* p, const char* who)
     return fail(OCEAN_ERR_INVALID, std::string(who) + ": null generator, or peers created for another generator");
   if (!p->connected)
     return fail(OCEAN_ERR_INVALID, std::string(who) + ": ocean_peers_connect has not run");
+  if (p->failed)
+    return fail(OCEAN_ERR_TIMEOUT, std::string(who) + ": a one-sided wait timed out earlier (ocean_peers_synchronize "
+                                                      "reported it); the ranks' flags are out of step: destroy and "
+                                                      "recreate the peers");
   if (!g->hslab || hslab_xbuf_bytes(g) != p->slot)
     return fail(OCEAN_ERR_INVALID, std::string(who) + ": the generator left the half-spectrum slab path (or its "
                                                       "exchange size changed) since ocean_peers_create");
@@ -1668,6 +1708,13 @@ int put_rows(ocean_generator* g, ocean_peers* p, bool pipelined = false)
     return fail(OCEAN_ERR_INVALID, "ocean_generator_slab_put_rows: no column pass issued for this frame");
   const int s = (int)(fr % 2);
   hipStream_t rs = pipelined ? p->row_stream : f->stream;
+  if (rs != f->stream)
+  {
+    // the row pass rewrites g->maps / jac: after the caller's work on the generator's stream (the
+    // header keeps the maps ordered there)
+    HIP_TRY(hipEventRecord(p->gen_ready, f->stream), "one-sided exchange: events");
+    HIP_TRY(hipStreamWaitEvent(rs, p->gen_ready, 0), "one-sided exchange: stream order");
+  }
   HIP_TRY(launch_peer_wait(peer_wait(p, kReadyWord, fr + 1), rs), "one-sided exchange: ready wait");
   const FrameParams newest = g->frame;
   g->frame = p->slot_frame[s];
@@ -1803,6 +1850,8 @@ int ocean_peers_create(ocean_peers** out, ocean_generator* g)
   if (e == hipSuccess)
     e = hipEventCreateWithFlags(&p->rows_done, hipEventDisableTiming);
   if (e == hipSuccess)
+    e = hipEventCreateWithFlags(&p->gen_ready, hipEventDisableTiming);
+  if (e == hipSuccess)
     e = hipDeviceSynchronize();
   int rc = e == hipSuccess ? peers_deadline(p) : OCEAN_OK;
   if (rc == OCEAN_OK && e == hipSuccess)
@@ -1835,8 +1884,9 @@ int ocean_peers_destroy(ocean_peers* p)
     for (hipEvent_t ev : {p->s1_done[k], p->put_done[k]})
       if (ev)
         (void)hipEventDestroy(ev);
-  if (p->rows_done)
-    (void)hipEventDestroy(p->rows_done);
+  for (hipEvent_t ev : {p->rows_done, p->gen_ready})
+    if (ev)
+      (void)hipEventDestroy(ev);
   for (void* q : {(void*)p->data, (void*)p->flags, (void*)p->table, (void*)p->parts2})
     if (q)
       (void)hipFree(q);
@@ -2036,10 +2086,29 @@ int ocean_peers_synchronize(ocean_peers* p)
   uint32_t err = 0;
   HIP_TRY(hipMemcpy(&err, p->flags + kErrWord, sizeof(err), hipMemcpyDeviceToHost), "ocean_peers_synchronize: status");
   if (err != 0)
+  {
+    // The word is sticky on the device (every later wait returns at once). Now that the streams are
+    // drained it is cleared, and the peers refuse further frames (check_peers): after a timeout the
+    // ranks' ready / freed counts no longer agree, so the only way on is a new peers object.
+    p->failed = true;
+    HIP_TRY(hipMemset(p->flags + kErrWord, 0, sizeof(uint32_t)), "ocean_peers_synchronize: clear status");
+    HIP_TRY(hipDeviceSynchronize(), "ocean_peers_synchronize: clear status");
     return fail(OCEAN_ERR_TIMEOUT, std::string("one-sided exchange: a wait for the peers' ") +
                                        (err - 1 == kReadyWord ? "blocks (ready)" : "slot release (freed)") +
                                        " timed out after " + std::to_string(p->timeout_ms) +
-                                       " ms; the frames since then are invalid");
+                                       " ms; the frames since then are invalid, and this peers object refuses new "
+                                       "frames");
+  }
+  return p->failed ? fail(OCEAN_ERR_TIMEOUT, "one-sided exchange: an earlier wait timed out; recreate the peers")
+                   : OCEAN_OK;
+}
+
+int ocean_peers_debug_slot(const ocean_peers* p, int slot, void** ptr, size_t* bytes)
+{
+  if (!p || !ptr || !bytes || slot < 0 || slot > 1)
+    return fail(OCEAN_ERR_INVALID, "ocean_peers_debug_slot: null argument or slot outside {0, 1}");
+  *ptr = p->data + (size_t)slot * p->slot;
+  *bytes = p->slot;
   return OCEAN_OK;
 }
 

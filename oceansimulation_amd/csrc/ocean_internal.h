@@ -152,6 +152,10 @@ size_t half_hs_bytes(int logn, int blocks);  // also the strip-dealt path's
 // h0's strip width for the whole-grid half path: the half-strip pass (4096, <= 2 cascades) reads
 // 2-column h0 strips (k_cols_half HB), the whole-strip pass the 4-column ones (spectrum_block)
 int half_h0_block(int logn, int cascades);
+// the layout the column pass writes / the row pass reads (launch_common.h HalfFieldLayout)
+struct HalfFieldLayout;
+HalfFieldLayout half_cols_layout(int logn, int cascades);
+HalfFieldLayout half_rows_layout(int logn, int cascades, int variant);
 // h0_blk: the strip width h0 is blocked in (0: spectrum_block; 2 only where the pass runs on half
 // strips, launch_common.h half_h0_block)
 hipError_t launch_half_columns(int logn, const FrameParams& fp, const float4* h0, float4* gab, float4* gcd, float2* ge,

@@ -178,12 +178,17 @@ __global__ __launch_bounds__(64) void k_peer_signal_release(uint32_t* const* __r
     __hip_atomic_store(flags[q] + word, value, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
-// k_peer_wait: one wave; lane q < ranks polls word `word0 + q` of this rank's flags until it reaches
-// `target` (as a wrapping difference). Every lane exits: on success, or when the wall clock passes
-// `deadline_ticks` after the start, in which case err[0] records the word range that timed out
-// (word0 + 1) and the frame goes on with whatever the slots hold; err is sticky, so the waits of
-// later frames return at once and the host reports the failure (ocean_peers_synchronize). A wait can
-// never hold the GPU past its deadline.
+// k_peer_wait: kPeerReleaseBlocks one-wave workgroups, dealt over the 8 XCDs like the release's; in
+// each, lane q < ranks polls word `word0 + q` of this rank's flags until it reaches `target` (as a
+// wrapping difference), then the wave runs a system-scope acquire fence. The acquire is symmetric to
+// the release (round 6): every XCD's L2 drops its clean copies of peer-written
+// lines (a slot the row pass of frame f - 2 read on all XCDs) from a wave running on that XCD, before
+// the row pass (the next launch on the stream, whose own kernel-start acquire also invalidates the
+// L1s and L2s) reads the slot; DESIGN.md §6 "Visibility". Every lane exits: on success, or when the
+// wall clock passes `deadline_ticks` after the start, in which case err[0] records the word range that
+// timed out (word0 + 1) and the frame goes on with whatever the slots hold; err stays set until
+// ocean_peers_synchronize reports it (the waits of later frames return at once), and the peers then
+// refuse new frames. A wait can never hold the GPU past its deadline.
 __global__ __launch_bounds__(64) void k_peer_wait(const uint32_t* __restrict__ flags, int word0, int ranks,
                                                   uint32_t target, long long deadline_ticks, uint32_t* __restrict__ err)
 {
@@ -225,8 +230,8 @@ hipError_t launch_peer_signal_release(uint32_t* const* flags, int ranks, int wor
 
 hipError_t launch_peer_wait(const PeerWait& w, hipStream_t stream)
 {
-  hipLaunchKernelGGL(k_peer_wait, dim3(1), dim3(64), 0, stream, w.flags, w.word0, w.ranks, w.target, w.deadline_ticks,
-                     w.err);
+  hipLaunchKernelGGL(k_peer_wait, dim3(kPeerReleaseBlocks), dim3(64), 0, stream, w.flags, w.word0, w.ranks, w.target,
+                     w.deadline_ticks, w.err);
   return hipGetLastError();
 }
 

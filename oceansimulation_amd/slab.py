@@ -254,6 +254,13 @@ class PeerExchange:
     def flush(self) -> None:
         check(lib().ocean_peers_flush(self._h), "ocean_peers_flush")
 
+    def debug_slot(self, slot: int):
+        """(device pointer, bytes) of receive slot `slot` (frame f lands in slot f % 2); debug only."""
+        ptr, nbytes = ctypes.c_void_p(), ctypes.c_size_t()
+        check(lib().ocean_peers_debug_slot(self._h, int(slot), ctypes.byref(ptr), ctypes.byref(nbytes)),
+              "ocean_peers_debug_slot")
+        return int(ptr.value), int(nbytes.value)
+
     def synchronize(self) -> None:
         """Wait for this rank's streams; raises OceanError (OCEAN_ERR_TIMEOUT) when a wait gave up."""
         check(lib().ocean_peers_synchronize(self._h), "ocean_peers_synchronize")

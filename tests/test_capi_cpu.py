@@ -220,3 +220,33 @@ def test_slab_layout_rejects_bad_geometry(capi):
     assert slab_layout(512, 1, 2, half=False)[:2] == (256, 256)
     with pytest.raises(OceanError):
         slab_layout(4096, 0, 2, half=2)  # the four-step path serves 8192 / 16384 only
+
+
+@pytest.mark.parametrize("n", [1024, 2048, 4096])
+def test_frame_plan_pairs_column_writes_with_row_reads(capi, n):
+    """ocean_frame_plan (host only): for every cascade count a launch can take and both row-pass variants,
+    the field layout the column pass writes (strip width, gab/gde and gc row groups) is the one the row
+    pass reads, and the h0 strips the column pass reads are the ones the seeding writes. Each launcher
+    picks its kernel from the descriptor reported here (launch_half.hip), so a mode that changed one
+    side's layout without the other's (round 4's fallback row pass) fails here, without a GPU."""
+    import ctypes
+
+    L = capi.lib()
+    seen = set()
+    for cascades in range(1, capi.OCEAN_MAX_CASCADES + 1):
+        for variant in (0, 1):
+            out = (ctypes.c_int32 * 8)()
+            assert L.ocean_frame_plan(n, cascades, variant, out) == capi.OCEAN_OK
+            cols, rows, seed_h0 = tuple(out[0:4]), tuple(out[4:7]), out[7]
+            assert cols[:3] == rows, (n, cascades, variant, cols, rows)
+            assert cols[3] == seed_h0, (n, cascades, variant, cols, seed_h0)
+            # whole 128-B lines per store: RG * FB * 16 B (gab / gde) and RGC * FB * 8 B (gc)
+            assert cols[1] * cols[0] * 16 == 128 and cols[2] * cols[0] * 8 == 128, cols
+            seen.add(cols)
+    # the half-strip shape exists only at 4096 (<= 2 cascades per launch)
+    assert (len(seen) == 2) == (n == 4096), seen
+    bad = (ctypes.c_int32 * 8)()
+    assert L.ocean_frame_plan(512, 1, 1, bad) == capi.OCEAN_ERR_INVALID  # below the half path
+    assert L.ocean_frame_plan(n, 0, 1, bad) == capi.OCEAN_ERR_INVALID
+    assert L.ocean_frame_plan(n, capi.OCEAN_MAX_CASCADES + 1, 1, bad) == capi.OCEAN_ERR_INVALID
+    assert L.ocean_frame_plan(n, 1, 2, bad) == capi.OCEAN_ERR_INVALID

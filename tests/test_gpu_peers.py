@@ -136,6 +136,201 @@ def test_put_exchange_in_one_process_bit_exact(ocean, n, P, four_step):
     fft.close()
 
 
+@pytest.mark.parametrize("n,P", [(8192, 2), (4096, 2)])
+def test_put_pipelined_reseeds_stream_changes_and_close_bit_exact(ocean, n, P):
+    """Stream-ordering cases of ADVICE r05, each bit-exact against the whole grid (re-seeded with the
+    seeding kernel, GenerateSpectrum, as the slabs are):
+    - pipelined put frames that re-seed h0 on every frame (the h0 memo off, so every re-seed writes
+      h0 on the generator's stream while the previous frame's step 1 / put may still read it on the
+      peers' streams), with a settings edit mid-run;
+    - the same after the put CU mask changes (the peers' streams destroyed and recreated) and on the
+      caller's streams (ocean_peers_set_streams), where the column pass must wait both for the last
+      column pass and for the h0 writes;
+    - after the peers are closed: device-copy frames whose column pass runs on the generator's
+      stream after the last one ran on a destroyed stream.
+    8192: the four-step slabs (step 1 and the put on two streams); 4096: the strip-dealt slabs."""
+    import torch
+
+    from oceansimulation_amd import capi
+    from oceansimulation_amd.hip import DeviceBuffer
+    from oceansimulation_amd.slab import PeerExchange, SlabGenerator, emulate_frame
+
+    L = capi.lib()
+    fft = ocean.FFTCalculator(n)
+    whole = ocean.Generator(fft, 1)
+    slabs = [SlabGenerator(fft, r, P) for r in range(P)]
+    for s in [whole.GetOceanSettings(0)] + [g.GetOceanSettings() for g in slabs]:
+        ocean.apply_settings(s, planeSize=777.0)
+    for g in slabs:
+        assert L.ocean_generator_set_h0_memo(g.handle, 0) == capi.OCEAN_OK
+    peers = [PeerExchange(g) for g in slabs]
+    for p in peers:
+        p.set_timeout(10000)
+    PeerExchange.connect_local(peers)
+
+    def edit(**kw):
+        for s in [whole.GetOceanSettings(0)] + [g.GetOceanSettings() for g in slabs]:
+            ocean.apply_settings(s, **kw)
+
+    def run(tag, steps, edits):
+        for k, dt in enumerate(steps):
+            if k in edits:
+                edit(**edits[k])
+            for g, p in zip(slabs, peers):
+                g.frame_put_pipelined(p, dt, True)
+            whole.GenerateSpectrum()
+            whole.CalculateOcean(dt)
+        for p in peers:
+            p.flush()
+        assert _same(L, slabs, whole, n) is None, (n, P, tag, _same(L, slabs, whole, n))
+
+    steps = [0.25, 1.0 / 30.0, 0.125, 0.5]
+    run("pipelined re-seeds", steps, {2: dict(U_10=31.0)})
+    for p in peers:
+        p.set_put_cu_mask(8)
+    run("re-seeds after a CU-mask change", steps, {1: dict(spread=0.4)})
+    sts = [torch.cuda.Stream() for _ in range(3)]
+    for p in peers:
+        p.set_streams(*(st.cuda_stream for st in sts))
+    run("re-seeds on the caller's streams", steps, {3: dict(swell=0.7)})
+    for p in peers:
+        p.synchronize()
+        p.set_streams(None, None, None)
+        p.close()
+    sends = [DeviceBuffer(g.exchange_bytes) for g in slabs]
+    recvs = [DeviceBuffer(g.exchange_bytes) for g in slabs]
+    edit(U_10=36.0)
+    for k, dt in enumerate((0.25, 1.0 / 60.0)):
+        emulate_frame(slabs, sends, recvs, dt, update_ocean=(k == 0))
+        if k == 0:
+            whole.GenerateSpectrum()
+        whole.CalculateOcean(dt)
+    assert _same(L, slabs, whole, n) is None, (n, P, "device-copy frames after close", _same(L, slabs, whole, n))
+    for g in slabs:
+        g.close()
+    whole.close()
+    fft.close()
+
+
+@pytest.mark.parametrize("n,P", [(1024, 2), (8192, 2)])
+def test_put_consumer_never_reads_stale_l2_lines(ocean, n, P):
+    """The consumer side of the one-sided exchange's memory ordering (DESIGN.md §6 "Visibility"): frame f's
+    blocks land in the slot frame f - 2's row pass read. Here every rank's slot is read into the L2s of
+    all XCDs (ocean_debug_copy, three grid shapes so each XCD's L2 holds its own share of the lines,
+    default-policy loads) just before the put that rewrites it; the stale copies differ from the new
+    blocks (another frame time). The row pass must still see the new blocks: its kernel-start acquire,
+    after the wait kernel observed every rank's ready word, drops every XCD's clean copies. Serial frames
+    on the generators' stream and pipelined frames on the caller's streams (the reads on the put stream
+    between frames), bit-exact against the whole grid. 1024: strip-dealt slabs, slots of ~21 MB (they fit
+    the 32 MB of L2); 8192: four-step slabs."""
+    import torch
+
+    from oceansimulation_amd import capi
+    from oceansimulation_amd.hip import DeviceBuffer
+    from oceansimulation_amd.slab import PeerExchange, SlabGenerator
+    from oceansimulation_amd.waves import debug_copy
+
+    L = capi.lib()
+    fft = ocean.FFTCalculator(n)
+    whole = ocean.Generator(fft, 1)
+    slabs = [SlabGenerator(fft, r, P) for r in range(P)]
+    for s in [whole.GetOceanSettings(0)] + [g.GetOceanSettings() for g in slabs]:
+        ocean.apply_settings(s, planeSize=61.0)
+    peers = [PeerExchange(g) for g in slabs]
+    for p in peers:
+        p.set_timeout(10000)
+    PeerExchange.connect_local(peers)
+    nbytes = peers[0].debug_slot(0)[1]
+    sink = DeviceBuffer(nbytes)
+
+    def touch(slot, stream=None):
+        for p in peers:
+            ptr, nb = p.debug_slot(slot)
+            for wgs in (1024, 1000, 1048):
+                debug_copy(sink.ptr, ptr, nb, wgs, stream)
+
+    steps = [0.5, 1.0 / 60.0, 0.25, 1.0 / 30.0, 0.125]
+    for k, dt in enumerate(steps):  # serial: frame k lands in slot k % 2
+        touch(k % 2)
+        for g, p in zip(slabs, peers):
+            g.put_columns(p, dt, k == 0)
+        for g, p in zip(slabs, peers):
+            g.put_rows(p)
+        whole.CalculateOcean(dt)
+        assert _same(L, slabs, whole, n) is None, (n, P, "serial", k, _same(L, slabs, whole, n))
+    sts = [torch.cuda.Stream() for _ in range(3)]
+    for p in peers:
+        p.set_streams(*(st.cuda_stream for st in sts))
+    f0 = len(steps)
+    for k, dt in enumerate(steps):  # pipelined: frame f0 + k's put follows the reads on the put stream
+        touch((f0 + k) % 2, sts[1].cuda_stream)
+        for g, p in zip(slabs, peers):
+            g.frame_put_pipelined(p, dt)
+        whole.CalculateOcean(dt)
+    for p in peers:
+        p.flush()
+    assert _same(L, slabs, whole, n) is None, (n, P, "pipelined", _same(L, slabs, whole, n))
+    for p in peers:
+        p.synchronize()
+        p.set_streams(None, None, None)
+        p.close()
+    for g in slabs:
+        g.close()
+    whole.close()
+    fft.close()
+
+
+def test_put_timeout_is_sticky_until_recreated(ocean):
+    """After a timed-out wait, ocean_peers_synchronize reports OCEAN_ERR_TIMEOUT once, clears the
+    device error word, and the peers refuse every further frame (the ranks' flag counts no longer
+    agree) instead of issuing frames whose waits return at once; new peers on the same generators work."""
+    from oceansimulation_amd import capi
+    from oceansimulation_amd.capi import OceanError
+    from oceansimulation_amd.slab import PeerExchange, SlabGenerator
+
+    L = capi.lib()
+    n = 8192
+    fft = ocean.FFTCalculator(n)
+    whole = ocean.Generator(fft, 1)
+    slabs = [SlabGenerator(fft, r, 2) for r in range(2)]
+    peers = [PeerExchange(g) for g in slabs]
+    PeerExchange.connect_local(peers)
+    peers[0].set_timeout(300)
+    slabs[0].put_columns(peers[0], 0.5, True)
+    slabs[0].put_rows(peers[0])
+    with pytest.raises(OceanError) as exc:
+        peers[0].synchronize()
+    assert exc.value.code == capi.OCEAN_ERR_TIMEOUT
+    with pytest.raises(OceanError) as exc:
+        slabs[0].frame_put(peers[0], 0.5)
+    assert exc.value.code == capi.OCEAN_ERR_TIMEOUT and "recreate" in str(exc.value)
+    with pytest.raises(OceanError):
+        peers[0].synchronize()
+    peers[1].synchronize()
+    for p in peers:
+        p.close()
+    # fresh peers: both ranks' frames land, bit-exact against the whole grid at the same time
+    peers = [PeerExchange(g) for g in slabs]
+    for p in peers:
+        p.set_timeout(10000)
+    PeerExchange.connect_local(peers)
+    for st in [whole.GetOceanSettings(0)] + [g.GetOceanSettings() for g in slabs]:
+        st.time = 0.0  # rank 0 advanced alone above
+    from oceansimulation_amd.slab import emulate_put_frame
+
+    emulate_put_frame(slabs, peers, 0.25, True)
+    whole.CalculateOcean(0.25)
+    for p in peers:
+        p.synchronize()
+    assert _same(L, slabs, whole, n) is None
+    for p in peers:
+        p.close()
+    for g in slabs:
+        g.close()
+    whole.close()
+    fft.close()
+
+
 def _free_port():
     s = socket.socket()
     s.bind(("127.0.0.1", 0))

@@ -833,6 +833,62 @@ int main(int argc, char** argv)
     }
     return 0;
   }
+  if (argc > 3 && std::strcmp(argv[3], "qx") == 0 && logn == 12)
+  {
+    // round 6: k_cols_half with quarter LDS exchanges (QX) so that all 8 H pairs stay on the CU (HL in
+    // the LDS + HK in VGPRs, no scratch), optionally with the next item's h0 loads before round 2's
+    // stores (EARLY 2 / 4), against production (HL 1 HK 4, split exchanges, 3 pairs in the scratch)
+    using S = FftShape<12>;
+    auto cols = [&](auto kern, int hl, bool qx) {
+      const int lds = ((S::TW_ENTRIES * 8 + 15) / 16) * 16 + 4 * S::PADDED * (qx ? 4 : 8) + hl * 1024 * 16;
+      return std::function<hipError_t()>([=] {
+        int grid = persistent_grid(kern, 1024, lds, fp.cascades * HalfCfg<12>::STRIPS, cus);
+        grid = grid > cus ? cus : grid;  // hs: cus slices of 16 x 1024 entries
+        hipLaunchKernelGGL(kern, dim3(grid), dim3(1024), lds, 0, fp, h0, gab, gcd, ge, tw, hs, HalfSlab{},
+                           (unsigned char*)spec, 1, nullptr);
+        return hipGetLastError();
+      });
+    };
+#define KQ(HL, HK, E, QX) k_cols_half<12, kStream, kStream, true, false, false, kHalfRG, kHalfRGC, 4, true, false, HL, HK, 0, 4, false, 4, E, true, QX>
+    std::vector<std::function<hipError_t()>> vc = {cols(KQ(1, 4, 0, false), 1, false), cols(KQ(1, 4, 0, true), 1, true),
+                                                   cols(KQ(4, 4, 0, true), 4, true),  cols(KQ(5, 3, 0, true), 5, true),
+                                                   cols(KQ(5, 3, 2, true), 5, true),  cols(KQ(4, 4, 2, true), 4, true),
+                                                   cols(KQ(5, 3, 4, true), 5, true)};
+#undef KQ
+    const char* nm[] = {"production (HL1 HK4)", "QX HL1 HK4", "QX HL4 HK4 (no scratch)", "QX HL5 HK3 (no scratch)",
+                        "QX HL5 HK3 EARLY 2", "QX HL4 HK4 EARLY 2", "QX HL5 HK3 EARLY 4"};
+    const int NV = 7;
+    CHECK(vc[0]());
+    CHECK(hipDeviceSynchronize());
+    auto pab = snap(gab, ht * sizeof(float4)), pde = snap(gcd, ht * sizeof(float4)), pc = snap(ge, ht * sizeof(float2));
+    std::vector<int> same(NV, 1);
+    for (int k = 1; k < NV; k++)
+    {
+      CHECK(hipMemset(gab, 0, ht * sizeof(float4)));
+      CHECK(hipMemset(gcd, 0, ht * sizeof(float4)));
+      CHECK(hipMemset(ge, 0, ht * sizeof(float2)));
+      CHECK(vc[k]());
+      CHECK(hipDeviceSynchronize());
+      std::printf("%s vs production: gab, gde, gc\n", nm[k]);
+      same[k] = (int)diff(snap(gab, ht * sizeof(float4)), pab) & (int)diff(snap(gcd, ht * sizeof(float4)), pde) &
+                (int)diff(snap(ge, ht * sizeof(float2)), pc);
+    }
+    std::vector<std::vector<float>> t(NV), tf(NV);
+    for (int r = 0; r < 9; r++)
+      for (int k = 0; k < NV; k++)
+      {
+        t[k].push_back(time_ms(vc[k], 10));
+        tf[k].push_back(time_ms([&] { CHECK(vc[k]()); return r1(); }, 10));
+      }
+    for (int k = 0; k < NV; k++)
+    {
+      std::sort(t[k].begin(), t[k].end());
+      std::sort(tf[k].begin(), tf[k].end());
+      std::printf("cols %-28s median %7.3f ms (%6.1f GB/s at 28.05 B/pt)  frame %7.3f ms  bit-identical %s\n", nm[k],
+                  t[k][4], 28.05 * pts / t[k][4] / 1e6, tf[k][4], same[k] ? "yes" : "NO");
+    }
+    return 0;
+  }
   if (argc > 3 && std::strcmp(argv[3], "hpe") == 0 && logn == 12)
   {
     // k_rows_hp with the next image's / row's loads issued before the stores (EARLY 1, 2) against

@@ -70,24 +70,26 @@ __global__ __launch_bounds__(RowCfg<LOGN>::WG, RowCfg<LOGN>::MIN_WAVES) void k_r
 // Column pass in place: strips of C texel columns, transformed along y.
 // GROUP: consecutive strips on blocks b, b + 8, ... (one XCD, xcd_group_slot), so the partial lines
 // of C-column pieces (C * 16 B) meet in one L2.
-template <int LOGN, int GROUP = 2>
-__global__ __launch_bounds__(ColCfg<LOGN>::WG) void k_cols(int n_images, float4* __restrict__ images,
-                                                           const float2* __restrict__ tw_glob)
+// CC: columns per strip (ColCfg's C by default: 16 at N <= 1024, one 1024-thread workgroup per strip).
+// With few images a 1024^2 image has only 64 such strips for 256 CUs; launch_cols then takes CC = 4
+// (256-thread workgroups, 256 strips per image), the same per-column arithmetic (round 6).
+template <int LOGN, int GROUP = 2, int CC = ColCfg<LOGN>::C>
+__global__ __launch_bounds__(FftShape<LOGN>::T * CC) void k_cols(int n_images, float4* __restrict__ images,
+                                                                 const float2* __restrict__ tw_glob)
 {
   using S = FftShape<LOGN>;
-  using K = ColCfg<LOGN>;
-  constexpr int T = S::T, C = K::C;
+  constexpr int T = S::T, C = CC, STRIPS = S::N / CC;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   float2* tw = reinterpret_cast<float2*>(smem);
   void* xch = smem + ((S::TW_ENTRIES * 8 + 15) / 16) * 16;
   load_twiddles<LOGN>(tw, tw_glob);
 
   const int c0 = threadIdx.x % C, i0 = threadIdx.x / C;
-  const int total = n_images * K::STRIPS;
+  const int total = n_images * STRIPS;
   for (int item = xcd_group_slot<GROUP>(blockIdx.x, gridDim.x); item < total; item += gridDim.x)
   {
     const int c = opaque(c0), i = opaque(i0);
-    const int img = item / K::STRIPS, strip = item - img * K::STRIPS;
+    const int img = item / STRIPS, strip = item - img * STRIPS;
     const int x = strip * C + c;
     // image rows i + mm*T: uniform base per mm (SGPR), lane offset (i*N + x)*16 shared by all mm
     float4* ibase = images + ((size_t)img << (2 * LOGN));

@@ -151,6 +151,12 @@ __device__ __forceinline__ void fft_cols_hx(CPair* v, int t, void* lds, const fl
 // 136 KiB at 4096, twice the barriers), so up to 5 of the thread's 8 H pairs fit in the LDS (HL) beside
 // HK in VGPRs: with HL + HK = 8 nothing goes through the scratch, and rounds 1 and 2 start on LDS reads
 // instead of scratch loads that a wave's vmcnt orders behind the previous round's field stores.
+// DELAY: see the kernel body (an A/B probe; production 0).
+// RSPLIT (round 6, small grids): one work slot per (item, field round), so the three rounds of a strip
+// run on three workgroups at once (each re-reads h0 and re-evolves H: 16 B of h0 per kept texel and
+// round instead of once); the slots of a strip sit on one XCD (xcd_group_slot<3>) so the two repeat
+// reads of its h0 lines are L2 hits. For grids whose column pass is one item's latency long (2048^2
+// with one cascade: 257 items on 512 workgroup slots).
 // NYQ (whole grids): the Nyquist-row term (k_half_nyquist's spec, written to `send` as float4[C][2][N])
 // is computed by the workgroup of the last item slot, which has the fewest items, after them: one
 // launch per frame fewer (half_nyquist_texel, the same arithmetic as the kernel the slab paths use).
@@ -161,7 +167,7 @@ __device__ __forceinline__ void fft_cols_hx(CPair* v, int t, void* lds, const fl
 template <int LOGN, int LA = 0, int SA = kStream, bool HS = false, bool SLAB = false, bool SEED = false, int RG = 1,
           int RGC = 1, int CPI = ColFirstCfg<LOGN>::B, bool HP = false, bool PC = false, int HL = 0, int HK = 0,
           int HX = 0, int FB = 4, bool PUT = false, int HB = ColFirstCfg<LOGN>::B, int EARLY = 0, bool NYQ = false,
-          bool QX = false>
+          bool QX = false, int DELAY = 0, bool RSPLIT = false>
 __global__ __launch_bounds__(FftShape<LOGN>::T * CPI, CPI < ColFirstCfg<LOGN>::B ? 4 : 1) void k_cols_half(FrameParams fp, const float4* __restrict__ h0,
                                                                      float4* __restrict__ gab, float4* __restrict__ gde,
                                                                      float2* __restrict__ gc,
@@ -191,9 +197,21 @@ __global__ __launch_bounds__(FftShape<LOGN>::T * CPI, CPI < ColFirstCfg<LOGN>::B
   void* xch = smem + ((S::TW_ENTRIES * 8 + 15) / 16) * 16;
   float4* hlds = reinterpret_cast<float4*>(static_cast<unsigned char*>(xch) + XB);  // HL pairs [p][thread]
   load_twiddles<LOGN>(tw, tw_glob);
+  if constexpr (DELAY > 0)
+    if ((int)blockIdx.x >= (int)gridDim.x / 2)
+    {
+      // DELAY (round 6, tools/microbench A/B): the second half of a two-per-CU grid starts DELAY
+      // wall-clock ticks (100 MHz) late, so the two workgroups of a CU run their store phases out of step
+      const long long t0 = wall_clock64();
+      while (wall_clock64() - t0 < DELAY)
+        __builtin_amdgcn_s_sleep(8);
+    }
 
   const int nstrips = SLAB ? hsl.nstrips : STRIPS;
   const int total = fp.cascades * nstrips * HALVES;
+  static_assert(!RSPLIT || (!HS && !SEED && !SLAB && HALVES == 1 && EARLY == 0 && !PC && !HX),
+                "RSPLIT: whole strips, h0 re-read per round");
+  constexpr int RS3 = RSPLIT ? 3 : 1;  // work slots per item
   const float dim = (float)N;
   constexpr int NPRE = 8 - HL - HK;  // scratch pairs per round (HP)
   constexpr bool EPAIR = (EARLY & 1) && HS && HP && !PC && NPRE > 0;
@@ -220,8 +238,11 @@ __global__ __launch_bounds__(FftShape<LOGN>::T * CPI, CPI < ColFirstCfg<LOGN>::B
       for (int m = 0; m < EH0; m++)
         apre[m] = ld4s<LA>(sp, lo, ((m + 8) & 15) * T * B * 16);
     }
-  for (int item = HALVES > 1 ? xcd_pair_slot(blockIdx.x, gridDim.x) : blockIdx.x; item < total; item += gridDim.x)
+  for (int slot = RSPLIT ? xcd_group_slot<3>(blockIdx.x, gridDim.x) : HALVES > 1 ? xcd_pair_slot(blockIdx.x, gridDim.x)
+                                                                              : (int)blockIdx.x;
+       slot < total * RS3; slot += gridDim.x)
   {
+    const int item = RSPLIT ? slot / 3 : slot;
     const int hh = HALVES > 1 ? item % HALVES : 0, si = HALVES > 1 ? item / HALVES : item;
     const int c = si / nstrips, s = si - c * nstrips;  // s: the rank's strip index
     const int sg = SLAB ? hsl.strip0 + s : s;           // global strip
@@ -502,7 +523,9 @@ __global__ __launch_bounds__(FftShape<LOGN>::T * CPI, CPI < ColFirstCfg<LOGN>::B
           st4s<SA>(gc + cgbase, half_group_offset<LOGN, RGC>(i, 0, ba) * 8, half_group_offset<LOGN, RGC>(m * T, 0) * 8, cc);
       }
     };
-    if constexpr (HS && PC)
+    if constexpr (RSPLIT)
+      run_round(slot % 3);
+    else if constexpr (HS && PC)
     {
       run_round(0);
       run_round(1);

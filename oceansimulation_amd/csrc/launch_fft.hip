@@ -297,8 +297,21 @@ hipError_t launch_cols(int logn, int n_images, float4* images, const float2* tw,
   return with_logn(logn, [&](auto L) -> hipError_t {
     constexpr int LOGN = decltype(L)::value;
     using K = ColCfg<LOGN>;
+    using S = FftShape<LOGN>;
     int lds = lds_bytes_cols<LOGN>();
     int items = n_images * K::STRIPS;
+    if constexpr (K::C > 4 && LOGN >= 8)
+      if (items < cus)
+      {
+        // fewer 16-column strips than CUs (one 1024^2 image: 64): 4-column strips, 256-thread
+        // workgroups; a strip pair's 64-B row pieces meet in one L2 (GROUP 2)
+        constexpr int CC = 4;
+        auto narrow = k_cols<LOGN, 2, CC>;
+        const int ldsn = ((S::TW_ENTRIES * 8 + 15) / 16) * 16 + CC * S::PADDED * 8;
+        const int grid = persistent_grid(narrow, S::T * CC, ldsn, n_images * (S::N / CC), cus);
+        hipLaunchKernelGGL(narrow, dim3(grid), dim3(S::T * CC), ldsn, stream, n_images, images, tw);
+        return hipGetLastError();
+      }
     auto kern = k_cols<LOGN>;
     int grid = persistent_grid(kern, K::WG, lds, items, cus);
     hipLaunchKernelGGL(kern, dim3(grid), dim3(K::WG), lds, stream, n_images, images, tw);

@@ -58,6 +58,26 @@ def _dev_equal(ptr_a: int, ptr_b: int, nbytes: int) -> bool:
     return eq
 
 
+# ---- configs[0..2]: bench.py's `configs` leg ------------------------------------------------------
+def test_bench_configs_leg_reports_every_small_config(ocean):
+    """bench.py's `configs` leg (BASELINE configs 1-3 on one GPU beside the CPU oracle), on a few steps:
+    every config reports points/s, kernel time and its roofline fraction against its own byte count
+    (116 B/pt on the 256^2 full-spectrum path, 64 B per EncodeIFFT texel, 84 B/pt at 2048^2), the
+    CPU oracle's rate beside it, and config 1's maps agree with the oracle's (1e-4 of each lane's max)."""
+    b = _bench()
+    out = b.configs_leg(steps=5, cpu_seconds=0.2)
+    for k in ("config1_256_scene", "config2_1024_encode_ifft", "config3_2048_full_payload", "config3_2048_x4_cascades"):
+        g, c = out[k]["gpu"], out[k]["cpu"]
+        assert g["points_per_s"] > 0 and c["points_per_s"] > 0, k
+        assert 0.0 < g["frac_hbm_peak"] < 1.0, (k, g)
+        assert out[k]["gpu_over_cpu"] > 1.0, k
+    assert out["config1_256_scene"]["gpu"]["frame_hbm_bytes_per_point"] == 116
+    assert abs(out["config3_2048_full_payload"]["gpu"]["frame_hbm_bytes_per_point"] - 84.1875) < 1e-9
+    assert out["config2_1024_encode_ifft"]["gpu"]["bytes_per_texel"] == 64
+    assert out["config1_256_scene"]["gpu"]["verified"], out["config1_256_scene"]["gpu"]
+    assert out["config3_2048_x4_cascades"]["gpu"]["points"] == 4 * 2048 * 2048
+
+
 # ---- configs[3]: 8 independent 4096^2 cascades, as bench.py times them ---------------------------
 def test_headline_batch_vs_oracle(ocean, oracle):
     """bench.py's step (rank 0's 8 cascades of 4096^2, plane sizes 5..4093 m) against the oracle

@@ -1064,4 +1064,69 @@ __global__ __launch_bounds__(1024) void k_rows_xs_r3(FrameParams fp, const float
   }
 }
 
+// Round 6: k_cols4_step2 on a resident grid (one 1024-thread workgroup per CU
+// looping over items) with the vmcnt ordering of k_rows_xs EARLY: the next item's first PF loads are
+// issued after this item's transform and before its 16 stores, so they do not queue behind the
+// stores; the last item re-reads its own (unconditional, so the registers are not kept live across
+// the loop as a second incoming value). Same arithmetic per column as production: bit-identical.
+template <int LOGN2, int PF, int CI = ColCfg<LOGN2>::C>
+__global__ __launch_bounds__(FftShape<LOGN2>::T * CI) void k_cols4_step2e(int images, int x0, int wc,
+                                                                         const float4* __restrict__ work,
+                                                                         float4* __restrict__ img,
+                                                                         const float2* __restrict__ tw_glob)
+{
+  using S = FftShape<LOGN2>;
+  constexpr int N2 = S::N, T = S::T, C = CI, LOGN = LOGN2 + 4, N = N2 * 16;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  float2* tw = reinterpret_cast<float2*>(smem);
+  void* xch = smem + ((S::TW_ENTRIES * 8 + 15) / 16) * 16;
+  load_twiddles<LOGN2>(tw, tw_glob);
+  const int c0 = threadIdx.x % C, i0 = threadIdx.x / C;
+  const int strips = wc / C;
+  const int total = images * 16 * strips;
+  auto src_of = [&](int item) __attribute__((always_inline)) {
+    const int strip = item % strips, rest = item / strips, k1 = rest & 15, im = rest >> 4;
+    return work + (size_t)im * N * wc + (size_t)N2 * k1 * wc + strip * C + opaque(c0);
+  };
+  auto ld = [&](const float4* src, int m) __attribute__((always_inline)) {
+    const f4v r = __builtin_nontemporal_load(reinterpret_cast<const f4v*>(src + (size_t)(opaque(i0) + m * T) * wc));
+    return raw_pair(make_float4(r.x, r.y, r.z, r.w));
+  };
+  CPair pre[PF > 0 ? PF : 1];
+  if (PF > 0 && (int)blockIdx.x < total)
+  {
+    const float4* s0 = src_of(blockIdx.x);
+#pragma unroll
+    for (int m = 0; m < PF; m++)
+      pre[m] = ld(s0, m);
+  }
+  for (int item = blockIdx.x; item < total; item += gridDim.x)
+  {
+    const int c = opaque(c0), i = opaque(i0);
+    const int strip = item % strips, rest = item / strips, k1 = rest & 15, im = rest >> 4;
+    const int xl = strip * C + c;
+    const float4* src = src_of(item);
+    CPair v[16];
+#pragma unroll
+    for (int m = 0; m < 16; m++)
+      v[m] = m < PF ? pre[m < PF ? m : 0] : ld(src, m);
+    fft_run<LOGN2, C, true>(v, i, c, xch, tw);
+    if constexpr (PF > 0)
+    {
+      const int nx = item + (int)gridDim.x < total ? item + (int)gridDim.x : item;
+      const float4* sn = src_of(nx);
+#pragma unroll
+      for (int m = 0; m < PF; m++)
+        pre[m] = ld(sn, m);
+    }
+    float4* dst = img + ((size_t)im << (2 * LOGN)) + (size_t)k1 * N + x0 + xl;
+#pragma unroll
+    for (int m = 0; m < 16; m++)
+    {
+      const float4 o = from_pair(v[m]);
+      __builtin_nontemporal_store(f4v{o.x, o.y, o.z, o.w}, reinterpret_cast<f4v*>(dst + (size_t)16 * (i + m * T) * N));
+    }
+  }
+}
+
 }  // namespace oceanfft

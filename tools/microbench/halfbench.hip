@@ -889,6 +889,284 @@ int main(int argc, char** argv)
     }
     return 0;
   }
+  if (argc > 3 && std::strcmp(argv[3], "qxh") == 0 && logn == 12 && C <= 2)
+  {
+    // round 6: the half-strip column pass (<= 2 cascades: 512-thread workgroups, two per CU, FB = 2
+    // fields, 2-column h0 strips) with quarter LDS exchanges so all 8 H pairs stay on the CU, against
+    // production; frame = + the production row pass (launch_half_rows reads the FB = 2 layout)
+    using S = FftShape<12>;
+    float4* h02;  // h0 in 2-column strips (half_h0_block): what the production half-strip pass reads
+    CHECK(hipMalloc(&h02, tex * C * sizeof(float4)));
+    for (int c = 0; c < C; c++)
+    {
+      OceanSettings st{};
+      st.seed[0] = 12342; st.seed[1] = 8934; st.U_10 = 40; st.theta_0 = 25; st.F = 800000; st.g = 9.8f;
+      st.swell = 0.5f; st.h = 100; st.displacement = 0.4f; st.planeSize = planes[c % 8]; st.scale = 1; st.spread = 0.2f;
+      CHECK(launch_generate_spectrum(st, n, h02 + tex * c, 0, cus, 0, 0, 2));
+    }
+    auto cols = [&](auto kern, int hl, bool qx) {
+      const int lds = ((S::TW_ENTRIES * 8 + 15) / 16) * 16 + 2 * S::PADDED * (qx ? 4 : 8) + hl * 512 * 16;
+      return std::function<hipError_t()>([=] {
+        int grid = persistent_grid(kern, 512, lds, fp.cascades * HalfCfg<12>::STRIPS * 2, cus);
+        grid = grid > 2 * cus ? 2 * cus : grid;  // hs: cus slices of 16 x 1024 entries = 2 cus half slices
+        hipLaunchKernelGGL(kern, dim3(grid), dim3(512), lds, 0, fp, h02, gab, gcd, ge, tw, hs, HalfSlab{},
+                           (unsigned char*)spec, 1, nullptr);
+        return hipGetLastError();
+      });
+    };
+#define KQH(HL, HK, QX) k_cols_half<12, kStream, kStream, true, false, false, kHalfRG2, kHalfRGC2, 2, true, false, HL, HK, 0, 2, false, 2, 0, true, QX>
+    std::vector<std::function<hipError_t()>> vc = {cols(KQH(1, 4, false), 1, false), cols(KQH(5, 3, true), 5, true),
+                                                   cols(KQH(4, 4, true), 4, true), cols(KQH(1, 4, true), 1, true)};
+#undef KQH
+    const char* nm[] = {"production half strips (HL1 HK4)", "QX HL5 HK3 (no scratch)", "QX HL4 HK4 (no scratch)",
+                        "QX HL1 HK4"};
+    const int NV = 4;
+    auto rows = [&] { return launch_half_rows(logn, fp, gab, gcd, ge, spec, maps, jac, foam, tw, 0, cus); };
+    CHECK(vc[0]());
+    CHECK(hipDeviceSynchronize());
+    auto pab = snap(gab, ht * sizeof(float4)), pde = snap(gcd, ht * sizeof(float4)), pc = snap(ge, ht * sizeof(float2));
+    std::vector<int> same(NV, 1);
+    for (int k = 1; k < NV; k++)
+    {
+      CHECK(hipMemset(gab, 0, ht * sizeof(float4)));
+      CHECK(hipMemset(gcd, 0, ht * sizeof(float4)));
+      CHECK(hipMemset(ge, 0, ht * sizeof(float2)));
+      CHECK(vc[k]());
+      CHECK(hipDeviceSynchronize());
+      std::printf("%s vs production: gab, gde, gc\n", nm[k]);
+      same[k] = (int)diff(snap(gab, ht * sizeof(float4)), pab) & (int)diff(snap(gcd, ht * sizeof(float4)), pde) &
+                (int)diff(snap(ge, ht * sizeof(float2)), pc);
+    }
+    std::vector<std::vector<float>> t(NV), tf(NV);
+    for (int r = 0; r < 9; r++)
+      for (int k = 0; k < NV; k++)
+      {
+        t[k].push_back(time_ms(vc[k], 20));
+        tf[k].push_back(time_ms([&] { CHECK(vc[k]()); return rows(); }, 20));
+      }
+    for (int k = 0; k < NV; k++)
+    {
+      std::sort(t[k].begin(), t[k].end());
+      std::sort(tf[k].begin(), tf[k].end());
+      std::printf("cols %-34s median %7.4f ms   frame %7.4f ms  bit-identical %s\n", nm[k], t[k][4], tf[k][4],
+                  same[k] ? "yes" : "NO");
+    }
+    CHECK(hipFree(h02));
+    return 0;
+  }
+  if (argc > 3 && std::strcmp(argv[3], "oneshot") == 0 && logn == 12)
+  {
+    // round 6: the whole-strip column pass on a one-shot grid (one workgroup per item, handed out in
+    // order by the dispatcher; the H scratch then needs one slice per item) against the production
+    // persistent grid of one workgroup per CU; fields bit-identical (same arithmetic per item)
+    using S = FftShape<12>;
+    const int items = fp.cascades * HalfCfg<12>::STRIPS;
+    float2* hsx;
+    CHECK(hipMalloc(&hsx, (size_t)items * 16 * 1024 * sizeof(float2)));
+    const int ldsw = ((S::TW_ENTRIES * 8 + 15) / 16) * 16 + ColFirstCfg<12>::LDS1 + kHalfHL * 1024 * 16;
+    auto kern = k_cols_half<12, kStream, kStream, true, false, false, kHalfRG, kHalfRGC, 4, true, false, kHalfHL, kHalfHK, 0, 4,
+                            false, 4, 0, true>;
+    auto run = [&](int grid, float2* scratch) {
+      return std::function<hipError_t()>([=] {
+        hipLaunchKernelGGL(kern, dim3(grid), dim3(1024), ldsw, 0, fp, h0, gab, gcd, ge, tw, scratch, HalfSlab{},
+                           (unsigned char*)spec, 1, nullptr);
+        return hipGetLastError();
+      });
+    };
+    std::vector<std::function<hipError_t()>> vc = {run(cus, hs), run(items, hsx), run(2 * cus, hsx), run(4 * cus, hsx)};
+    const char* nm[] = {"persistent, 1 per CU (production)", "one-shot (one workgroup per item)", "persistent, 2 x CUs",
+                        "persistent, 4 x CUs"};
+    const int NV = 4;
+    CHECK(vc[0]());
+    CHECK(hipDeviceSynchronize());
+    auto pab = snap(gab, ht * sizeof(float4)), pde = snap(gcd, ht * sizeof(float4)), pc = snap(ge, ht * sizeof(float2));
+    std::vector<int> same(NV, 1);
+    for (int k = 1; k < NV; k++)
+    {
+      CHECK(hipMemset(gab, 0, ht * sizeof(float4)));
+      CHECK(hipMemset(gcd, 0, ht * sizeof(float4)));
+      CHECK(hipMemset(ge, 0, ht * sizeof(float2)));
+      CHECK(vc[k]());
+      CHECK(hipDeviceSynchronize());
+      std::printf("%s vs production: gab, gde, gc\n", nm[k]);
+      same[k] = (int)diff(snap(gab, ht * sizeof(float4)), pab) & (int)diff(snap(gcd, ht * sizeof(float4)), pde) &
+                (int)diff(snap(ge, ht * sizeof(float2)), pc);
+    }
+    std::vector<std::vector<float>> t(NV), tf(NV);
+    for (int r = 0; r < 9; r++)
+      for (int k = 0; k < NV; k++)
+      {
+        t[k].push_back(time_ms(vc[k], 10));
+        tf[k].push_back(time_ms([&] { CHECK(vc[k]()); return r1(); }, 10));
+      }
+    for (int k = 0; k < NV; k++)
+    {
+      std::sort(t[k].begin(), t[k].end());
+      std::sort(tf[k].begin(), tf[k].end());
+      std::printf("cols %-36s median %7.4f ms (%6.1f GB/s at 28.05 B/pt)  frame %7.4f ms  bit-identical %s\n", nm[k],
+                  t[k][4], 28.05 * pts / t[k][4] / 1e6, tf[k][4], same[k] ? "yes" : "NO");
+    }
+    CHECK(hipFree(hsx));
+    return 0;
+  }
+  if (argc > 3 && std::strcmp(argv[3], "rsplit") == 0)
+  {
+    // round 6: one workgroup per (strip, field round) on a one-shot grid (k_cols_half RSPLIT: h0
+    // re-read and H re-evolved per round, the three slots of a strip on one XCD) against production;
+    // frame = + the production row pass. For the latency-bound small grids (BASELINE config 3: 2048^2,
+    // one cascade). Fields bit-identical (the same evolve and transform per round).
+    auto prod = [&] { return launch_half_columns(logn, fp, h0, gab, gcd, ge, spec, tw, 0, cus, hs, cus); };
+    auto rows = [&] { return launch_half_rows(logn, fp, gab, gcd, ge, spec, maps, jac, foam, tw, 0, cus); };
+    auto rsplit = [&](auto L, auto kern) {
+      constexpr int LG = decltype(L)::value;
+      using K = ColFirstCfg<LG>;
+      using S = FftShape<LG>;
+      const int lds = ((S::TW_ENTRIES * 8 + 15) / 16) * 16 + K::LDS1;
+      return std::function<hipError_t()>([=] {
+        const int slots = fp.cascades * HalfCfg<LG>::STRIPS * 3;
+        const int grid = (slots + 23) / 24 * 24;
+        (void)persistent_grid(kern, K::WG1, lds, slots, cus);  // sets the dynamic-LDS attribute
+        hipLaunchKernelGGL(kern, dim3(grid), dim3(K::WG1), lds, 0, fp, h0, gab, gcd, ge, tw, (float2*)nullptr, HalfSlab{},
+                           (unsigned char*)spec, 1, nullptr);
+        return hipGetLastError();
+      });
+    };
+    std::vector<std::function<hipError_t()>> vc = {prod};
+    auto add = [&](auto L) {
+      constexpr int LG = decltype(L)::value;
+      using K = ColFirstCfg<LG>;
+      vc.push_back(rsplit(L, k_cols_half<LG, 0, kStream, false, false, false, kHalfRG, kHalfRGC, K::B, false, false, 0, 0, 0,
+                                         4, false, K::B, 0, true, false, 0, true>));
+      vc.push_back(rsplit(L, k_cols_half<LG, kStream, kStream, false, false, false, kHalfRG, kHalfRGC, K::B, false, false, 0,
+                                         0, 0, 4, false, K::B, 0, true, false, 0, true>));
+    };
+    if (logn == 10)
+      add(std::integral_constant<int, 10>{});
+    else if (logn == 11)
+      add(std::integral_constant<int, 11>{});
+    else
+      add(std::integral_constant<int, 12>{});
+    const char* nm[] = {"production", "RSPLIT, h0 default policy", "RSPLIT, h0 streamed"};
+    const int NV = 3;
+    CHECK(vc[0]());
+    CHECK(hipDeviceSynchronize());
+    auto pab = snap(gab, ht * sizeof(float4)), pde = snap(gcd, ht * sizeof(float4)), pc = snap(ge, ht * sizeof(float2));
+    std::vector<int> same(NV, 1);
+    for (int k = 1; k < NV; k++)
+    {
+      CHECK(hipMemset(gab, 0, ht * sizeof(float4)));
+      CHECK(hipMemset(gcd, 0, ht * sizeof(float4)));
+      CHECK(hipMemset(ge, 0, ht * sizeof(float2)));
+      CHECK(vc[k]());
+      CHECK(hipDeviceSynchronize());
+      std::printf("%s vs production: gab, gde, gc\n", nm[k]);
+      same[k] = (int)diff(snap(gab, ht * sizeof(float4)), pab) & (int)diff(snap(gcd, ht * sizeof(float4)), pde) &
+                (int)diff(snap(ge, ht * sizeof(float2)), pc);
+    }
+    std::vector<std::vector<float>> t(NV), tf(NV);
+    for (int r = 0; r < 9; r++)
+      for (int k = 0; k < NV; k++)
+      {
+        t[k].push_back(time_ms(vc[k], 50));
+        tf[k].push_back(time_ms([&] { CHECK(vc[k]()); return rows(); }, 50));
+      }
+    std::printf("N=%d cascades=%d, rows alone %7.4f ms\n", n, C, time_ms(rows, 50));
+    for (int k = 0; k < NV; k++)
+    {
+      std::sort(t[k].begin(), t[k].end());
+      std::sort(tf[k].begin(), tf[k].end());
+      std::printf("cols %-28s median %7.4f ms   frame %7.4f ms (%5.3f of 8 TB/s at 84 B/pt)  bit-identical %s\n", nm[k],
+                  t[k][4], tf[k][4], 84.19 * pts / tf[k][4] / 1e6 / 8000.0, same[k] ? "yes" : "NO");
+    }
+    return 0;
+  }
+  if (argc > 3 && std::strcmp(argv[3], "desync") == 0 && logn == 12)
+  {
+    // round 6: half-strip column pass (512-thread workgroups, two per CU, FB = 2 fields, 2-column h0
+    // strips) at any cascade count, with the second half of the grid starting DELAY ticks late so the two
+    // workgroups of a CU store out of step; against the whole-strip production pass. Frames: + the row
+    // pass of each layout (k_rows_hp FB = 4 three per CU / FB = 2 four per CU). Fields compared per layout.
+    using S = FftShape<12>;
+    float4* h02;
+    CHECK(hipMalloc(&h02, tex * C * sizeof(float4)));
+    for (int c = 0; c < C; c++)
+    {
+      OceanSettings st{};
+      st.seed[0] = 12342; st.seed[1] = 8934; st.U_10 = 40; st.theta_0 = 25; st.F = 800000; st.g = 9.8f;
+      st.swell = 0.5f; st.h = 100; st.displacement = 0.4f; st.planeSize = planes[c % 8]; st.scale = 1; st.spread = 0.2f;
+      CHECK(launch_generate_spectrum(st, n, h02 + tex * c, 0, cus, 0, 0, 2));
+    }
+    const int ldsw = ((S::TW_ENTRIES * 8 + 15) / 16) * 16 + ColFirstCfg<12>::LDS1 + kHalfHL * 1024 * 16;
+    const int ldsh = ((S::TW_ENTRIES * 8 + 15) / 16) * 16 + 2 * S::PADDED * 8 + kHalfHL * 512 * 16;
+    auto whole = [&] {
+      auto kern = k_cols_half<12, kStream, kStream, true, false, false, kHalfRG, kHalfRGC, 4, true, false, kHalfHL, kHalfHK, 0, 4,
+                              false, 4, 0, true>;
+      int grid = persistent_grid(kern, 1024, ldsw, fp.cascades * HalfCfg<12>::STRIPS, cus);
+      grid = grid > cus ? cus : grid;
+      hipLaunchKernelGGL(kern, dim3(grid), dim3(1024), ldsw, 0, fp, h0, gab, gcd, ge, tw, hs, HalfSlab{}, (unsigned char*)spec,
+                         1, nullptr);
+      return hipGetLastError();
+    };
+    auto half = [&](auto kern, bool resident) {
+      return std::function<hipError_t()>([=] {
+        int grid = resident ? 2 * cus : persistent_grid(kern, 512, ldsh, fp.cascades * HalfCfg<12>::STRIPS * 2, cus);
+        grid = grid > 2 * cus ? 2 * cus : grid;
+        hipLaunchKernelGGL(kern, dim3(grid), dim3(512), ldsh, 0, fp, h02, gab, gcd, ge, tw, hs, HalfSlab{},
+                           (unsigned char*)spec, 1, nullptr);
+        return hipGetLastError();
+      });
+    };
+#define KD(D) k_cols_half<12, kStream, kStream, true, false, false, kHalfRG2, kHalfRGC2, 2, true, false, kHalfHL, kHalfHK, 0, 2, false, 2, 0, true, false, D>
+    std::vector<std::function<hipError_t()>> vc = {whole, half(KD(0), false), half(KD(0), true), half(KD(400), true),
+                                                   half(KD(800), true), half(KD(1600), true)};
+#undef KD
+    const char* nm[] = {"whole strips (production >= 3)", "half strips", "half strips, resident grid",
+                        "half, resident, delay 4 us", "half, resident, delay 8 us", "half, resident, delay 16 us"};
+    const int NV = 6;
+    auto rows4 = [&] {
+      auto kern = k_rows_hp<kHalfRG, kHalfRGC, false, false, 4, 4, 1, 3>;
+      const int grid = persistent_grid(kern, 256, HpCfg::LDS, fp.cascades * n, cus);
+      hipLaunchKernelGGL(kern, dim3(grid), dim3(256), HpCfg::LDS, 0, fp, gab, gcd, ge, spec, maps, jac, foam, tw, 0, RowSrc{});
+      return hipGetLastError();
+    };
+    auto rows2 = [&] {
+      auto kern = k_rows_hp<kHalfRG2, kHalfRGC2, false, false, 2, kHalfRGC2>;
+      const int grid = persistent_grid(kern, 256, HpCfg::LDS, fp.cascades * n, cus);
+      hipLaunchKernelGGL(kern, dim3(grid), dim3(256), HpCfg::LDS, 0, fp, gab, gcd, ge, spec, maps, jac, foam, tw, 0, RowSrc{});
+      return hipGetLastError();
+    };
+    CHECK(vc[0]());
+    CHECK(rows4());
+    CHECK(hipDeviceSynchronize());
+    auto pm = snap(maps, mb), pj = snap(jac, jb);
+    std::vector<int> same(NV, 1);
+    for (int k = 1; k < NV; k++)
+    {
+      CHECK(hipMemset(maps, 0, mb));
+      CHECK(hipMemset(jac, 0, jb));
+      CHECK(vc[k]());
+      CHECK(rows2());
+      CHECK(hipDeviceSynchronize());
+      std::printf("%s vs whole strips: maps, jacobian\n", nm[k]);
+      same[k] = (int)diff(snap(maps, mb), pm) & (int)diff(snap(jac, jb), pj);
+    }
+    std::vector<std::vector<float>> t(NV), tf(NV);
+    for (int r = 0; r < 9; r++)
+      for (int k = 0; k < NV; k++)
+      {
+        t[k].push_back(time_ms(vc[k], 10));
+        tf[k].push_back(time_ms([&] { CHECK(vc[k]()); return k == 0 ? rows4() : rows2(); }, 10));
+      }
+    for (int k = 0; k < NV; k++)
+    {
+      std::sort(t[k].begin(), t[k].end());
+      std::sort(tf[k].begin(), tf[k].end());
+      std::printf("cols %-34s median %7.4f ms   frame %7.4f ms  maps bit-identical %s\n", nm[k], t[k][4], tf[k][4],
+                  same[k] ? "yes" : "NO");
+    }
+    CHECK(hipFree(h02));
+    return 0;
+  }
   if (argc > 3 && std::strcmp(argv[3], "hpe") == 0 && logn == 12)
   {
     // k_rows_hp with the next image's / row's loads issued before the stores (EARLY 1, 2) against

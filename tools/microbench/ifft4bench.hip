@@ -188,6 +188,76 @@ static int ci_mode(int cus)
   return 0;
 }
 
+// "early": 2 images of 16384^2 through a 2048-column work slab; step 2 as production (one-shot grid)
+// against k_cols4_step2e (resident grid, the next item's first PF loads before this item's stores),
+// PF = 0 / 4 / 8 / 16; all bit-identical (round 6).
+static int early_mode(int cus)
+{
+  constexpr int logn = 14, n = 1 << logn, imgs = 2, wc = 2048;
+  const size_t tex = (size_t)n * n * imgs;
+  float4 *img, *work;
+  CHECK(hipMalloc(&img, tex * 16));
+  CHECK(hipMalloc(&work, ifft_fourstep_work_texels(logn, wc) * 16));
+  hipLaunchKernelGGL(fill_img, dim3(4096), dim3(256), 0, 0, img, tex);
+  auto t1 = table(logn), t2 = table(logn - 4);
+  float2 *tw, *tw2;
+  CHECK(hipMalloc(&tw, t1.size() * 8));
+  CHECK(hipMalloc(&tw2, t2.size() * 8));
+  CHECK(hipMemcpy(tw, t1.data(), t1.size() * 8, hipMemcpyHostToDevice));
+  CHECK(hipMemcpy(tw2, t2.data(), t2.size() * 8, hipMemcpyHostToDevice));
+  std::vector<float4> base(tex), ref(tex), got(tex);
+  CHECK(hipDeviceSynchronize());
+  CHECK(hipMemcpy(base.data(), img, tex * 16, hipMemcpyDeviceToHost));
+  using S2 = FftShape<logn - 4>;
+  using K2 = ColCfg<logn - 4>;
+  const int lds2 = lds_bytes_cols<logn - 4>();
+  auto with_step2 = [&](auto k2, bool resident) {
+    return std::function<hipError_t()>([=] {
+      hipError_t e = launch_rows_ifft(logn, imgs, img, tw, 0, cus);
+      if (e != hipSuccess)
+        return e;
+      auto k1 = k_cols4_step1<logn>;
+      for (int im = 0; im < imgs; im++)
+        for (int x0 = 0; x0 < n; x0 += wc)
+        {
+          float4* im0 = img + ((size_t)im << (2 * logn));
+          const int g1 = persistent_grid(k1, 256, 0, (wc / 64) * ((n / 16) / 4), cus);
+          hipLaunchKernelGGL(k1, dim3(g1), dim3(256), 0, 0, 1, x0, wc, im0, work, tw);
+          const int items = 16 * (wc / K2::C);
+          const int g2 = resident ? resident_grid(k2, K2::WG, lds2, items, cus) : persistent_grid(k2, K2::WG, lds2, items, cus);
+          hipLaunchKernelGGL(k2, dim3(g2), dim3(K2::WG), lds2, 0, 1, x0, wc, work, im0, tw2);
+        }
+      return hipGetLastError();
+    });
+  };
+  std::vector<std::string> names = {"production (one-shot)", "step2e PF 0 (resident)", "step2e PF 4", "step2e PF 8",
+                                    "step2e PF 16"};
+  std::vector<std::function<hipError_t()>> runs = {
+      with_step2(k_cols4_step2<logn - 4>, false), with_step2(k_cols4_step2e<logn - 4, 0>, true),
+      with_step2(k_cols4_step2e<logn - 4, 4>, true), with_step2(k_cols4_step2e<logn - 4, 8>, true),
+      with_step2(k_cols4_step2e<logn - 4, 16>, true)};
+  (void)sizeof(S2);
+  for (size_t k = 0; k < runs.size(); k++)
+  {
+    CHECK(hipMemcpy(img, base.data(), tex * 16, hipMemcpyHostToDevice));
+    CHECK(runs[k]());
+    CHECK(hipDeviceSynchronize());
+    CHECK(hipMemcpy(k == 0 ? ref.data() : got.data(), img, tex * 16, hipMemcpyDeviceToHost));
+    if (k > 0)
+      std::printf("%s: %s\n", names[k].c_str(), std::memcmp(ref.data(), got.data(), tex * 16) == 0 ? "bit-identical" : "DIFFERS");
+  }
+  std::vector<std::vector<float>> t(runs.size());
+  for (int r = 0; r < 5; r++)
+    for (size_t k = 0; k < runs.size(); k++)
+      t[k].push_back(time_ms(runs[k], 3));
+  for (size_t k = 0; k < runs.size(); k++)
+  {
+    std::sort(t[k].begin(), t[k].end());
+    std::printf("2 x 16384^2 EncodeIFFT, step 2 %-24s median %7.3f ms\n", names[k].c_str(), t[k][2]);
+  }
+  return 0;
+}
+
 int main(int argc, char** argv)
 {
   int cus = 0;
@@ -196,6 +266,8 @@ int main(int argc, char** argv)
     return mall_mode(cus);
   if (argc > 1 && std::strcmp(argv[1], "ci") == 0)
     return ci_mode(cus);
+  if (argc > 1 && std::strcmp(argv[1], "early") == 0)
+    return early_mode(cus);
   for (int logn : {13, 14})
   {
     const int n = 1 << logn, imgs = logn == 13 ? (argc > 1 ? std::atoi(argv[1]) : 4) : 1;

@@ -231,11 +231,11 @@ static int early_mode(int cus)
     });
   };
   std::vector<std::string> names = {"production (one-shot)", "step2e PF 0 (resident)", "step2e PF 4", "step2e PF 8",
-                                    "step2e PF 16"};
+                                    "step2e PF 16", "step2e PF 0 one-shot"};
   std::vector<std::function<hipError_t()>> runs = {
       with_step2(k_cols4_step2<logn - 4>, false), with_step2(k_cols4_step2e<logn - 4, 0>, true),
       with_step2(k_cols4_step2e<logn - 4, 4>, true), with_step2(k_cols4_step2e<logn - 4, 8>, true),
-      with_step2(k_cols4_step2e<logn - 4, 16>, true)};
+      with_step2(k_cols4_step2e<logn - 4, 16>, true), with_step2(k_cols4_step2e<logn - 4, 0>, false)};
   (void)sizeof(S2);
   for (size_t k = 0; k < runs.size(); k++)
   {

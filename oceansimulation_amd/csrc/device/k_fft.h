@@ -350,6 +350,10 @@ __global__ __launch_bounds__(256) void k_cols4_step1(int images, int x0, int wc,
 // reference layout. Loads and stores are C * 16 = 256-byte row pieces. tw_glob: the N2-point table.
 // CI: columns per workgroup (ColCfg's 16 = 1024 threads at N2 = 1024, production; 8 = 512 threads, two
 // per CU, as k_gen4_step2: 10.62 against 10.00 ms for 2 x 16384^2, tools/microbench/ifft4bench ci).
+// Round 6: the item's source address and the lane offsets are formed per load from opaque() values
+// (src_of / ld), which keeps the kernel at 112 VGPRs; the earlier form spilled 8 VGPRs (36 B) at the
+// 128 of a 1024-thread workgroup. 2 x 16384^2: 10.009 -> 9.753 ms on one box (ifft4bench early,
+// profiles/r06_ifft4bench_early2.log), bit-identical.
 template <int LOGN2, bool WNT = true, int CI = ColCfg<LOGN2>::C>
 __global__ __launch_bounds__(FftShape<LOGN2>::T * CI) void k_cols4_step2(int images, int x0, int wc,
                                                                         const float4* __restrict__ work,
@@ -365,24 +369,30 @@ __global__ __launch_bounds__(FftShape<LOGN2>::T * CI) void k_cols4_step2(int ima
   const int c0 = threadIdx.x % C, i0 = threadIdx.x / C;
   const int strips = wc / C;
   const int total = images * 16 * strips;
+  auto src_of = [&](int item) __attribute__((always_inline)) {
+    const int strip = item % strips, rest = item / strips, k1 = rest & 15, im = rest >> 4;
+    return work + (size_t)im * N * wc + (size_t)N2 * k1 * wc + strip * C + opaque(c0);
+  };
+  auto ld = [&](const float4* src, int m) __attribute__((always_inline)) {
+    const float4* p = src + (size_t)(opaque(i0) + m * T) * wc;
+    if constexpr (WNT)
+    {
+      const f4v r = __builtin_nontemporal_load(reinterpret_cast<const f4v*>(p));
+      return raw_pair(make_float4(r.x, r.y, r.z, r.w));
+    }
+    else
+      return raw_pair(*p);
+  };
   for (int item = blockIdx.x; item < total; item += gridDim.x)
   {
     const int c = opaque(c0), i = opaque(i0);
     const int strip = item % strips, rest = item / strips, k1 = rest & 15, im = rest >> 4;
     const int xl = strip * C + c;
-    const float4* src = work + (size_t)im * N * wc + (size_t)N2 * k1 * wc + xl;
+    const float4* src = src_of(item);
     CPair v[16];
 #pragma unroll
     for (int m = 0; m < 16; m++)
-    {
-      if constexpr (WNT)
-      {
-        const f4v r = __builtin_nontemporal_load(reinterpret_cast<const f4v*>(src + (size_t)(i + m * T) * wc));
-        v[m] = raw_pair(make_float4(r.x, r.y, r.z, r.w));
-      }
-      else
-        v[m] = raw_pair(src[(size_t)(i + m * T) * wc]);
-    }
+      v[m] = ld(src, m);
     fft_run<LOGN2, C, true>(v, i, c, xch, tw);
     float4* dst = img + ((size_t)im << (2 * LOGN)) + (size_t)k1 * N + x0 + xl;
 #pragma unroll

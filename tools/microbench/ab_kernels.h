@@ -1129,4 +1129,140 @@ __global__ __launch_bounds__(FftShape<LOGN2>::T * CI) void k_cols4_step2e(int im
   }
 }
 
+// Round 6: the in-place EncodeIFFT row pass (k_rows_ifft, one 1024-thread workgroup per 16384-point row)
+// on a resident grid with the next row's first PF loads issued after this row's transform and before
+// its 16 stores (k_rows_xs EARLY); the last row re-reads its own. Whole rows only (N = 16384, RPW 1).
+template <int LOGN, int PF>
+__global__ __launch_bounds__(RowCfg<LOGN>::WG, RowCfg<LOGN>::MIN_WAVES) void k_rows_ifft_early(
+    int rows, float4* __restrict__ images, const float2* __restrict__ tw_glob)
+{
+  using S = FftShape<LOGN>;
+  using R = RowCfg<LOGN>;
+  static_assert(R::RPW == 1, "whole rows");
+  constexpr int N = S::N, T = S::T;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  float2* tw = reinterpret_cast<float2*>(smem);
+  void* xch = smem + ((S::TW_ENTRIES * 8 + 15) / 16) * 16;
+  load_twiddles<LOGN>(tw, tw_glob);
+  const int i0 = threadIdx.x;
+  auto ld = [&](int row, int m) __attribute__((always_inline)) {
+    return to_pair(ld4(images + ((size_t)row << LOGN) + ((m + 8) & 15) * T, opaque(i0) * 16));
+  };
+  CPair pre[PF > 0 ? PF : 1];
+  if (PF > 0 && (int)blockIdx.x < rows)
+  {
+#pragma unroll
+    for (int m = 0; m < PF; m++)
+      pre[m] = ld(blockIdx.x, m);
+  }
+  for (int row = blockIdx.x; row < rows; row += gridDim.x)
+  {
+    const int i = opaque(i0);
+    CPair v[16];
+#pragma unroll
+    for (int m = 0; m < 16; m++)
+      v[m] = m < PF ? pre[m < PF ? m : 0] : ld(row, m);
+    fft_run<LOGN, 0, R::SPLIT>(v, i, 0, xch, tw);
+    if constexpr (PF > 0)
+    {
+      const int nx = row + (int)gridDim.x < rows ? row + (int)gridDim.x : row;
+#pragma unroll
+      for (int m = 0; m < PF; m++)
+        pre[m] = ld(nx, m);
+    }
+    float4* line = images + ((size_t)row << LOGN);
+#pragma unroll
+    for (int m = 0; m < 16; m++)
+      st4(line + m * T, i * 16, from_pair(v[m]));
+  }
+}
+
+// Round 6: the 16384 four-step work slab blocked in strips of 16 columns, [strip][N rows][16], so that
+// step 2's item (k1, strip) reads one contiguous 256-KiB run (1 KiB per wave load) instead of 256-B
+// pieces 32 KiB apart; step 1 then stores 256-B pieces (4 per wave store) instead of 1-KiB runs.
+// Same arithmetic as k_cols4_step1 / k_cols4_step2: bit-identical images.
+template <int LOGN>
+__global__ __launch_bounds__(256) void k_cols4_step1b(int images, int x0, int wc, const float4* __restrict__ img,
+                                                      float4* __restrict__ work, const float2* __restrict__ tw_glob)
+{
+  using S = FftShape<LOGN>;
+  constexpr int N = S::N, N2 = N / 16;
+  __shared__ float2 tw[S::TW_ENTRIES];
+  load_twiddles<LOGN>(tw, tw_glob);
+  const int xblocks = wc / 64;
+  const int total = images * xblocks * (N2 / 4);
+  for (int item = blockIdx.x; item < total; item += gridDim.x)
+  {
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    int t = item;
+    const int xbk = t % xblocks;
+    t /= xblocks;
+    const int n2 = (t % (N2 / 4)) * 4 + wv, im = t / (N2 / 4);
+    const int xl = xbk * 64 + lane;
+    const float4* src = img + ((size_t)im << (2 * LOGN)) + x0 + xl;
+    CPair v[16];
+#pragma unroll
+    for (int n1 = 0; n1 < 16; n1++)
+    {
+      const f4v r = __builtin_nontemporal_load(reinterpret_cast<const f4v*>(src + (size_t)(N2 * ((n1 + 8) & 15) + n2) * N));
+      v[n1] = to_pair(make_float4(r.x, r.y, r.z, r.w));
+    }
+    idft16(v);
+    apply_stage_twiddles<LOGN>(v, n2, tw);
+    float4* dst = work + (size_t)im * N * wc + (size_t)(xl >> 4) * N * 16 + (xl & 15);
+#pragma unroll
+    for (int k1 = 0; k1 < 16; k1++)
+    {
+      const float4 o = pair_raw(v[k1]);
+      __builtin_nontemporal_store(f4v{o.x, o.y, o.z, o.w}, reinterpret_cast<f4v*>(dst + (size_t)(N2 * k1 + n2) * 16));
+    }
+  }
+}
+
+template <int LOGN2, int CI = ColCfg<LOGN2>::C>
+__global__ __launch_bounds__(FftShape<LOGN2>::T * CI) void k_cols4_step2b(int images, int x0, int wc,
+                                                                         const float4* __restrict__ work,
+                                                                         float4* __restrict__ img,
+                                                                         const float2* __restrict__ tw_glob)
+{
+  using S = FftShape<LOGN2>;
+  constexpr int N2 = S::N, T = S::T, C = CI, LOGN = LOGN2 + 4, N = N2 * 16;
+  static_assert(C == 16, "16-column strips");
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  float2* tw = reinterpret_cast<float2*>(smem);
+  void* xch = smem + ((S::TW_ENTRIES * 8 + 15) / 16) * 16;
+  load_twiddles<LOGN2>(tw, tw_glob);
+  const int c0 = threadIdx.x % C, i0 = threadIdx.x / C;
+  const int strips = wc / C;
+  const int total = images * 16 * strips;
+  auto src_of = [&](int item) __attribute__((always_inline)) {
+    const int strip = item % strips, rest = item / strips, k1 = rest & 15, im = rest >> 4;
+    return work + (size_t)im * N * wc + ((size_t)strip * N + (size_t)N2 * k1) * 16 + opaque(c0);
+  };
+  auto ld = [&](const float4* src, int m) __attribute__((always_inline)) {
+    const f4v r = __builtin_nontemporal_load(reinterpret_cast<const f4v*>(src + (size_t)(opaque(i0) + m * T) * 16));
+    return raw_pair(make_float4(r.x, r.y, r.z, r.w));
+  };
+  for (int item = blockIdx.x; item < total; item += gridDim.x)
+  {
+    const int c = opaque(c0), i = opaque(i0);
+    const int strip = item % strips, rest = item / strips, k1 = rest & 15, im = rest >> 4;
+    const int xl = strip * C + c;
+    const float4* src = src_of(item);
+    CPair v[16];
+#pragma unroll
+    for (int m = 0; m < 16; m++)
+      v[m] = ld(src, m);
+    fft_run<LOGN2, C, true>(v, i, c, xch, tw);
+    float4* dst = img + ((size_t)im << (2 * LOGN)) + (size_t)k1 * N + x0 + xl;
+#pragma unroll
+    for (int m = 0; m < 16; m++)
+    {
+      const float4 o = from_pair(v[m]);
+      __builtin_nontemporal_store(f4v{o.x, o.y, o.z, o.w},
+                                  reinterpret_cast<f4v*>(dst + (size_t)16 * (i + m * T) * N));
+    }
+  }
+}
+
 }  // namespace oceanfft

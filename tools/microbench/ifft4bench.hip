@@ -211,12 +211,12 @@ static int early_mode(int cus)
   using S2 = FftShape<logn - 4>;
   using K2 = ColCfg<logn - 4>;
   const int lds2 = lds_bytes_cols<logn - 4>();
-  auto with_step2 = [&](auto k2, bool resident) {
+  auto with_step2 = [&](auto k2, bool resident, bool blocked = false) {
     return std::function<hipError_t()>([=] {
       hipError_t e = launch_rows_ifft(logn, imgs, img, tw, 0, cus);
       if (e != hipSuccess)
         return e;
-      auto k1 = k_cols4_step1<logn>;
+      auto k1 = blocked ? k_cols4_step1b<logn> : k_cols4_step1<logn>;
       for (int im = 0; im < imgs; im++)
         for (int x0 = 0; x0 < n; x0 += wc)
         {
@@ -236,14 +236,33 @@ static int early_mode(int cus)
       with_step2(k_cols4_step2<logn - 4>, false), with_step2(k_cols4_step2e<logn - 4, 0>, true),
       with_step2(k_cols4_step2e<logn - 4, 4>, true), with_step2(k_cols4_step2e<logn - 4, 8>, true),
       with_step2(k_cols4_step2e<logn - 4, 16>, true), with_step2(k_cols4_step2e<logn - 4, 0>, false)};
+  names.push_back("slab blocked in 16-column strips");
+  runs.push_back(with_step2(k_cols4_step2b<logn - 4>, false, true));
+  // the row pass alone: production k_rows_ifft (one-shot) against k_rows_ifft_early PF 0 / 4 / 8 (resident)
+  const int ldsr = lds_bytes_rows<logn>();
+  auto rows_with = [&](auto kern, bool resident) {
+    return std::function<hipError_t()>([=] {
+      const int items = imgs * n;
+      const int g = resident ? resident_grid(kern, RowCfg<logn>::WG, ldsr, items, cus)
+                             : persistent_grid(kern, RowCfg<logn>::WG, ldsr, items, cus);
+      hipLaunchKernelGGL(kern, dim3(g), dim3(RowCfg<logn>::WG), ldsr, 0, items, img, tw);
+      return hipGetLastError();
+    });
+  };
+  const size_t first_rows = runs.size();
+  names.insert(names.end(), {"rows: production (one-shot)", "rows: early PF 0 (resident)", "rows: early PF 4",
+                             "rows: early PF 8"});
+  runs.insert(runs.end(), {rows_with(k_rows_ifft<logn>, false), rows_with(k_rows_ifft_early<logn, 0>, true),
+                           rows_with(k_rows_ifft_early<logn, 4>, true), rows_with(k_rows_ifft_early<logn, 8>, true)});
   (void)sizeof(S2);
   for (size_t k = 0; k < runs.size(); k++)
   {
+    const bool first = k == 0 || k == first_rows;
     CHECK(hipMemcpy(img, base.data(), tex * 16, hipMemcpyHostToDevice));
     CHECK(runs[k]());
     CHECK(hipDeviceSynchronize());
-    CHECK(hipMemcpy(k == 0 ? ref.data() : got.data(), img, tex * 16, hipMemcpyDeviceToHost));
-    if (k > 0)
+    CHECK(hipMemcpy(first ? ref.data() : got.data(), img, tex * 16, hipMemcpyDeviceToHost));
+    if (!first)
       std::printf("%s: %s\n", names[k].c_str(), std::memcmp(ref.data(), got.data(), tex * 16) == 0 ? "bit-identical" : "DIFFERS");
   }
   std::vector<std::vector<float>> t(runs.size());
@@ -253,7 +272,7 @@ static int early_mode(int cus)
   for (size_t k = 0; k < runs.size(); k++)
   {
     std::sort(t[k].begin(), t[k].end());
-    std::printf("2 x 16384^2 EncodeIFFT, step 2 %-24s median %7.3f ms\n", names[k].c_str(), t[k][2]);
+    std::printf("2 x 16384^2 EncodeIFFT, %-30s median %7.3f ms\n", names[k].c_str(), t[k][2]);
   }
   return 0;
 }

@@ -239,7 +239,8 @@ int ocean_generator_slab_flush(ocean_generator* gen);
  * straight into rank q's receive slot, through a mapping of rank q's device memory (hipIpc handles
  * exchanged by the caller), and the row pass reads its own slot. Per frame each rank raises one
  * flag word in every rank's flag array after its stores ("ready") and one after its row pass has
- * read its slot ("freed"); the waits for them are one-wave kernels on the streams, bounded by a
+ * read its slot ("freed"); the waits for them are small kernels on the streams (one wave per workgroup,
+ * dealt over every XCD, each ending in a system-scope acquire), bounded by a
  * timeout (ocean_peers_set_timeout), so a missing peer never holds the GPU: the frame goes on, and
  * ocean_peers_synchronize reports OCEAN_ERR_TIMEOUT. Every half-spectrum slab path (N >= 1024): on the
  * four-step slabs (N = 8192 / 16384) step 2 puts, on the strip-dealt ones the column pass itself; the

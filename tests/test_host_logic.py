@@ -296,3 +296,21 @@ def test_cu_mask_sets_split_every_xcd():
 
     with pytest.raises(ValueError):
         b.reserved_cu_set("stride", dev, 32)
+
+
+def test_fft8_index_model():
+    """device/k_cols_small.h's radix-8 Stockham schedule (first stage radix 2^(log2 N mod 3), then radix 8;
+    thread i holds x[i + m N/8] and ends with X[i + m N/8]), played on the host (tools/fft8_model.py),
+    equals N * ifft at every size the small-grid column pass runs (1024, 2048) and beside them."""
+    import importlib.util
+
+    spec = importlib.util.spec_from_file_location("fft8_model", os.path.join(ROOT, "tools", "fft8_model.py"))
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    rng = np.random.default_rng(0)
+    for logn in (9, 10, 11):
+        n = 1 << logn
+        x = rng.standard_normal(n) + 1j * rng.standard_normal(n)
+        got = mod.fft8_model(x, logn)
+        ref = np.fft.ifft(x) * n
+        assert np.max(np.abs(got - ref)) <= 1e-9 * np.max(np.abs(ref)), logn

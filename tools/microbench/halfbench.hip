@@ -1009,6 +1009,76 @@ int main(int argc, char** argv)
     CHECK(hipFree(hsx));
     return 0;
   }
+  if (argc > 3 && std::strcmp(argv[3], "small") == 0 && logn <= 11)
+  {
+    // round 6: the small-grid column pass (k_cols_small: 8 points per thread, radix-8 Stockham, H in
+    // VGPRs, N / 8 threads per column) against production k_cols_half; frame = + the production row
+    // pass. The fields differ by FFT rounding only: max |diff| / max |field| is printed per field.
+    auto prod = [&] { return launch_half_columns(logn, fp, h0, gab, gcd, ge, spec, tw, 0, cus, hs, cus); };
+    auto rows = [&] { return launch_half_rows(logn, fp, gab, gcd, ge, spec, maps, jac, foam, tw, 0, cus); };
+    std::function<hipError_t()> small;
+    auto mk = [&](auto L) {
+      constexpr int LG = decltype(L)::value;
+      using CS = ColsSmallCfg<LG>;
+      auto kern = k_cols_small<LG, kHalfRG, kHalfRGC>;
+      small = [=] {
+        const int grid = persistent_grid(kern, CS::WG, CS::LDS, fp.cascades * HalfCfg<LG>::STRIPS, cus);
+        hipLaunchKernelGGL(kern, dim3(grid), dim3(CS::WG), CS::LDS, 0, fp, h0, gab, gcd, ge, tw, spec);
+        return hipGetLastError();
+      };
+    };
+    if (logn == 10)
+      mk(std::integral_constant<int, 10>{});
+    else
+      mk(std::integral_constant<int, 11>{});
+    auto rel = [](const std::vector<unsigned char>& a, const std::vector<unsigned char>& b) {
+      const float* x = reinterpret_cast<const float*>(a.data());
+      const float* y = reinterpret_cast<const float*>(b.data());
+      double mx = 0, er = 0;
+      for (size_t k = 0; k < a.size() / 4; k++)
+      {
+        mx = std::max(mx, (double)std::fabs(x[k]));
+        er = std::max(er, (double)std::fabs(x[k] - y[k]));
+      }
+      return er / (mx > 0 ? mx : 1);
+    };
+    CHECK(prod());
+    CHECK(hipDeviceSynchronize());
+    auto pab = snap(gab, ht * sizeof(float4)), pde = snap(gcd, ht * sizeof(float4)), pc = snap(ge, ht * sizeof(float2));
+    auto psp = snap(spec, (size_t)C * 2 * n * sizeof(float4));
+    CHECK(rows());
+    CHECK(hipDeviceSynchronize());
+    auto pm = snap(maps, mb);
+    CHECK(hipMemset(gab, 0, ht * sizeof(float4)));
+    CHECK(hipMemset(gcd, 0, ht * sizeof(float4)));
+    CHECK(hipMemset(ge, 0, ht * sizeof(float2)));
+    CHECK(hipMemset(spec, 0, (size_t)C * 2 * n * sizeof(float4)));
+    CHECK(small());
+    CHECK(hipDeviceSynchronize());
+    std::printf("k_cols_small vs production, max |diff| / max: gab %.3g  gde %.3g  gc %.3g  spec %.3g\n",
+                rel(pab, snap(gab, ht * sizeof(float4))), rel(pde, snap(gcd, ht * sizeof(float4))),
+                rel(pc, snap(ge, ht * sizeof(float2))), rel(psp, snap(spec, (size_t)C * 2 * n * sizeof(float4))));
+    CHECK(rows());
+    CHECK(hipDeviceSynchronize());
+    std::printf("maps from k_cols_small's fields vs production: max |diff| / max %.3g\n", rel(pm, snap(maps, mb)));
+    std::vector<std::function<hipError_t()>> vc = {prod, small};
+    const char* nm[] = {"production k_cols_half", "k_cols_small (8 points/thread)"};
+    std::vector<std::vector<float>> t(2), tf(2);
+    for (int r = 0; r < 9; r++)
+      for (int k = 0; k < 2; k++)
+      {
+        t[k].push_back(time_ms(vc[k], 50));
+        tf[k].push_back(time_ms([&] { CHECK(vc[k]()); return rows(); }, 50));
+      }
+    for (int k = 0; k < 2; k++)
+    {
+      std::sort(t[k].begin(), t[k].end());
+      std::sort(tf[k].begin(), tf[k].end());
+      std::printf("N=%d C=%d cols %-32s median %7.4f ms   frame %7.4f ms (%5.3f of 8 TB/s at 84 B/pt)\n", n, C, nm[k],
+                  t[k][4], tf[k][4], 84.19 * pts / tf[k][4] / 1e6 / 8000.0);
+    }
+    return 0;
+  }
   if (argc > 3 && std::strcmp(argv[3], "rsplit") == 0)
   {
     // round 6: one workgroup per (strip, field round) on a one-shot grid (k_cols_half RSPLIT: h0

@@ -12,7 +12,6 @@
 #include "launch_common.h"
 #include "device/grid.h"
 #include "device/k_half_cols.h"
-#include "device/k_cols_small.h"
 #include "device/k_half_rows.h"
 #include "device/k_rows_hp.h"
 #include "device/spectrum.h"

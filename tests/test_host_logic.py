@@ -299,7 +299,7 @@ def test_cu_mask_sets_split_every_xcd():
 
 
 def test_fft8_index_model():
-    """device/k_cols_small.h's radix-8 Stockham schedule (first stage radix 2^(log2 N mod 3), then radix 8;
+    """tools/microbench/k_cols_small.h's radix-8 Stockham schedule (first stage radix 2^(log2 N mod 3), then radix 8;
     thread i holds x[i + m N/8] and ends with X[i + m N/8]), played on the host (tools/fft8_model.py),
     equals N * ifft at every size the small-grid column pass runs (1024, 2048) and beside them."""
     import importlib.util

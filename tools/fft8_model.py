@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Host model of device/k_cols_small.h's fft8_run: the radix-8 Stockham index arithmetic (a first stage
+"""Host model of tools/microbench/k_cols_small.h's fft8_run: the radix-8 Stockham index arithmetic (a first stage
 of radix R0 = 2^(log2 N mod 3) with span 1, then radix-8 stages with span p; thread i holds x[i + m T],
 T = N / 8, and ends holding X[i + m T]) played on the host against N * ifft
 (tests/test_host_logic.py::test_fft8_index_model)."""

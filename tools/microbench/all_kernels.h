@@ -9,3 +9,4 @@
 #include "k_rows_xp.h"
 #include "../../oceansimulation_amd/csrc/device/k_rows_hp.h"
 #include "ab_kernels.h"
+#include "k_cols_small.h"

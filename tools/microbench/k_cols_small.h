@@ -1,4 +1,4 @@
-// device/k_cols_small.h — the half-spectrum column pass for whole grids that fill only part of the GPU
+// tools/microbench/k_cols_small.h (round 6, measured and not kept: DESIGN.md §4) — the half-spectrum column pass for whole grids that fill only part of the GPU
 // (N = 1024 / 2048 with one or two cascades; BASELINE config 3 is one cascade of 2048^2): the same
 // evolve (resources/spectrum.compute:183-240) and y iFFT of the five Hermitian field multiples of H as
 // k_cols_half (device/k_half_cols.h), with EIGHT points per thread instead of sixteen.

@@ -1009,6 +1009,93 @@ int main(int argc, char** argv)
     CHECK(hipFree(hsx));
     return 0;
   }
+  if (argc > 3 && std::strcmp(argv[3], "hs4d") == 0 && logn == 12)
+  {
+    // round 6: half-strip pass 1 (two 512-thread workgroups per CU, 2-column h0 strips) into the whole
+    // strips' 4-column fields, each 128-B field line written as two 64-B halves by the two items of a
+    // strip (paired on one XCD), with DEFAULT-policy stores so that L2 merges the halves before writing
+    // the line back; round 5's hs4 measured this layout with streamed (nt) stores: 2.48 ms. Frames with
+    // the production whole-strip row pass (k_rows_hp FB 4, three per CU, EARLY 1; four per CU at <= 2
+    // cascades); at <= 2 cascades also the production half-strip shape (FB 2). Maps vs production.
+    using K = ColFirstCfg<12>;
+    using S = FftShape<12>;
+    float4* h0b2;
+    CHECK(hipMalloc(&h0b2, tex * C * sizeof(float4)));
+    for (int c = 0; c < C; c++)
+    {
+      OceanSettings st{};
+      st.seed[0] = 12342; st.seed[1] = 8934; st.U_10 = 40; st.theta_0 = 25; st.F = 800000; st.g = 9.8f;
+      st.swell = 0.5f; st.h = 100; st.displacement = 0.4f; st.planeSize = planes[c % 8]; st.scale = 1; st.spread = 0.2f;
+      CHECK(launch_generate_spectrum(st, n, h0b2 + tex * c, 0, cus, 0, 0, 2));
+    }
+    const int tw0 = ((S::TW_ENTRIES * 8 + 15) / 16) * 16;
+    const int lds4 = tw0 + K::LDS1 + kHalfHL * 1024 * 16, lds2 = tw0 + 2 * S::PADDED * 8 + kHalfHL * 512 * 16;
+    auto cols = [&](auto kern, int wg, int lds, const float4* hsrc) {
+      return std::function<hipError_t()>([=] {
+        const int items = fp.cascades * HalfCfg<12>::STRIPS * (K::WG1 / wg);
+        int grid = persistent_grid(kern, wg, lds, items, cus);
+        const int slices = cus * (1024 / wg);
+        grid = grid > slices ? slices : grid;
+        hipLaunchKernelGGL(kern, dim3(grid), dim3(wg), lds, 0, fp, hsrc, gab, gcd, ge, tw, hs, HalfSlab{},
+                           (unsigned char*)spec, 1, nullptr);
+        return hipGetLastError();
+      });
+    };
+    auto rows4 = [&] {
+      auto kern = C <= 2 ? k_rows_hp<kHalfRG, kHalfRGC> : k_rows_hp<kHalfRG, kHalfRGC, false, false, 4, 4, 1, 3>;
+      const int grid = persistent_grid(kern, 256, HpCfg::LDS, fp.cascades * n, cus);
+      hipLaunchKernelGGL(kern, dim3(grid), dim3(256), HpCfg::LDS, 0, fp, gab, gcd, ge, spec, maps, jac, foam, tw, 0, RowSrc{});
+      return hipGetLastError();
+    };
+    auto prod_cols = [&] { return launch_half_columns(logn, fp, C <= 2 ? h0b2 : h0, gab, gcd, ge, spec, tw, 0, cus, hs, cus, nullptr, C <= 2 ? 2 : 0); };
+    auto prod_rows = [&] { return launch_half_rows(logn, fp, gab, gcd, ge, spec, maps, jac, foam, tw, 0, cus); };
+    std::vector<std::function<hipError_t()>> vc = {
+        cols(k_cols_half<12, kStream, kStream, true, false, false, kHalfRG, kHalfRGC, 4, true, false, kHalfHL, kHalfHK, 0, 4, false, 4, 0, true>, 1024, lds4, h0),
+        cols(k_cols_half<12, kStream, kStream, true, false, false, kHalfRG, kHalfRGC, 2, true, false, kHalfHL, 4, 0, 4, false, 2, 0, true>, 512, lds2, h0b2),
+        cols(k_cols_half<12, kStream, 0, true, false, false, kHalfRG, kHalfRGC, 2, true, false, kHalfHL, 4, 0, 4, false, 2, 0, true>, 512, lds2, h0b2)};
+    std::vector<std::function<hipError_t()>> vr = {rows4, rows4, rows4};
+    std::vector<const char*> nm = {"whole strips (FB 4)", "half strips -> FB 4, nt stores", "half strips -> FB 4, default stores"};
+    if (C <= 2)
+    {
+      vc.push_back(prod_cols);
+      vr.push_back(prod_rows);
+      nm.push_back("production at <= 2 (FB 2)");
+    }
+    const int NV = (int)vc.size();
+    CHECK(vc[0]());
+    CHECK(vr[0]());
+    CHECK(hipDeviceSynchronize());
+    auto pm = snap(maps, mb), pj = snap(jac, jb);
+    std::vector<int> same(NV, 1);
+    for (int k = 1; k < NV; k++)
+    {
+      CHECK(hipMemset(maps, 0, mb));
+      CHECK(hipMemset(jac, 0, jb));
+      CHECK(vc[k]());
+      CHECK(vr[k]());
+      CHECK(hipDeviceSynchronize());
+      std::printf("%s vs whole strips: maps, jacobian\n", nm[k]);
+      same[k] = (int)diff(snap(maps, mb), pm) & (int)diff(snap(jac, jb), pj);
+    }
+    std::vector<std::vector<float>> t(NV), tr(NV), tf(NV);
+    for (int r = 0; r < 9; r++)
+      for (int k = 0; k < NV; k++)
+      {
+        t[k].push_back(time_ms(vc[k], 10));
+        tr[k].push_back(time_ms(vr[k], 10));
+        tf[k].push_back(time_ms([&] { CHECK(vc[k]()); return vr[k](); }, 10));
+      }
+    for (int k = 0; k < NV; k++)
+    {
+      std::sort(t[k].begin(), t[k].end());
+      std::sort(tr[k].begin(), tr[k].end());
+      std::sort(tf[k].begin(), tf[k].end());
+      std::printf("C=%d %-38s cols %7.4f  rows %7.4f  frame %7.4f ms  maps bit-identical %s\n", C, nm[k], t[k][4],
+                  tr[k][4], tf[k][4], same[k] ? "yes" : "NO");
+    }
+    CHECK(hipFree(h0b2));
+    return 0;
+  }
   if (argc > 3 && std::strcmp(argv[3], "small") == 0 && logn <= 11)
   {
     // round 6: the small-grid column pass (k_cols_small: 8 points per thread, radix-8 Stockham, H in

@@ -51,12 +51,15 @@ struct ColFirstCfg
   using S = FftShape<LOGN>;
   static constexpr int N = S::N, T = S::T;
   static constexpr int B = T >= 1024 ? 1 : (T >= 512 ? 2 : (T < 4 ? T : 4));  // texels per block row
-  static constexpr int SPW_RAW = 256 / (T * B) < 1 ? 1 : 256 / (T * B);
+  // Below N = 1024 (the full-spectrum path: the reference's own 256^2 cascades) an item is one wave's
+  // worth of strips / rows (64 threads) instead of four waves' (round 6: a 3 x 256^2 frame had 48 column
+  // and 96 row workgroups for 256 CUs); the per-column arithmetic is the same.
+  static constexpr int SPW_RAW = T >= 64 ? (256 / (T * B) < 1 ? 1 : 256 / (T * B)) : (64 / (T * B) < 1 ? 1 : 64 / (T * B));
   static constexpr int SPW = SPW_RAW > N / B ? N / B : SPW_RAW;  // strips per pass-1 item
   static constexpr int C1 = B * SPW;                              // columns per pass-1 item
   static constexpr int WG1 = T * C1;
   static constexpr int LDS1 = C1 * S::PADDED * 8;  // float2 (split-lane) exchange
-  static constexpr int RPW2_RAW = 256 / T >= 4 ? 256 / T : (1024 / T < 4 ? 1024 / T : 4);
+  static constexpr int RPW2_RAW = T < 64 ? 64 / T : (256 / T >= 4 ? 256 / T : (1024 / T < 4 ? 1024 / T : 4));
   static constexpr int RPW2 = RPW2_RAW > N ? N : RPW2_RAW;  // rows per pass-2 item
   static constexpr int WG2 = T * RPW2;
   static constexpr int LDS2 = lds_row_slots<LOGN>(RPW2) * 8;

@@ -633,7 +633,7 @@ def _slab_run(ocean, n, ranks, steps, settings):
     return h, d, j
 
 
-@pytest.mark.parametrize("n,ranks", [(512, 2), (256, 2), (256, 4), (1024, 1), (1024, 8), (4096, 4), (2048, 16),
+@pytest.mark.parametrize("n,ranks", [(512, 2), (256, 2), (256, 4), (64, 4), (1024, 1), (1024, 8), (4096, 4), (2048, 16),
                                      (1024, 16)])
 def test_slab_decomposition_matches_whole_grid(ocean, n, ranks):
     """Rank-split column pass + all-to-all + rank-split row pass == the single-GPU generator,
@@ -773,7 +773,7 @@ def test_slab_rejects_too_narrow_slabs(ocean):
 
     fft = ocean.FFTCalculator(64)
     with pytest.raises(OceanError):
-        SlabGenerator(fft, 0, 2)  # 32-wide slabs < the 64-column work item at N = 64
+        SlabGenerator(fft, 0, 8)  # 8-wide slabs < the 16-column work item at N = 64 (one wave's strips)
     with pytest.raises(OceanError):
         SlabGenerator(ocean.FFTCalculator(256), 0, 3)  # not a power of two
 

@@ -304,8 +304,10 @@ __global__ __launch_bounds__(RowCfg<LOGN>::WG, RowCfg<LOGN>::MIN_WAVES) void k_r
 // policy, so that a slab of <= 128 MiB could stay in the Infinity Cache between the two steps: measured
 // and not kept (2 x 16384^2: 10.02 ms at best, slab 1024 columns, against 10.00 for 2048 nt;
 // profiles/r04_ifft4bench_mall.log).
-template <int LOGN, bool WNT = true>
-__global__ __launch_bounds__(256) void k_cols4_step1(int images, int x0, int wc, const float4* __restrict__ img,
+// MINW: the launch bound's minimum waves per SIMD; 4 keeps the kernel at <= 128 VGPRs, so four of its
+// one-wave-per-SIMD workgroups share a CU (without it: 138 VGPRs, three).
+template <int LOGN, bool WNT = true, int MINW = 4>
+__global__ __launch_bounds__(256, MINW) void k_cols4_step1(int images, int x0, int wc, const float4* __restrict__ img,
                                                      float4* __restrict__ work, const float2* __restrict__ tw_glob)
 {
   using S = FftShape<LOGN>;
@@ -354,8 +356,10 @@ __global__ __launch_bounds__(256) void k_cols4_step1(int images, int x0, int wc,
 // (src_of / ld), which keeps the kernel at 112 VGPRs; the earlier form spilled 8 VGPRs (36 B) at the
 // 128 of a 1024-thread workgroup. 2 x 16384^2: 10.009 -> 9.753 ms on one box (ifft4bench early,
 // profiles/r06_ifft4bench_early2.log), bit-identical.
-template <int LOGN2, bool WNT = true, int CI = ColCfg<LOGN2>::C>
-__global__ __launch_bounds__(FftShape<LOGN2>::T * CI) void k_cols4_step2(int images, int x0, int wc,
+// MINW (round 6): the launch bound's minimum waves per SIMD. CI 8 needs 4 for two 512-thread workgroups
+// per CU: without it the kernel compiles to 134 VGPRs and only one fits (round 5's CI 8 measurement).
+template <int LOGN2, bool WNT = true, int CI = ColCfg<LOGN2>::C, int MINW = (CI < ColCfg<LOGN2>::C ? 4 : 1)>
+__global__ __launch_bounds__(FftShape<LOGN2>::T * CI, MINW) void k_cols4_step2(int images, int x0, int wc,
                                                                         const float4* __restrict__ work,
                                                                         float4* __restrict__ img,
                                                                         const float2* __restrict__ tw_glob)

@@ -245,8 +245,14 @@ hipError_t launch_peer_wait(const PeerWait& w, hipStream_t stream)
 // the oracle restatement (oracle_surface_vertex) is matched bit for bit. Memory: the maps of a
 // scene (3 x 256^2 x 36 B) live in L2; per vertex 32 B are written.
 // ------------------------------------------------------------------------------------------------
-template <int CH>
-__device__ __forceinline__ void sample_linear_repeat(const float* __restrict__ tex, int n, float u, float v, float* out)
+// The four taps and weights of one sample: the texel indices of (i0, j0), (i1, j0), (i0, j1), (i1, j1).
+struct LinearTaps
+{
+  int o00, o10, o01, o11;
+  float w00, w10, w01, w11;
+};
+
+__device__ __forceinline__ LinearTaps linear_repeat_taps(int n, float u, float v)
 {
 #pragma clang fp contract(off)
   const float s = u * (float)n - 0.5f, t = v * (float)n - 0.5f;
@@ -254,22 +260,20 @@ __device__ __forceinline__ void sample_linear_repeat(const float* __restrict__ t
   const float a = s - fs, b = t - ft;
   const int m = n - 1;  // n is a power of two: & m is the repeat wrap, also for negative indices
   const int i0 = (int)fs & m, j0 = (int)ft & m, i1 = (i0 + 1) & m, j1 = (j0 + 1) & m;
-  const float w00 = (1.0f - a) * (1.0f - b), w10 = a * (1.0f - b), w01 = (1.0f - a) * b, w11 = a * b;
-  const float* t00 = tex + ((size_t)j0 * n + i0) * CH;
-  const float* t10 = tex + ((size_t)j0 * n + i1) * CH;
-  const float* t01 = tex + ((size_t)j1 * n + i0) * CH;
-  const float* t11 = tex + ((size_t)j1 * n + i1) * CH;
-  if constexpr (CH == 4)
-  {
-    const float4 q00 = *reinterpret_cast<const float4*>(t00), q10 = *reinterpret_cast<const float4*>(t10);
-    const float4 q01 = *reinterpret_cast<const float4*>(t01), q11 = *reinterpret_cast<const float4*>(t11);
-    out[0] = w00 * q00.x + w10 * q10.x + w01 * q01.x + w11 * q11.x;
-    out[1] = w00 * q00.y + w10 * q10.y + w01 * q01.y + w11 * q11.y;
-    out[2] = w00 * q00.z + w10 * q10.z + w01 * q01.z + w11 * q11.z;
-    out[3] = w00 * q00.w + w10 * q10.w + w01 * q01.w + w11 * q11.w;
-  }
-  else
-    out[0] = w00 * t00[0] + w10 * t10[0] + w01 * t01[0] + w11 * t11[0];
+  return LinearTaps{j0 * n + i0, j0 * n + i1, j1 * n + i0, j1 * n + i1, (1.0f - a) * (1.0f - b), a * (1.0f - b),
+                    (1.0f - a) * b, a * b};
+}
+
+// Channel ch of a map of CH floats per texel, filtered: each stage loads only the channels it uses, one
+// dword per tap (the vertex stage 3 of 8, the normal stage 5 of 9): 2.95 -> 2.49 ms for the 4096^2-quad
+// mesh, bit-identical (tools/microbench/surfbench, profiles/r06_surfbench.log).
+template <int CH>
+__device__ __forceinline__ float linear_channel(const float* __restrict__ tex, const LinearTaps& k, int ch)
+{
+#pragma clang fp contract(off)
+  const float q00 = tex[k.o00 * CH + ch], q10 = tex[k.o10 * CH + ch], q01 = tex[k.o01 * CH + ch],
+              q11 = tex[k.o11 * CH + ch];
+  return k.w00 * q00 + k.w10 * q10 + k.w01 * q01 + k.w11 * q11;
 }
 
 __global__ __launch_bounds__(256) void k_surface(SurfaceParams p, SurfacePlane plane, const float2* __restrict__ xz,
@@ -312,28 +316,28 @@ __global__ __launch_bounds__(256) void k_surface(SurfaceParams p, SurfacePlane p
     float py = 0.0f;
     for (int c = 0; c < p.count; c++)
     {
-      float d1[4], d2[4];
       const float u = px / p.c[c].plane, v = pz / p.c[c].plane;
-      sample_linear_repeat<4>(reinterpret_cast<const float*>(p.c[c].height), p.n, u, v, d1);
-      sample_linear_repeat<4>(reinterpret_cast<const float*>(p.c[c].disp), p.n, u, v, d2);
-      px += p.c[c].scale * d1[3];
-      py += d1[0];
-      pz += p.c[c].scale * d2[0];
+      const LinearTaps k = linear_repeat_taps(p.n, u, v);
+      const float* hm = reinterpret_cast<const float*>(p.c[c].height);
+      const float* dm = reinterpret_cast<const float*>(p.c[c].disp);
+      const float h = linear_channel<4>(hm, k, 0), dx = linear_channel<4>(hm, k, 3), dz = linear_channel<4>(dm, k, 0);
+      px += p.c[c].scale * dx;
+      py += h;
+      pz += p.c[c].scale * dz;
     }
     float d[4] = {0.0f, 0.0f, 0.0f, 0.0f}, jac = 0.0f;
     for (int c = 0; c < p.count; c++)
     {
-      float d1[4], d2[4], j;
       const float u = px / p.c[c].plane, v = pz / p.c[c].plane;
-      sample_linear_repeat<4>(reinterpret_cast<const float*>(p.c[c].height), p.n, u, v, d1);
-      sample_linear_repeat<4>(reinterpret_cast<const float*>(p.c[c].disp), p.n, u, v, d2);
-      sample_linear_repeat<1>(p.c[c].jac, p.n, u, v, &j);
-      jac += j / (float)p.count;
+      const LinearTaps k = linear_repeat_taps(p.n, u, v);
+      const float* hm = reinterpret_cast<const float*>(p.c[c].height);
+      const float* dm = reinterpret_cast<const float*>(p.c[c].disp);
+      jac += linear_channel<1>(p.c[c].jac, k, 0) / (float)p.count;
       const float f = p.c[c].scale;
-      d[0] += d1[1];
-      d[1] += d2[1] * f;
-      d[2] += d1[2];
-      d[3] += d2[2] * f;
+      d[0] += linear_channel<4>(hm, k, 1);               // dh/dx
+      d[1] += linear_channel<4>(dm, k, 1) * f;           // dDx/dx
+      d[2] += linear_channel<4>(hm, k, 2);               // dh/dz
+      d[3] += linear_channel<4>(dm, k, 2) * f;           // dDz/dz
     }
     const float sx = d[0] / (1.0f + d[1]), sz = d[2] / (1.0f + d[3]);
     const float nx = -sx, ny = 1.0f, nz = -sz;

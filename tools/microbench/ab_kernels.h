@@ -215,7 +215,7 @@ hipError_t launch_half_columns_ab(int logn, const FrameParams& fp, const float4*
   const SpectrumConsts* seed = static_cast<const SpectrumConsts*>(seed_consts);
   return with_logn(logn, [&](auto L) -> hipError_t {
     constexpr int LOGN = decltype(L)::value;
-    if constexpr (!HalfCfg<LOGN>::SUPPORTED)
+    if constexpr (!HalfCfg<LOGN>::SUPPORTED || LOGN < 10)  // the half path: N = 1024 .. 4096
       return hipErrorInvalidValue;
     else
     {
@@ -1069,8 +1069,10 @@ __global__ __launch_bounds__(1024) void k_rows_xs_r3(FrameParams fp, const float
 // issued after this item's transform and before its 16 stores, so they do not queue behind the
 // stores; the last item re-reads its own (unconditional, so the registers are not kept live across
 // the loop as a second incoming value). Same arithmetic per column as production: bit-identical.
-template <int LOGN2, int PF, int CI = ColCfg<LOGN2>::C>
-__global__ __launch_bounds__(FftShape<LOGN2>::T * CI) void k_cols4_step2e(int images, int x0, int wc,
+// MINB (round 6): the launch bound's second argument; 4 keeps a 512-thread (CI 8) workgroup at <= 128
+// VGPRs, so two fit on a CU (without it CI 8 compiles to 134 VGPRs: one workgroup per CU).
+template <int LOGN2, int PF, int CI = ColCfg<LOGN2>::C, int MINB = 1>
+__global__ __launch_bounds__(FftShape<LOGN2>::T * CI, MINB) void k_cols4_step2e(int images, int x0, int wc,
                                                                          const float4* __restrict__ work,
                                                                          float4* __restrict__ img,
                                                                          const float2* __restrict__ tw_glob)

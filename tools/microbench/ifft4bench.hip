@@ -141,11 +141,14 @@ static int ci_mode(int cus)
   std::vector<float4> base(tex), ref(tex), got(tex);
   CHECK(hipDeviceSynchronize());
   CHECK(hipMemcpy(base.data(), img, tex * 16, hipMemcpyDeviceToHost));
-  struct R { const char* name; int wc; bool ci8; std::vector<float> t; };
-  std::vector<R> rs = {{"CI 16, slab 2048", 2048, false, {}}, {"CI 8, slab 2048", 2048, true, {}},
-                       {"CI 16, whole image", n, false, {}}, {"CI 8, whole image", n, true, {}}};
-  // CI 8: rows, then per image and slab step 1 + k_cols4_step2<10, true, 8> (512-thread workgroups)
-  auto ci8 = [&](int wc) -> hipError_t {
+  struct R { const char* name; int wc; int ci8; std::vector<float> t; };
+  std::vector<R> rs = {{"CI 16, slab 2048", 2048, 0, {}}, {"CI 8, slab 2048", 2048, 1, {}},
+                       {"CI 16, whole image", n, 0, {}}, {"CI 8, whole image", n, 1, {}},
+                       {"CI 8 MINB 4, slab 2048", 2048, 2, {}}, {"CI 8 MINB 4, slab 4096", 4096, 2, {}},
+                       {"CI 8 MINB 4 PF 4 res, slab 2048", 2048, 3, {}}, {"CI 8 MINB 4, whole image", n, 2, {}}};
+  // CI 8: rows, then per image and slab step 1 + k_cols4_step2<10, true, 8> (512-thread workgroups);
+  // variant 2: k_cols4_step2e<10, 0, 8, 4> (<= 128 VGPRs, two workgroups per CU), 3: PF 4 on a resident grid
+  auto ci8 = [&](int wc, int var) -> hipError_t {
     hipError_t e = launch_rows_ifft(logn, imgs, img, tw, 0, cus);
     if (e != hipSuccess)
       return e;
@@ -160,13 +163,28 @@ static int ci_mode(int cus)
         float4* im0 = img + ((size_t)im << (2 * logn));
         const int g1 = persistent_grid(k1, 256, 0, (wc / 64) * ((n / 16) / 4), cus);
         hipLaunchKernelGGL(k1, dim3(g1), dim3(256), 0, 0, 1, x0, wc, im0, work, tw);
-        const int g2 = persistent_grid(k2, WG2, lds2, 16 * (wc / CI), cus);
-        hipLaunchKernelGGL(k2, dim3(g2), dim3(WG2), lds2, 0, 1, x0, wc, work, im0, tw2);
+        if (var == 1)
+        {
+          const int g2 = persistent_grid(k2, WG2, lds2, 16 * (wc / CI), cus);
+          hipLaunchKernelGGL(k2, dim3(g2), dim3(WG2), lds2, 0, 1, x0, wc, work, im0, tw2);
+        }
+        else if (var == 2)
+        {
+          auto k2m = k_cols4_step2e<logn - 4, 0, CI, 4>;
+          const int g2 = persistent_grid(k2m, WG2, lds2, 16 * (wc / CI), cus);
+          hipLaunchKernelGGL(k2m, dim3(g2), dim3(WG2), lds2, 0, 1, x0, wc, work, im0, tw2);
+        }
+        else
+        {
+          auto k2m = k_cols4_step2e<logn - 4, 4, CI, 4>;
+          const int g2 = resident_grid(k2m, WG2, lds2, 16 * (wc / CI), cus);
+          hipLaunchKernelGGL(k2m, dim3(g2), dim3(WG2), lds2, 0, 1, x0, wc, work, im0, tw2);
+        }
       }
     return hipGetLastError();
   };
   auto run = [&](const R& v) {
-    return v.ci8 ? ci8(v.wc) : launch_ifft_fourstep(logn, imgs, img, work, v.wc, tw, tw2, 0, cus);
+    return v.ci8 ? ci8(v.wc, v.ci8) : launch_ifft_fourstep(logn, imgs, img, work, v.wc, tw, tw2, 0, cus);
   };
   for (size_t k = 0; k < rs.size(); k++)
   {
@@ -277,6 +295,178 @@ static int early_mode(int cus)
   return 0;
 }
 
+
+// "occ" (round 6): 2 images of 16384^2 through a 2048-column slab; step 1 at 138 VGPRs (three 256-thread
+// workgroups per CU; MINW 1) or <= 128 (four; MINW 4, 28 B of spills) against step 2 on 16 columns per
+// 1024-thread workgroup or 8 per 512-thread workgroup at <= 128 VGPRs (two per CU). Each combination is
+// timed whole (rows + columns) and per step (the slabs' step-1 or step-2 launches alone).
+static int occ_mode(int cus)
+{
+  constexpr int logn = 14, n = 1 << logn, imgs = 2, wc = 2048;
+  const size_t tex = (size_t)n * n * imgs;
+  float4 *img, *work;
+  CHECK(hipMalloc(&img, tex * 16));
+  CHECK(hipMalloc(&work, ifft_fourstep_work_texels(logn, wc) * 16));
+  hipLaunchKernelGGL(fill_img, dim3(4096), dim3(256), 0, 0, img, tex);
+  auto t1 = table(logn), t2 = table(logn - 4);
+  float2 *tw, *tw2;
+  CHECK(hipMalloc(&tw, t1.size() * 8));
+  CHECK(hipMalloc(&tw2, t2.size() * 8));
+  CHECK(hipMemcpy(tw, t1.data(), t1.size() * 8, hipMemcpyHostToDevice));
+  CHECK(hipMemcpy(tw2, t2.data(), t2.size() * 8, hipMemcpyHostToDevice));
+  std::vector<float4> base(tex), ref(tex), got(tex);
+  CHECK(hipDeviceSynchronize());
+  CHECK(hipMemcpy(base.data(), img, tex * 16, hipMemcpyDeviceToHost));
+  using S2 = FftShape<logn - 4>;
+  // parts: 1 = rows, 2 = step 1, 4 = step 2
+  auto make = [&](auto k1, auto k2, int ci, int parts) {
+    return std::function<hipError_t()>([=] {
+      if (parts & 1)
+      {
+        hipError_t e = launch_rows_ifft(logn, imgs, img, tw, 0, cus);
+        if (e != hipSuccess)
+          return e;
+      }
+      const int wg2 = S2::T * ci, lds2 = ((S2::TW_ENTRIES * 8 + 15) / 16) * 16 + ci * S2::PADDED * 8;
+      for (int im = 0; im < imgs; im++)
+        for (int x0 = 0; x0 < n; x0 += wc)
+        {
+          float4* im0 = img + ((size_t)im << (2 * logn));
+          if (parts & 2)
+          {
+            const int g1 = persistent_grid(k1, 256, 0, (wc / 64) * ((n / 16) / 4), cus);
+            hipLaunchKernelGGL(k1, dim3(g1), dim3(256), 0, 0, 1, x0, wc, im0, work, tw);
+          }
+          if (parts & 4)
+          {
+            const int g2 = persistent_grid(k2, wg2, lds2, 16 * (wc / ci), cus);
+            hipLaunchKernelGGL(k2, dim3(g2), dim3(wg2), lds2, 0, 1, x0, wc, work, im0, tw2);
+          }
+        }
+      return hipGetLastError();
+    });
+  };
+  auto s1a = k_cols4_step1<logn, true, 1>;
+  auto s1b = k_cols4_step1<logn, true, 4>;
+  auto s2a = k_cols4_step2<logn - 4, true, 16>;
+  auto s2b = k_cols4_step2<logn - 4, true, 8>;
+  std::vector<std::string> names = {"step1 MINW 1 + step2 CI 16 (r06e production)", "step1 MINW 4 + step2 CI 16",
+                                    "step1 MINW 1 + step2 CI 8 MINW 4", "step1 MINW 4 + step2 CI 8 MINW 4",
+                                    "step 1 alone, MINW 1", "step 1 alone, MINW 4", "step 2 alone, CI 16",
+                                    "step 2 alone, CI 8 MINW 4"};
+  std::vector<std::function<hipError_t()>> runs = {make(s1a, s2a, 16, 7), make(s1b, s2a, 16, 7), make(s1a, s2b, 8, 7),
+                                                   make(s1b, s2b, 8, 7), make(s1a, s2a, 16, 2), make(s1b, s2a, 16, 2),
+                                                   make(s1a, s2a, 16, 4), make(s1a, s2b, 8, 4)};
+  for (size_t k = 0; k < 4; k++)
+  {
+    CHECK(hipMemcpy(img, base.data(), tex * 16, hipMemcpyHostToDevice));
+    CHECK(runs[k]());
+    CHECK(hipDeviceSynchronize());
+    CHECK(hipMemcpy(k == 0 ? ref.data() : got.data(), img, tex * 16, hipMemcpyDeviceToHost));
+    if (k > 0)
+      std::printf("%s: %s\n", names[k].c_str(), std::memcmp(ref.data(), got.data(), tex * 16) == 0 ? "bit-identical" : "DIFFERS");
+  }
+  std::vector<std::vector<float>> t(runs.size());
+  for (int r = 0; r < 7; r++)
+    for (size_t k = 0; k < runs.size(); k++)
+      t[k].push_back(time_ms(runs[k], 3));
+  for (size_t k = 0; k < runs.size(); k++)
+  {
+    std::sort(t[k].begin(), t[k].end());
+    std::printf("2 x 16384^2 EncodeIFFT, %-46s median %7.3f ms (min %7.3f)\n", names[k].c_str(), t[k][3], t[k][0]);
+  }
+  return 0;
+}
+
+// "pipe" (round 6): 2 images of 16384^2; the column steps of consecutive slabs overlapped on two streams
+// with two work slabs: step 1 of slab s + 1 (streaming, 256-thread workgroups) beside step 2 of slab s
+// (LDS-bound, 1024-thread workgroups), against production (one stream). Bit-identical by construction.
+static int pipe_mode(int cus)
+{
+  constexpr int logn = 14, n = 1 << logn, imgs = 2;
+  const size_t tex = (size_t)n * n * imgs;
+  float4 *img, *work;
+  CHECK(hipMalloc(&img, tex * 16));
+  CHECK(hipMalloc(&work, 2 * ifft_fourstep_work_texels(logn, 4096) * 16));
+  hipLaunchKernelGGL(fill_img, dim3(4096), dim3(256), 0, 0, img, tex);
+  auto t1 = table(logn), t2 = table(logn - 4);
+  float2 *tw, *tw2;
+  CHECK(hipMalloc(&tw, t1.size() * 8));
+  CHECK(hipMalloc(&tw2, t2.size() * 8));
+  CHECK(hipMemcpy(tw, t1.data(), t1.size() * 8, hipMemcpyHostToDevice));
+  CHECK(hipMemcpy(tw2, t2.data(), t2.size() * 8, hipMemcpyHostToDevice));
+  std::vector<float4> base(tex), ref(tex), got(tex);
+  CHECK(hipDeviceSynchronize());
+  CHECK(hipMemcpy(base.data(), img, tex * 16, hipMemcpyDeviceToHost));
+  hipStream_t sb;
+  CHECK(hipStreamCreateWithFlags(&sb, hipStreamNonBlocking));
+  constexpr int kMaxSlabs = 64;
+  hipEvent_t e1[kMaxSlabs], e2[kMaxSlabs], er;
+  for (int k = 0; k < kMaxSlabs; k++)
+  {
+    CHECK(hipEventCreateWithFlags(&e1[k], hipEventDisableTiming));
+    CHECK(hipEventCreateWithFlags(&e2[k], hipEventDisableTiming));
+  }
+  CHECK(hipEventCreateWithFlags(&er, hipEventDisableTiming));
+  using K2 = ColCfg<logn - 4>;
+  const int lds2 = lds_bytes_cols<logn - 4>();
+  auto k1 = k_cols4_step1<logn>;
+  auto k2 = k_cols4_step2<logn - 4>;
+  auto piped = [&](int wc, int cap1, int cap2) {
+    return std::function<hipError_t()>([=] {
+      hipError_t e = launch_rows_ifft(logn, imgs, img, tw, 0, cus);
+      if (e != hipSuccess)
+        return e;
+      const size_t wslab = ifft_fourstep_work_texels(logn, wc);
+      int s = 0;
+      for (int im = 0; im < imgs; im++)
+        for (int x0 = 0; x0 < n; x0 += wc, s++)
+        {
+          float4* im0 = img + ((size_t)im << (2 * logn));
+          float4* w = work + (s & 1) * wslab;
+          if (s >= 2)
+            CHECK(hipStreamWaitEvent(0, e2[s - 2], 0));  // slab s - 2's step 2 has read this work slab
+          const int g1 = std::min(cap1, persistent_grid(k1, 256, 0, (wc / 64) * ((n / 16) / 4), cus));
+          hipLaunchKernelGGL(k1, dim3(g1), dim3(256), 0, 0, 1, x0, wc, im0, w, tw);
+          CHECK(hipEventRecord(e1[s], 0));
+          CHECK(hipStreamWaitEvent(sb, e1[s], 0));
+          const int g2 = std::min(cap2, persistent_grid(k2, K2::WG, lds2, 16 * (wc / K2::C), cus));
+          hipLaunchKernelGGL(k2, dim3(g2), dim3(K2::WG), lds2, sb, 1, x0, wc, w, im0, tw2);
+          CHECK(hipEventRecord(e2[s], sb));
+        }
+      CHECK(hipEventRecord(er, sb));
+      CHECK(hipStreamWaitEvent(0, er, 0));
+      return hipGetLastError();
+    });
+  };
+  std::vector<std::string> names = {"production (one stream, slab 2048)", "piped, slab 2048", "piped, slab 1024",
+                                    "piped, slab 4096", "piped, slab 2048, step 2 on 192 CUs' grid",
+                                    "piped, slab 2048, step 1 grid 256"};
+  std::vector<std::function<hipError_t()>> runs = {
+      std::function<hipError_t()>([=] { return launch_ifft_fourstep(logn, imgs, img, work, 2048, tw, tw2, 0, cus); }),
+      piped(2048, 1 << 30, 1 << 30), piped(1024, 1 << 30, 1 << 30), piped(4096, 1 << 30, 1 << 30),
+      piped(2048, 1 << 30, 192), piped(2048, 256, 1 << 30)};
+  for (size_t k = 0; k < runs.size(); k++)
+  {
+    CHECK(hipMemcpy(img, base.data(), tex * 16, hipMemcpyHostToDevice));
+    CHECK(runs[k]());
+    CHECK(hipDeviceSynchronize());
+    CHECK(hipMemcpy(k == 0 ? ref.data() : got.data(), img, tex * 16, hipMemcpyDeviceToHost));
+    if (k > 0)
+      std::printf("%s: %s\n", names[k].c_str(), std::memcmp(ref.data(), got.data(), tex * 16) == 0 ? "bit-identical" : "DIFFERS");
+  }
+  std::vector<std::vector<float>> t(runs.size());
+  for (int r = 0; r < 7; r++)
+    for (size_t k = 0; k < runs.size(); k++)
+      t[k].push_back(time_ms(runs[k], 3));
+  for (size_t k = 0; k < runs.size(); k++)
+  {
+    std::sort(t[k].begin(), t[k].end());
+    std::printf("2 x 16384^2 EncodeIFFT, %-46s median %7.3f ms (min %7.3f)\n", names[k].c_str(), t[k][3], t[k][0]);
+  }
+  return 0;
+}
+
 int main(int argc, char** argv)
 {
   int cus = 0;
@@ -285,6 +475,10 @@ int main(int argc, char** argv)
     return mall_mode(cus);
   if (argc > 1 && std::strcmp(argv[1], "ci") == 0)
     return ci_mode(cus);
+  if (argc > 1 && std::strcmp(argv[1], "pipe") == 0)
+    return pipe_mode(cus);
+  if (argc > 1 && std::strcmp(argv[1], "occ") == 0)
+    return occ_mode(cus);
   if (argc > 1 && std::strcmp(argv[1], "early") == 0)
     return early_mode(cus);
   for (int logn : {13, 14})

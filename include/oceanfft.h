@@ -343,7 +343,10 @@ int ocean_debug_copy(void* dst, const void* src, size_t bytes, int workgroups, v
  * normal and Jacobian average (:127-144). Sampling is GL_LINEAR + GL_REPEAT in fp32
  * (src/Generator.cpp:116-119). Output per vertex: 8 floats (x, y, z, jacobian, nx, ny, nz, 0),
  * device memory, written on the first generator's stream. planeSize / displacement come from each
- * cascade's settings (Renderer.cpp:70-71). No reference counterpart as a call: it replaces the
+ * cascade's settings (Renderer.cpp:70-71). A request of at least 65536 vertices and 4 per map
+ * texel first repacks the channels each stage reads into an atlas (2 x 16 B per texel and cascade,
+ * at most 256 MiB, owned by the first generator's FFT plan and kept for later requests), then samples
+ * it: the same bits, fewer load instructions. No reference counterpart as a call: it replaces the
  * vertex + fragment shader sampling. */
 int ocean_surface_sample(ocean_generator* const* gens, const int* cascades, int count, const float* xz,
                          int64_t points, float* out);

@@ -73,6 +73,8 @@ struct ocean_fft
   float4* work = nullptr;      // column-first EncodeIFFT work image (the reference's workImage)
   int work_images = 0;
   size_t work_texels = 0;      // four-step EncodeIFFT (N = 16384): work slab of N x kFourStepSlab texels
+  float4* surf_atlas = nullptr;  // the surface consumer's repacked maps (launch_surface), grown on demand
+  size_t surf_atlas_texels = 0;
 };
 
 // Four-step EncodeIFFT work slab width at N = 16384 (tools/microbench/ifft4bench,
@@ -287,6 +289,8 @@ int ocean_fft_destroy(ocean_fft* fft)
     (void)hipFree(fft->twiddles);
   if (fft->work)
     (void)hipFree(fft->work);
+  if (fft->surf_atlas)
+    (void)hipFree(fft->surf_atlas);
   delete fft;
   return OCEAN_OK;
 }
@@ -2210,6 +2214,30 @@ static int surface_params(ocean_generator* const* gens, const int* cascades, int
     p.c[i].scale = g->settings[c].displacement;
   }
   p.n = fft->n;
+  p.atlas = nullptr;
+  return OCEAN_OK;
+}
+
+// The surface atlas of a request (surface_use_atlas), owned by the plan whose stream runs the request:
+// requests on one plan are stream-ordered, so one buffer serves them all.
+static int surface_atlas(ocean_fft* fft, SurfaceParams& p, int64_t points, const char* who)
+{
+  if (!surface_use_atlas(p, points))
+    return OCEAN_OK;
+  const size_t texels = surface_atlas_texels(p);
+  if (fft->surf_atlas_texels < texels)
+  {
+    if (fft->surf_atlas)
+    {
+      HIP_TRY(hipStreamSynchronize(fft->stream), who);  // an earlier request may still read the old one
+      HIP_TRY(hipFree(fft->surf_atlas), who);
+      fft->surf_atlas = nullptr;
+      fft->surf_atlas_texels = 0;
+    }
+    HIP_TRY(hipMalloc(&fft->surf_atlas, texels * sizeof(float4)), who);
+    fft->surf_atlas_texels = texels;
+  }
+  p.atlas = fft->surf_atlas;
   return OCEAN_OK;
 }
 
@@ -2223,6 +2251,9 @@ int ocean_surface_sample(ocean_generator* const* gens, const int* cascades, int 
     return rc;
   if (points < 0 || (points > 0 && (!xz || !out)))
     return fail(OCEAN_ERR_INVALID, "ocean_surface_sample: null positions/output or negative count");
+  rc = surface_atlas(fft, p, points, "ocean_surface_sample");
+  if (rc != OCEAN_OK)
+    return rc;
   HIP_TRY(launch_surface(p, SurfacePlane{}, reinterpret_cast<const float2*>(xz), points, reinterpret_cast<float4*>(out),
                          fft->stream, fft->cus),
           "ocean_surface_sample");
@@ -2243,6 +2274,9 @@ int ocean_surface_sample_plane(ocean_generator* const* gens, const int* cascades
     return fail(OCEAN_ERR_INVALID, "ocean_surface_sample_plane: camera forward has no horizontal component");
   const SurfacePlane plane{res, camera[0], camera[1], camera[2], camera[3], camera[4]};
   const int64_t pts = (int64_t)(res + 1) * (res + 1);
+  rc = surface_atlas(fft, p, pts, "ocean_surface_sample_plane");
+  if (rc != OCEAN_OK)
+    return rc;
   HIP_TRY(launch_surface(p, plane, nullptr, pts, reinterpret_cast<float4*>(out), fft->stream, fft->cus),
           "ocean_surface_sample_plane");
   return OCEAN_OK;

@@ -47,6 +47,9 @@ struct SurfaceParams
   int count;  // cascades
   int n;      // map side (power of two)
   SurfaceCascade c[kMaxSurfaceCascades];
+  // null: the stages sample the maps; else the surface atlas [cascade][2][n * n] (launch_surface):
+  // (h, Dx, Dz, 0) for the vertex stage, (dh/dx, dh/dz, dDx/dx, dDz/dz) for the normal stage
+  float4* atlas;
 };
 // The reference plane mesh and camera (waveShader.glsl:77-98); res == 0: explicit positions.
 struct SurfacePlane
@@ -261,8 +264,12 @@ hipError_t launch_ifft_colfirst(int logn, int n_images, float4* images, float4* 
 bool ifft_pre_supported(int logn);
 hipError_t launch_ifft_pre(int logn, int n_images, float4* images, float4* work, const float2* twn, const float2* twm,
                            hipStream_t stream, int cus);
+// p.atlas non-null: the maps are first repacked into it (surface_atlas_texels(p) float4), then sampled
+// from it; bit-identical to the direct path.
 hipError_t launch_surface(const SurfaceParams& p, const SurfacePlane& plane, const float2* xz, int64_t count,
                           float4* out, hipStream_t stream, int cus);
+size_t surface_atlas_texels(const SurfaceParams& p);
+bool surface_use_atlas(const SurfaceParams& p, int64_t points);
 hipError_t launch_hash(const uint32_t* xy, int count, uint32_t* raw, float2* uv, hipStream_t stream);
 hipError_t launch_debug_copy(void* dst, const void* src, size_t bytes, int workgroups, hipStream_t stream);
 // Generator frame: pass 1 (evolve + y iFFT, destination-block-ordered output), pass 2 (x iFFT +

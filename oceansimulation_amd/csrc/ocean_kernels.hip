@@ -266,7 +266,11 @@ __device__ __forceinline__ LinearTaps linear_repeat_taps(int n, float u, float v
 
 // Channel ch of a map of CH floats per texel, filtered: each stage loads only the channels it uses, one
 // dword per tap (the vertex stage 3 of 8, the normal stage 5 of 9): 2.95 -> 2.49 ms for the 4096^2-quad
-// mesh, bit-identical (tools/microbench/surfbench, profiles/r06_surfbench.log).
+// mesh, bit-identical (tools/microbench/surfbench, profiles/r06_surfbench.log). A sampling wave's taps
+// are scattered (the camera warp spreads far vertices ~10 texels apart on a 5 m cascade), so the cost
+// is per load instruction: ATLAS repacks the channels each stage uses into one 16-B texel (one load per
+// tap and stage, plus the Jacobian's dword): 2.47 -> 1.35 ms with the repack included, 0.212 -> 0.121 ms
+// for the 1024^2-quad mesh, bit-identical (profiles/r06_surfbench2.log).
 template <int CH>
 __device__ __forceinline__ float linear_channel(const float* __restrict__ tex, const LinearTaps& k, int ch)
 {
@@ -276,6 +280,31 @@ __device__ __forceinline__ float linear_channel(const float* __restrict__ tex, c
   return k.w00 * q00 + k.w10 * q10 + k.w01 * q01 + k.w11 * q11;
 }
 
+// The bilinear sum of the four taps' lanes x, y, z, w (each as linear_channel's sum)
+__device__ __forceinline__ float4 linear_texel(const float4* __restrict__ tex, const LinearTaps& k)
+{
+#pragma clang fp contract(off)
+  const float4 q00 = tex[k.o00], q10 = tex[k.o10], q01 = tex[k.o01], q11 = tex[k.o11];
+  return make_float4(k.w00 * q00.x + k.w10 * q10.x + k.w01 * q01.x + k.w11 * q11.x,
+                     k.w00 * q00.y + k.w10 * q10.y + k.w01 * q01.y + k.w11 * q11.y,
+                     k.w00 * q00.z + k.w10 * q10.z + k.w01 * q01.z + k.w11 * q11.z,
+                     k.w00 * q00.w + k.w10 * q10.w + k.w01 * q01.w + k.w11 * q11.w);
+}
+
+// the surface atlas of the cascades' maps (SurfaceParams::atlas)
+__global__ __launch_bounds__(256) void k_surface_atlas(SurfaceParams p)
+{
+  const int nn = p.n * p.n;
+  for (int idx = blockIdx.x * blockDim.x + threadIdx.x; idx < p.count * nn; idx += gridDim.x * blockDim.x)
+  {
+    const int c = idx / nn, t = idx - c * nn;
+    const float4 h = p.c[c].height[t], d = p.c[c].disp[t];
+    p.atlas[(size_t)(2 * c) * nn + t] = make_float4(h.x, h.w, d.x, 0.0f);
+    p.atlas[(size_t)(2 * c + 1) * nn + t] = make_float4(h.y, h.z, d.y, d.z);
+  }
+}
+
+template <bool ATLAS>
 __global__ __launch_bounds__(256) void k_surface(SurfaceParams p, SurfacePlane plane, const float2* __restrict__ xz,
                                                  int64_t count, float4* __restrict__ out)
 {
@@ -314,13 +343,27 @@ __global__ __launch_bounds__(256) void k_surface(SurfaceParams p, SurfacePlane p
       pz = q.y;
     }
     float py = 0.0f;
+    const int nn = p.n * p.n;
     for (int c = 0; c < p.count; c++)
     {
       const float u = px / p.c[c].plane, v = pz / p.c[c].plane;
       const LinearTaps k = linear_repeat_taps(p.n, u, v);
-      const float* hm = reinterpret_cast<const float*>(p.c[c].height);
-      const float* dm = reinterpret_cast<const float*>(p.c[c].disp);
-      const float h = linear_channel<4>(hm, k, 0), dx = linear_channel<4>(hm, k, 3), dz = linear_channel<4>(dm, k, 0);
+      float h, dx, dz;
+      if constexpr (ATLAS)
+      {
+        const float4 a = linear_texel(p.atlas + (size_t)(2 * c) * nn, k);
+        h = a.x;
+        dx = a.y;
+        dz = a.z;
+      }
+      else
+      {
+        const float* hm = reinterpret_cast<const float*>(p.c[c].height);
+        const float* dm = reinterpret_cast<const float*>(p.c[c].disp);
+        h = linear_channel<4>(hm, k, 0);
+        dx = linear_channel<4>(hm, k, 3);
+        dz = linear_channel<4>(dm, k, 0);
+      }
       px += p.c[c].scale * dx;
       py += h;
       pz += p.c[c].scale * dz;
@@ -330,14 +373,30 @@ __global__ __launch_bounds__(256) void k_surface(SurfaceParams p, SurfacePlane p
     {
       const float u = px / p.c[c].plane, v = pz / p.c[c].plane;
       const LinearTaps k = linear_repeat_taps(p.n, u, v);
-      const float* hm = reinterpret_cast<const float*>(p.c[c].height);
-      const float* dm = reinterpret_cast<const float*>(p.c[c].disp);
+      float hx, dxx, hz, dzz;
+      if constexpr (ATLAS)
+      {
+        const float4 b = linear_texel(p.atlas + (size_t)(2 * c + 1) * nn, k);
+        hx = b.x;
+        hz = b.y;
+        dxx = b.z;
+        dzz = b.w;
+      }
+      else
+      {
+        const float* hm = reinterpret_cast<const float*>(p.c[c].height);
+        const float* dm = reinterpret_cast<const float*>(p.c[c].disp);
+        hx = linear_channel<4>(hm, k, 1);
+        dxx = linear_channel<4>(dm, k, 1);
+        hz = linear_channel<4>(hm, k, 2);
+        dzz = linear_channel<4>(dm, k, 2);
+      }
       jac += linear_channel<1>(p.c[c].jac, k, 0) / (float)p.count;
       const float f = p.c[c].scale;
-      d[0] += linear_channel<4>(hm, k, 1);               // dh/dx
-      d[1] += linear_channel<4>(dm, k, 1) * f;           // dDx/dx
-      d[2] += linear_channel<4>(hm, k, 2);               // dh/dz
-      d[3] += linear_channel<4>(dm, k, 2) * f;           // dDz/dz
+      d[0] += hx;        // dh/dx
+      d[1] += dxx * f;   // dDx/dx
+      d[2] += hz;        // dh/dz
+      d[3] += dzz * f;   // dDz/dz
     }
     const float sx = d[0] / (1.0f + d[1]), sz = d[2] / (1.0f + d[3]);
     const float nx = -sx, ny = 1.0f, nz = -sz;
@@ -399,8 +458,29 @@ hipError_t launch_surface(const SurfaceParams& p, const SurfacePlane& plane, con
   const long cap = (long)cus * 8;
   if (blocks > cap)
     blocks = cap;
-  hipLaunchKernelGGL(k_surface, dim3((unsigned)blocks), dim3(256), 0, stream, p, plane, xz, count, out);
+  if (p.atlas)
+  {
+    const long texels = (long)p.count * p.n * p.n;
+    long ab = (texels + 255) / 256;
+    if (ab > (long)cus * 4)
+      ab = (long)cus * 4;
+    hipLaunchKernelGGL(k_surface_atlas, dim3((unsigned)ab), dim3(256), 0, stream, p);
+    hipLaunchKernelGGL(k_surface<true>, dim3((unsigned)blocks), dim3(256), 0, stream, p, plane, xz, count, out);
+  }
+  else
+    hipLaunchKernelGGL(k_surface<false>, dim3((unsigned)blocks), dim3(256), 0, stream, p, plane, xz, count, out);
   return hipGetLastError();
+}
+
+size_t surface_atlas_texels(const SurfaceParams& p) { return (size_t)2 * p.count * p.n * p.n; }
+
+// The repack reads 36 B and writes 32 B per map texel and launches one more kernel; sampling from the
+// atlas saves ~90 ps per vertex (profiles/r06_surfbench2.log). Used when the request's vertices
+// outnumber the maps' texels 4 : 1 (and are at least 64 Ki) and the atlas stays within 256 MiB.
+bool surface_use_atlas(const SurfaceParams& p, int64_t points)
+{
+  const size_t texels = surface_atlas_texels(p);
+  return points >= 65536 && (uint64_t)points >= 2 * (uint64_t)texels && texels * 16 <= ((size_t)256 << 20);
 }
 
 // A plain 16-B copy on a fixed number of 256-thread workgroups (ocean_debug_copy): bench.py paces the

@@ -883,6 +883,35 @@ def test_surface_plane_mesh_vs_oracle(ocean, oracle):
     assert np.array_equal(got, want), np.max(np.abs(got - want))
 
 
+def test_surface_atlas_path_bit_exact_vs_oracle(ocean, oracle):
+    """Requests of >= 4 vertices per map texel sample a repacked atlas of the maps (launch_surface,
+    surface_use_atlas): the plane mesh at 1024^2 quads and 1.1 M explicit positions, bit-exact with the
+    oracle as the direct path below that size; a smaller request after them takes the direct path again
+    on the same plan."""
+    from oceansimulation_amd.surface import SurfaceSampler, host_cascades
+
+    cam = [3.0, 5.0, -2.0, -0.6, 0.8]
+    res = 1024  # 1025^2 vertices against 3 x 256^2 texels: the atlas path
+    fft0, flat = _scene(ocean, 256)
+    for g in flat:
+        ocean.apply_settings(g.GetOceanSettings(0), scale=0.0)
+        g.CalculateOcean(0.0, update_ocean=True)
+    base = SurfaceSampler([(g, 0) for g in flat]).plane_host(cam, res)
+    fft, gens = _scene(ocean, 256)
+    pairs = [(g, 0) for g in gens]
+    sampler = SurfaceSampler(pairs)
+    host = host_cascades(pairs)
+    got = sampler.plane_host(cam, res)
+    want = oracle.surface_points(host, base[:, [0, 2]].copy())
+    assert np.array_equal(got, want), np.max(np.abs(got - want))
+    rng = np.random.default_rng(11)
+    xz = rng.uniform(-400.0, 400.0, (1 << 20 | 4096, 2)).astype(np.float32)
+    got = sampler.sample_host(xz)
+    assert np.array_equal(got, oracle.surface_points(host, xz))
+    small = xz[:3000].copy()  # direct path
+    assert np.array_equal(sampler.sample_host(small), got[:3000])
+
+
 def test_surface_batched_generator_and_errors(ocean):
     """(generator, cascade) pairs from one batched generator equal three single generators;
     invalid requests fail loudly."""

@@ -90,7 +90,9 @@ __device__ __forceinline__ float tap_sum(const float* __restrict__ tex, const Ta
 
 // SEL: channel-selective dword loads (else float4 loads as production); NC > 0: the normal stage
 // unrolled over exactly NC cascades (all its loads issued together), else a runtime loop
-template <bool SEL, int NC>
+// INC: the vertex's (i, j) advanced by the grid stride's (di, dj) with a carry instead of a 64-bit
+// division and remainder per vertex
+template <bool SEL, int NC, bool INC = false>
 __global__ __launch_bounds__(256) void k_surface_v(SurfaceParams p, SurfacePlane plane, int64_t count,
                                                    float4* __restrict__ out)
 {
@@ -104,11 +106,31 @@ __global__ __launch_bounds__(256) void k_surface_v(SurfaceParams p, SurfacePlane
     cam_y = fmaxf(plane.cam_y, 10.0f);
   }
   const int ncas = NC > 0 ? NC : p.count;
-  for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < count;
-       idx += (int64_t)gridDim.x * blockDim.x)
+  const int side = plane.res + 1;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  const int64_t idx0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int di = (int)(stride % side), dj = (int)(stride / side);
+  int ic = (int)(idx0 % side), jc = (int)(idx0 / side);
+  for (int64_t idx = idx0; idx < count; idx += stride)
   {
-    const int side = plane.res + 1;
-    const int i = (int)(idx % side), j = (int)(idx / side);
+    int i, j;
+    if constexpr (INC)
+    {
+      i = ic;
+      j = jc;
+      ic += di;
+      jc += dj;
+      if (ic >= side)
+      {
+        ic -= side;
+        jc++;
+      }
+    }
+    else
+    {
+      i = (int)(idx % side);
+      j = (int)(idx / side);
+    }
     const float x = -20.0f + 40.0f * (float)i / (float)plane.res + 15.0f;
     const float z = -20.0f + 40.0f * (float)j / (float)plane.res + 15.0f;
     float rx = tx * x - tz * z, rz = x * tz + z * tx;
@@ -193,6 +215,86 @@ __global__ __launch_bounds__(256) void k_surface_v(SurfaceParams p, SurfacePlane
   }
 }
 
+
+// ATLAS: per cascade two repacked maps, a[texel] = (h, Dx, Dz, 0) for the vertex stage and
+// b[texel] = (dh/dx, dh/dz, dDx/dx, dDz/dz) + jac[texel] for the normal stage: one 16-B load per tap
+// and stage (plus the Jacobian's dword) instead of one dword per channel
+struct Atlas
+{
+  const float4* a[3];
+  const float4* b[3];
+};
+
+__global__ void k_atlas(SurfaceParams p, float4* a0, float4* b0)
+{
+  const int nn = p.n * p.n;
+  for (int idx = blockIdx.x * blockDim.x + threadIdx.x; idx < p.count * nn; idx += gridDim.x * blockDim.x)
+  {
+    const int c = idx / nn, t = idx - c * nn;
+    const float4 h = p.c[c].height[t], d = p.c[c].disp[t];
+    a0[idx] = make_float4(h.x, h.w, d.x, 0.0f);
+    b0[idx] = make_float4(h.y, h.z, d.y, d.z);
+  }
+}
+
+__global__ __launch_bounds__(256) void k_surface_atlas(SurfaceParams p, Atlas at, SurfacePlane plane, int64_t count,
+                                                       float4* __restrict__ out)
+{
+#pragma clang fp contract(off)
+  float tx = 0.0f, tz = 0.0f, cam_y = 0.0f;
+  {
+    const float fl = sqrtf(plane.fwd_x * plane.fwd_x + plane.fwd_z * plane.fwd_z);
+    const float tx0 = plane.fwd_x / fl, tz0 = plane.fwd_z / fl;
+    tx = (tx0 - tz0) * 0.70711f;
+    tz = (tx0 + tz0) * 0.70711f;
+    cam_y = fmaxf(plane.cam_y, 10.0f);
+  }
+  const int ncas = p.count;
+  for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < count; idx += (int64_t)gridDim.x * blockDim.x)
+  {
+    const int side = plane.res + 1;
+    const int i = (int)(idx % side), j = (int)(idx / side);
+    const float x = -20.0f + 40.0f * (float)i / (float)plane.res + 15.0f;
+    const float z = -20.0f + 40.0f * (float)j / (float)plane.res + 15.0f;
+    float rx = tx * x - tz * z, rz = x * tz + z * tx;
+    const float len0 = sqrtf(rx * rx + rz * rz);
+    const float kk = powf(fmaxf(len0, 1.0f), 1.2f) * cam_y * 0.04f;
+    float px = rx * kk + plane.cam_x;
+    float pz = rz * kk + plane.cam_z;
+    float py = 0.0f;
+    for (int c = 0; c < ncas; c++)
+    {
+      const float u = px / p.c[c].plane, v = pz / p.c[c].plane;
+      const Taps k = taps_of(p.n, u, v);
+      const float4 q00 = at.a[c][k.o00], q10 = at.a[c][k.o10], q01 = at.a[c][k.o01], q11 = at.a[c][k.o11];
+      const float h0 = k.w00 * q00.x + k.w10 * q10.x + k.w01 * q01.x + k.w11 * q11.x;
+      const float h3 = k.w00 * q00.y + k.w10 * q10.y + k.w01 * q01.y + k.w11 * q11.y;
+      const float d0 = k.w00 * q00.z + k.w10 * q10.z + k.w01 * q01.z + k.w11 * q11.z;
+      px += p.c[c].scale * h3;
+      py += h0;
+      pz += p.c[c].scale * d0;
+    }
+    float d[4] = {0.0f, 0.0f, 0.0f, 0.0f}, jac = 0.0f;
+    for (int c = 0; c < ncas; c++)
+    {
+      const float u = px / p.c[c].plane, v = pz / p.c[c].plane;
+      const Taps k = taps_of(p.n, u, v);
+      const float4 q00 = at.b[c][k.o00], q10 = at.b[c][k.o10], q01 = at.b[c][k.o01], q11 = at.b[c][k.o11];
+      jac += tap_sum<1>(p.c[c].jac, k, 0) / (float)ncas;
+      const float f = p.c[c].scale;
+      d[0] += k.w00 * q00.x + k.w10 * q10.x + k.w01 * q01.x + k.w11 * q11.x;
+      d[1] += (k.w00 * q00.z + k.w10 * q10.z + k.w01 * q01.z + k.w11 * q11.z) * f;
+      d[2] += k.w00 * q00.y + k.w10 * q10.y + k.w01 * q01.y + k.w11 * q11.y;
+      d[3] += (k.w00 * q00.w + k.w10 * q10.w + k.w01 * q01.w + k.w11 * q11.w) * f;
+    }
+    const float sx = d[0] / (1.0f + d[1]), sz = d[2] / (1.0f + d[3]);
+    const float nx = -sx, ny = 1.0f, nz = -sz;
+    const float len = sqrtf(nx * nx + ny * ny + nz * nz);
+    out[2 * idx] = make_float4(px, py, pz, jac);
+    out[2 * idx + 1] = make_float4(nx / len, ny / len, nz / len, 0.0f);
+  }
+}
+
 __global__ void fill_maps(float* p, size_t n, unsigned seed, float amp)
 {
   for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
@@ -248,6 +350,15 @@ int main()
     hipLaunchKernelGGL(fill_maps, dim3(256), dim3(256), 0, 0, j, (size_t)n * n, 37u + c, 1.0f);
     p.c[c] = SurfaceCascade{h, d, j, planes[c], 1.0f};
   }
+  float4 *atl_a, *atl_b;
+  CHECK(hipMalloc(&atl_a, (size_t)C * n * n * 16));
+  CHECK(hipMalloc(&atl_b, (size_t)C * n * n * 16));
+  Atlas atl{};
+  for (int c = 0; c < C; c++)
+  {
+    atl.a[c] = atl_a + (size_t)c * n * n;
+    atl.b[c] = atl_b + (size_t)c * n * n;
+  }
   for (int res : {1024, 4096})
   {
     const SurfacePlane plane{res, 3.0f, 5.0f, -2.0f, -0.6f, 0.8f};
@@ -259,7 +370,9 @@ int main()
     const long blocks = std::min<long>((pts + 255) / 256, cap);
     std::vector<std::string> names = {"production k_surface (dword channels)", "float4 loads (round-6 production before)",
                                       "dword channels, runtime loops", "dword channels, normal stage unrolled (3)",
-                                      "dword channels, unrolled, grid x2", "dword channels, unrolled, grid x4"};
+                                      "dword channels, unrolled, grid x2", "dword channels, unrolled, grid x4",
+                                      "dword channels, incremental (i, j)", "dword channels, incremental, grid x4",
+                                      "atlas: repack + sample", "atlas: sample only"};
     std::vector<std::function<hipError_t()>> runs = {
         [&] { return launch_surface(p, plane, nullptr, pts, o0, 0, cus); },
         [&] {
@@ -282,6 +395,24 @@ int main()
         [&] {
           const long b4 = std::min<long>((pts + 255) / 256, cap * 4);
           hipLaunchKernelGGL((k_surface_v<true, 3>), dim3(b4), dim3(256), 0, 0, p, plane, pts, o1);
+          return hipGetLastError();
+        },
+        [&] {
+          hipLaunchKernelGGL((k_surface_v<true, 0, true>), dim3(blocks), dim3(256), 0, 0, p, plane, pts, o1);
+          return hipGetLastError();
+        },
+        [&] {
+          const long b4 = std::min<long>((pts + 255) / 256, cap * 4);
+          hipLaunchKernelGGL((k_surface_v<true, 0, true>), dim3(b4), dim3(256), 0, 0, p, plane, pts, o1);
+          return hipGetLastError();
+        },
+        [&] {
+          hipLaunchKernelGGL(k_atlas, dim3(cus * 4), dim3(256), 0, 0, p, atl_a, atl_b);
+          hipLaunchKernelGGL(k_surface_atlas, dim3(blocks), dim3(256), 0, 0, p, atl, plane, pts, o1);
+          return hipGetLastError();
+        },
+        [&] {
+          hipLaunchKernelGGL(k_surface_atlas, dim3(blocks), dim3(256), 0, 0, p, atl, plane, pts, o1);
           return hipGetLastError();
         }};
     std::vector<float> ref(pts * 8), got(pts * 8);

@@ -889,6 +889,71 @@ int main(int argc, char** argv)
     }
     return 0;
   }
+  if (argc > 3 && std::strcmp(argv[3], "hp1") == 0 && logn == 12 && C <= 2)
+  {
+    // round 6: the row pass at <= 2 cascades (FB = 2 fields of the half-strip column pass) with the next
+    // image's loads before the stores (EARLY) and three or four workgroups per CU (MINB), against
+    // production (EARLY 0, MINB 4); maps bit-identical, medians of 9 x 20 launches
+    using S = FftShape<12>;
+    float4* h02;
+    CHECK(hipMalloc(&h02, tex * C * sizeof(float4)));
+    for (int c = 0; c < C; c++)
+    {
+      OceanSettings st{};
+      st.seed[0] = 12342; st.seed[1] = 8934; st.U_10 = 40; st.theta_0 = 25; st.F = 800000; st.g = 9.8f;
+      st.swell = 0.5f; st.h = 100; st.displacement = 0.4f; st.planeSize = planes[c % 8]; st.scale = 1; st.spread = 0.2f;
+      CHECK(launch_generate_spectrum(st, n, h02 + tex * c, 0, cus, 0, 0, 2));
+    }
+    auto cols = [&] { return launch_half_columns(logn, fp, h02, gab, gcd, ge, spec, tw, 0, cus, hs, cus); };
+    (void)sizeof(S);
+    auto rows = [&](auto kern) {
+      return std::function<hipError_t()>([=] {
+        const int grid = persistent_grid(kern, 256, HpCfg::LDS, fp.cascades * n, cus);
+        hipLaunchKernelGGL(kern, dim3(grid), dim3(256), HpCfg::LDS, 0, fp, gab, gcd, ge, spec, maps, jac, foam, tw, 0,
+                           RowSrc{});
+        return hipGetLastError();
+      });
+    };
+    std::vector<std::function<hipError_t()>> vr = {
+        [&] { return launch_half_rows(logn, fp, gab, gcd, ge, spec, maps, jac, foam, tw, 0, cus); },
+        rows(k_rows_hp<kHalfRG2, kHalfRGC2, false, false, 2, kHalfRGC2, 1, 4>),
+        rows(k_rows_hp<kHalfRG2, kHalfRGC2, false, false, 2, kHalfRGC2, 1, 3>),
+        rows(k_rows_hp<kHalfRG2, kHalfRGC2, false, false, 2, kHalfRGC2, 2, 3>),
+        rows(k_rows_hp<kHalfRG2, kHalfRGC2, false, false, 2, kHalfRGC2, 0, 3>)};
+    const char* nm[] = {"production (EARLY 0, 4 WG/CU)", "EARLY 1, 4 WG/CU", "EARLY 1, 3 WG/CU", "EARLY 2, 3 WG/CU",
+                        "EARLY 0, 3 WG/CU"};
+    const int NV = 5;
+    CHECK(cols());
+    CHECK(vr[0]());
+    CHECK(hipDeviceSynchronize());
+    auto pm = snap(maps, mb), pj = snap(jac, jb);
+    std::vector<int> same(NV, 1);
+    for (int k = 1; k < NV; k++)
+    {
+      CHECK(hipMemset(maps, 0, mb));
+      CHECK(hipMemset(jac, 0, jb));
+      CHECK(vr[k]());
+      CHECK(hipDeviceSynchronize());
+      std::printf("%s vs production: maps, jacobian\n", nm[k]);
+      same[k] = (int)diff(snap(maps, mb), pm) & (int)diff(snap(jac, jb), pj);
+    }
+    std::vector<std::vector<float>> t(NV), tf(NV);
+    for (int r = 0; r < 9; r++)
+      for (int k = 0; k < NV; k++)
+      {
+        t[k].push_back(time_ms(vr[k], 20));
+        tf[k].push_back(time_ms([&] { CHECK(cols()); return vr[k](); }, 20));
+      }
+    for (int k = 0; k < NV; k++)
+    {
+      std::sort(t[k].begin(), t[k].end());
+      std::sort(tf[k].begin(), tf[k].end());
+      std::printf("rows %-32s median %7.4f ms   frame %7.4f ms  bit-identical %s\n", nm[k], t[k][4], tf[k][4],
+                  same[k] ? "yes" : "NO");
+    }
+    CHECK(hipFree(h02));
+    return 0;
+  }
   if (argc > 3 && std::strcmp(argv[3], "qxh") == 0 && logn == 12 && C <= 2)
   {
     // round 6: the half-strip column pass (<= 2 cascades: 512-thread workgroups, two per CU, FB = 2

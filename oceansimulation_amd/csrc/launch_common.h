@@ -72,7 +72,13 @@ inline int half_rows_variant = 1;
 // Same per-column arithmetic as the 4-column strips, so the maps are bit-identical to them; at one
 // cascade the frame takes 0.319 against 0.339 ms, at two 0.597 against 0.609, at three and more it
 // loses (profiles/r04_halfbench_fb2h_{1,2,3,4,8}.log). Both launchers take the layout from here.
-inline int half_fields_fb(int logn, int cascades) { return logn == 12 && cascades <= 2 ? 2 : 4; }
+// N = 2048 (round 6) likewise: 256-thread half-strip workgroups, up to four per CU. At one cascade the
+// 4-column pass has 257 items for 256 CUs, and the CU that runs two sets the pass's time (0.0577 ms
+// against 0.0345 with 256 items, profiles/r06_halfbench_tail_11.log); the 513 half-strip items fit the
+// 1024 slots at once: column pass 0.0431 -> 0.0311 ms, frame 0.0945 -> 0.0862 ms, at two cascades
+// 0.1642 -> 0.1621 ms, at four it loses (0.2960 -> 0.3322), maps bit-identical
+// (profiles/r06_halfbench_h2k_{1,2,4}.log).
+inline int half_fields_fb(int logn, int cascades) { return (logn == 12 || logn == 11) && cascades <= 2 ? 2 : 4; }
 constexpr int kHalfRG2 = 4, kHalfRGC2 = 8;  // the FB = 2 layout's row groups
 
 // The whole-grid half-spectrum fields as one launcher writes / the other reads them: field strip width

@@ -38,7 +38,7 @@ HalfFieldLayout half_rows_layout(int logn, int cascades, int variant)
   const int hb = spectrum_block(logn);  // not read by the row pass: reported as the whole-strip width
   if (logn == 12 && variant == 1)
     return half_fields_fb(logn, cascades) == 2 ? HalfFieldLayout{2, kHalfRG2, kHalfRGC2, 2} : HalfFieldLayout{4, kHalfRG, kHalfRGC, hb};
-  if (logn == 12 && half_fields_fb(logn, cascades) == 2)
+  if (half_fields_fb(logn, cascades) == 2)
     return {2, kHalfRG2, kHalfRGC2, 2};
   return {4, kHalfRG, kHalfRGC, hb};
 }
@@ -82,22 +82,23 @@ hipError_t launch_half_columns(int logn, const FrameParams& fp, const float4* h0
       constexpr int RG = kHalfRG, RGC = kHalfRGC;
       constexpr int HKW = LOGN == 12 ? kHalfHK : 2;
       const HalfFieldLayout lay = half_cols_layout(LOGN, fp.cascades);
-      if constexpr (LOGN == 12)
+      if constexpr (LOGN == 12 || LOGN == 11)
       {
         if (lay.fb == 2)
         {
           if (lay.rg != kHalfRG2 || lay.rgc != kHalfRGC2)
             return hipErrorInvalidValue;  // the kernels below are instantiated for this layout only
-          // half strips (FB = 2): 512-thread workgroups, two per CU (a 68-KiB exchange each)
+          // half strips (FB = 2): 2T-thread workgroups (512 at 4096, two per CU with a 68-KiB exchange
+          // each; 256 at 2048, up to four per CU, two H pairs in VGPRs: with four, 8 B of spills)
           // h0 in 2-column strips (hb = 2, half_h0_block): each item streams its own strip
-          constexpr int WGH = S::T * 2;
+          constexpr int WGH = S::T * 2, HKH = LOGN == 12 ? kHalfHK : 2;
           auto kern = seed ? k_cols_half<LOGN, 0, kStream, true, false, true, kHalfRG2, kHalfRGC2, 2, true, false, kHalfHL,
                                          kHalfHKSeed, 0, 2, false, K::B, 0, true>
                            : k_cols_half<LOGN, kStream, kStream, true, false, false, kHalfRG2, kHalfRGC2, 2, true, false,
-                                         kHalfHL, kHalfHK, 0, 2, false, K::B, 0, true>;
+                                         kHalfHL, HKH, 0, 2, false, K::B, 0, true>;
           if (!seed && hb == 2)
             kern = k_cols_half<LOGN, kStream, kStream, true, false, false, kHalfRG2, kHalfRGC2, 2, true, false, kHalfHL,
-                               kHalfHK, 0, 2, false, 2, 0, true>;
+                               HKH, 0, 2, false, 2, 0, true>;
           const int lds = ((S::TW_ENTRIES * 8 + 15) / 16) * 16 + 2 * S::PADDED * 8 + kHalfHL * WGH * 16;
           int grid = persistent_grid(kern, WGH, lds, fp.cascades * HalfCfg<LOGN>::STRIPS * 2, cus);
           const int slices = hs_blocks * (1024 / WGH);
@@ -169,9 +170,9 @@ hipError_t launch_half_rows(int logn, const FrameParams& fp, const float4* gab, 
       }
       constexpr int RPW = LOGN == 12 ? 1 : 2, GRP = LOGN == 12 ? 4 : 2;
       // the column pass chose the field layout by cascade count (half_fields_fb): the fallback reads
-      // the same one (FB = 2 with row groups 4 / 8 at 4096 and <= 2 cascades)
+      // the same one (FB = 2 with row groups 4 / 8 at 2048 / 4096 and <= 2 cascades)
       auto kern = k_rows_half<LOGN, 0, kStream, 0, RPW, true, false, RG, RGC, 4, GRP>;
-      if constexpr (LOGN == 12)
+      if constexpr (LOGN == 12 || LOGN == 11)
         if (lay.fb == 2)
           kern = k_rows_half<LOGN, 0, kStream, 0, RPW, true, false, kHalfRG2, kHalfRGC2, 2, GRP>;
       const int lds = ((S::TW_ENTRIES * 8 + 15) / 16) * 16 + lds_row_slots<LOGN>(RPW) * 8;

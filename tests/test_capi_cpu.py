@@ -243,8 +243,8 @@ def test_frame_plan_pairs_column_writes_with_row_reads(capi, n):
             # whole 128-B lines per store: RG * FB * 16 B (gab / gde) and RGC * FB * 8 B (gc)
             assert cols[1] * cols[0] * 16 == 128 and cols[2] * cols[0] * 8 == 128, cols
             seen.add(cols)
-    # the half-strip shape exists only at 4096 (<= 2 cascades per launch)
-    assert (len(seen) == 2) == (n == 4096), seen
+    # the half-strip shape exists at 2048 and 4096 (<= 2 cascades per launch)
+    assert (len(seen) == 2) == (n in (2048, 4096)), seen
     bad = (ctypes.c_int32 * 8)()
     assert L.ocean_frame_plan(512, 1, 1, bad) == capi.OCEAN_ERR_INVALID  # below the half path
     assert L.ocean_frame_plan(n, 0, 1, bad) == capi.OCEAN_ERR_INVALID

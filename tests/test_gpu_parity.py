@@ -411,13 +411,13 @@ def test_batched_cascades_equal_individual(ocean):
         assert np.array_equal(one.jacobian_map_host(0), batch.jacobian_map_host(c))
 
 
-def test_half_strip_shape_bit_exact_across_cascade_counts(ocean):
-    """At 4096 the column pass runs on half strips (FB = 2 fields, two 512-thread workgroups per CU)
-    when a launch holds <= 2 cascades and on whole strips above (launch_common.h half_fields_fb). A
+@pytest.mark.parametrize("n", [2048, 4096])
+def test_half_strip_shape_bit_exact_across_cascade_counts(ocean, n):
+    """At 2048 and 4096 the column pass runs on half strips (FB = 2 fields, 2T-thread workgroups) when
+    a launch holds <= 2 cascades and on whole strips above (launch_common.h half_fields_fb). A
     cascade's maps and Jacobian are bit-identical in 1-, 2- and 3-cascade generators, for plain
     frames and for the fused re-seed frames of the reference app's loop (src/Generator.cpp:45-83,
     src/Waves.cpp:91-94)."""
-    n = 4096
     planes = [5.0, 251.0, 4093.0]
     fft = ocean.FFTCalculator(n)
     gens = {k: ocean.Generator(fft, k) for k in (1, 2, 3)}

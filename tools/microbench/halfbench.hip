@@ -889,6 +889,114 @@ int main(int argc, char** argv)
     }
     return 0;
   }
+  if (argc > 3 && std::strcmp(argv[3], "h2k") == 0 && logn == 11)
+  {
+    // round 6: N = 2048 on half strips (2-column items of 256 threads, up to four per CU, FB = 2 fields,
+    // 2-column h0 strips) against production (4-column items of 512 threads, two per CU): at one cascade
+    // the production pass has 257 items for 256 CUs, so one CU runs two and the pass takes ~1.7 items'
+    // time (halfbench tail); the half-strip pass spreads 513 items over 1024 slots. Maps compared.
+    using S = FftShape<11>;
+    float4* h02;
+    CHECK(hipMalloc(&h02, tex * C * sizeof(float4)));
+    for (int c = 0; c < C; c++)
+    {
+      OceanSettings st{};
+      st.seed[0] = 12342; st.seed[1] = 8934; st.U_10 = 40; st.theta_0 = 25; st.F = 800000; st.g = 9.8f;
+      st.swell = 0.5f; st.h = 100; st.displacement = 0.4f; st.planeSize = planes[c % 8]; st.scale = 1; st.spread = 0.2f;
+      CHECK(launch_generate_spectrum(st, n, h02 + tex * c, 0, cus, 0, 0, 2));
+    }
+    auto prod_c = [&] { return launch_half_columns(logn, fp, h0, gab, gcd, ge, spec, tw, 0, cus, hs, cus); };
+    auto prod_r = [&] { return launch_half_rows(logn, fp, gab, gcd, ge, spec, maps, jac, foam, tw, 0, cus); };
+    auto hcols = [&](auto kern) {
+      constexpr int WGH = S::T * 2;
+      const int lds = ((S::TW_ENTRIES * 8 + 15) / 16) * 16 + 2 * S::PADDED * 8 + kHalfHL * WGH * 16;
+      return std::function<hipError_t()>([=] {
+        int grid = persistent_grid(kern, WGH, lds, fp.cascades * HalfCfg<11>::STRIPS * 2, cus);
+        const int slices = cus * (1024 / WGH);
+        grid = grid > slices ? slices : grid;
+        hipLaunchKernelGGL(kern, dim3(grid), dim3(WGH), lds, 0, fp, h02, gab, gcd, ge, tw, hs, HalfSlab{},
+                           reinterpret_cast<unsigned char*>(spec), 1, nullptr);
+        return hipGetLastError();
+      });
+    };
+    auto hrows = [&](auto kern, int rpw) {
+      const int lds = ((S::TW_ENTRIES * 8 + 15) / 16) * 16 + lds_row_slots<11>(rpw) * 8;
+      return std::function<hipError_t()>([=] {
+        const int grid = persistent_grid(kern, S::T * rpw, lds, fp.cascades * (n / rpw), cus);
+        hipLaunchKernelGGL(kern, dim3(grid), dim3(S::T * rpw), lds, 0, fp, gab, gcd, ge, spec, maps, jac, foam, tw, n,
+                           RowSrc{}, (const float2*)nullptr);
+        return hipGetLastError();
+      });
+    };
+#define KH2(HK) k_cols_half<11, kStream, kStream, true, false, false, kHalfRG2, kHalfRGC2, 2, true, false, kHalfHL, HK, 0, 2, false, 2, 0, true>
+    std::vector<std::function<hipError_t()>> vc = {prod_c, hcols(KH2(2)), hcols(KH2(4))};
+    std::vector<std::function<hipError_t()>> vr = {prod_r,
+                                                   hrows(k_rows_half<11, 0, kStream, 0, 2, true, false, kHalfRG2, kHalfRGC2, 2, 2>, 2),
+                                                   hrows(k_rows_half<11, 0, kStream, 0, 2, true, false, kHalfRG2, kHalfRGC2, 2, 2>, 2)};
+#undef KH2
+    const char* nm[] = {"production (whole strips, FB 4)", "half strips HK 2 (FB 2)", "half strips HK 4 (FB 2)"};
+    const int NV = 3;
+    CHECK(vc[0]());
+    CHECK(vr[0]());
+    CHECK(hipDeviceSynchronize());
+    auto pm = snap(maps, mb), pj = snap(jac, jb);
+    std::vector<int> same(NV, 1);
+    for (int k = 1; k < NV; k++)
+    {
+      CHECK(hipMemset(maps, 0, mb));
+      CHECK(hipMemset(jac, 0, jb));
+      CHECK(vc[k]());
+      CHECK(vr[k]());
+      CHECK(hipDeviceSynchronize());
+      std::printf("%s vs production: maps, jacobian\n", nm[k]);
+      same[k] = (int)diff(snap(maps, mb), pm) & (int)diff(snap(jac, jb), pj);
+    }
+    std::vector<std::vector<float>> tc(NV), tr(NV), tf(NV);
+    for (int r = 0; r < 9; r++)
+      for (int k = 0; k < NV; k++)
+      {
+        tc[k].push_back(time_ms(vc[k], 20));
+        tr[k].push_back(time_ms(vr[k], 20));
+        tf[k].push_back(time_ms([&] { CHECK(vc[k]()); return vr[k](); }, 20));
+      }
+    for (int k = 0; k < NV; k++)
+    {
+      std::sort(tc[k].begin(), tc[k].end());
+      std::sort(tr[k].begin(), tr[k].end());
+      std::sort(tf[k].begin(), tf[k].end());
+      std::printf("%-34s cols %7.4f ms  rows %7.4f ms  frame %7.4f ms  bit-identical %s\n", nm[k], tc[k][4], tr[k][4],
+                  tf[k][4], same[k] ? "yes" : "NO");
+    }
+    CHECK(hipFree(h02));
+    return 0;
+  }
+  if (argc > 3 && std::strcmp(argv[3], "tail") == 0 && logn <= 12)
+  {
+    // round 6: is the one-cascade column pass bound by the one CU that holds two items? The strip-dealt
+    // column pass (one rank) over the first ns strips, ns = STRIPS (the whole grid: N/8 + 1 items for
+    // 256 CUs at 2048) down to fewer: timing only (the Nyquist-row term kernel included in every line)
+    const int S0 = HalfCfg<11>::STRIPS;
+    const int strips_all = logn == 11 ? S0 : logn == 12 ? HalfCfg<12>::STRIPS : HalfCfg<10>::STRIPS;
+    unsigned char* send;
+    const HalfSlab full{0, strips_all, strips_all, n};
+    CHECK(hipMalloc(&send, half_slab_block_bytes(logn, C, full)));
+    std::vector<int> counts = {strips_all, strips_all - 1, strips_all - 2, strips_all - 8, strips_all - 32,
+                               (strips_all - 1) / 2 + 1, (strips_all - 1) / 2};
+    for (int ns : counts)
+    {
+      const HalfSlab h{0, ns, strips_all, n};
+      auto run = [&] {
+        return launch_half_slab_columns(logn, fp, h, 1, h0, true, nullptr, send, tw, 0, cus, hs, cus, nullptr);
+      };
+      std::vector<float> t;
+      for (int r = 0; r < 9; r++)
+        t.push_back(time_ms(run, 20));
+      std::sort(t.begin(), t.end());
+      std::printf("strip-dealt column pass, N %d, %4d strips: median %7.4f ms\n", n, ns, t[4]);
+    }
+    CHECK(hipFree(send));
+    return 0;
+  }
   if (argc > 3 && std::strcmp(argv[3], "hp1") == 0 && logn == 12 && C <= 2)
   {
     // round 6: the row pass at <= 2 cascades (FB = 2 fields of the half-strip column pass) with the next

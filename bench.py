@@ -1767,7 +1767,8 @@ def main(argv=None):
                 }
         else:
             out["roofline"]["traffic_note"] = ("no committed PMC summary of this device code "
-                                               f"(sha256 {device_source_sha256()[:12]}); tools/profile_gpu.sh")
+                                               f"(sha256 {device_source_sha256()[:12]}) for this launch shape "
+                                               f"({n}^2 x {C} cascades per GPU); tools/profile_gpu.sh")
         frame_gbs = (pass_bytes[0] + pass_bytes[1]) * per_launch_pts / ((p1_ms + p2_ms) * 1e-3) / 1e9
         out["kernels"] = {
             k: {"avg_ms": v["avg_ms"], "GB_per_s": v["bytes"] / (v["avg_ms"] * 1e-3) / 1e9,

@@ -929,13 +929,16 @@ int main(int argc, char** argv)
       });
     };
 #define KH2(HK) k_cols_half<11, kStream, kStream, true, false, false, kHalfRG2, kHalfRGC2, 2, true, false, kHalfHL, HK, 0, 2, false, 2, 0, true>
-    std::vector<std::function<hipError_t()>> vc = {prod_c, hcols(KH2(2)), hcols(KH2(4))};
+    std::vector<std::function<hipError_t()>> vc = {prod_c, hcols(KH2(2)), hcols(KH2(4)), hcols(KH2(2)), hcols(KH2(2))};
     std::vector<std::function<hipError_t()>> vr = {prod_r,
                                                    hrows(k_rows_half<11, 0, kStream, 0, 2, true, false, kHalfRG2, kHalfRGC2, 2, 2>, 2),
-                                                   hrows(k_rows_half<11, 0, kStream, 0, 2, true, false, kHalfRG2, kHalfRGC2, 2, 2>, 2)};
+                                                   hrows(k_rows_half<11, 0, kStream, 0, 2, true, false, kHalfRG2, kHalfRGC2, 2, 2>, 2),
+                                                   hrows(k_rows_half<11, 0, kStream, 0, 2, true, false, kHalfRG2, kHalfRGC2, 2, 4>, 2),
+                                                   hrows(k_rows_half<11, 0, kStream, 0, 1, true, false, kHalfRG2, kHalfRGC2, 2, 8>, 1)};
 #undef KH2
-    const char* nm[] = {"production (whole strips, FB 4)", "half strips HK 2 (FB 2)", "half strips HK 4 (FB 2)"};
-    const int NV = 3;
+    const char* nm[] = {"production (whole strips, FB 4)", "half strips HK 2 (FB 2)", "half strips HK 4 (FB 2)",
+                        "HK 2, rows grouped 4 (FB 2)", "HK 2, one-row items grouped 8"};
+    const int NV = 5;
     CHECK(vc[0]());
     CHECK(vr[0]());
     CHECK(hipDeviceSynchronize());

@@ -443,13 +443,14 @@ def weak_leg(ocean, fft, args, rank: int, world: int, dt: float) -> dict:
 
 def use_frame_overlap(args, cascades: int, path: str, n: int) -> bool:
     """The headline's frame-overlap mode: on at <= 2 cascades per GPU (the 4- and 8-GPU strong-scaling
-    shares) on the blocked half-spectrum path below 4096, where the passes' launch tails dominate. At
-    4096 those shares run pass 1 on half strips (launch_common.h half_fields_fb), whose serial frame
-    is the faster one: 0.318 against 0.346 ms overlapped at one cascade, 0.599 against 0.656 at two
-    (profiles/r04_halfbench_xgrid_fb2_{1,2}.log)."""
+    shares) on the blocked half-spectrum path below 2048, where the passes' launch tails dominate. At
+    4096 (and 2048 since round 6) those shares run pass 1 on half strips (launch_common.h
+    half_fields_fb), whose serial frame is the faster one: 0.318 against 0.346 ms overlapped at one
+    cascade of 4096, 0.599 against 0.656 at two (profiles/r04_halfbench_xgrid_fb2_{1,2}.log); at one
+    cascade of 2048 0.087 against 0.091 ms (profiles/r06g_configs.md)."""
     if args.frame_overlap != "auto":
         return args.frame_overlap == "on" and path == "half"
-    return path == "half" and cascades <= 2 and n < 4096
+    return path == "half" and cascades <= 2 and n < 2048
 
 
 def one_cascade_leg(ocean, fft, args, dt: float) -> dict:

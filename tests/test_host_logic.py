@@ -65,8 +65,9 @@ def test_frame_overlap_mode_choice():
     cascades per GPU on the blocked half path; --frame-overlap on/off overrides, never on other paths."""
     b = _bench()
     auto = b.parse([])
-    assert [b.use_frame_overlap(auto, c, "half", 2048) for c in (8, 4, 2, 1)] == [False, False, True, True]
-    assert not any(b.use_frame_overlap(auto, c, "half", 4096) for c in (8, 4, 2, 1))  # half strips: serial
+    assert [b.use_frame_overlap(auto, c, "half", 1024) for c in (8, 4, 2, 1)] == [False, False, True, True]
+    for n in (2048, 4096):  # half strips at <= 2 cascades: serial
+        assert not any(b.use_frame_overlap(auto, c, "half", n) for c in (8, 4, 2, 1))
     assert not b.use_frame_overlap(auto, 1, "full", 2048) and not b.use_frame_overlap(auto, 1, "four-step", 8192)
     assert b.use_frame_overlap(b.parse(["--frame-overlap", "on"]), 8, "half", 4096)
     assert not b.use_frame_overlap(b.parse(["--frame-overlap", "on"]), 8, "full", 4096)

@@ -167,10 +167,11 @@ int ocean_generator_set_h0_memo(ocean_generator* gen, int enable);
  * the generator's stream whenever the library writes h0 (seeding, re-seeds) and after the h0 pointer
  * is handed out (ocean_generator_initial_spectrum); other work the caller enqueues on that stream
  * between frames is not waited for, so it must not write the generator's buffers. Costs 20 B of
- * device memory per point. Pays at 1-2 cascades per generator below 4096 (8 x 4096^2: slower, leave it
- * off). At 4096 with 1-2 cascades the column pass runs on half strips (two workgroups per CU), which
- * share CUs with the overlapped row pass: there the serial frame is faster (0.318 against 0.346 ms at
- * one cascade, profiles/r04_halfbench_xgrid_fb2_1.log), so leave it off as well.
+ * device memory per point. Pays at 1-2 cascades per generator of 1024^2 (8 x 4096^2: slower, leave it
+ * off). At 2048 and 4096 with 1-2 cascades the column pass runs on half strips, which share CUs with
+ * the overlapped row pass: there the serial frame is faster (0.318 against 0.346 ms at one cascade of
+ * 4096, profiles/r04_halfbench_xgrid_fb2_1.log; 0.087 against 0.091 ms at one of 2048,
+ * profiles/r06g_configs.md), so leave it off as well.
  * Default 0. No reference counterpart (the reference barriers after every dispatch). */
 int ocean_generator_set_frame_overlap(ocean_generator* gen, int enable);
 /* Algorithmic HBM bytes per height-field point of the column pass [0] and the row pass [1] of the
